@@ -1,0 +1,67 @@
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "mpi-test_amd")
+for p in (ROOT, PKG):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (run on the GPU box)")
+
+
+@pytest.fixture(scope="session")
+def orc():
+    from oracle import orc as _orc
+    _orc.lib()
+    return _orc
+
+
+@pytest.fixture(scope="session")
+def ref_cases():
+    with open(os.path.join(GOLDEN, "ref_cases.json")) as f:
+        return json.load(f)["cases"]
+
+
+@pytest.fixture(scope="session")
+def ref_outputs():
+    z = np.load(os.path.join(GOLDEN, "ref_outputs.npz"))
+    return {k: z[k] for k in z.files}
+
+
+def case_input(orc, spec):
+    """Rebuild a golden case's input from its spec (tests/golden/make_golden.py)."""
+    if "literal" in spec:
+        return np.array(spec["literal"], dtype=np.int32)
+    if "text" in spec:
+        return None
+    dist = orc.UNIFORM if spec["gen"] == "uniform" else orc.ZIPF
+    keys = orc.gen(dist, spec["seed"], spec["n"])
+    if "mod" in spec:
+        keys = keys % spec["mod"]
+    for i, v in spec.get("set", []):
+        keys[i] = v
+    return keys
+
+
+def case_output(case, ref_outputs):
+    if "output_sha256" not in case:
+        return None
+    return ref_outputs["h_" + case["output_sha256"][:16]]
+
+
+@pytest.fixture(scope="session")
+def gsort():
+    """The product's Python binding (ctypes over libgsort.so).  Loads torch first so both
+    share one HIP runtime ('one runtime per process')."""
+    import torch  # noqa: F401
+    import gsort as _g
+    return _g

@@ -1,0 +1,168 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures under tests/golden/ by running the REFERENCE programs.
+
+The reference (/root/reference, acgrid/mpi-test) ships no tests and no fixtures,
+so its own sorted output is captured here: oracle/Makefile compiles mpi_radix_sort.c and
+mpi_sample_sort.c unchanged into oracle/_ref/, and this script runs them under MPICH's mpirun
+on inputs from the repo's splitmix64 generator (oracle.orc.gen) plus a few hand-written quirk
+inputs (SURVEY.md 8 Q-list).  Only data is committed: inputs are regenerable from their spec
+(and carry a sha256 to prove it); outputs are the reference's full sorted dumps.
+
+Capture: rank-0 lines matching ^[0-9]+\\|[0-9]+$ at debug 3 (radix) or
+debug 1 (sample), values re-signed from %u; sample's "[MASTER] Splitter" and
+"[COMMON] r: Bucket j=len" lines; the stdout median line and "Each bucket" line; exit status.
+
+Run from the repo root:  python tests/golden/make_golden.py
+"""
+import hashlib
+import json
+import os
+import re
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+from oracle import orc  # noqa: E402
+
+MPIRUN = "/opt/conda/bin/mpirun"
+OUT = os.path.join(ROOT, "tests", "golden")
+DUMP = re.compile(r"^(\d+)\|(\d+)$")
+SPLIT = re.compile(r"^\[MASTER\] Splitter: (\d+)\.$")
+BUCKET = re.compile(r"^\[COMMON\] (\d+): Bucket (\d+)=(\d+)$")
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a, dtype="<i4").tobytes()).hexdigest()
+
+
+def resign(u):
+    u = int(u)
+    return u - (1 << 32) if u >= (1 << 31) else u
+
+
+def run_ref(prog, P, path, debug, timeout=120):
+    tmp = tempfile.mkdtemp(prefix="gold_")
+    cmd = [MPIRUN, "-np", str(P), "-outfile-pattern", f"{tmp}/o.%r", "-errfile-pattern",
+           f"{tmp}/e.%r", os.path.join(orc.REF_DIR, prog), path, str(debug)]
+    try:
+        rc = subprocess.run(cmd, timeout=timeout, stdout=subprocess.DEVNULL,
+                            stderr=subprocess.DEVNULL).returncode
+    except subprocess.TimeoutExpired:
+        rc = "timeout"
+
+    def rd(name):
+        p = os.path.join(tmp, name)
+        return open(p, errors="replace").read().splitlines() if os.path.exists(p) else []
+
+    out0, err0 = rd("o.0"), rd("e.0")
+    others = [rd(f"o.{r}") for r in range(1, P)]
+    subprocess.run(["rm", "-rf", tmp])
+    dump = {}
+    for ln in out0:
+        m = DUMP.match(ln)
+        if m:
+            dump[int(m.group(1))] = resign(m.group(2))
+    res = {
+        "rc": rc,
+        "dump": np.array([dump[i] for i in sorted(dump)], dtype=np.int32),
+        "median_line": next((l for l in out0 if l.startswith("The n/2-th")), None),
+        "each_bucket_line": next((l for l in out0 if l.startswith("Each bucket")), None),
+        "stderr0": [re.sub(r"= [0-9.]+ sec", "= <t> sec", l) for l in err0],
+        "splitters": [resign(SPLIT.match(l).group(1)) for l in out0 if SPLIT.match(l)],
+    }
+    mat = {}
+    for lines in [out0] + others:
+        for ln in lines:
+            m = BUCKET.match(ln)
+            if m:
+                mat[(int(m.group(1)), int(m.group(2)))] = int(m.group(3))
+    if mat:
+        res["bucket_matrix"] = [[mat.get((r, j), 0) for j in range(P)] for r in range(P)]
+    return res
+
+
+def main():
+    orc.build()
+    tmpdir = tempfile.mkdtemp(prefix="goldin_")
+    cases = []
+    arrays = {}
+
+    def add_case(name, prog, P, keys, spec, text=None):
+        path = os.path.join(tmpdir, name + ".txt")
+        if text is None:
+            orc.write_text(path, keys)
+        else:
+            with open(path, "w") as f:
+                f.write(text)
+        debug = 3 if prog == "radix_sort" else 1
+        r = run_ref(prog, P, path, debug)
+        key = f"{name}__{prog}__P{P}"
+        c = {"id": key, "prog": prog, "P": P, "input": spec, "rc": r["rc"],
+             "median_line": r["median_line"], "each_bucket_line": r["each_bucket_line"],
+             "stderr0": r["stderr0"], "n_dump": int(r["dump"].size)}
+        if keys is not None:
+            c["input_sha256"] = sha(keys)
+        if r["dump"].size:
+            c["output_sha256"] = sha(r["dump"])
+            arrays[key] = r["dump"]
+        if prog == "sample_sort":
+            c["splitters"] = r["splitters"]
+            c["bucket_matrix"] = r.get("bucket_matrix")
+        cases.append(c)
+        print(key, "rc", r["rc"], "n", r["dump"].size, flush=True)
+
+    # canonical generated inputs, inside the parity domain
+    for dist, dname, n, seed in [(orc.UNIFORM, "uniform", 1 << 10, 42),
+                                 (orc.UNIFORM, "uniform", 1 << 16, 42),
+                                 (orc.ZIPF, "zipf", 1 << 16, 7)]:
+        keys = orc.gen(dist, seed, n)
+        spec = {"gen": dname, "n": n, "seed": seed}
+        for P in (2, 4, 8):
+            add_case(f"{dname}{n}s{seed}", "radix_sort", P, keys, spec)
+        for P in ((2, 4, 8) if dist == orc.UNIFORM else (2, 4)):
+            add_case(f"{dname}{n}s{seed}", "sample_sort", P, keys, spec)
+    # P = 3 (Q3 pass-count under-count at 243) and P = 1 (Q1 zero passes)
+    keys = orc.gen(orc.UNIFORM, 5, 999) % 1000
+    keys[17] = 243
+    add_case("u999mod1000", "radix_sort", 3, keys, {"gen": "uniform", "n": 999, "seed": 5,
+                                                     "mod": 1000, "set": [[17, 243]]})
+    keys = np.array([250, 7, 243, 1, 242, 9], dtype=np.int32)
+    add_case("q3_max243", "radix_sort", 3, keys, {"literal": keys.tolist()})
+    keys = orc.gen(orc.UNIFORM, 42, 1000)
+    add_case("uniform1000s42", "radix_sort", 1, keys, {"gen": "uniform", "n": 1000, "seed": 42})
+    # Q2 negative keys (ref-radix sorts by |v| mod P^loop, stable)
+    neg = np.array([-7, 3, 7, -2, 2, -3, 5, 0], dtype=np.int32)
+    for P in (2, 4, 8):
+        add_case("q2_neg8", "radix_sort", P, neg, {"literal": neg.tolist()})
+    # Q6 trailing newline phantom, Q7 %d wrap of out-of-range text
+    add_case("q6_trailing_nl", "radix_sort", 2, None, {"text": "5\n3\n9\n1\n"},
+             text="5\n3\n9\n1\n")
+    add_case("q7_wrap", "radix_sort", 2, None,
+             {"text": "2147483648 4294967295 12 -5 0 4294967296 77 1"},
+             text="2147483648 4294967295 12 -5 0 4294967296 77 1")
+    # Q9 "no enough sample" abort (N=9, P=4)
+    k9 = np.arange(9, 0, -1, dtype=np.int32)
+    add_case("q9_n9", "sample_sort", 4, k9, {"literal": k9.tolist()})
+
+    with open(os.path.join(OUT, "ref_cases.json"), "w") as f:
+        json.dump({"generator": "tests/golden/make_golden.py", "mpirun": MPIRUN,
+                   "cases": cases}, f, indent=1)
+    # outputs are identical across P inside the parity domain: store each distinct array once
+    uniq, index = {}, {}
+    for k, a in arrays.items():
+        h = sha(a)
+        if h not in uniq:
+            uniq[h] = a
+        index[k] = h
+    np.savez_compressed(os.path.join(OUT, "ref_outputs.npz"),
+                        **{"h_" + h[:16]: a for h, a in uniq.items()})
+    subprocess.run(["rm", "-rf", tmpdir])
+    print("wrote", len(cases), "cases,", len(uniq), "distinct output arrays")
+
+
+if __name__ == "__main__":
+    main()
