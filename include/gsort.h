@@ -1,0 +1,156 @@
+/*
+ * gsort.h -- C-ABI of libgsort, the MI355X-native distributed integer sorter.
+ *
+ * Drop-in boundary.  The reference (acgrid/mpi-test) has no library API: its boundary is the
+ * program (argv + text file + stdout/stderr + exit status) and, inside it, one function
+ *     void sort(const int rank, const int size, const char *file, const int debug)
+ * (mpi_radix_sort/mpi_radix_sort.c:60, mpi_sample_sort/mpi_sample_sort.c:28), called from
+ * main (mpi_radix_sort.c:224, mpi_sample_sort.c:237).  The host CLIs radix_sort / sample_sort
+ * (mpi-test_amd/host/) keep that program contract and call the entry points below; each entry
+ * point names the reference code it replaces.
+ *
+ * Conventions: plain pointers and sizes, no torch types.  One context per rank == one GPU;
+ * not thread-safe (one thread per context).  Every call is blocking on return (its stream is
+ * synchronised), matching the reference's blocking MPI semantics.  Counts are size_t (the
+ * reference's int counts cap N at 2^31-1).  The library never aborts: it returns
+ * a status and the host maps non-OK to the reference's stderr + MPI_Abort convention.
+ * Keys are int32 and the output order is ascending signed order.
+ */
+#ifndef GSORT_H
+#define GSORT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct gsort_ctx gsort_ctx;
+typedef struct gsort_group gsort_group;
+
+typedef enum {
+    GSORT_OK = 0,
+    GSORT_EINVAL = 1,    /* bad argument / shape                                          */
+    GSORT_ENOMEM = 2,    /* device or host allocation failed                               */
+    GSORT_EHIP = 3,      /* HIP runtime error                                              */
+    GSORT_ERCCL = 4,     /* RCCL error                                                     */
+    GSORT_ENOSAMPLE = 5, /* sample sort: a block is too small for 2P-1 regular samples;
+                            the reference aborts with "no enough sample"
+                            (mpi_sample_sort.c:94-99)                                      */
+    GSORT_ECOMM = 6      /* in-process rank group misuse / peer failure                   */
+} gsort_status;
+
+/* Wraps an ncclUniqueId (rccl.h:43).  Rank 0 creates it, the host broadcasts it (MPI_Bcast in
+ * the CLIs, torch.distributed in bench.py).  Replaces the reference's MPI_COMM_WORLD. */
+typedef struct { char internal[128]; } gsort_uid;
+
+/* Per-call device-time breakdown (hipEvents on the context's stream), filled when non-NULL. */
+typedef struct {
+    double ms_total;          /* whole call, device time                                    */
+    double ms_hist;           /* K1 digit histograms                                        */
+    double ms_pass[4];        /* K3 onesweep passes of the final local sort, by digit        */
+    double ms_local_sort;     /* all local-sort kernels (K1+K3), every local sort in the call */
+    double ms_exchange;       /* RCCL key exchange(s), all passes                           */
+    double ms_place;          /* K8 receive-side placement (radix, P > 1)                   */
+    double ms_sample;         /* K4-K6 sampling, splitters, bucket bounds (sample)          */
+    double ms_merge;          /* K7 final merge (sample, P > 1)                             */
+    uint64_t keys_local_in;   /* keys this rank held before the call                        */
+    uint64_t keys_local_out;  /* keys this rank holds after the call                        */
+    uint64_t bytes_sent;      /* key bytes this rank sent to OTHER ranks, all passes        */
+    uint64_t max_pair_bytes;  /* largest single (this rank -> peer) message, bytes          */
+    int passes_run;           /* onesweep passes run by the final local sort (<= 4)         */
+    int exchanges;            /* RCCL all-to-all rounds                                      */
+} gsort_stats;
+
+/* ---- context -------------------------------------------------------------------------- */
+gsort_status gsort_get_uid(gsort_uid *out);
+/* RCCL-backed context (one process per GPU).  nranks == 1 needs no uid (uid may be NULL).
+ * hip_device >= 0 selects that GPU; hip_device = -1 - local_rank selects
+ * local_rank % (visible GPUs), the usual one-rank-per-GPU placement.
+ * Replaces MPI_Init/MPI_Comm_size/MPI_Comm_rank + the MPI communicator
+ * (mpi_radix_sort.c:212-214, mpi_sample_sort.c:225-227). */
+gsort_status gsort_create(gsort_ctx **ctx, int rank, int nranks, int hip_device,
+                          const gsort_uid *uid);
+/* In-process rank group: nranks contexts driven by nranks threads of ONE process, exchanging
+ * through device-to-device copies (all on one GPU or on xGMI peers).  Used to run the
+ * distributed algorithm with P ranks on a single GPU. */
+gsort_status gsort_group_create(gsort_group **grp, int nranks);
+gsort_status gsort_group_destroy(gsort_group *grp);
+gsort_status gsort_create_in_group(gsort_ctx **ctx, gsort_group *grp, int rank, int hip_device);
+gsort_status gsort_destroy(gsort_ctx *ctx);
+/* Pre-size device scratch for n_local keys (keeps hipMalloc out of timed regions). */
+gsort_status gsort_reserve(gsort_ctx *ctx, size_t n_local);
+const char *gsort_strerror(gsort_status st);
+const char *gsort_last_error(const gsort_ctx *ctx);
+int gsort_rank(const gsort_ctx *ctx);
+int gsort_nranks(const gsort_ctx *ctx);
+
+/* ---- device-resident hot path ----------------------------------------------------------
+ * d_keys: this rank's n_local keys, already on this GPU (block layout, like the reference's
+ * initial_sort after MPI_Scatter).  On return *d_out holds this rank's slice of the globally
+ * sorted sequence (ctx-owned, valid until the next sort call on ctx); d_keys is unchanged.
+ *
+ * gsort_radix replaces the radix pass loop mpi_radix_sort.c:133-195 (digit extraction
+ * :144-147, count + data all-to-all :150-174, gather/scatter through rank 0 :139,:180-192).
+ * Output: balanced blocks -- rank q holds global positions [q*B, min((q+1)*B, N)),
+ * B = ceil(N / P), N = sum of n_local over ranks (the reference's size_batch, radix:114).
+ *
+ * gsort_sample replaces mpi_sample_sort.c:76-197 (local qsort :85, regular sampling
+ * :89-105, splitter selection :109-128, splitter broadcast :126-133, bucket partition
+ * :148-155, all-to-all :160-170, final qsort :174).  Output: rank q holds bucket q (keys in
+ * (s[q-1], s[q]]), so *n_out varies by rank exactly as the reference's size_current_bucket. */
+gsort_status gsort_radix(gsort_ctx *ctx, const int32_t *d_keys, size_t n_local,
+                         int32_t **d_out, size_t *n_out, gsort_stats *stats);
+gsort_status gsort_sample(gsort_ctx *ctx, const int32_t *d_keys, size_t n_local,
+                          int32_t **d_out, size_t *n_out, gsort_stats *stats);
+/* After gsort_sample: the P-1 splitters (mpi_sample_sort.c:123, "[MASTER] Splitter" lines)
+ * and this rank's P bucket lengths ("[COMMON] r: Bucket j=len", :156-158). */
+gsort_status gsort_sample_info(const gsort_ctx *ctx, int32_t *splitters,
+                               uint64_t *bucket_counts);
+
+/* ---- drop-in staging (replaces MPI_Scatter / MPI_Gather(v) through rank 0) ---------------
+ * gsort_scatter_from_root: rank 0's host array (n_total keys; h_root ignored elsewhere) ->
+ * each rank's block [r*B, min((r+1)*B, N)) on its GPU.  Replaces MPI_Scatter
+ * (mpi_radix_sort.c:139, mpi_sample_sort.c:82).  *d_keys is ctx-owned.
+ * gsort_gather_to_root: every rank's (d_out, n_out) -> rank 0's host array in rank order.
+ * Replaces MPI_Gather + MPI_Gatherv (mpi_radix_sort.c:181-192, mpi_sample_sort.c:183-195). */
+gsort_status gsort_scatter_from_root(gsort_ctx *ctx, const int32_t *h_root, size_t n_total,
+                                     int32_t **d_keys, size_t *n_local);
+gsort_status gsort_gather_to_root(gsort_ctx *ctx, const int32_t *d_out, size_t n_out,
+                                  int32_t *h_root);
+
+/* ---- device utilities (bench + parity; not in the reference) ------------------------------
+ * gsort_generate: K10, the canonical splitmix64 stream; dist 0 = uniform
+ * [0, 2^31-1], 1 = zipf s=1.5.  Key i of the stream is written to d_out[i - start].
+ * gsort_fingerprint: K9, order-independent multiset fingerprint (sum and xor of mix64(key))
+ * plus is-sorted; first/last keys let the host check order across ranks. */
+gsort_status gsort_generate(gsort_ctx *ctx, int dist, uint64_t seed, uint64_t start, size_t n,
+                            int32_t *d_out);
+gsort_status gsort_fingerprint(gsort_ctx *ctx, const int32_t *d_keys, size_t n, uint64_t *sum,
+                               uint64_t *xr, int *sorted, int32_t *first, int32_t *last);
+/* Copy helpers for hosts that have no HIP headers (the C CLIs, ctypes). */
+gsort_status gsort_device_alloc(gsort_ctx *ctx, size_t bytes, void **d_ptr);
+gsort_status gsort_device_free(gsort_ctx *ctx, void *d_ptr);
+gsort_status gsort_copy_to_host(gsort_ctx *ctx, void *h_dst, const void *d_src, size_t bytes);
+gsort_status gsort_copy_to_device(gsort_ctx *ctx, void *d_dst, const void *h_src, size_t bytes);
+/* Which kernel configuration the local sort uses (tile = keys per workgroup). */
+size_t gsort_onesweep_tile(void);
+
+/* ---- host-only planning (no GPU; exported so CPU tests can check it) ----------------------
+ * gsort_plan_radix_route: the K8 routing of one distributed LSD pass.  hist = P x 256 per-rank
+ * digit counts, B = block size.  Fills send[P] / recv[P] key counts for rank `me` and the
+ * receive-side placement rows seg[4*k] = {src rank, offset in src's chunk, dest offset,
+ * length}; *nseg = k (<= P*256).  Semantics of mpi_radix_sort.c:150-192 (stable: digit, then
+ * source rank, then source order).
+ * gsort_plan_splitters: sort the P*(2P-1) rank-ordered samples and pick
+ * splitters[i] = S[(i+1)(2P-1)] (mpi_sample_sort.c:116-123). */
+gsort_status gsort_plan_radix_route(int P, const uint64_t *hist, uint64_t B, int me,
+                                    uint64_t *send, uint64_t *recv, uint64_t *seg,
+                                    size_t *nseg);
+gsort_status gsort_plan_splitters(int P, const int32_t *samples, int32_t *splitters);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GSORT_H */

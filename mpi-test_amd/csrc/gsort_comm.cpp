@@ -1,0 +1,187 @@
+// gsort_comm.cpp -- RCCL and in-process transports (see gsort_comm.h).
+#include "gsort_comm.h"
+
+#include <rccl/rccl.h>
+#include <string.h>
+
+#include <chrono>
+#include <condition_variable>
+#include <mutex>
+#include <vector>
+
+namespace gsort {
+
+// ---------------------------------------------------------------------------------------
+// RCCL over xGMI
+// ---------------------------------------------------------------------------------------
+class RcclComm : public Comm {
+  public:
+    RcclComm(ncclComm_t c, int rank, int n) : comm_(c) { rank_ = rank; size_ = n; }
+    ~RcclComm() override { ncclCommDestroy(comm_); }
+
+    gsort_status check(ncclResult_t r, const char *what) {
+        if (r == ncclSuccess) return GSORT_OK;
+        err = std::string(what) + ": " + ncclGetErrorString(r);
+        return GSORT_ERCCL;
+    }
+    gsort_status allgather(const void *send, void *recv, size_t bytes, hipStream_t s) override {
+        return check(ncclAllGather(send, recv, bytes, ncclChar, comm_, s), "ncclAllGather");
+    }
+    // One grouped send/recv round: every (src, dst) pair with a non-zero count is one
+    // message of exactly that many bytes (the reference sends fixed 1.5B-int messages with
+    // the real length in the tag, mpi_sample_sort.c:161,168).
+    gsort_status alltoallv(const void *send, const size_t *scount, const size_t *sdispl,
+                           void *recv, const size_t *rcount, const size_t *rdispl,
+                           hipStream_t s) override {
+        gsort_status st = check(ncclGroupStart(), "ncclGroupStart");
+        if (st != GSORT_OK) return st;
+        for (int q = 0; q < size_; ++q) {
+            if (scount[q])
+                st = check(ncclSend((const char *)send + sdispl[q], scount[q], ncclChar, q,
+                                    comm_, s), "ncclSend");
+            if (st == GSORT_OK && rcount[q])
+                st = check(ncclRecv((char *)recv + rdispl[q], rcount[q], ncclChar, q, comm_, s),
+                           "ncclRecv");
+            if (st != GSORT_OK) break;
+        }
+        gsort_status st2 = check(ncclGroupEnd(), "ncclGroupEnd");
+        return st != GSORT_OK ? st : st2;
+    }
+    gsort_status bcast(void *buf, size_t bytes, int root, hipStream_t s) override {
+        return check(ncclBroadcast(buf, buf, bytes, ncclChar, root, comm_, s), "ncclBroadcast");
+    }
+
+  private:
+    ncclComm_t comm_;
+};
+
+gsort_status rccl_get_uid(gsort_uid *out) {
+    static_assert(sizeof(ncclUniqueId) == sizeof(gsort_uid), "uid size");
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return GSORT_ERCCL;
+    memcpy(out, &id, sizeof(id));
+    return GSORT_OK;
+}
+
+Comm *make_rccl_comm(int rank, int nranks, const gsort_uid *uid, std::string *err) {
+    ncclUniqueId id;
+    memcpy(&id, uid, sizeof(id));
+    ncclComm_t c;
+    ncclResult_t r = ncclCommInitRank(&c, nranks, id, rank);
+    if (r != ncclSuccess) {
+        *err = std::string("ncclCommInitRank: ") + ncclGetErrorString(r);
+        return nullptr;
+    }
+    return new RcclComm(c, rank, nranks);
+}
+
+// ---------------------------------------------------------------------------------------
+// In-process rank group.  Each collective: every rank synchronises its stream (its send data
+// is complete), publishes pointers, meets the others at a barrier, pulls what it needs with
+// hipMemcpyAsync on its own stream, synchronises, and meets them again (so no sender reuses a
+// buffer a peer is still reading).
+// ---------------------------------------------------------------------------------------
+struct GroupState {
+    int n;
+    std::mutex m;
+    std::condition_variable cv;
+    int arrived = 0;
+    uint64_t generation = 0;
+    bool broken = false;
+    std::vector<const void *> ptr;
+    std::vector<const size_t *> count, displ;
+    explicit GroupState(int n_) : n(n_), ptr(n_), count(n_), displ(n_) {}
+};
+
+GroupState *group_state_create(int nranks) { return new GroupState(nranks); }
+void group_state_destroy(GroupState *g) { delete g; }
+int group_state_size(const GroupState *g) { return g->n; }
+
+class GroupComm : public Comm {
+  public:
+    GroupComm(GroupState *g, int rank) : g_(g) { rank_ = rank; size_ = g->n; }
+
+    // generation barrier with a generous timeout so a dead peer cannot hang the process
+    bool barrier() {
+        std::unique_lock<std::mutex> lk(g_->m);
+        if (g_->broken) return false;
+        const uint64_t gen = g_->generation;
+        if (++g_->arrived == g_->n) {
+            g_->arrived = 0;
+            ++g_->generation;
+            g_->cv.notify_all();
+            return true;
+        }
+        const bool ok = g_->cv.wait_for(lk, std::chrono::seconds(300),
+                                        [&] { return g_->generation != gen || g_->broken; });
+        if (!ok || g_->broken) {
+            g_->broken = true;
+            g_->cv.notify_all();
+            return false;
+        }
+        return true;
+    }
+    gsort_status fail(const char *what) {
+        err = std::string("in-process group: ") + what;
+        return GSORT_ECOMM;
+    }
+    gsort_status hip(hipError_t e, const char *what) {
+        if (e == hipSuccess) return GSORT_OK;
+        err = std::string(what) + ": " + hipGetErrorString(e);
+        return GSORT_EHIP;
+    }
+
+    gsort_status allgather(const void *send, void *recv, size_t bytes, hipStream_t s) override {
+        gsort_status st = hip(hipStreamSynchronize(s), "hipStreamSynchronize");
+        if (st != GSORT_OK) return st;
+        g_->ptr[rank_] = send;
+        if (!barrier()) return fail("barrier timeout");
+        for (int r = 0; r < size_ && st == GSORT_OK; ++r)
+            if (bytes)
+                st = hip(hipMemcpyAsync((char *)recv + (size_t)r * bytes, g_->ptr[r], bytes,
+                                        hipMemcpyDeviceToDevice, s), "hipMemcpyAsync");
+        if (st == GSORT_OK) st = hip(hipStreamSynchronize(s), "hipStreamSynchronize");
+        if (!barrier()) return fail("barrier timeout");
+        return st;
+    }
+    gsort_status alltoallv(const void *send, const size_t *scount, const size_t *sdispl,
+                           void *recv, const size_t *rcount, const size_t *rdispl,
+                           hipStream_t s) override {
+        gsort_status st = hip(hipStreamSynchronize(s), "hipStreamSynchronize");
+        if (st != GSORT_OK) return st;
+        g_->ptr[rank_] = send;
+        g_->count[rank_] = scount;
+        g_->displ[rank_] = sdispl;
+        if (!barrier()) return fail("barrier timeout");
+        for (int r = 0; r < size_ && st == GSORT_OK; ++r) {
+            const size_t c = g_->count[r][rank_];
+            if (c != rcount[r]) { st = fail("send/recv count mismatch"); break; }
+            if (c)
+                st = hip(hipMemcpyAsync((char *)recv + rdispl[r],
+                                        (const char *)g_->ptr[r] + g_->displ[r][rank_], c,
+                                        hipMemcpyDeviceToDevice, s), "hipMemcpyAsync");
+        }
+        gsort_status st2 = hip(hipStreamSynchronize(s), "hipStreamSynchronize");
+        if (!barrier()) return fail("barrier timeout");
+        return st != GSORT_OK ? st : st2;
+    }
+    gsort_status bcast(void *buf, size_t bytes, int root, hipStream_t s) override {
+        gsort_status st = hip(hipStreamSynchronize(s), "hipStreamSynchronize");
+        if (st != GSORT_OK) return st;
+        g_->ptr[rank_] = buf;
+        if (!barrier()) return fail("barrier timeout");
+        if (rank_ != root && bytes)
+            st = hip(hipMemcpyAsync(buf, g_->ptr[root], bytes, hipMemcpyDeviceToDevice, s),
+                     "hipMemcpyAsync");
+        gsort_status st2 = hip(hipStreamSynchronize(s), "hipStreamSynchronize");
+        if (!barrier()) return fail("barrier timeout");
+        return st != GSORT_OK ? st : st2;
+    }
+
+  private:
+    GroupState *g_;
+};
+
+Comm *make_group_comm(GroupState *g, int rank) { return new GroupComm(g, rank); }
+
+}  // namespace gsort

@@ -1,0 +1,839 @@
+// gsort_runtime.cpp -- the C-ABI of libgsort (include/gsort.h): contexts, the local sort,
+// the distributed radix and sample sort orchestration, and drop-in staging.
+//
+// Reference being replaced: sort() of mpi_radix_sort.c:60-205 and mpi_sample_sort.c:28-218.
+// Data stays resident on each rank's GPU for the whole sort; the host only moves per-pass
+// digit counts (a few KB) to size the RCCL messages, which need host-side counts.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "gsort.h"
+#include "gsort_comm.h"
+#include "gsort_kernels.h"
+
+using namespace gsort;
+
+struct gsort_group {
+    GroupState *st;
+};
+
+namespace {
+
+enum Slot { S_TMP, S_OUT, S_CUR, S_SORTED, S_RECV, S_IN, S_STAGE, S_NSLOTS };
+enum Phase { PH_HIST, PH_PASS0, PH_PASS1, PH_PASS2, PH_PASS3, PH_EXCH, PH_PLACE, PH_SAMPLE,
+             PH_MERGE, PH_TOTAL, PH_N };
+
+constexpr size_t kSmallBytes = 256 * 1024;  // device + pinned scratch for counts, plans
+constexpr int kMaxCounters = 64;           // tile counters per call
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+};
+
+}  // namespace
+
+struct gsort_ctx {
+    int rank = 0, nranks = 1, device = 0;
+    hipStream_t stream = nullptr;
+    Comm *comm = nullptr;
+    std::string err;
+    DevBuf slot[S_NSLOTS];
+    DevBuf status;
+    uint32_t epoch = 1;
+    int next_counter = 0;
+    // device small area: [0, 8K) hist4 (4x256 u64) | [8K, 16K) bases (4x256 u64) |
+    // [16K, 18K) next-digit hist | [18K, 18K+256) tile counters | [20K, 256K) plans/samples
+    char *d_small = nullptr;
+    char *h_small = nullptr;  // pinned mirror
+    std::vector<int32_t> splitters;
+    std::vector<uint64_t> bucket_counts;
+    // timing
+    bool timing = false;
+    std::vector<hipEvent_t> ev_pool;
+    size_t ev_used = 0;
+    struct Span { int phase; hipEvent_t a, b; };
+    std::vector<Span> spans;
+};
+
+namespace {
+
+constexpr size_t OFF_HIST = 0, OFF_BASE = 8192, OFF_NHIST = 16384, OFF_CTR = 18432,
+                 OFF_PLAN = 20480;
+
+gsort_status set_err(gsort_ctx *c, gsort_status st, const std::string &msg) {
+    if (c) c->err = msg;
+    return st;
+}
+
+#define HIP_TRY(ctx, expr)                                                                   \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess)                                                                \
+            return set_err(ctx, GSORT_EHIP,                                                  \
+                           std::string(#expr) + ": " + hipGetErrorString(e_));              \
+    } while (0)
+
+#define ST_TRY(expr)                         \
+    do {                                     \
+        gsort_status s_ = (expr);            \
+        if (s_ != GSORT_OK) return s_;       \
+    } while (0)
+
+gsort_status comm_try(gsort_ctx *c, gsort_status st) {
+    if (st != GSORT_OK) c->err = c->comm->err;
+    return st;
+}
+
+gsort_status ensure(gsort_ctx *c, DevBuf &b, size_t bytes) {
+    if (bytes <= b.cap) return GSORT_OK;
+    if (b.p) HIP_TRY(c, hipFree(b.p));
+    b.p = nullptr;
+    b.cap = 0;
+    const size_t want = (bytes + 4095) & ~size_t(4095);
+    if (hipMalloc(&b.p, want) != hipSuccess) {
+        (void)hipGetLastError();
+        b.p = nullptr;
+        return set_err(c, GSORT_ENOMEM, "hipMalloc of " + std::to_string(want) + " bytes failed");
+    }
+    b.cap = want;
+    return GSORT_OK;
+}
+
+template <class T>
+T *slot_ptr(gsort_ctx *c, Slot s) { return reinterpret_cast<T *>(c->slot[s].p); }
+
+// ---- timing ---------------------------------------------------------------------------
+hipEvent_t next_event(gsort_ctx *c) {
+    if (c->ev_used == c->ev_pool.size()) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        c->ev_pool.push_back(e);
+    }
+    return c->ev_pool[c->ev_used++];
+}
+hipEvent_t tic(gsort_ctx *c) {
+    if (!c->timing) return nullptr;
+    hipEvent_t e = next_event(c);
+    if (e && hipEventRecord(e, c->stream) != hipSuccess) e = nullptr;
+    return e;
+}
+void toc(gsort_ctx *c, int phase, hipEvent_t a) {
+    if (!c->timing || !a) return;
+    hipEvent_t b = next_event(c);
+    if (!b || hipEventRecord(b, c->stream) != hipSuccess) return;
+    c->spans.push_back({phase, a, b});
+}
+void timing_begin(gsort_ctx *c, gsort_stats *st) {
+    c->timing = st != nullptr;
+    c->ev_used = 0;
+    c->spans.clear();
+    if (st) memset(st, 0, sizeof(*st));
+}
+void timing_finish(gsort_ctx *c, gsort_stats *st) {
+    if (!st) return;
+    for (auto &sp : c->spans) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, sp.a, sp.b) != hipSuccess) continue;
+        switch (sp.phase) {
+            case PH_HIST: st->ms_hist += ms; st->ms_local_sort += ms; break;
+            case PH_PASS0: case PH_PASS1: case PH_PASS2: case PH_PASS3:
+                st->ms_pass[sp.phase - PH_PASS0] += ms; st->ms_local_sort += ms; break;
+            case PH_EXCH: st->ms_exchange += ms; break;
+            case PH_PLACE: st->ms_place += ms; break;
+            case PH_SAMPLE: st->ms_sample += ms; break;
+            case PH_MERGE: st->ms_merge += ms; break;
+            case PH_TOTAL: st->ms_total += ms; break;
+        }
+    }
+    c->timing = false;
+}
+
+// ---- onesweep pass with status/epoch bookkeeping ----------------------------------------
+gsort_status ensure_status(gsort_ctx *c, uint64_t n) {
+    const size_t need = (size_t)std::max<uint64_t>(sweep_tiles(n), 1) * kRadix * 8;
+    if (need > c->status.cap) {
+        ST_TRY(ensure(c, c->status, need));
+        HIP_TRY(c, hipMemsetAsync(c->status.p, 0, c->status.cap, c->stream));
+        c->epoch = 1;
+    }
+    return GSORT_OK;
+}
+
+gsort_status run_pass(gsort_ctx *c, const uint32_t *src, uint32_t *dst, uint64_t n, int digit,
+                      const uint64_t *d_base, bool flip_in, bool flip_out) {
+    if (c->next_counter >= kMaxCounters) return set_err(c, GSORT_EINVAL, "too many passes");
+    if (c->epoch >= 0xFFFF) {  // epochs tag the status words; re-zero once per 65k passes
+        HIP_TRY(c, hipMemsetAsync(c->status.p, 0, c->status.cap, c->stream));
+        c->epoch = 1;
+    }
+    uint32_t *ctrs = reinterpret_cast<uint32_t *>(c->d_small + OFF_CTR);
+    hipEvent_t t = tic(c);
+    HIP_TRY(c, launch_onesweep(src, dst, n, 8 * digit, d_base,
+                               reinterpret_cast<uint64_t *>(c->status.p),
+                               ctrs + c->next_counter++, ctrs + kMaxCounters, c->epoch++,
+                               flip_in, flip_out, c->stream));
+    toc(c, PH_PASS0 + digit, t);
+    return GSORT_OK;
+}
+
+// Exclusive scan of a 256-bin histogram into the pinned mirror at `hb`.
+void exclusive_256(const uint64_t *h, uint64_t *out) {
+    uint64_t s = 0;
+    for (int d = 0; d < kRadix; ++d) { out[d] = s; s += h[d]; }
+}
+
+gsort_status reset_call(gsort_ctx *c) {
+    c->next_counter = 0;
+    HIP_TRY(c, hipSetDevice(c->device));
+    // tile counters + the lookback-timeout word behind them
+    HIP_TRY(c, hipMemsetAsync(c->d_small + OFF_CTR, 0, (kMaxCounters + 1) * 4, c->stream));
+    return GSORT_OK;
+}
+
+// After the stream is synchronised: did any onesweep lookback give up?
+gsort_status check_kernel_err(gsort_ctx *c) {
+    uint32_t *h = reinterpret_cast<uint32_t *>(c->h_small + OFF_CTR);
+    HIP_TRY(c, hipMemcpyAsync(h, c->d_small + OFF_CTR + kMaxCounters * 4, 4,
+                              hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (*h) return set_err(c, GSORT_EHIP, "onesweep decoupled lookback timed out");
+    return GSORT_OK;
+}
+
+// ---- local sort: K1 + up to four K3 passes (in -> out, tmp as ping-pong) -----------------
+// Reference: the per-key digit loop mpi_radix_sort.c:144-147 (there: base P, all passes
+// through rank 0) and the local qsort mpi_sample_sort.c:85 / :174.
+gsort_status local_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *out,
+                        uint32_t *tmp, int *passes_run) {
+    if (passes_run) *passes_run = 0;
+    if (n == 0) return GSORT_OK;
+    ST_TRY(ensure_status(c, n));
+    uint64_t *d_hist = reinterpret_cast<uint64_t *>(c->d_small + OFF_HIST);
+    uint64_t *d_base = reinterpret_cast<uint64_t *>(c->d_small + OFF_BASE);
+    uint64_t *h_hist = reinterpret_cast<uint64_t *>(c->h_small + OFF_HIST);
+    uint64_t *h_base = reinterpret_cast<uint64_t *>(c->h_small + OFF_BASE);
+    HIP_TRY(c, hipMemsetAsync(d_hist, 0, 4 * kRadix * 8, c->stream));
+    hipEvent_t t = tic(c);
+    HIP_TRY(c, launch_hist4(in, n, d_hist, c->stream));
+    toc(c, PH_HIST, t);
+    HIP_TRY(c, hipMemcpyAsync(h_hist, d_hist, 4 * kRadix * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    int active[4], k = 0;
+    for (int p = 0; p < 4; ++p) {
+        const uint64_t *h = h_hist + p * kRadix;
+        if (*std::max_element(h, h + kRadix) < n) active[k++] = p;  // skip trivial digits
+        exclusive_256(h, h_base + p * kRadix);
+    }
+    if (k == 0) {
+        HIP_TRY(c, launch_copy(in, out, n, c->stream));
+        return GSORT_OK;
+    }
+    HIP_TRY(c, hipMemcpyAsync(d_base, h_base, 4 * kRadix * 8, hipMemcpyHostToDevice, c->stream));
+    const uint32_t *src = in;
+    for (int i = 0; i < k; ++i) {
+        uint32_t *dst = ((k - 1 - i) % 2 == 0) ? out : tmp;
+        ST_TRY(run_pass(c, src, dst, n, active[i], d_base + active[i] * kRadix, i == 0,
+                        i == k - 1));
+        src = dst;
+    }
+    if (passes_run) *passes_run = k;
+    return GSORT_OK;
+}
+
+// Allgather one u64 per rank into host memory (counts used to size RCCL messages).
+gsort_status allgather_u64(gsort_ctx *c, uint64_t v, std::vector<uint64_t> &out) {
+    out.assign(c->nranks, 0);
+    if (c->nranks == 1) { out[0] = v; return GSORT_OK; }
+    uint64_t *h = reinterpret_cast<uint64_t *>(c->h_small + OFF_PLAN);
+    uint64_t *d = reinterpret_cast<uint64_t *>(c->d_small + OFF_PLAN);
+    h[0] = v;
+    HIP_TRY(c, hipMemcpyAsync(d, h, 8, hipMemcpyHostToDevice, c->stream));
+    ST_TRY(comm_try(c, c->comm->allgather(d, d + 1, 8, c->stream)));
+    HIP_TRY(c, hipMemcpyAsync(h + 1, d + 1, 8 * c->nranks, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    for (int r = 0; r < c->nranks; ++r) out[r] = h[1 + r];
+    return GSORT_OK;
+}
+
+void block_of(uint64_t N, int P, int r, uint64_t *B, uint64_t *len) {
+    *B = P ? (N + P - 1) / P : 0;
+    const uint64_t lo = (uint64_t)r * *B;
+    *len = lo >= N ? 0 : std::min(*B, N - lo);
+}
+
+// ---- distributed LSD radix (P > 1) ------------------------------------------------------
+// Per non-trivial digit: local onesweep pass (stable by digit), all-gather per-rank digit
+// counts, route contiguous slices to the ranks owning their global positions (grouped
+// send/recv), then place received runs (K8) and histogram the next digit in the same sweep.
+// Keeps the reference's invariant that rank q holds positions [qB, (q+1)B) after each pass
+// (mpi_radix_sort.c:139,:192) without moving any key through rank 0.
+gsort_status radix_dist(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in, int32_t **d_out,
+                        uint64_t *n_out, gsort_stats *stats) {
+    const int P = c->nranks, me = c->rank;
+    std::vector<uint64_t> n_all;
+    ST_TRY(allgather_u64(c, n_in, n_all));
+    uint64_t N = 0;
+    for (uint64_t v : n_all) N += v;
+    uint64_t B, mine;
+    block_of(N, P, me, &B, &mine);
+    const uint64_t cap = std::max<uint64_t>(std::max(n_in, B), 1);
+    for (Slot s : {S_CUR, S_SORTED, S_RECV, S_OUT}) ST_TRY(ensure(c, c->slot[s], cap * 4));
+    ST_TRY(ensure_status(c, cap));
+    if (N == 0) { *d_out = slot_ptr<int32_t>(c, S_OUT); *n_out = 0; return GSORT_OK; }
+
+    // K1 on the input: all four digit histograms; all-gathered they give the global digit
+    // totals (invariant under the exchange), so every rank skips the same trivial digits.
+    uint64_t *d_hist = reinterpret_cast<uint64_t *>(c->d_small + OFF_HIST);
+    uint64_t *d_base = reinterpret_cast<uint64_t *>(c->d_small + OFF_BASE);
+    uint64_t *d_nhist = reinterpret_cast<uint64_t *>(c->d_small + OFF_NHIST);
+    uint64_t *h_base = reinterpret_cast<uint64_t *>(c->h_small + OFF_BASE);
+    HIP_TRY(c, hipMemsetAsync(d_hist, 0, 4 * kRadix * 8, c->stream));
+    hipEvent_t t = tic(c);
+    HIP_TRY(c, launch_hist4(reinterpret_cast<const uint32_t *>(d_keys), n_in, d_hist, c->stream));
+    toc(c, PH_HIST, t);
+    DevBuf &allh = c->slot[S_STAGE];
+    ST_TRY(ensure(c, allh, (size_t)P * 4 * kRadix * 8));
+    ST_TRY(comm_try(c, c->comm->allgather(d_hist, allh.p, 4 * kRadix * 8, c->stream)));
+    std::vector<uint64_t> H((size_t)P * 4 * kRadix);
+    HIP_TRY(c, hipMemcpyAsync(H.data(), allh.p, H.size() * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    std::vector<int> active;
+    for (int p = 0; p < 4; ++p) {
+        uint64_t mx = 0;
+        for (int d = 0; d < kRadix; ++d) {
+            uint64_t tot = 0;
+            for (int r = 0; r < P; ++r) tot += H[((size_t)r * 4 + p) * kRadix + d];
+            mx = std::max(mx, tot);
+        }
+        if (mx < N) active.push_back(p);
+    }
+    if (active.empty()) active.push_back(0);  // still redistribute to balanced blocks
+
+    std::vector<uint64_t> hp((size_t)P * kRadix), send(P), recv(P), seg((size_t)4 * P * kRadix);
+    std::vector<size_t> sc(P), sd(P), rc(P), rd(P);
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(d_keys);
+    uint64_t n_src = n_in;
+    uint32_t *placed[2] = {slot_ptr<uint32_t>(c, S_CUR), slot_ptr<uint32_t>(c, S_OUT)};
+    const int k = (int)active.size();
+    for (int i = 0; i < k; ++i) {
+        const int p = active[i];
+        const bool first = i == 0, last = i == k - 1;
+        // per-rank counts of digit p for the current distribution
+        if (first) {
+            for (int r = 0; r < P; ++r)
+                memcpy(&hp[(size_t)r * kRadix], &H[((size_t)r * 4 + p) * kRadix], kRadix * 8);
+        } else {
+            uint64_t *d_allnh = reinterpret_cast<uint64_t *>(allh.p);
+            ST_TRY(comm_try(c, c->comm->allgather(d_nhist, d_allnh, kRadix * 8, c->stream)));
+            HIP_TRY(c, hipMemcpyAsync(hp.data(), d_allnh, hp.size() * 8, hipMemcpyDeviceToHost,
+                                      c->stream));
+            HIP_TRY(c, hipStreamSynchronize(c->stream));
+        }
+        exclusive_256(&hp[(size_t)me * kRadix], h_base);
+        HIP_TRY(c, hipMemcpyAsync(d_base, h_base, kRadix * 8, hipMemcpyHostToDevice, c->stream));
+        uint32_t *sorted = slot_ptr<uint32_t>(c, S_SORTED);
+        ST_TRY(run_pass(c, src, sorted, n_src, p, d_base, first, false));
+
+        size_t nseg = 0;
+        ST_TRY(gsort_plan_radix_route(P, hp.data(), B, me, send.data(), recv.data(), seg.data(),
+                                      &nseg));
+        size_t so = 0, ro = 0;
+        for (int q = 0; q < P; ++q) {
+            sc[q] = send[q] * 4; sd[q] = so; so += sc[q];
+            rc[q] = recv[q] * 4; rd[q] = ro; ro += rc[q];
+            if (stats && q != me) {
+                stats->bytes_sent += sc[q];
+                stats->max_pair_bytes = std::max<uint64_t>(stats->max_pair_bytes, sc[q]);
+            }
+        }
+        uint32_t *rbuf = slot_ptr<uint32_t>(c, S_RECV);
+        t = tic(c);
+        ST_TRY(comm_try(c, c->comm->alltoallv(sorted, sc.data(), sd.data(), rbuf, rc.data(),
+                                              rd.data(), c->stream)));
+        toc(c, PH_EXCH, t);
+        if (stats) stats->exchanges++;
+        // placement table: {offset in recv buffer, dest offset, length}
+        uint64_t *h_seg = reinterpret_cast<uint64_t *>(c->h_small + OFF_PLAN);
+        uint64_t *d_seg = reinterpret_cast<uint64_t *>(c->d_small + OFF_PLAN);
+        if (nseg * 24 > kSmallBytes - OFF_PLAN) return set_err(c, GSORT_EINVAL, "segment table");
+        HIP_TRY(c, hipStreamSynchronize(c->stream));  // h_seg may still feed an earlier copy
+        for (size_t s = 0; s < nseg; ++s) {
+            const uint64_t r = seg[4 * s];
+            h_seg[3 * s + 0] = rd[r] / 4 + seg[4 * s + 1];
+            h_seg[3 * s + 1] = seg[4 * s + 2];
+            h_seg[3 * s + 2] = seg[4 * s + 3];
+        }
+        HIP_TRY(c, hipMemcpyAsync(d_seg, h_seg, nseg * 24, hipMemcpyHostToDevice, c->stream));
+        uint32_t *dst = last ? slot_ptr<uint32_t>(c, S_OUT) : placed[i & 1];
+        if (!last) HIP_TRY(c, hipMemsetAsync(d_nhist, 0, kRadix * 8, c->stream));
+        t = tic(c);
+        HIP_TRY(c, launch_place(rbuf, dst, d_seg, (int)nseg, mine, last ? nullptr : d_nhist,
+                                last ? 0 : 8 * active[i + 1], last, c->stream));
+        toc(c, PH_PLACE, t);
+        src = dst;
+        n_src = mine;
+    }
+    if (stats) stats->passes_run = k;
+    *d_out = slot_ptr<int32_t>(c, S_OUT);
+    *n_out = mine;
+    return GSORT_OK;
+}
+
+// ---- sample sort ------------------------------------------------------------------------
+gsort_status sample_dist(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in, int32_t **d_out,
+                         uint64_t *n_out, gsort_stats *stats) {
+    const int P = c->nranks, me = c->rank;
+    std::vector<uint64_t> n_all;
+    ST_TRY(allgather_u64(c, n_in, n_all));
+    uint64_t N = 0;
+    for (uint64_t v : n_all) N += v;
+    // mpi_sample_sort.c:72 size_bucket = ceil(N/P); :89-90 k = 2P-1, interval = B / k
+    const uint64_t B = (N + P - 1) / P;
+    const int k = 2 * P - 1;
+    const uint64_t interval = B / k;
+    if (P * k > 1024) return set_err(c, GSORT_EINVAL, "too many ranks for sample sort");
+    for (int r = 0; r < P; ++r)  // :94-99, decided identically on every rank
+        if ((uint64_t)(k - 1) * interval >= n_all[r])
+            return set_err(c, GSORT_ENOSAMPLE,
+                           "no enough sample: rank " + std::to_string(r) + " holds " +
+                               std::to_string(n_all[r]) + " keys, needs index " +
+                               std::to_string((uint64_t)(k - 1) * interval));
+    const uint64_t cap = std::max<uint64_t>(n_in, 1);
+    ST_TRY(ensure(c, c->slot[S_SORTED], cap * 4));
+    ST_TRY(ensure(c, c->slot[S_TMP], cap * 4));
+    int32_t *sorted = slot_ptr<int32_t>(c, S_SORTED);
+    int pr = 0;
+    ST_TRY(local_sort(c, reinterpret_cast<const uint32_t *>(d_keys), n_in,
+                      reinterpret_cast<uint32_t *>(sorted), slot_ptr<uint32_t>(c, S_TMP), &pr));
+
+    // K4 samples -> root (grouped send/recv), K5 on root, broadcast splitters
+    hipEvent_t t = tic(c);
+    int32_t *d_samp = reinterpret_cast<int32_t *>(c->d_small + OFF_PLAN);
+    int32_t *d_all = d_samp + 64;
+    int32_t *d_spl = d_all + 1024 + 64;
+    uint64_t *d_bounds = reinterpret_cast<uint64_t *>(d_spl + 64);
+    HIP_TRY(c, launch_regular_sample(sorted, interval, k, d_samp, c->stream));
+    std::vector<size_t> sc(P, 0), sd(P, 0), rc(P, 0), rd(P, 0);
+    sc[0] = (size_t)k * 4;
+    if (me == 0)
+        for (int r = 0; r < P; ++r) { rc[r] = (size_t)k * 4; rd[r] = (size_t)r * k * 4; }
+    ST_TRY(comm_try(c, c->comm->alltoallv(d_samp, sc.data(), sd.data(), d_all, rc.data(),
+                                          rd.data(), c->stream)));
+    if (me == 0) HIP_TRY(c, launch_select_splitters(d_all, P * k, k, P - 1, d_spl, c->stream));
+    ST_TRY(comm_try(c, c->comm->bcast(d_spl, (size_t)(P - 1) * 4, 0, c->stream)));
+    HIP_TRY(c, launch_bucket_bounds(sorted, n_in, d_spl, P - 1, d_bounds, c->stream));
+    toc(c, PH_SAMPLE, t);
+    int32_t *h_spl = reinterpret_cast<int32_t *>(c->h_small + OFF_PLAN);
+    uint64_t *h_bounds = reinterpret_cast<uint64_t *>(c->h_small + OFF_PLAN + 1024);
+    HIP_TRY(c, hipMemcpyAsync(h_spl, d_spl, (size_t)(P - 1) * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(h_bounds, d_bounds, (size_t)(P - 1) * 8, hipMemcpyDeviceToHost,
+                              c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    c->splitters.assign(h_spl, h_spl + P - 1);
+    c->bucket_counts.assign(P, 0);
+    uint64_t prev = 0;
+    for (int j = 0; j < P; ++j) {
+        const uint64_t end = j < P - 1 ? h_bounds[j] : n_in;
+        c->bucket_counts[j] = end - prev;
+        prev = end;
+    }
+    // bucket-count matrix: allgather P counts per rank (mpi_sample_sort.c:161,:168 sends the
+    // length in the MPI tag of a fixed-size message; here exact lengths size the messages)
+    uint64_t *d_cnt = reinterpret_cast<uint64_t *>(c->d_small + OFF_PLAN + 16384);
+    uint64_t *d_mat = d_cnt + 64;
+    uint64_t *h_cnt = reinterpret_cast<uint64_t *>(c->h_small + OFF_PLAN + 16384);
+    memcpy(h_cnt, c->bucket_counts.data(), (size_t)P * 8);
+    HIP_TRY(c, hipMemcpyAsync(d_cnt, h_cnt, (size_t)P * 8, hipMemcpyHostToDevice, c->stream));
+    ST_TRY(comm_try(c, c->comm->allgather(d_cnt, d_mat, (size_t)P * 8, c->stream)));
+    std::vector<uint64_t> M((size_t)P * P);
+    HIP_TRY(c, hipMemcpyAsync(M.data(), d_mat, M.size() * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    uint64_t total = 0;
+    size_t so = 0, ro = 0;
+    for (int q = 0; q < P; ++q) {
+        sc[q] = c->bucket_counts[q] * 4; sd[q] = so; so += sc[q];
+        rc[q] = M[(size_t)q * P + me] * 4; rd[q] = ro; ro += rc[q];
+        total += M[(size_t)q * P + me];
+        if (stats && q != me) {
+            stats->bytes_sent += sc[q];
+            stats->max_pair_bytes = std::max<uint64_t>(stats->max_pair_bytes, sc[q]);
+        }
+    }
+    const uint64_t cap2 = std::max<uint64_t>(total, 1);
+    ST_TRY(ensure(c, c->slot[S_RECV], cap2 * 4));
+    ST_TRY(ensure(c, c->slot[S_OUT], cap2 * 4));
+    ST_TRY(ensure(c, c->slot[S_TMP], cap2 * 4));
+    int32_t *rbuf = slot_ptr<int32_t>(c, S_RECV);
+    t = tic(c);
+    ST_TRY(comm_try(c, c->comm->alltoallv(sorted, sc.data(), sd.data(), rbuf, rc.data(),
+                                          rd.data(), c->stream)));
+    toc(c, PH_EXCH, t);
+    if (stats) stats->exchanges = 1;
+    // final local order of the received bucket (mpi_sample_sort.c:174): re-sort the P runs
+    t = tic(c);
+    ST_TRY(local_sort(c, reinterpret_cast<const uint32_t *>(rbuf), total,
+                      slot_ptr<uint32_t>(c, S_OUT), slot_ptr<uint32_t>(c, S_TMP), &pr));
+    toc(c, PH_MERGE, t);
+    if (stats) stats->passes_run = pr;
+    *d_out = slot_ptr<int32_t>(c, S_OUT);
+    *n_out = total;
+    return GSORT_OK;
+}
+
+gsort_status check_ctx(gsort_ctx *c) { return c ? GSORT_OK : GSORT_EINVAL; }
+
+// The sort writes its scratch slots; an input living in one of them would be overwritten.
+gsort_status check_input(gsort_ctx *c, const int32_t *d_keys) {
+    for (int s = 0; s < S_NSLOTS; ++s)
+        if (s != S_IN && c->slot[s].p && (const void *)d_keys == c->slot[s].p)
+            return set_err(c, GSORT_EINVAL, "d_keys aliases a context-owned scratch buffer");
+    return GSORT_OK;
+}
+
+gsort_status create_common(gsort_ctx *c, int hip_device) {
+    if (hip_device < 0) {  // -1 - local_rank: pick the local rank's GPU
+        int count = 0;
+        HIP_TRY(c, hipGetDeviceCount(&count));
+        if (count < 1) return set_err(c, GSORT_EHIP, "no HIP device visible");
+        hip_device = (-1 - hip_device) % count;
+    }
+    c->device = hip_device;
+    HIP_TRY(c, hipSetDevice(hip_device));
+    HIP_TRY(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIP_TRY(c, hipMalloc(&c->d_small, kSmallBytes));
+    HIP_TRY(c, hipHostMalloc(&c->h_small, kSmallBytes, hipHostMallocDefault));
+    HIP_TRY(c, hipMemset(c->d_small, 0, kSmallBytes));
+    return GSORT_OK;
+}
+
+}  // namespace
+
+// =========================================================================================
+// C-ABI
+// =========================================================================================
+extern "C" {
+
+const char *gsort_strerror(gsort_status st) {
+    switch (st) {
+        case GSORT_OK: return "ok";
+        case GSORT_EINVAL: return "invalid argument";
+        case GSORT_ENOMEM: return "out of memory";
+        case GSORT_EHIP: return "HIP error";
+        case GSORT_ERCCL: return "RCCL error";
+        case GSORT_ENOSAMPLE: return "not enough keys for regular sampling";
+        case GSORT_ECOMM: return "in-process group error";
+    }
+    return "unknown status";
+}
+
+const char *gsort_last_error(const gsort_ctx *ctx) { return ctx ? ctx->err.c_str() : ""; }
+int gsort_rank(const gsort_ctx *ctx) { return ctx ? ctx->rank : -1; }
+int gsort_nranks(const gsort_ctx *ctx) { return ctx ? ctx->nranks : -1; }
+size_t gsort_onesweep_tile(void) { return kSweepTile; }
+
+gsort_status gsort_get_uid(gsort_uid *out) {
+    if (!out) return GSORT_EINVAL;
+    return rccl_get_uid(out);
+}
+
+gsort_status gsort_create(gsort_ctx **ctx, int rank, int nranks, int hip_device,
+                          const gsort_uid *uid) {
+    if (!ctx || nranks < 1 || rank < 0 || rank >= nranks || (nranks > 1 && !uid))
+        return GSORT_EINVAL;
+    *ctx = nullptr;
+    gsort_ctx *c = new gsort_ctx();
+    c->rank = rank;
+    c->nranks = nranks;
+    gsort_status st = create_common(c, hip_device);
+    if (st == GSORT_OK && nranks > 1) {
+        std::string e;
+        c->comm = make_rccl_comm(rank, nranks, uid, &e);
+        if (!c->comm) st = set_err(c, GSORT_ERCCL, e);
+    }
+    if (st != GSORT_OK) {
+        fprintf(stderr, "gsort_create: %s\n", c->err.c_str());
+        gsort_destroy(c);
+        return st;
+    }
+    *ctx = c;
+    return GSORT_OK;
+}
+
+gsort_status gsort_group_create(gsort_group **grp, int nranks) {
+    if (!grp || nranks < 1) return GSORT_EINVAL;
+    *grp = new gsort_group{group_state_create(nranks)};
+    return GSORT_OK;
+}
+
+gsort_status gsort_group_destroy(gsort_group *grp) {
+    if (!grp) return GSORT_EINVAL;
+    group_state_destroy(grp->st);
+    delete grp;
+    return GSORT_OK;
+}
+
+gsort_status gsort_create_in_group(gsort_ctx **ctx, gsort_group *grp, int rank, int hip_device) {
+    if (!ctx || !grp || rank < 0 || rank >= group_state_size(grp->st)) return GSORT_EINVAL;
+    *ctx = nullptr;
+    gsort_ctx *c = new gsort_ctx();
+    c->rank = rank;
+    c->nranks = group_state_size(grp->st);
+    gsort_status st = create_common(c, hip_device);
+    if (st != GSORT_OK) { gsort_destroy(c); return st; }
+    if (c->nranks > 1) c->comm = make_group_comm(grp->st, rank);
+    *ctx = c;
+    return GSORT_OK;
+}
+
+gsort_status gsort_destroy(gsort_ctx *c) {
+    if (!c) return GSORT_EINVAL;
+    // teardown: errors are not actionable here, so every status is deliberately dropped
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    delete c->comm;
+    for (auto &b : c->slot) if (b.p) (void)hipFree(b.p);
+    if (c->status.p) (void)hipFree(c->status.p);
+    if (c->d_small) (void)hipFree(c->d_small);
+    if (c->h_small) (void)hipHostFree(c->h_small);
+    for (auto e : c->ev_pool) (void)hipEventDestroy(e);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return GSORT_OK;
+}
+
+gsort_status gsort_reserve(gsort_ctx *c, size_t n) {
+    ST_TRY(check_ctx(c));
+    HIP_TRY(c, hipSetDevice(c->device));
+    const size_t cap = std::max<size_t>(n, 1) * 4;
+    for (Slot s : {S_TMP, S_OUT}) ST_TRY(ensure(c, c->slot[s], cap));
+    if (c->nranks > 1)
+        for (Slot s : {S_CUR, S_SORTED, S_RECV}) ST_TRY(ensure(c, c->slot[s], cap));
+    ST_TRY(ensure_status(c, n));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return GSORT_OK;
+}
+
+gsort_status gsort_radix(gsort_ctx *c, const int32_t *d_keys, size_t n_local, int32_t **d_out,
+                         size_t *n_out, gsort_stats *stats) {
+    ST_TRY(check_ctx(c));
+    if (!d_out || !n_out || (n_local && !d_keys)) return set_err(c, GSORT_EINVAL, "null argument");
+    ST_TRY(check_input(c, d_keys));
+    ST_TRY(reset_call(c));
+    timing_begin(c, stats);
+    hipEvent_t t0 = tic(c);
+    gsort_status st;
+    uint64_t nout = 0;
+    if (c->nranks == 1) {
+        const size_t cap = std::max<size_t>(n_local, 1) * 4;
+        ST_TRY(ensure(c, c->slot[S_TMP], cap));
+        ST_TRY(ensure(c, c->slot[S_OUT], cap));
+        int pr = 0;
+        st = local_sort(c, reinterpret_cast<const uint32_t *>(d_keys), n_local,
+                        slot_ptr<uint32_t>(c, S_OUT), slot_ptr<uint32_t>(c, S_TMP), &pr);
+        if (stats) stats->passes_run = pr;
+        *d_out = slot_ptr<int32_t>(c, S_OUT);
+        nout = n_local;
+    } else {
+        st = radix_dist(c, d_keys, n_local, d_out, &nout, stats);
+    }
+    if (st != GSORT_OK) return st;
+    toc(c, PH_TOTAL, t0);
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    ST_TRY(check_kernel_err(c));
+    *n_out = nout;
+    if (stats) { stats->keys_local_in = n_local; stats->keys_local_out = nout; }
+    timing_finish(c, stats);
+    return GSORT_OK;
+}
+
+gsort_status gsort_sample(gsort_ctx *c, const int32_t *d_keys, size_t n_local, int32_t **d_out,
+                          size_t *n_out, gsort_stats *stats) {
+    ST_TRY(check_ctx(c));
+    if (!d_out || !n_out || (n_local && !d_keys)) return set_err(c, GSORT_EINVAL, "null argument");
+    ST_TRY(check_input(c, d_keys));
+    ST_TRY(reset_call(c));
+    timing_begin(c, stats);
+    hipEvent_t t0 = tic(c);
+    uint64_t nout = 0;
+    if (c->nranks == 1) {
+        // one rank: no splitters, one bucket (the reference reads splitters[-1] here, Q10)
+        const size_t cap = std::max<size_t>(n_local, 1) * 4;
+        ST_TRY(ensure(c, c->slot[S_TMP], cap));
+        ST_TRY(ensure(c, c->slot[S_OUT], cap));
+        int pr = 0;
+        ST_TRY(local_sort(c, reinterpret_cast<const uint32_t *>(d_keys), n_local,
+                          slot_ptr<uint32_t>(c, S_OUT), slot_ptr<uint32_t>(c, S_TMP), &pr));
+        if (stats) stats->passes_run = pr;
+        c->splitters.clear();
+        c->bucket_counts.assign(1, n_local);
+        *d_out = slot_ptr<int32_t>(c, S_OUT);
+        nout = n_local;
+    } else {
+        ST_TRY(sample_dist(c, d_keys, n_local, d_out, &nout, stats));
+    }
+    toc(c, PH_TOTAL, t0);
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    ST_TRY(check_kernel_err(c));
+    *n_out = nout;
+    if (stats) { stats->keys_local_in = n_local; stats->keys_local_out = nout; }
+    timing_finish(c, stats);
+    return GSORT_OK;
+}
+
+gsort_status gsort_sample_info(const gsort_ctx *c, int32_t *splitters, uint64_t *bucket_counts) {
+    if (!c) return GSORT_EINVAL;
+    if (splitters) std::copy(c->splitters.begin(), c->splitters.end(), splitters);
+    if (bucket_counts) std::copy(c->bucket_counts.begin(), c->bucket_counts.end(), bucket_counts);
+    return GSORT_OK;
+}
+
+gsort_status gsort_scatter_from_root(gsort_ctx *c, const int32_t *h_root, size_t n_total,
+                                     int32_t **d_keys, size_t *n_local) {
+    ST_TRY(check_ctx(c));
+    if (!d_keys || !n_local || (c->rank == 0 && n_total && !h_root)) return GSORT_EINVAL;
+    ST_TRY(reset_call(c));
+    const int P = c->nranks;
+    uint64_t B, mine;
+    block_of(n_total, P, c->rank, &B, &mine);
+    ST_TRY(ensure(c, c->slot[S_IN], std::max<uint64_t>(mine, 1) * 4));
+    int32_t *d_in = slot_ptr<int32_t>(c, S_IN);
+    if (P == 1) {
+        if (n_total)
+            HIP_TRY(c, hipMemcpyAsync(d_in, h_root, n_total * 4, hipMemcpyHostToDevice, c->stream));
+    } else {
+        std::vector<size_t> sc(P, 0), sd(P, 0), rc(P, 0), rd(P, 0);
+        const void *src = nullptr;
+        if (c->rank == 0) {
+            ST_TRY(ensure(c, c->slot[S_STAGE], std::max<size_t>(n_total, 1) * 4));
+            if (n_total)
+                HIP_TRY(c, hipMemcpyAsync(c->slot[S_STAGE].p, h_root, n_total * 4,
+                                          hipMemcpyHostToDevice, c->stream));
+            for (int q = 0; q < P; ++q) {
+                uint64_t bq, lq;
+                block_of(n_total, P, q, &bq, &lq);
+                sc[q] = lq * 4;
+                sd[q] = std::min<uint64_t>((uint64_t)q * B, n_total) * 4;
+            }
+            src = c->slot[S_STAGE].p;
+        }
+        rc[0] = mine * 4;
+        ST_TRY(comm_try(c, c->comm->alltoallv(src, sc.data(), sd.data(), d_in, rc.data(),
+                                              rd.data(), c->stream)));
+    }
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    *d_keys = d_in;
+    *n_local = mine;
+    return GSORT_OK;
+}
+
+gsort_status gsort_gather_to_root(gsort_ctx *c, const int32_t *d_out, size_t n_out,
+                                  int32_t *h_root) {
+    ST_TRY(check_ctx(c));
+    if ((n_out && !d_out) || (c->rank == 0 && !h_root)) return GSORT_EINVAL;
+    ST_TRY(reset_call(c));
+    const int P = c->nranks;
+    if (P == 1) {
+        if (n_out)
+            HIP_TRY(c, hipMemcpyAsync(h_root, d_out, n_out * 4, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        return GSORT_OK;
+    }
+    std::vector<uint64_t> sizes;
+    ST_TRY(allgather_u64(c, n_out, sizes));
+    uint64_t total = 0;
+    std::vector<size_t> sc(P, 0), sd(P, 0), rc(P, 0), rd(P, 0);
+    for (int r = 0; r < P; ++r) {
+        if (c->rank == 0) { rc[r] = sizes[r] * 4; rd[r] = total * 4; }
+        total += sizes[r];
+    }
+    sc[0] = n_out * 4;
+    void *dst = nullptr;
+    if (c->rank == 0) {
+        ST_TRY(ensure(c, c->slot[S_STAGE], std::max<uint64_t>(total, 1) * 4));
+        dst = c->slot[S_STAGE].p;
+    }
+    ST_TRY(comm_try(c, c->comm->alltoallv(d_out, sc.data(), sd.data(), dst, rc.data(), rd.data(),
+                                          c->stream)));
+    if (c->rank == 0 && total)
+        HIP_TRY(c, hipMemcpyAsync(h_root, dst, total * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return GSORT_OK;
+}
+
+gsort_status gsort_generate(gsort_ctx *c, int dist, uint64_t seed, uint64_t start, size_t n,
+                            int32_t *d_out) {
+    ST_TRY(check_ctx(c));
+    if ((dist != 0 && dist != 1) || (n && !d_out)) return GSORT_EINVAL;
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, launch_generate(dist, seed, start, n, d_out, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return GSORT_OK;
+}
+
+gsort_status gsort_fingerprint(gsort_ctx *c, const int32_t *d_keys, size_t n, uint64_t *sum,
+                               uint64_t *xr, int *sorted, int32_t *first, int32_t *last) {
+    ST_TRY(check_ctx(c));
+    if (n && !d_keys) return GSORT_EINVAL;
+    HIP_TRY(c, hipSetDevice(c->device));
+    unsigned long long *d_acc = reinterpret_cast<unsigned long long *>(c->d_small + OFF_PLAN);
+    uint64_t *h = reinterpret_cast<uint64_t *>(c->h_small + OFF_PLAN);
+    HIP_TRY(c, hipMemsetAsync(d_acc, 0, 24, c->stream));
+    HIP_TRY(c, launch_fingerprint(d_keys, n, d_acc, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(h, d_acc, 24, hipMemcpyDeviceToHost, c->stream));
+    int32_t *h_fl = reinterpret_cast<int32_t *>(h + 3);
+    h_fl[0] = h_fl[1] = 0;
+    if (n) {
+        HIP_TRY(c, hipMemcpyAsync(h_fl, d_keys, 4, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipMemcpyAsync(h_fl + 1, d_keys + n - 1, 4, hipMemcpyDeviceToHost, c->stream));
+    }
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (sum) *sum = h[0];
+    if (xr) *xr = h[1];
+    if (sorted) *sorted = h[2] == 0;
+    if (first) *first = h_fl[0];
+    if (last) *last = h_fl[1];
+    return GSORT_OK;
+}
+
+gsort_status gsort_device_alloc(gsort_ctx *c, size_t bytes, void **d_ptr) {
+    ST_TRY(check_ctx(c));
+    if (!d_ptr) return GSORT_EINVAL;
+    HIP_TRY(c, hipSetDevice(c->device));
+    if (hipMalloc(d_ptr, std::max<size_t>(bytes, 4)) != hipSuccess) {
+        (void)hipGetLastError();
+        return set_err(c, GSORT_ENOMEM, "hipMalloc failed");
+    }
+    return GSORT_OK;
+}
+
+gsort_status gsort_device_free(gsort_ctx *c, void *d_ptr) {
+    ST_TRY(check_ctx(c));
+    HIP_TRY(c, hipSetDevice(c->device));
+    if (d_ptr) HIP_TRY(c, hipFree(d_ptr));
+    return GSORT_OK;
+}
+
+gsort_status gsort_copy_to_host(gsort_ctx *c, void *h_dst, const void *d_src, size_t bytes) {
+    ST_TRY(check_ctx(c));
+    HIP_TRY(c, hipSetDevice(c->device));
+    if (bytes) HIP_TRY(c, hipMemcpyAsync(h_dst, d_src, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return GSORT_OK;
+}
+
+gsort_status gsort_copy_to_device(gsort_ctx *c, void *d_dst, const void *h_src, size_t bytes) {
+    ST_TRY(check_ctx(c));
+    HIP_TRY(c, hipSetDevice(c->device));
+    if (bytes) HIP_TRY(c, hipMemcpyAsync(d_dst, h_src, bytes, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return GSORT_OK;
+}
+
+}  // extern "C"

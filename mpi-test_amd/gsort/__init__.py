@@ -1,0 +1,269 @@
+"""Python binding of libgsort (include/gsort.h) over ctypes.
+
+Host-side mirror of the reference's sort entry point for Python callers (tests, bench.py):
+`Context.radix` / `Context.sample` are the device-resident hot paths that replace the pass
+loops of sort() in mpi_radix_sort.c:60-205 / mpi_sample_sort.c:28-218; `run_sort` mirrors the
+reference's `sort(rank, size, file, debug)` end to end (read on rank 0, scatter, sort, gather,
+print).  Everything runs in libgsort.so's HIP kernels; there is no CPU fallback: if the library
+is missing or no GPU is visible, calls raise.
+
+Import torch BEFORE this module in processes that also use torch, so libgsort binds to the
+same HIP runtime torch loaded (both resolve libamdhip64.so.7 by soname).
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.dirname(HERE)
+LIB_PATH = os.path.join(PKG, "lib", "libgsort.so")
+
+OK, EINVAL, ENOMEM, EHIP, ERCCL, ENOSAMPLE, ECOMM = range(7)
+UNIFORM, ZIPF = 0, 1
+
+
+class GsortError(RuntimeError):
+    def __init__(self, status, msg):
+        super().__init__(f"gsort status {status}: {msg}")
+        self.status = status
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("ms_total", ctypes.c_double), ("ms_hist", ctypes.c_double),
+                ("ms_pass", ctypes.c_double * 4), ("ms_local_sort", ctypes.c_double),
+                ("ms_exchange", ctypes.c_double), ("ms_place", ctypes.c_double),
+                ("ms_sample", ctypes.c_double), ("ms_merge", ctypes.c_double),
+                ("keys_local_in", ctypes.c_uint64), ("keys_local_out", ctypes.c_uint64),
+                ("bytes_sent", ctypes.c_uint64), ("max_pair_bytes", ctypes.c_uint64),
+                ("passes_run", ctypes.c_int), ("exchanges", ctypes.c_int)]
+
+    def as_dict(self):
+        d = {k: getattr(self, k) for k, _ in self._fields_}
+        d["ms_pass"] = list(self.ms_pass)
+        return d
+
+
+class Uid(ctypes.Structure):
+    _fields_ = [("internal", ctypes.c_char * 128)]
+
+
+EXPORTS = [
+    "gsort_get_uid", "gsort_create", "gsort_group_create", "gsort_group_destroy",
+    "gsort_create_in_group", "gsort_destroy", "gsort_reserve", "gsort_strerror",
+    "gsort_last_error", "gsort_rank", "gsort_nranks", "gsort_radix", "gsort_sample",
+    "gsort_sample_info", "gsort_scatter_from_root", "gsort_gather_to_root", "gsort_generate",
+    "gsort_fingerprint", "gsort_device_alloc", "gsort_device_free", "gsort_copy_to_host",
+    "gsort_copy_to_device", "gsort_onesweep_tile", "gsort_plan_radix_route",
+    "gsort_plan_splitters",
+]
+
+_lib = None
+
+
+def lib():
+    """Load libgsort.so (built by `make -C mpi-test_amd`); raises if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"libgsort.so not built at {LIB_PATH}: run __graft_entry__.build()")
+    L = ctypes.CDLL(LIB_PATH)
+    P, VP, SZ, I, U64 = (ctypes.POINTER, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                         ctypes.c_uint64)
+    for name in EXPORTS:
+        getattr(L, name).restype = ctypes.c_int
+    L.gsort_strerror.restype = ctypes.c_char_p
+    L.gsort_last_error.restype = ctypes.c_char_p
+    L.gsort_onesweep_tile.restype = SZ
+    L.gsort_get_uid.argtypes = [P(Uid)]
+    L.gsort_create.argtypes = [P(VP), I, I, I, P(Uid)]
+    L.gsort_group_create.argtypes = [P(VP), I]
+    L.gsort_group_destroy.argtypes = [VP]
+    L.gsort_create_in_group.argtypes = [P(VP), VP, I, I]
+    L.gsort_destroy.argtypes = [VP]
+    L.gsort_reserve.argtypes = [VP, SZ]
+    L.gsort_strerror.argtypes = [I]
+    L.gsort_last_error.argtypes = [VP]
+    L.gsort_rank.argtypes = [VP]
+    L.gsort_nranks.argtypes = [VP]
+    for fn in (L.gsort_radix, L.gsort_sample):
+        fn.argtypes = [VP, VP, SZ, P(VP), P(SZ), P(Stats)]
+    L.gsort_sample_info.argtypes = [VP, VP, VP]
+    L.gsort_scatter_from_root.argtypes = [VP, VP, SZ, P(VP), P(SZ)]
+    L.gsort_gather_to_root.argtypes = [VP, VP, SZ, VP]
+    L.gsort_generate.argtypes = [VP, I, U64, U64, SZ, VP]
+    L.gsort_fingerprint.argtypes = [VP, VP, SZ, P(U64), P(U64), P(I), P(ctypes.c_int32),
+                                    P(ctypes.c_int32)]
+    L.gsort_device_alloc.argtypes = [VP, SZ, P(VP)]
+    L.gsort_device_free.argtypes = [VP, VP]
+    L.gsort_copy_to_host.argtypes = [VP, VP, VP, SZ]
+    L.gsort_copy_to_device.argtypes = [VP, VP, VP, SZ]
+    L.gsort_plan_radix_route.argtypes = [I, VP, U64, I, VP, VP, VP, P(SZ)]
+    L.gsort_plan_splitters.argtypes = [I, VP, VP]
+    _lib = L
+    return L
+
+
+def get_uid():
+    u = Uid()
+    _check(lib().gsort_get_uid(ctypes.byref(u)), None)
+    return bytes(u.internal)
+
+
+def _check(st, ctx):
+    if st != OK:
+        L = lib()
+        msg = L.gsort_strerror(st).decode()
+        if ctx:
+            detail = L.gsort_last_error(ctx).decode()
+            if detail:
+                msg += ": " + detail
+        raise GsortError(st, msg)
+
+
+class Group:
+    """In-process rank group: `nranks` contexts, one per thread, on one process."""
+
+    def __init__(self, nranks):
+        self.h = ctypes.c_void_p()
+        _check(lib().gsort_group_create(ctypes.byref(self.h), nranks), None)
+        self.nranks = nranks
+
+    def close(self):
+        if self.h:
+            lib().gsort_group_destroy(self.h)
+            self.h = ctypes.c_void_p()
+
+
+class Context:
+    """One rank == one GPU.  Not thread-safe; one thread per context."""
+
+    def __init__(self, rank=0, nranks=1, device=0, uid=None, group=None):
+        self.h = ctypes.c_void_p()
+        L = lib()
+        if group is not None:
+            _check(L.gsort_create_in_group(ctypes.byref(self.h), group.h, rank, device), None)
+        else:
+            u = None
+            if uid is not None:
+                u = Uid()
+                u.internal = uid
+            _check(L.gsort_create(ctypes.byref(self.h), rank, nranks, device,
+                                  ctypes.byref(u) if u is not None else None), None)
+        self.rank, self.nranks, self.device = rank, (group.nranks if group else nranks), device
+
+    def close(self):
+        if self.h:
+            lib().gsort_destroy(self.h)
+            self.h = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _c(self, st):
+        _check(st, self.h)
+
+    def reserve(self, n):
+        self._c(lib().gsort_reserve(self.h, n))
+
+    def _sort(self, fn, d_keys, n):
+        out, nout, st = ctypes.c_void_p(), ctypes.c_size_t(), Stats()
+        self._c(fn(self.h, ctypes.c_void_p(d_keys), n, ctypes.byref(out), ctypes.byref(nout),
+                   ctypes.byref(st)))
+        return out.value or 0, nout.value, st.as_dict()
+
+    def radix(self, d_keys, n):
+        """Device-resident radix sort: returns (d_out, n_out, stats); d_out is ctx-owned."""
+        return self._sort(lib().gsort_radix, d_keys, n)
+
+    def sample(self, d_keys, n):
+        return self._sort(lib().gsort_sample, d_keys, n)
+
+    def sample_info(self):
+        import numpy as np
+        spl = np.zeros(max(self.nranks - 1, 1), dtype=np.int32)
+        cnt = np.zeros(self.nranks, dtype=np.uint64)
+        self._c(lib().gsort_sample_info(self.h, spl.ctypes.data, cnt.ctypes.data))
+        return spl[: self.nranks - 1], cnt
+
+    def generate(self, dist, seed, start, n, d_out):
+        self._c(lib().gsort_generate(self.h, dist, seed, start, n, ctypes.c_void_p(d_out)))
+
+    def fingerprint(self, d_keys, n):
+        s, x, ok = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_int()
+        f, l = ctypes.c_int32(), ctypes.c_int32()
+        self._c(lib().gsort_fingerprint(self.h, ctypes.c_void_p(d_keys), n, ctypes.byref(s),
+                                        ctypes.byref(x), ctypes.byref(ok), ctypes.byref(f),
+                                        ctypes.byref(l)))
+        return {"sum": s.value, "xor": x.value, "sorted": bool(ok.value), "first": f.value,
+                "last": l.value}
+
+    def alloc(self, nbytes):
+        p = ctypes.c_void_p()
+        self._c(lib().gsort_device_alloc(self.h, nbytes, ctypes.byref(p)))
+        return p.value
+
+    def free(self, p):
+        self._c(lib().gsort_device_free(self.h, ctypes.c_void_p(p)))
+
+    def to_host(self, d_ptr, n):
+        import numpy as np
+        a = np.empty(n, dtype=np.int32)
+        if n:
+            self._c(lib().gsort_copy_to_host(self.h, a.ctypes.data, ctypes.c_void_p(d_ptr),
+                                             n * 4))
+        return a
+
+    def to_device(self, a, d_ptr):
+        import numpy as np
+        a = np.ascontiguousarray(a, dtype=np.int32)
+        if a.size:
+            self._c(lib().gsort_copy_to_device(self.h, ctypes.c_void_p(d_ptr), a.ctypes.data,
+                                               a.size * 4))
+
+    def scatter_from_root(self, h_root, n_total):
+        import numpy as np
+        ptr = None
+        if h_root is not None:
+            h_root = np.ascontiguousarray(h_root, dtype=np.int32)
+            ptr = h_root.ctypes.data
+        d, n = ctypes.c_void_p(), ctypes.c_size_t()
+        self._c(lib().gsort_scatter_from_root(self.h, ptr, n_total, ctypes.byref(d),
+                                              ctypes.byref(n)))
+        return d.value, n.value
+
+    def gather_to_root(self, d_out, n_out, n_total):
+        import numpy as np
+        h = np.empty(max(n_total, 1), dtype=np.int32) if self.rank == 0 else None
+        self._c(lib().gsort_gather_to_root(self.h, ctypes.c_void_p(d_out), n_out,
+                                           h.ctypes.data if h is not None else None))
+        return h[:n_total] if h is not None else None
+
+
+def onesweep_tile():
+    return lib().gsort_onesweep_tile()
+
+
+def plan_radix_route(hist, B, me):
+    """Host-only K8 routing (gsort_plan_radix_route): returns (send, recv, seg rows)."""
+    import numpy as np
+    hist = np.ascontiguousarray(hist, dtype=np.uint64)
+    P = hist.shape[0]
+    send = np.zeros(P, dtype=np.uint64)
+    recv = np.zeros(P, dtype=np.uint64)
+    seg = np.zeros(4 * P * 256, dtype=np.uint64)
+    n = ctypes.c_size_t()
+    _check(lib().gsort_plan_radix_route(P, hist.ctypes.data, B, me, send.ctypes.data,
+                                        recv.ctypes.data, seg.ctypes.data, ctypes.byref(n)),
+           None)
+    return send, recv, seg[: 4 * n.value].reshape(-1, 4)
+
+
+def plan_splitters(samples, P):
+    import numpy as np
+    samples = np.ascontiguousarray(samples, dtype=np.int32)
+    out = np.zeros(max(P - 1, 1), dtype=np.int32)
+    _check(lib().gsort_plan_splitters(P, samples.ctypes.data, out.ctypes.data), None)
+    return out[: P - 1]

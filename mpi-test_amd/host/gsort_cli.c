@@ -1,0 +1,196 @@
+/*
+ * gsort_cli.c -- host side of the drop-in radix_sort / sample_sort programs (C + MPI
+ * bootstrap).  Keeps the reference's program contract:
+ *   mpirun -np P ./radix_sort|./sample_sort <file> [debug]
+ *   argc not in {2,3}      -> rank 0: "Usage: %s <file: Data file to read>\n", abort(1)
+ *                             (mpi_radix_sort.c:217-221, mpi_sample_sort.c:230-234)
+ *   unreadable file        -> "sort(): '%s' is not a valid file for read.\n", abort(1)
+ *                             (mpi_radix_sort.c:80-83)
+ *   sample stdout          -> "Each bucket will be put %u items.\n" (mpi_sample_sort.c:74)
+ *   debug dump             -> "%u|%u\n" index|value, radix at debug > 2 (radix:198-200),
+ *                             sample at debug >= 1 (sample:202-204); sample debug also prints
+ *                             "[MASTER] Splitter: %u.\n" and "[COMMON] r: Bucket j=len"
+ *   stdout                 -> "The n/2-th sorted element: %d\n" = sorted[N/2-1] (radix:201)
+ *   stderr                 -> "Endtime()-Starttime() = %.5f sec\n" (radix:203); the timer
+ *                             starts after the rank-0 read and stops after the final gather
+ * MPI carries only the bootstrap: the RCCL unique id and N.  Keys move H2D on rank 0, over
+ * xGMI between GPUs (RCCL), and D2H on rank 0 -- never over MPI.
+ */
+#include <errno.h>
+#include <limits.h>
+#include <mpi.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/stat.h>
+
+#include "gsort.h"
+#include "gsort_cli.h"
+
+static int is_space(char c)
+{
+    return c == ' ' || c == '\t' || c == '\n' || c == '\v' || c == '\f' || c == '\r';
+}
+
+long gsort_cli_parse(const char *buf, long len, int *out, long cap)
+{
+    long n = 0, i = 0;
+    for (;;) {
+        while (i < len && is_space(buf[i])) i++;
+        if (i >= len) break;
+        int neg = 0;
+        if (buf[i] == '+' || buf[i] == '-') neg = buf[i++] == '-';
+        if (i >= len || buf[i] < '0' || buf[i] > '9') return -1;
+        /* glibc's %d converts through strtol: the long saturates, then truncates to int */
+        unsigned long long mag = 0;
+        int sat = 0;
+        for (; i < len && buf[i] >= '0' && buf[i] <= '9'; i++) {
+            unsigned d = (unsigned)(buf[i] - '0');
+            if (mag > (ULLONG_MAX - d) / 10) sat = 1; else mag = mag * 10 + d;
+        }
+        long long v;
+        if (!neg) v = (sat || mag > (unsigned long long)LLONG_MAX) ? LLONG_MAX : (long long)mag;
+        else v = (sat || mag > (unsigned long long)LLONG_MAX + 1ULL) ? LLONG_MIN
+                                                                     : (long long)(0ULL - mag);
+        if (i < len && !is_space(buf[i])) return -1; /* e.g. "12,13": ref spins forever */
+        if (n < cap) out[n] = (int)(uint32_t)(unsigned long long)v;
+        n++;
+    }
+    return n;
+}
+
+static void die(const char *msg)
+{
+    fprintf(stderr, "%s\n", msg);
+    MPI_Abort(MPI_COMM_WORLD, EXIT_FAILURE);
+    exit(EXIT_FAILURE);
+}
+
+static void check(gsort_status st, gsort_ctx *ctx, const char *what)
+{
+    if (st == GSORT_OK) return;
+    char msg[1024];
+    snprintf(msg, sizeof msg, "%s(): %s: %s", what, gsort_strerror(st),
+             ctx ? gsort_last_error(ctx) : "");
+    die(msg);
+}
+
+/* rank-0 reader (mpi_radix_sort.c:73-97): whole file, then one %d-compatible scan */
+static int *read_keys(const char *file, size_t *n_out)
+{
+    char msg[4096 + 64];
+    snprintf(msg, sizeof msg, "sort(): '%s' is not a valid file for read.", file);
+    FILE *fp = fopen(file, "rb");
+    if (!fp) die(msg);
+    struct stat sb;
+    if (fstat(fileno(fp), &sb) != 0) die(msg);
+    long len = (long)sb.st_size;
+    char *buf = malloc(len > 0 ? (size_t)len : 1);
+    if (!buf || (len > 0 && fread(buf, 1, (size_t)len, fp) != (size_t)len)) die(msg);
+    fclose(fp);
+    long cap = len / 2 + 1; /* every key takes >= 2 bytes except possibly the last */
+    int *keys = malloc((size_t)cap * sizeof(int));
+    if (!keys) die(msg);
+    long n = gsort_cli_parse(buf, len, keys, cap);
+    free(buf);
+    if (n <= 0) die(msg); /* empty or non-numeric: the reference never yields a valid run */
+    *n_out = (size_t)n;
+    return keys;
+}
+
+static int local_rank(int rank)
+{
+    const char *vars[] = {"MPI_LOCALRANKID", "OMPI_COMM_WORLD_LOCAL_RANK", "LOCAL_RANK"};
+    for (int i = 0; i < 3; i++) {
+        const char *v = getenv(vars[i]);
+        if (v && *v) return atoi(v);
+    }
+    return rank;
+}
+
+int gsort_cli_main(int argc, char **argv, int algo)
+{
+    int rank, size;
+    MPI_Init(&argc, &argv);
+    MPI_Comm_size(MPI_COMM_WORLD, &size);
+    MPI_Comm_rank(MPI_COMM_WORLD, &rank);
+    if (argc != 2 && argc != 3) {
+        if (rank == 0) fprintf(stderr, "Usage: %s <file: Data file to read>\n", argv[0]);
+        MPI_Abort(MPI_COMM_WORLD, EXIT_FAILURE);
+        exit(EXIT_FAILURE);
+    }
+    const char *file = argv[1];
+    const int debug = argc == 3 ? atoi(argv[2]) : 0;
+
+    /* bootstrap: one context per rank == one GPU; RCCL id broadcast over MPI */
+    gsort_uid uid;
+    memset(&uid, 0, sizeof uid);
+    if (size > 1) {
+        if (rank == 0) check(gsort_get_uid(&uid), NULL, "gsort_get_uid");
+        MPI_Bcast(&uid, (int)sizeof uid, MPI_BYTE, 0, MPI_COMM_WORLD);
+    }
+    gsort_ctx *ctx = NULL;
+    check(gsort_create(&ctx, rank, size, -1 - local_rank(rank), size > 1 ? &uid : NULL), NULL,
+          "gsort_create");
+
+    int *int_buf = NULL;
+    unsigned long long n_total = 0;
+    double start = 0.0;
+    if (rank == 0) {
+        size_t n;
+        int_buf = read_keys(file, &n);
+        n_total = n;
+        start = MPI_Wtime();
+    }
+    MPI_Bcast(&n_total, 1, MPI_UNSIGNED_LONG_LONG, 0, MPI_COMM_WORLD);
+    const unsigned long long B = (n_total + (unsigned long long)size - 1) / (unsigned long long)size;
+    if (algo == CLI_SAMPLE && rank == 0) printf("Each bucket will be put %llu items.\n", B);
+
+    int32_t *d_keys = NULL, *d_out = NULL;
+    size_t n_local = 0, n_out = 0;
+    check(gsort_scatter_from_root(ctx, int_buf, n_total, &d_keys, &n_local), ctx,
+          "gsort_scatter_from_root");
+    if (algo == CLI_RADIX) {
+        check(gsort_radix(ctx, d_keys, n_local, &d_out, &n_out, NULL), ctx, "gsort_radix");
+        if (debug) printf("[COMMON] %d: sorted block of %zu keys\n", rank, n_out);
+    } else {
+        gsort_status st = gsort_sample(ctx, d_keys, n_local, &d_out, &n_out, NULL);
+        if (st == GSORT_ENOSAMPLE) {
+            fprintf(stderr, "[ERROR] %d: no enough sample, try smaller processes. %s\n", rank,
+                    gsort_last_error(ctx));
+            MPI_Abort(MPI_COMM_WORLD, EXIT_FAILURE);
+        }
+        check(st, ctx, "gsort_sample");
+        if (debug) {
+            int32_t *spl = calloc((size_t)size, sizeof(int32_t));
+            uint64_t *cnt = calloc((size_t)size, sizeof(uint64_t));
+            check(gsort_sample_info(ctx, spl, cnt), ctx, "gsort_sample_info");
+            if (rank == 0)
+                for (int i = 0; i < size - 1; i++) printf("[MASTER] Splitter: %u.\n", (unsigned)spl[i]);
+            for (int j = 0; j < size; j++)
+                printf("[COMMON] %d: Bucket %d=%llu\n", rank, j, (unsigned long long)cnt[j]);
+            free(spl);
+            free(cnt);
+        }
+    }
+    check(gsort_gather_to_root(ctx, d_out, n_out, int_buf), ctx, "gsort_gather_to_root");
+    if (rank == 0) {
+        const double end = MPI_Wtime();
+        if ((algo == CLI_RADIX && debug > 2) || (algo == CLI_SAMPLE && debug)) {
+            static char obuf[1 << 20];
+            setvbuf(stdout, obuf, _IOFBF, sizeof obuf);
+            for (unsigned long long i = 0; i < n_total; i++)
+                printf("%llu|%u\n", i, (unsigned)int_buf[i]);
+        }
+        /* index N/2-1 (radix:201); N = 1 would read int_buf[-1] in the reference (Q14) */
+        const long long med = n_total >= 2 ? (long long)(n_total / 2) - 1 : 0;
+        printf("The n/2-th sorted element: %d\n", int_buf[med]);
+        fflush(stdout);
+        free(int_buf);
+        fprintf(stderr, "Endtime()-Starttime() = %.5f sec\n", end - start);
+    }
+    gsort_destroy(ctx);
+    MPI_Finalize();
+    return EXIT_SUCCESS;
+}
