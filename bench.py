@@ -1,0 +1,255 @@
+#!/usr/bin/env python3
+"""bench.py -- sorted keys/sec of the MI355X-native distributed sorter (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--algo radix|sample]
+                    [--keys-log2 28] [--dist uniform|zipf] [--no-cpu-baseline]
+
+One step = one gsort_radix (or gsort_sample) call over keys already resident in HBM: at N = 1
+this is BASELINE.json configs[1] ("Radix sort 2^28 uniform random 32-bit keys on 1 MI355X");
+at N > 1 every GPU holds 2^28 keys (weak scaling: 2^28 * N keys sorted globally, with a per-pass
+RCCL all-to-all over xGMI -- configs[2] is the N = 8 point, 2^31 keys).  Keys come from the
+canonical splitmix64 generator on device (K10), so the data is synthetic and identical to what
+the oracle and the reference CPU run see.
+
+The timed region is K steps bracketed by a barrier + torch.cuda.synchronize() on both sides;
+the slowest rank's time is reported.  `roofline` prices the dominant kernel (the onesweep pass,
+8 B/key algorithmic traffic) with its average duration measured live by HIP events recorded on
+libgsort's own stream around every launch; `traffic` is the HBM bytes per launch from the
+rocprofv3 PMC summary in profiles/ (FETCH_SIZE x 2 + WRITE_SIZE, gfx950 correction) when one
+exists for this configuration, else null.  `cpu_baseline` runs the reference radix_sort
+(oracle/_ref, built unchanged from its source) under mpirun on a bounded 2^24-key sample of the
+same stream on the host's cores (rank 0, N = 1 only), before the GPU is touched.
+"""
+import argparse
+import json
+import os
+import re
+import shutil
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "mpi-test_amd")
+for _p in (ROOT, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+METRIC = "sorted keys/sec (GKeys/s) at 1/2/4/8 GPUs + % HBM/xGMI roofline"
+HBM_PEAK_GBPS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level table)
+XGMI_LINK_GBPS = 153.0      # one xGMI link, per direction
+PASS_BYTES_PER_KEY = 8      # onesweep pass: read 4 B + write 4 B per key
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--algo", choices=["radix", "sample"], default="radix")
+    ap.add_argument("--keys-log2", type=int, default=28)
+    ap.add_argument("--dist", choices=["uniform", "zipf"], default="uniform")
+    ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+# ---------------------------------------------------------------------------------------
+# CPU baseline: the reference itself, on the host cores, before any GPU work
+# ---------------------------------------------------------------------------------------
+def cpu_baseline(dist, seed):
+    keys_log2, np_ = 24, 4  # BASELINE configs[0]: reference radix, mpirun -np 4, 2^24 keys
+    n = 1 << keys_log2
+    ref = os.path.join(ROOT, "oracle", "_ref", "radix_sort")
+    gen = os.path.join(PKG, "bin", "gen_keys")
+    mpirun = shutil.which("mpirun") or "/opt/conda/bin/mpirun"
+    tmp = tempfile.mkdtemp(prefix="gsort_cpu_")
+    try:
+        path = os.path.join(tmp, "keys.txt")
+        subprocess.run([gen, dist, str(n), str(seed), path], check=True)
+        if os.path.exists(ref) and os.path.exists(mpirun):
+            t0 = time.time()
+            r = subprocess.run([mpirun, "-np", str(np_), ref, path], capture_output=True,
+                               text=True, timeout=300)
+            wall = time.time() - t0
+            m = re.search(r"Endtime\(\)-Starttime\(\) = ([0-9.]+) sec", r.stderr)
+            if r.returncode == 0 and m:
+                t = float(m.group(1))
+                return {"value": n / t / 1e9, "unit": "GKeys/s", "cores": np_,
+                        "kind": "reference",
+                        "sample": f"reference radix_sort (oracle/_ref, -O0 as shipped) under "
+                                  f"mpirun -np {np_}, 2^{keys_log2} {dist} keys seed {seed}; "
+                                  f"program timer {t:.3f} s (excludes its text read), "
+                                  f"wall {wall:.1f} s",
+                        "median_line": r.stdout.strip().splitlines()[-1]}
+        # fallback: the oracle's scalar port of the build's algorithm, one core
+        from oracle import orc
+        keys = orc.read_ints(path, cap=n)
+        t0 = time.perf_counter()
+        orc.lsd8(keys)
+        t = time.perf_counter() - t0
+        return {"value": n / t / 1e9, "unit": "GKeys/s", "cores": 1, "kind": "port",
+                "sample": f"oracle lsd8 (scalar C port), 2^{keys_log2} {dist} keys, {t:.3f} s"}
+    except Exception as e:  # the baseline is reported, never fatal
+        return {"value": None, "unit": "GKeys/s", "cores": None, "kind": None,
+                "sample": f"cpu baseline failed: {e!r}"}
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
+def pmc_traffic(algo, n_local, n_gpus):
+    """HBM bytes per onesweep launch from the committed rocprofv3 PMC summary, if it was
+    collected for this exact configuration (tools/profile_pmc.sh writes it)."""
+    path = os.path.join(ROOT, "profiles", "pmc_onesweep.json")
+    try:
+        d = json.load(open(path))
+        if d.get("algo") == algo and d.get("n_local") == n_local and n_gpus == 1:
+            return d.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        if a.gpus > 1 and world == 1:
+            sys.exit("--gpus N>1 must be launched with torch.distributed.run (one rank/GPU)")
+    dist_name = a.dist
+
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        cpu = cpu_baseline(dist_name, a.seed)
+
+    import torch
+    import torch.distributed as dist
+    import gsort
+
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("gloo")  # bootstrap only: uid broadcast, barrier, max-time
+    uid = None
+    if world > 1:
+        buf = torch.zeros(128, dtype=torch.uint8)
+        if rank == 0:
+            buf = torch.tensor(list(gsort.get_uid()), dtype=torch.uint8)
+        dist.broadcast(buf, 0)
+        uid = bytes(buf.tolist())
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    n_local = 1 << a.keys_log2
+    ctx = gsort.Context(rank=rank, nranks=world, device=local, uid=uid)
+    d_in = ctx.alloc(n_local * 4)
+    ctx.generate(gsort.UNIFORM if dist_name == "uniform" else gsort.ZIPF, a.seed,
+                 rank * n_local, n_local, d_in)
+    ctx.reserve(n_local)
+    fn = ctx.radix if a.algo == "radix" else ctx.sample
+
+    for _ in range(a.warmup):
+        fn(d_in, n_local)
+    barrier()
+    torch.cuda.synchronize()
+    stats = []
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        _, n_out, st = fn(d_in, n_local)
+        stats.append(st)
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # correctness of the last step's output, checked on device (K9)
+    out_ptr, n_out, _ = fn(d_in, n_local)
+    fp = ctx.fingerprint(out_ptr, n_out)
+    fin = ctx.fingerprint(d_in, n_local)
+    ok = fp["sorted"]
+    if world > 1:
+        v = torch.tensor([fin["sum"] % (1 << 40), fp["sum"] % (1 << 40), 0 if ok else 1],
+                         dtype=torch.int64)
+        dist.all_reduce(v)
+        ok = ok and int(v[2]) == 0 and int(v[0]) % (1 << 40) == int(v[1]) % (1 << 40)
+    else:
+        ok = ok and fp["sum"] == fin["sum"] and fp["xor"] == fin["xor"]
+
+    n_total = n_local * world
+    ms_step = elapsed * 1e3 / a.steps
+    value = n_total / (ms_step / 1e3) / 1e9
+
+    # dominant kernel: the onesweep pass (HIP events on libgsort's stream, every launch)
+    passes = [st["ms_pass"] for st in stats]
+    launches = sum(1 for p in passes for x in p if x > 0)
+    pass_ms = sum(x for p in passes for x in p) / max(launches, 1)
+    if a.algo == "radix":
+        keys_per_launch = n_local
+    else:
+        keys_per_launch = n_local  # first local sort; the merge re-sort sees ~n_local too
+    achieved = keys_per_launch * PASS_BYTES_PER_KEY / (pass_ms * 1e-3) / 1e9
+    traffic = pmc_traffic(a.algo, n_local, world)
+    last = stats[-1]
+    phases = {k: round(sum(s[k] for s in stats) / len(stats), 4)
+              for k in ("ms_total", "ms_hist", "ms_local_sort", "ms_exchange", "ms_place",
+                        "ms_sample", "ms_merge")}
+    phases["ms_pass"] = [round(sum(s["ms_pass"][i] for s in stats) / len(stats), 4)
+                         for i in range(4)]
+    line = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "GKeys/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": f"synthetic: splitmix64 {dist_name} keys (seed {a.seed}) generated on device",
+        "config": {
+            "workload": (f"{a.algo} sort, 2^{a.keys_log2} {dist_name} int32 keys per GPU "
+                         f"(BASELINE configs[1] at N=1; 2^{a.keys_log2}*N keys sorted "
+                         f"globally at N GPUs)"),
+            "keys_per_gpu": n_local, "total_keys": n_total, "algo": a.algo,
+            "parallelism": f"dp{world}", "onesweep_tile": gsort.onesweep_tile(),
+        },
+        "roofline": {"bound": "hbm", "kernel": "k_onesweep (one LSD pass)",
+                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                     "traffic": traffic,
+                     "algorithmic_bytes_per_launch": keys_per_launch * PASS_BYTES_PER_KEY,
+                     "avg_launch_ms": round(pass_ms, 5), "launches_timed": launches},
+        "cpu_baseline": cpu,
+        "phases_ms_avg": phases,
+        "passes_run": last["passes_run"],
+        "verified": bool(ok),
+    }
+    if world > 1:
+        ex = sum(s["ms_exchange"] for s in stats) / len(stats) / max(last["exchanges"], 1)
+        pair = last["max_pair_bytes"]
+        line["exchange"] = {"bound": "xgmi", "per_exchange_ms": round(ex, 4),
+                            "max_pair_bytes": pair,
+                            "achieved_link_GBps": round(pair / (ex * 1e-3) / 1e9, 2) if ex else None,
+                            "peak_link_GBps": XGMI_LINK_GBPS,
+                            "frac": round(pair / (ex * 1e-3) / 1e9 / XGMI_LINK_GBPS, 4) if ex else None}
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    ctx.free(d_in)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+    if not ok:
+        sys.exit("bench: output failed verification")
+
+
+if __name__ == "__main__":
+    main()
