@@ -137,6 +137,15 @@ gsort_status gsort_copy_to_device(gsort_ctx *ctx, void *d_dst, const void *h_src
 /* Which kernel configuration the local sort uses (tile = keys per workgroup). */
 size_t gsort_onesweep_tile(void);
 
+/* ---- rank-0 text input (host only) ---------------------------------------------------------
+ * gsort_parse_text: parse whitespace-separated decimal keys with the reference reader's
+ * fscanf("%d") semantics (mpi_radix_sort.c:85-97, mpi_sample_sort.c:50-60): optional sign,
+ * values wrap mod 2^32 after saturating at the 64-bit long range.  Writes up to cap keys to out
+ * (out may be NULL to count) and returns the key count, or -1 on a non-numeric token (the
+ * reference spins on such a token until realloc fails and then reports the file invalid).  A
+ * trailing delimiter adds no phantom element.  threads > 1 parses in chunks. */
+long long gsort_parse_text(const char *buf, size_t len, int32_t *out, size_t cap, int threads);
+
 /* ---- host-only planning (no GPU; exported so CPU tests can check it) ----------------------
  * gsort_plan_radix_route: the K8 routing of one distributed LSD pass.  hist = P x 256 per-rank
  * digit counts, B = block size.  Fills send[P] / recv[P] key counts for rank `me` and the

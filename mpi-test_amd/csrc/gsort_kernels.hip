@@ -102,19 +102,86 @@ __global__ __launch_bounds__(BLOCK) void k_hist4(const uint32_t *__restrict__ in
 }
 
 // ---------------------------------------------------------------------------------------
+// Decoupled lookback for digit d of `tile` (one thread): W predecessor status words are in
+// flight per round trip (MI355X cross-XCD sc1 loads cost ~1 us under load, so a one-word walk
+// over the tiles still in flight was the pass's bottleneck).  Sums AGGREGATEs back to the
+// first INCLUSIVE; on a not-yet-published word it sleeps and re-polls from there.  Bounded:
+// gives up (sets *err) instead of hanging.
+// ---------------------------------------------------------------------------------------
+#ifdef GSORT_KBENCH_STAMPS
+// Diagnostic build only (tools/kbench.hip defines the macro; the product never does): per-tile
+// phase timestamps (s_memrealtime, 100 MHz) and digit-0 lookback round trips / spins.
+__device__ unsigned long long *g_stamps;
+#define GSORT_STAMP(slot) \
+    if (threadIdx.x == 0) g_stamps[(uint64_t)tile * 8 + (slot)] = __builtin_amdgcn_s_memrealtime()
+#else
+#define GSORT_STAMP(slot)
+#endif
+// rounds / spins report the round trips and not-ready re-polls (diagnostics; dead otherwise)
+template <int W>
+__device__ __forceinline__ uint64_t lookback(const unsigned long long *status, uint32_t tile,
+                                             int d, uint32_t epoch, uint32_t *err,
+                                             uint32_t &rounds, uint32_t &spins_out) {
+    uint64_t prefix = 0;
+    int64_t t = (int64_t)tile - 1;  // nearest predecessor not yet consumed
+    uint32_t spins = 0;
+    while (t >= 0) {
+        uint64_t wv[W];
+#pragma unroll
+        for (int j = 0; j < W; ++j)
+            wv[j] = (t - j >= 0) ? ld_agent(status + (uint64_t)(t - j) * kRadix + d)
+                                 : pack_status(epoch, kFlagInc, 0);
+        int consumed = 0;
+        bool stop = false, fin = false;
+#pragma unroll
+        for (int j = 0; j < W; ++j) {
+            if (!stop) {
+                const uint32_t ep = (uint32_t)(wv[j] >> 48);
+                const uint64_t fl = (wv[j] >> 46) & 3u;
+                if (ep != epoch || fl == 0) {
+                    stop = true;
+                } else {
+                    prefix += wv[j] & kCountMask;
+                    ++consumed;
+                    if (fl == kFlagInc) stop = fin = true;
+                }
+            }
+        }
+        ++rounds;
+        if (fin) break;
+        t -= consumed;
+        if (consumed < W) {
+            if (++spins > (1u << 22)) {
+                atomicOr(err, 1u);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    spins_out = spins;
+    return prefix;
+}
+
+// ---------------------------------------------------------------------------------------
 // K3: one stable onesweep LSD pass.
 //   tile = BLOCK * ITEMS keys; wave w owns keys [w*64*ITEMS, (w+1)*64*ITEMS) of the tile,
 //   round i of the wave holds keys i*64 + lane, so (round, lane) order == memory order.
-//   1. rank: for each round, 8 ballots give each lane the mask of lanes with its digit; the
-//      lane's rank = (wave's running count of the digit) + (#peers below it); the lowest peer
-//      advances the wave's running count.
-//   2. per-digit block counts -> publish AGGREGATE, block-exclusive digit starts.
-//   3. scatter keys into LDS in block-sorted order (stable), then decoupled lookback over
-//      previous tiles' status words gives this tile's global offset per digit.
-//   4. stream LDS out in order: consecutive threads hit consecutive addresses within a digit.
+//   1. rank: for each round, 8 ballots give each lane the mask of lanes sharing its digit
+//      (per bit: v_bfe_i32, v_cmp, two v_bitop3); rank = (wave's running count of the digit)
+//      + (#peers below the lane); every peer writes the same advanced count (branch-free).
+//   2. per-digit tile counts -> publish AGGREGATE; block-exclusive digit starts folded into
+//      the per-wave offset table.
+//   3. scatter keys into LDS in block-sorted order (stable); meanwhile one thread per digit
+//      runs the decoupled lookback over previous tiles' status words -> global offsets.
+//   4. stream LDS out in order: consecutive lanes hit consecutive addresses within a digit.
 // Tile ids come from an atomic counter, so every tile a lookback waits on is already running.
+// LB_EARLY runs the lookback right after publishing the aggregate (so this tile's inclusive
+// prefix is published as early as possible) instead of after the LDS scatter.
+// NO_LOOKBACK is an ablation switch for timing-only builds (tools/kbench.hip): it skips the
+// lookback wait (prefix = 0, wrong output) and is never set in the product.
 // ---------------------------------------------------------------------------------------
-template <int BLOCK, int ITEMS, bool FIN, bool FOUT>
+template <int BLOCK, int ITEMS, bool FIN, bool FOUT, bool NO_LOOKBACK = false,
+          bool LB_EARLY = true, int LB_W = 8>
 __global__ __launch_bounds__(BLOCK) void k_onesweep(const uint32_t *__restrict__ in,
                                                     uint32_t *__restrict__ out, uint64_t n,
                                                     int shift,
@@ -125,10 +192,10 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(const uint32_t *__restrict__
     constexpr int WAVES = BLOCK / 64;
     constexpr int TILE = BLOCK * ITEMS;
     static_assert(BLOCK >= kRadix, "one thread per digit in the scan/lookback");
+    static_assert(TILE <= 65536, "ranks are packed as 16 bits");
     __shared__ uint32_t s_keys[TILE];
-    __shared__ uint32_t s_wcnt[WAVES * kRadix];
-    __shared__ uint32_t s_start[kRadix];
-    __shared__ long long s_gofs[kRadix];
+    __shared__ uint32_t s_wofs[WAVES * kRadix];  // per-wave counts, then per-wave tile offsets
+    __shared__ uint32_t *s_dst[kRadix];          // out + global offset - tile start, by digit
     __shared__ uint32_t s_wsum[kRadix / 64];
     __shared__ uint32_t s_tile;
 
@@ -136,11 +203,12 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(const uint32_t *__restrict__
     const int lane = tid & 63;
     const int w = tid >> 6;
     if (tid == 0) s_tile = atomicAdd(tile_ctr, 1u);
-    for (int i = tid; i < WAVES * kRadix; i += BLOCK) s_wcnt[i] = 0;
+    for (int i = tid; i < WAVES * kRadix; i += BLOCK) s_wofs[i] = 0;
     __syncthreads();
     const uint32_t tile = s_tile;
     const uint64_t tbase = (uint64_t)tile * TILE;
     const bool full = tbase + TILE <= n;
+    GSORT_STAMP(0);
 
     uint32_t k[ITEMS];
     {
@@ -161,37 +229,49 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(const uint32_t *__restrict__
     }
 
     // 1. wave-level stable ranking
-    uint32_t r[ITEMS];
-    uint32_t *wc = s_wcnt + w * kRadix;
+    uint32_t rk[(ITEMS + 1) / 2];  // two 16-bit ranks per register
+    uint32_t *wc = s_wofs + w * kRadix;
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
         const uint32_t d = (k[i] >> shift) & 255u;
-        uint64_t peers = ~0ULL;
+        uint32_t plo = ~0u, phi = ~0u;
 #pragma unroll
         for (int b = 0; b < 8; ++b) {
-            const bool bit = (d >> b) & 1u;
-            const uint64_t bal = __ballot(bit);
-            peers &= bit ? bal : ~bal;
+            // 4 VALU per bit: m = sign-extended bit (v_bfe_i32), ballot of m (v_cmp, asm so
+            // hipcc does not re-derive the bit), peers &= ~(ballot ^ m) (v_bitop3 0x90)
+            const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int32_t)d, b, 1);
+            uint64_t bal;
+            asm("v_cmp_ne_u32_e64 %0, 0, %1" : "=s"(bal) : "v"(m));
+            plo = __builtin_amdgcn_bitop3_b32(plo, (uint32_t)bal, m, 0x90);
+            phi = __builtin_amdgcn_bitop3_b32(phi, (uint32_t)(bal >> 32), m, 0x90);
         }
-        const uint32_t below = __builtin_amdgcn_mbcnt_hi(
-            (uint32_t)(peers >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)peers, 0u));
+        const uint32_t below =
+            __builtin_amdgcn_mbcnt_hi(phi, __builtin_amdgcn_mbcnt_lo(plo, 0u));
         const uint32_t prev = wc[d];
-        r[i] = prev + below;
-        if (below == 0) wc[d] = prev + (uint32_t)__popcll(peers);
+        const uint32_t r = prev + below;
+        wc[d] = prev + (uint32_t)(__popc(plo) + __popc(phi));  // same value from every peer
+        if (i & 1) rk[i >> 1] |= r << 16; else rk[i >> 1] = r;
     }
     __syncthreads();
+    GSORT_STAMP(1);
 
-    // 2. per-digit tile counts, per-wave exclusive offsets, publish the aggregate
-    uint32_t tcount = 0;
+    // 2. per-digit tile counts; publish the aggregate; (early) lookback; digit starts
+    uint32_t tcount = 0, excl = 0, lb_rounds = 0, lb_spins = 0;
+    uint64_t prefix = 0;
+    uint32_t c[WAVES];
     if (tid < kRadix) {
 #pragma unroll
         for (int ww = 0; ww < WAVES; ++ww) {
-            const uint32_t c = s_wcnt[ww * kRadix + tid];
-            s_wcnt[ww * kRadix + tid] = tcount;
-            tcount += c;
+            c[ww] = s_wofs[ww * kRadix + tid];
+            tcount += c[ww];
         }
-        unsigned long long *my_status = status + (uint64_t)tile * kRadix + tid;
-        st_agent(my_status, pack_status(epoch, tile == 0 ? kFlagInc : kFlagAgg, tcount));
+        st_agent(status + (uint64_t)tile * kRadix + tid,
+                 pack_status(epoch, tile == 0 ? kFlagInc : kFlagAgg, tcount));
+        if (LB_EARLY && tile > 0 && !NO_LOOKBACK) {
+            prefix = lookback<LB_W>(status, tile, tid, epoch, err, lb_rounds, lb_spins);
+            st_agent(status + (uint64_t)tile * kRadix + tid,
+                     pack_status(epoch, kFlagInc, prefix + tcount));
+        }
         uint32_t v = tcount;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
@@ -199,13 +279,19 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(const uint32_t *__restrict__
             if (lane >= o) v += t;
         }
         if (lane == 63) s_wsum[w] = v;
-        s_start[tid] = v - tcount;  // exclusive within the wave; wave offsets added below
+        excl = v - tcount;
     }
     __syncthreads();
+    uint32_t start = 0;
     if (tid < kRadix) {
-        uint32_t off = 0;
-        for (int ww = 0; ww < w; ++ww) off += s_wsum[ww];
-        s_start[tid] += off;
+        start = excl;
+        for (int ww = 0; ww < w; ++ww) start += s_wsum[ww];
+        uint32_t off = start;
+#pragma unroll
+        for (int ww = 0; ww < WAVES; ++ww) {
+            s_wofs[ww * kRadix + tid] = off;
+            off += c[ww];
+        }
     }
     __syncthreads();
 
@@ -213,48 +299,41 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(const uint32_t *__restrict__
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
         const uint32_t d = (k[i] >> shift) & 255u;
-        s_keys[s_start[d] + wc[d] + r[i]] = k[i];
+        const uint32_t r = (i & 1) ? (rk[i >> 1] >> 16) : (rk[i >> 1] & 0xFFFFu);
+        s_keys[wc[d] + r] = k[i];
     }
-    // 3b. decoupled lookback, one thread per digit
+    // 3b. (late) lookback, one thread per digit; global destination base per digit
     if (tid < kRadix) {
-        uint64_t prefix = 0;
-        if (tile > 0) {
-            const unsigned long long *p = status + (uint64_t)(tile - 1) * kRadix + tid;
-            uint32_t spins = 0;
-            for (;;) {
-                const uint64_t wv = ld_agent(p);
-                const uint32_t ep = (uint32_t)(wv >> 48);
-                const uint64_t fl = (wv >> 46) & 3u;
-                if (ep != epoch || fl == 0) {
-                    if (++spins > (1u << 22)) {  // bounded: never hang the GPU; host reports
-                        atomicOr(err, 1u);
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(2);
-                    continue;
-                }
-                prefix += wv & kCountMask;
-                if (fl == kFlagInc) break;
-                p -= kRadix;
-            }
+        if (!LB_EARLY && tile > 0 && !NO_LOOKBACK) {
+            prefix = lookback<LB_W>(status, tile, tid, epoch, err, lb_rounds, lb_spins);
             st_agent(status + (uint64_t)tile * kRadix + tid,
                      pack_status(epoch, kFlagInc, prefix + tcount));
         }
-        s_gofs[tid] = (long long)(base[tid] + prefix) - (long long)s_start[tid];
+        s_dst[tid] = out + (base[tid] + prefix) - start;
     }
     __syncthreads();
+    GSORT_STAMP(2);
+#ifdef GSORT_KBENCH_STAMPS
+    if (tid == 0) {
+        g_stamps[(uint64_t)tile * 8 + 4] = lb_rounds;
+        g_stamps[(uint64_t)tile * 8 + 5] = lb_spins;
+        uint32_t hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(hw));
+        g_stamps[(uint64_t)tile * 8 + 6] = hw & 0xF;
+    }
+#endif
 
     // 4. ordered write-out
-    const uint64_t lim = full ? (uint64_t)TILE : n - tbase;
+    const uint32_t lim = full ? (uint32_t)TILE : (uint32_t)(n - tbase);
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
         const uint32_t j = (uint32_t)(i * BLOCK + tid);
         if (full || j < lim) {
             const uint32_t key = s_keys[j];
-            const uint32_t d = (key >> shift) & 255u;
-            out[s_gofs[d] + (long long)j] = FOUT ? (key ^ kFlip) : key;
+            s_dst[(key >> shift) & 255u][j] = FOUT ? (key ^ kFlip) : key;
         }
     }
+    GSORT_STAMP(3);
 }
 
 // ---------------------------------------------------------------------------------------

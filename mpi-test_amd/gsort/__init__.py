@@ -53,7 +53,7 @@ EXPORTS = [
     "gsort_sample_info", "gsort_scatter_from_root", "gsort_gather_to_root", "gsort_generate",
     "gsort_fingerprint", "gsort_device_alloc", "gsort_device_free", "gsort_copy_to_host",
     "gsort_copy_to_device", "gsort_onesweep_tile", "gsort_plan_radix_route",
-    "gsort_plan_splitters",
+    "gsort_plan_splitters", "gsort_parse_text",
 ]
 
 _lib = None
@@ -99,6 +99,8 @@ def lib():
     L.gsort_copy_to_device.argtypes = [VP, VP, VP, SZ]
     L.gsort_plan_radix_route.argtypes = [I, VP, U64, I, VP, VP, VP, P(SZ)]
     L.gsort_plan_splitters.argtypes = [I, VP, VP]
+    L.gsort_parse_text.argtypes = [ctypes.c_char_p, SZ, VP, SZ, I]
+    L.gsort_parse_text.restype = ctypes.c_longlong
     _lib = L
     return L
 
@@ -267,3 +269,18 @@ def plan_splitters(samples, P):
     out = np.zeros(max(P - 1, 1), dtype=np.int32)
     _check(lib().gsort_plan_splitters(P, samples.ctypes.data, out.ctypes.data), None)
     return out[: P - 1]
+
+
+def parse_text(data, threads=1):
+    """gsort_parse_text: the rank-0 reader's %d-compatible parse.  Returns int32 array or None
+    on a non-numeric token."""
+    import numpy as np
+    if isinstance(data, str):
+        data = data.encode()
+    n = lib().gsort_parse_text(data, len(data), None, 0, threads)
+    if n < 0:
+        return None
+    out = np.empty(max(n, 1), dtype=np.int32)
+    n2 = lib().gsort_parse_text(data, len(data), out.ctypes.data, n, threads)
+    assert n2 == n
+    return out[:n]

@@ -11,13 +11,13 @@
  *                             sample at debug >= 1 (sample:202-204); sample debug also prints
  *                             "[MASTER] Splitter: %u.\n" and "[COMMON] r: Bucket j=len"
  *   stdout                 -> "The n/2-th sorted element: %d\n" = sorted[N/2-1] (radix:201)
- *   stderr                 -> "Endtime()-Starttime() = %.5f sec\n" (radix:203); the timer
- *                             starts after the rank-0 read and stops after the final gather
- * MPI carries only the bootstrap: the RCCL unique id and N.  Keys move H2D on rank 0, over
+ *   stderr                 -> "Endtime()-Starttime() = %.5f sec\n" (radix:203)
+ * The timer spans what the reference's spans -- from after the rank-0 read to after the final
+ * gather (radix:98,197; sample:61,201) -- and, like the reference's, excludes process setup
+ * (MPI_Init there; MPI_Init + GPU context + RCCL communicator here).
+ * MPI carries only the bootstrap: N and the RCCL unique id.  Keys move H2D on rank 0, over
  * xGMI between GPUs (RCCL), and D2H on rank 0 -- never over MPI.
  */
-#include <errno.h>
-#include <limits.h>
 #include <mpi.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -28,41 +28,10 @@
 #include "gsort.h"
 #include "gsort_cli.h"
 
-static int is_space(char c)
-{
-    return c == ' ' || c == '\t' || c == '\n' || c == '\v' || c == '\f' || c == '\r';
-}
-
-long gsort_cli_parse(const char *buf, long len, int *out, long cap)
-{
-    long n = 0, i = 0;
-    for (;;) {
-        while (i < len && is_space(buf[i])) i++;
-        if (i >= len) break;
-        int neg = 0;
-        if (buf[i] == '+' || buf[i] == '-') neg = buf[i++] == '-';
-        if (i >= len || buf[i] < '0' || buf[i] > '9') return -1;
-        /* glibc's %d converts through strtol: the long saturates, then truncates to int */
-        unsigned long long mag = 0;
-        int sat = 0;
-        for (; i < len && buf[i] >= '0' && buf[i] <= '9'; i++) {
-            unsigned d = (unsigned)(buf[i] - '0');
-            if (mag > (ULLONG_MAX - d) / 10) sat = 1; else mag = mag * 10 + d;
-        }
-        long long v;
-        if (!neg) v = (sat || mag > (unsigned long long)LLONG_MAX) ? LLONG_MAX : (long long)mag;
-        else v = (sat || mag > (unsigned long long)LLONG_MAX + 1ULL) ? LLONG_MIN
-                                                                     : (long long)(0ULL - mag);
-        if (i < len && !is_space(buf[i])) return -1; /* e.g. "12,13": ref spins forever */
-        if (n < cap) out[n] = (int)(uint32_t)(unsigned long long)v;
-        n++;
-    }
-    return n;
-}
-
 static void die(const char *msg)
 {
     fprintf(stderr, "%s\n", msg);
+    fflush(stderr);
     MPI_Abort(MPI_COMM_WORLD, EXIT_FAILURE);
     exit(EXIT_FAILURE);
 }
@@ -76,8 +45,8 @@ static void check(gsort_status st, gsort_ctx *ctx, const char *what)
     die(msg);
 }
 
-/* rank-0 reader (mpi_radix_sort.c:73-97): whole file, then one %d-compatible scan */
-static int *read_keys(const char *file, size_t *n_out)
+/* rank-0 reader (mpi_radix_sort.c:73-97): whole file, then a %d-compatible parse */
+static int32_t *read_keys(const char *file, size_t *n_out)
 {
     char msg[4096 + 64];
     snprintf(msg, sizeof msg, "sort(): '%s' is not a valid file for read.", file);
@@ -85,16 +54,16 @@ static int *read_keys(const char *file, size_t *n_out)
     if (!fp) die(msg);
     struct stat sb;
     if (fstat(fileno(fp), &sb) != 0) die(msg);
-    long len = (long)sb.st_size;
-    char *buf = malloc(len > 0 ? (size_t)len : 1);
-    if (!buf || (len > 0 && fread(buf, 1, (size_t)len, fp) != (size_t)len)) die(msg);
+    size_t len = (size_t)sb.st_size;
+    char *buf = malloc(len ? len : 1);
+    if (!buf || (len && fread(buf, 1, len, fp) != len)) die(msg);
     fclose(fp);
-    long cap = len / 2 + 1; /* every key takes >= 2 bytes except possibly the last */
-    int *keys = malloc((size_t)cap * sizeof(int));
+    size_t cap = len / 2 + 1; /* every key but the last takes >= 2 bytes */
+    int32_t *keys = malloc(cap * sizeof(int32_t));
     if (!keys) die(msg);
-    long n = gsort_cli_parse(buf, len, keys, cap);
+    long long n = gsort_parse_text(buf, len, keys, cap, 16);
     free(buf);
-    if (n <= 0) die(msg); /* empty or non-numeric: the reference never yields a valid run */
+    if (n <= 0) die(msg); /* empty or non-numeric: the reference never completes a valid run */
     *n_out = (size_t)n;
     return keys;
 }
@@ -123,6 +92,14 @@ int gsort_cli_main(int argc, char **argv, int algo)
     const char *file = argv[1];
     const int debug = argc == 3 ? atoi(argv[2]) : 0;
 
+    int32_t *int_buf = NULL;
+    unsigned long long n_total = 0;
+    if (rank == 0) {
+        size_t n;
+        int_buf = read_keys(file, &n);
+        n_total = n;
+    }
+
     /* bootstrap: one context per rank == one GPU; RCCL id broadcast over MPI */
     gsort_uid uid;
     memset(&uid, 0, sizeof uid);
@@ -134,15 +111,8 @@ int gsort_cli_main(int argc, char **argv, int algo)
     check(gsort_create(&ctx, rank, size, -1 - local_rank(rank), size > 1 ? &uid : NULL), NULL,
           "gsort_create");
 
-    int *int_buf = NULL;
-    unsigned long long n_total = 0;
-    double start = 0.0;
-    if (rank == 0) {
-        size_t n;
-        int_buf = read_keys(file, &n);
-        n_total = n;
-        start = MPI_Wtime();
-    }
+    MPI_Barrier(MPI_COMM_WORLD);
+    const double start = MPI_Wtime();
     MPI_Bcast(&n_total, 1, MPI_UNSIGNED_LONG_LONG, 0, MPI_COMM_WORLD);
     const unsigned long long B = (n_total + (unsigned long long)size - 1) / (unsigned long long)size;
     if (algo == CLI_SAMPLE && rank == 0) printf("Each bucket will be put %llu items.\n", B);
@@ -157,8 +127,11 @@ int gsort_cli_main(int argc, char **argv, int algo)
     } else {
         gsort_status st = gsort_sample(ctx, d_keys, n_local, &d_out, &n_out, NULL);
         if (st == GSORT_ENOSAMPLE) {
-            fprintf(stderr, "[ERROR] %d: no enough sample, try smaller processes. %s\n", rank,
-                    gsort_last_error(ctx));
+            /* mpi_sample_sort.c:97 prints from the short rank; every rank knows here */
+            if (rank == 0)
+                fprintf(stderr, "[ERROR] %d: no enough sample, try smaller processes. %s\n",
+                        rank, gsort_last_error(ctx));
+            fflush(stderr);
             MPI_Abort(MPI_COMM_WORLD, EXIT_FAILURE);
         }
         check(st, ctx, "gsort_sample");
@@ -167,7 +140,8 @@ int gsort_cli_main(int argc, char **argv, int algo)
             uint64_t *cnt = calloc((size_t)size, sizeof(uint64_t));
             check(gsort_sample_info(ctx, spl, cnt), ctx, "gsort_sample_info");
             if (rank == 0)
-                for (int i = 0; i < size - 1; i++) printf("[MASTER] Splitter: %u.\n", (unsigned)spl[i]);
+                for (int i = 0; i < size - 1; i++)
+                    printf("[MASTER] Splitter: %u.\n", (unsigned)spl[i]);
             for (int j = 0; j < size; j++)
                 printf("[COMMON] %d: Bucket %d=%llu\n", rank, j, (unsigned long long)cnt[j]);
             free(spl);

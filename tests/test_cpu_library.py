@@ -68,3 +68,53 @@ def test_no_cpu_fallback_without_gpu(gsort):
         pytest.skip("a GPU is visible")
     with pytest.raises(gsort.GsortError):
         gsort.Context()
+
+
+def test_text_parser_matches_glibc_fscanf(gsort, orc, tmp_path):
+    """gsort_parse_text (the CLIs' rank-0 reader) == the reference's fscanf("%d") loop
+    (mpi_radix_sort.c:85-97) without its trailing-delimiter phantom (Q6)."""
+    rng = np.random.default_rng(5)
+    toks = ["0", "-0", "+7", "2147483647", "2147483648", "-2147483648", "-2147483649",
+            "4294967295", "4294967296", "99999999999999999999", "-99999999999999999999",
+            "9223372036854775807", "9223372036854775808", "-9223372036854775809", "00012"]
+    toks += [str(int(x)) for x in rng.integers(-2**40, 2**40, 300)]
+    seps = [" ", "\n", "\t", "  \r\n", "\v", "\f"]
+    for trial in range(20):
+        picked = rng.choice(toks, 200)
+        text = "".join(t + seps[int(rng.integers(0, len(seps)))] for t in picked)
+        if trial % 2:
+            text = text.rstrip()
+        p = tmp_path / f"t{trial}.txt"
+        p.write_text(text)
+        want = orc.read_ints(str(p), with_phantom=False)
+        for th in (1, 4):
+            got = gsort.parse_text(text, threads=th)
+            assert got is not None and np.array_equal(got, want), (trial, th)
+    assert gsort.parse_text("1 2 x 3") is None
+    assert gsort.parse_text("12,13") is None
+    assert gsort.parse_text("") is not None and gsort.parse_text("").size == 0
+
+
+def test_text_parser_parallel_large(gsort, orc):
+    keys = orc.gen(orc.UNIFORM, 3, 1 << 20) - (1 << 30)
+    text = "\n".join(map(str, keys.tolist()))
+    assert np.array_equal(gsort.parse_text(text, threads=8), keys)
+
+
+def test_cli_contract_without_gpu(tmp_path):
+    """argv / invalid-file handling happens before any GPU call."""
+    import subprocess
+    exe = os.path.join(ROOT, "mpi-test_amd", "bin", "radix_sort")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert r.returncode != 0 and f"Usage: {exe} <file: Data file to read>" in r.stderr
+    r = subprocess.run([exe, "a", "b", "c"], capture_output=True, text=True, timeout=60)
+    assert r.returncode != 0 and "Usage:" in r.stderr
+    missing = str(tmp_path / "missing.txt")
+    r = subprocess.run([exe, missing], capture_output=True, text=True, timeout=60)
+    assert r.returncode != 0
+    assert f"sort(): '{missing}' is not a valid file for read." in r.stderr
+    bad = tmp_path / "bad.txt"
+    bad.write_text("1 2 three")
+    r = subprocess.run([os.path.join(ROOT, "mpi-test_amd", "bin", "sample_sort"), str(bad)],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode != 0 and "is not a valid file for read." in r.stderr
