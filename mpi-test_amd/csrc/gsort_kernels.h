@@ -5,31 +5,34 @@
 
 namespace gsort {
 
-// Onesweep geometry (gsort_kernels.hip): 512 threads = 8 waves, 16 keys per thread.
+// Pass geometry (gsort_kernels.hip): K3 tiles of 512 threads = 8 waves x 16 keys per thread.
 constexpr int kSweepBlock = 512;
 constexpr int kSweepItems = 16;
 constexpr int kSweepTile = kSweepBlock * kSweepItems;  // 8192 keys per workgroup tile
+constexpr int kScanGroup = 32;                           // tiles per K2a scan group
 constexpr int kRadix = 256;
 
-// Status word of the decoupled lookback: [63:48] epoch, [47:46] flag, [45:0] count.
-constexpr uint64_t kFlagAgg = 1, kFlagInc = 2;
-
 inline uint64_t sweep_tiles(uint64_t n) { return (n + kSweepTile - 1) / kSweepTile; }
+inline uint64_t scan_groups(uint64_t n) { return (sweep_tiles(n) + kScanGroup - 1) / kScanGroup; }
 
 // K10 canonical generator.
 hipError_t launch_generate(int dist, uint64_t seed, uint64_t start, uint64_t n, int32_t *out,
                            hipStream_t s);
-// K1: all four 8-bit digit histograms of (key ^ 0x80000000) in one read; hist[4][256] u64
-// must be zeroed by the caller.
-hipError_t launch_hist4(const uint32_t *in, uint64_t n, uint64_t *hist, hipStream_t s);
-// K3: one stable onesweep pass over digit `shift/8`.  base[256] = exclusive digit offsets
-// for this pass (u64).  status: >= tiles*256 words, tile_ctr: one zeroed u32.  A lookback
-// that spins past its bound sets *err (and the pass output is garbage) instead of hanging.
-// flip_in / flip_out apply the int32 <-> ordered-u32 map on load / store.
-hipError_t launch_onesweep(const uint32_t *in, uint32_t *out, uint64_t n, int shift,
-                           const uint64_t *base, uint64_t *status, uint32_t *tile_ctr,
-                           uint32_t *err, uint32_t epoch, bool flip_in, bool flip_out,
-                           hipStream_t s);
+// K1: tcounts[tile][256] = digit (shift/8) counts of every kSweepTile-key tile (u32).  With
+// hist4 != nullptr (shift must be 0) it also adds all four digit histograms of the keys into
+// hist4[4][256] (u64, zeroed by the caller).  flip maps int32 input to ordered u32.
+hipError_t launch_tile_counts(const uint32_t *in, uint64_t n, int shift, bool flip,
+                              uint32_t *tcounts, uint64_t *hist4, hipStream_t s);
+// K2: tcounts -> group-local exclusive tile offsets (in place); gsum[scan_groups(n)][256] ->
+// per-group exclusive digit prefix; totals[256] = the pass's digit histogram; bases[256] =
+// exclusive scan of totals.  totals and bases are device arrays of 256 u64 (required).
+hipError_t launch_scan_tiles(uint32_t *tcounts, uint64_t n, uint64_t *gsum, uint64_t *totals,
+                             uint64_t *bases, hipStream_t s);
+// K3: one stable LSD pass over digit shift/8 using the K2 offsets; flip_in / flip_out apply
+// the int32 <-> ordered-u32 map on load / store.
+hipError_t launch_scatter(const uint32_t *in, uint32_t *out, uint64_t n, int shift,
+                          const uint32_t *toff, const uint64_t *gpfx, const uint64_t *bases,
+                          bool flip_in, bool flip_out, hipStream_t s);
 // K8 receive-side placement: segs[k] = {src_off (in recv buffer), dst_off, len}; copies the
 // segments into out and (if hist != nullptr) accumulates the 256-bin histogram of digit
 // `next_shift/8` of the placed keys (ordered-u32 form); flip_out maps back to int32 on store.

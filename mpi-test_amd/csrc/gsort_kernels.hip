@@ -2,10 +2,10 @@
 //
 // Keys are int32; every kernel that compares digits works on the order-preserving map
 // u = key ^ 0x80000000 (unsigned order of u == signed order of key).  The local sort is an
-// 8-bit LSD radix sort in "onesweep" form: one read builds all four digit histograms (K1),
-// then each pass (K3) ranks a tile with wave64 ballots, takes its global digit offsets from a
-// single-pass decoupled lookback, and scatters through LDS so the global stores come out in
-// digit runs.  Algorithmic traffic: 4 B/key for K1 + 8 B/key per pass.
+// 8-bit LSD radix sort; each pass counts digits per tile (K1; the first pass also builds all
+// four global digit histograms), scans the tile offsets (K2), then ranks every tile with
+// wave64 ballots and scatters it through LDS so the global stores come out in digit runs
+// (K3).  Algorithmic traffic: 4 B/key (K1) + 8 B/key (K3) per pass.
 //
 // Reference hot loops these replace (cites /root/reference/...):
 //   K1/K3  mpi_radix_sort.c:144-147 (number_digit_at + bucket_push per key), :54-58, :33-43;
@@ -21,22 +21,11 @@ namespace {
 
 constexpr uint32_t kFlip = 0x80000000u;
 constexpr uint64_t kGolden = 0x9E3779B97F4A7C15ULL;
-constexpr uint64_t kCountMask = (1ULL << 46) - 1;
 
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
     return z ^ (z >> 31);
-}
-
-__device__ __forceinline__ uint64_t ld_agent(const unsigned long long *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_agent(unsigned long long *p, uint64_t v) {
-    __hip_atomic_store(p, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint64_t pack_status(uint32_t epoch, uint64_t flag, uint64_t cnt) {
-    return ((uint64_t)epoch << 48) | (flag << 46) | cnt;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -61,154 +50,199 @@ __global__ void k_generate(int dist, uint64_t seed, uint64_t start, uint64_t n, 
 }
 
 // ---------------------------------------------------------------------------------------
-// K1: all four digit histograms in one read.  Per-wave private LDS bins (4 x 256 per wave)
-// absorb the contention of duplicate-heavy inputs; one global atomic per non-zero bin.
+// One LSD pass = K1 (per-tile digit counts) + K2 (two-level scan of the tile offsets) + K3
+// (rank + stable scatter).  A single-pass "onesweep" with a decoupled lookback was measured
+// first: on MI355X a cross-XCD status round trip costs ~1.35 us under streaming
+// load, so at the tile rate an HBM-bound pass needs (~90 tiles/us) every tile walked ~40
+// predecessors and read more status bytes than key bytes.  Counting first costs 4 B/key more
+// per pass but makes K3 free of inter-workgroup communication.
 // ---------------------------------------------------------------------------------------
-template <int BLOCK, bool VEC>
-__global__ __launch_bounds__(BLOCK) void k_hist4(const uint32_t *__restrict__ in, uint64_t n,
-                                                 unsigned long long *__restrict__ hist) {
+
+// K1: digit counts of every kSweepTile-key tile (tcounts[tile][256], u32).  ALL4 (first pass,
+// digit 0) also accumulates the four global digit histograms (hist4[4][256]) in the same read;
+// they decide which passes are trivial and, in the distributed sort, are all-gathered.
+template <int BLOCK, bool ALL4, bool VEC>
+__global__ __launch_bounds__(BLOCK) void k_tile_counts(const uint32_t *__restrict__ in,
+                                                       uint64_t n, int shift, uint32_t flip,
+                                                       uint32_t *__restrict__ tcounts,
+                                                       unsigned long long *__restrict__ hist4,
+                                                       uint32_t ntiles) {
     constexpr int WAVES = BLOCK / 64;
-    __shared__ uint32_t sh[WAVES * 4 * kRadix];
-    for (int i = threadIdx.x; i < WAVES * 4 * kRadix; i += BLOCK) sh[i] = 0;
-    __syncthreads();
-    uint32_t *my = sh + (threadIdx.x >> 6) * 4 * kRadix;
+    __shared__ uint32_t s_t[kRadix];
+    __shared__ uint32_t s_h[ALL4 ? WAVES * 3 * kRadix : 1];  // digits 1..3, per wave
+    const int tid = threadIdx.x;
+    uint32_t *hw = s_h + (ALL4 ? (tid >> 6) * 3 * kRadix : 0);
+    if (ALL4)
+        for (int i = tid; i < WAVES * 3 * kRadix; i += BLOCK) s_h[i] = 0;
+    uint64_t acc0 = 0;  // ALL4: this thread's digit of hist4[0] (= sum of its tile counts)
     auto count = [&](uint32_t u) {
-        u ^= kFlip;
-        atomicAdd(&my[u & 255u], 1u);
-        atomicAdd(&my[kRadix + ((u >> 8) & 255u)], 1u);
-        atomicAdd(&my[2 * kRadix + ((u >> 16) & 255u)], 1u);
-        atomicAdd(&my[3 * kRadix + (u >> 24)], 1u);
+        u ^= flip;
+        atomicAdd(&s_t[(u >> shift) & 255u], 1u);
+        if (ALL4) {
+            atomicAdd(&hw[(u >> 8) & 255u], 1u);
+            atomicAdd(&hw[kRadix + ((u >> 16) & 255u)], 1u);
+            atomicAdd(&hw[2 * kRadix + (u >> 24)], 1u);
+        }
     };
-    const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
-    const uint64_t t0 = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
-    uint64_t done = 0;
-    if (VEC) {
-        const uint64_t nv = n / 4;
-        const uint4 *in4 = reinterpret_cast<const uint4 *>(in);
-        for (uint64_t v = t0; v < nv; v += stride) {
-            const uint4 q = in4[v];
-            count(q.x); count(q.y); count(q.z); count(q.w);
+    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        if (tid < kRadix) s_t[tid] = 0;
+        __syncthreads();
+        const uint64_t t0 = (uint64_t)tile * kSweepTile;
+        if (VEC && t0 + kSweepTile <= n) {
+            const uint4 *p = reinterpret_cast<const uint4 *>(in + t0);
+#pragma unroll
+            for (int j = 0; j < kSweepTile / 4 / BLOCK; ++j) {
+                const uint4 q = p[j * BLOCK + tid];
+                count(q.x); count(q.y); count(q.z); count(q.w);
+            }
+        } else {
+            const uint64_t t1 = t0 + kSweepTile < n ? t0 + kSweepTile : n;
+            for (uint64_t i = t0 + tid; i < t1; i += BLOCK) count(in[i]);
         }
-        done = nv * 4;
+        __syncthreads();
+        if (tid < kRadix) {
+            tcounts[(uint64_t)tile * kRadix + tid] = s_t[tid];
+            acc0 += s_t[tid];
+        }
     }
-    for (uint64_t i = done + t0; i < n; i += stride) count(in[i]);
+    if (ALL4) {
+        __syncthreads();
+        if (tid < kRadix && acc0) atomicAdd(&hist4[tid], (unsigned long long)acc0);
+        for (int b = tid; b < 3 * kRadix; b += BLOCK) {
+            uint32_t s = 0;
+#pragma unroll
+            for (int w = 0; w < WAVES; ++w) s += s_h[w * 3 * kRadix + b];
+            if (s) atomicAdd(&hist4[kRadix + b], (unsigned long long)s);
+        }
+    }
+}
+
+// K2a: group-local exclusive scan over the kScanGroup tiles of group g, one thread per digit
+// (all 32 loads of a thread in flight at once): tcounts[t][d] becomes the offset of tile t's
+// digit-d keys inside its group; gsum[g][d] = the group's total.
+__global__ __launch_bounds__(kRadix) void k_scan_tiles(uint32_t *__restrict__ tcounts,
+                                                       uint32_t ntiles,
+                                                       unsigned long long *__restrict__ gsum) {
+    const uint32_t g = blockIdx.x, d = threadIdx.x;
+    const uint32_t t0 = g * kScanGroup;
+    uint32_t c[kScanGroup];
+#pragma unroll
+    for (int j = 0; j < kScanGroup; ++j)
+        c[j] = t0 + j < ntiles ? tcounts[(uint64_t)(t0 + j) * kRadix + d] : 0u;
+    uint32_t run = 0;
+#pragma unroll
+    for (int j = 0; j < kScanGroup; ++j) {
+        if (t0 + j < ntiles) tcounts[(uint64_t)(t0 + j) * kRadix + d] = run;
+        run += c[j];
+    }
+    gsum[(uint64_t)g * kRadix + d] = run;
+}
+
+// K2b: one workgroup per digit: exclusive scan of gsum[.][d] over the groups (in place) and
+// totals[d] = the pass's count of digit d.
+__global__ __launch_bounds__(1024) void k_scan_groups(unsigned long long *__restrict__ gsum,
+                                                      uint32_t ngroups,
+                                                      unsigned long long *__restrict__ totals) {
+    __shared__ unsigned long long s_w[16];
+    const uint32_t d = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint32_t per = (ngroups + 1023) / 1024;
+    const uint32_t g0 = tid * per;
+    unsigned long long sum = 0;
+    for (uint32_t j = 0; j < per; ++j)
+        if (g0 + j < ngroups) sum += gsum[(uint64_t)(g0 + j) * kRadix + d];
+    unsigned long long v = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned long long t = __shfl_up(v, o);
+        if (lane >= o) v += t;
+    }
+    if (lane == 63) s_w[w] = v;
     __syncthreads();
-    for (int b = threadIdx.x; b < 4 * kRadix; b += BLOCK) {
-        uint32_t s = 0;
-#pragma unroll
-        for (int w = 0; w < WAVES; ++w) s += sh[w * 4 * kRadix + b];
-        if (s) atomicAdd(&hist[b], (unsigned long long)s);
+    unsigned long long run = v - sum;
+    for (uint32_t ww = 0; ww < w; ++ww) run += s_w[ww];
+    if (tid == 1023) {
+        unsigned long long tot = 0;
+        for (int ww = 0; ww < 16; ++ww) tot += s_w[ww];
+        totals[d] = tot;
     }
+    for (uint32_t j = 0; j < per; ++j)
+        if (g0 + j < ngroups) {
+            const unsigned long long c = gsum[(uint64_t)(g0 + j) * kRadix + d];
+            gsum[(uint64_t)(g0 + j) * kRadix + d] = run;
+            run += c;
+        }
+}
+
+// K2c: bases[d] = exclusive scan of the digit totals (where digit d starts in the output).
+__global__ __launch_bounds__(kRadix) void k_scan_digits(const unsigned long long *__restrict__ totals,
+                                                        unsigned long long *__restrict__ bases) {
+    __shared__ unsigned long long s_w[kRadix / 64];
+    const int d = threadIdx.x, lane = d & 63, w = d >> 6;
+    const unsigned long long tot = totals[d];
+    unsigned long long v = tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned long long t = __shfl_up(v, o);
+        if (lane >= o) v += t;
+    }
+    if (lane == 63) s_w[w] = v;
+    __syncthreads();
+    unsigned long long run = v - tot;
+    for (int ww = 0; ww < w; ++ww) run += s_w[ww];
+    bases[d] = run;
+}
+
+// XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md,
+// dispatch), so workgroup b runs on XCD b % 8.  Giving each XCD a contiguous range of tiles
+// keeps the partial 128-B lines shared by neighbouring tiles' digit runs in one L2, where they
+// merge before write-back.  Bijective for any tile count; speed only, never correctness.
+__device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t ntiles) {
+    const uint32_t q = ntiles >> 3, r = ntiles & 7, x = b & 7, i = b >> 3;
+    return x < r ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
 }
 
 // ---------------------------------------------------------------------------------------
-// Decoupled lookback for digit d of `tile` (one thread): W predecessor status words are in
-// flight per round trip (MI355X cross-XCD sc1 loads cost ~1 us under load, so a one-word walk
-// over the tiles still in flight was the pass's bottleneck).  Sums AGGREGATEs back to the
-// first INCLUSIVE; on a not-yet-published word it sleeps and re-polls from there.  Bounded:
-// gives up (sets *err) instead of hanging.
-// ---------------------------------------------------------------------------------------
-#ifdef GSORT_KBENCH_STAMPS
-// Diagnostic build only (tools/kbench.hip defines the macro; the product never does): per-tile
-// phase timestamps (s_memrealtime, 100 MHz) and digit-0 lookback round trips / spins.
-__device__ unsigned long long *g_stamps;
-#define GSORT_STAMP(slot) \
-    if (threadIdx.x == 0) g_stamps[(uint64_t)tile * 8 + (slot)] = __builtin_amdgcn_s_memrealtime()
-#else
-#define GSORT_STAMP(slot)
-#endif
-// rounds / spins report the round trips and not-ready re-polls (diagnostics; dead otherwise)
-template <int W>
-__device__ __forceinline__ uint64_t lookback(const unsigned long long *status, uint32_t tile,
-                                             int d, uint32_t epoch, uint32_t *err,
-                                             uint32_t &rounds, uint32_t &spins_out) {
-    uint64_t prefix = 0;
-    int64_t t = (int64_t)tile - 1;  // nearest predecessor not yet consumed
-    uint32_t spins = 0;
-    while (t >= 0) {
-        uint64_t wv[W];
-#pragma unroll
-        for (int j = 0; j < W; ++j)
-            wv[j] = (t - j >= 0) ? ld_agent(status + (uint64_t)(t - j) * kRadix + d)
-                                 : pack_status(epoch, kFlagInc, 0);
-        int consumed = 0;
-        bool stop = false, fin = false;
-#pragma unroll
-        for (int j = 0; j < W; ++j) {
-            if (!stop) {
-                const uint32_t ep = (uint32_t)(wv[j] >> 48);
-                const uint64_t fl = (wv[j] >> 46) & 3u;
-                if (ep != epoch || fl == 0) {
-                    stop = true;
-                } else {
-                    prefix += wv[j] & kCountMask;
-                    ++consumed;
-                    if (fl == kFlagInc) stop = fin = true;
-                }
-            }
-        }
-        ++rounds;
-        if (fin) break;
-        t -= consumed;
-        if (consumed < W) {
-            if (++spins > (1u << 22)) {
-                atomicOr(err, 1u);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-    }
-    spins_out = spins;
-    return prefix;
-}
-
-// ---------------------------------------------------------------------------------------
-// K3: one stable onesweep LSD pass.
+// K3: rank + stable scatter of one tile (no inter-workgroup communication).
 //   tile = BLOCK * ITEMS keys; wave w owns keys [w*64*ITEMS, (w+1)*64*ITEMS) of the tile,
 //   round i of the wave holds keys i*64 + lane, so (round, lane) order == memory order.
 //   1. rank: for each round, 8 ballots give each lane the mask of lanes sharing its digit
 //      (per bit: v_bfe_i32, v_cmp, two v_bitop3); rank = (wave's running count of the digit)
 //      + (#peers below the lane); every peer writes the same advanced count (branch-free).
-//   2. per-digit tile counts -> publish AGGREGATE; block-exclusive digit starts folded into
-//      the per-wave offset table.
-//   3. scatter keys into LDS in block-sorted order (stable); meanwhile one thread per digit
-//      runs the decoupled lookback over previous tiles' status words -> global offsets.
+//   2. block-exclusive digit starts + per-wave counts -> per-wave tile offsets.
+//   3. scatter keys into LDS in block-sorted order (stable); the tile's global destination
+//      per digit = digit base (K2c) + group prefix (K2b) + in-group tile offset (K2a), loaded
+//      at kernel start.  Tiles are assigned to workgroups XCD-contiguously (xcd_tile).
 //   4. stream LDS out in order: consecutive lanes hit consecutive addresses within a digit.
-// Tile ids come from an atomic counter, so every tile a lookback waits on is already running.
-// LB_EARLY runs the lookback right after publishing the aggregate (so this tile's inclusive
-// prefix is published as early as possible) instead of after the LDS scatter.
-// NO_LOOKBACK is an ablation switch for timing-only builds (tools/kbench.hip): it skips the
-// lookback wait (prefix = 0, wrong output) and is never set in the product.
 // ---------------------------------------------------------------------------------------
-template <int BLOCK, int ITEMS, bool FIN, bool FOUT, bool NO_LOOKBACK = false,
-          bool LB_EARLY = true, int LB_W = 8>
-__global__ __launch_bounds__(BLOCK) void k_onesweep(const uint32_t *__restrict__ in,
-                                                    uint32_t *__restrict__ out, uint64_t n,
-                                                    int shift,
-                                                    const unsigned long long *__restrict__ base,
-                                                    unsigned long long *status,
-                                                    uint32_t *tile_ctr, uint32_t *err,
-                                                    uint32_t epoch) {
+template <int BLOCK, int ITEMS, bool FIN, bool FOUT>
+__global__ __launch_bounds__(BLOCK) void k_scatter(const uint32_t *__restrict__ in,
+                                                   uint32_t *__restrict__ out, uint64_t n,
+                                                   int shift,
+                                                   const uint32_t *__restrict__ toff,
+                                                   const unsigned long long *__restrict__ gpfx,
+                                                   const unsigned long long *__restrict__ bases) {
     constexpr int WAVES = BLOCK / 64;
     constexpr int TILE = BLOCK * ITEMS;
-    static_assert(BLOCK >= kRadix, "one thread per digit in the scan/lookback");
+    static_assert(TILE == kSweepTile, "K1/K2 count tiles of kSweepTile keys");
+    static_assert(BLOCK >= kRadix, "one thread per digit in the scan");
     static_assert(TILE <= 65536, "ranks are packed as 16 bits");
     __shared__ uint32_t s_keys[TILE];
     __shared__ uint32_t s_wofs[WAVES * kRadix];  // per-wave counts, then per-wave tile offsets
     __shared__ uint32_t *s_dst[kRadix];          // out + global offset - tile start, by digit
     __shared__ uint32_t s_wsum[kRadix / 64];
-    __shared__ uint32_t s_tile;
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int w = tid >> 6;
-    if (tid == 0) s_tile = atomicAdd(tile_ctr, 1u);
-    for (int i = tid; i < WAVES * kRadix; i += BLOCK) s_wofs[i] = 0;
-    __syncthreads();
-    const uint32_t tile = s_tile;
+    const uint32_t tile = xcd_tile(blockIdx.x, gridDim.x);
     const uint64_t tbase = (uint64_t)tile * TILE;
     const bool full = tbase + TILE <= n;
-    GSORT_STAMP(0);
+    for (int i = tid; i < WAVES * kRadix; i += BLOCK) s_wofs[i] = 0;
+    // this tile's global base per digit, fetched early (latency hidden behind the ranking)
+    uint32_t *dst_base = nullptr;
+    if (tid < kRadix)
+        dst_base = out + bases[tid] + gpfx[(uint64_t)(tile / kScanGroup) * kRadix + tid] +
+                   toff[(uint64_t)tile * kRadix + tid];
 
     uint32_t k[ITEMS];
     {
@@ -227,6 +261,7 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(const uint32_t *__restrict__
             }
         }
     }
+    __syncthreads();
 
     // 1. wave-level stable ranking
     uint32_t rk[(ITEMS + 1) / 2];  // two 16-bit ranks per register
@@ -253,25 +288,12 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(const uint32_t *__restrict__
         if (i & 1) rk[i >> 1] |= r << 16; else rk[i >> 1] = r;
     }
     __syncthreads();
-    GSORT_STAMP(1);
 
-    // 2. per-digit tile counts; publish the aggregate; (early) lookback; digit starts
-    uint32_t tcount = 0, excl = 0, lb_rounds = 0, lb_spins = 0;
-    uint64_t prefix = 0;
-    uint32_t c[WAVES];
+    // 2. per-wave tile offsets = block-exclusive digit start + counts of earlier waves
+    uint32_t tcount = 0, excl = 0;
     if (tid < kRadix) {
 #pragma unroll
-        for (int ww = 0; ww < WAVES; ++ww) {
-            c[ww] = s_wofs[ww * kRadix + tid];
-            tcount += c[ww];
-        }
-        st_agent(status + (uint64_t)tile * kRadix + tid,
-                 pack_status(epoch, tile == 0 ? kFlagInc : kFlagAgg, tcount));
-        if (LB_EARLY && tile > 0 && !NO_LOOKBACK) {
-            prefix = lookback<LB_W>(status, tile, tid, epoch, err, lb_rounds, lb_spins);
-            st_agent(status + (uint64_t)tile * kRadix + tid,
-                     pack_status(epoch, kFlagInc, prefix + tcount));
-        }
+        for (int ww = 0; ww < WAVES; ++ww) tcount += s_wofs[ww * kRadix + tid];
         uint32_t v = tcount;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
@@ -282,46 +304,28 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(const uint32_t *__restrict__
         excl = v - tcount;
     }
     __syncthreads();
-    uint32_t start = 0;
     if (tid < kRadix) {
-        start = excl;
+        uint32_t start = excl;
         for (int ww = 0; ww < w; ++ww) start += s_wsum[ww];
+        s_dst[tid] = dst_base - start;
         uint32_t off = start;
 #pragma unroll
         for (int ww = 0; ww < WAVES; ++ww) {
+            const uint32_t cw = s_wofs[ww * kRadix + tid];
             s_wofs[ww * kRadix + tid] = off;
-            off += c[ww];
+            off += cw;
         }
     }
     __syncthreads();
 
-    // 3a. stable scatter into LDS (block-sorted order)
+    // 3. stable scatter into LDS (block-sorted order)
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
         const uint32_t d = (k[i] >> shift) & 255u;
         const uint32_t r = (i & 1) ? (rk[i >> 1] >> 16) : (rk[i >> 1] & 0xFFFFu);
         s_keys[wc[d] + r] = k[i];
     }
-    // 3b. (late) lookback, one thread per digit; global destination base per digit
-    if (tid < kRadix) {
-        if (!LB_EARLY && tile > 0 && !NO_LOOKBACK) {
-            prefix = lookback<LB_W>(status, tile, tid, epoch, err, lb_rounds, lb_spins);
-            st_agent(status + (uint64_t)tile * kRadix + tid,
-                     pack_status(epoch, kFlagInc, prefix + tcount));
-        }
-        s_dst[tid] = out + (base[tid] + prefix) - start;
-    }
     __syncthreads();
-    GSORT_STAMP(2);
-#ifdef GSORT_KBENCH_STAMPS
-    if (tid == 0) {
-        g_stamps[(uint64_t)tile * 8 + 4] = lb_rounds;
-        g_stamps[(uint64_t)tile * 8 + 5] = lb_spins;
-        uint32_t hw;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(hw));
-        g_stamps[(uint64_t)tile * 8 + 6] = hw & 0xF;
-    }
-#endif
 
     // 4. ordered write-out
     const uint32_t lim = full ? (uint32_t)TILE : (uint32_t)(n - tbase);
@@ -333,7 +337,6 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(const uint32_t *__restrict__
             s_dst[(key >> shift) & 255u][j] = FOUT ? (key ^ kFlip) : key;
         }
     }
-    GSORT_STAMP(3);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -485,35 +488,55 @@ hipError_t launch_generate(int dist, uint64_t seed, uint64_t start, uint64_t n, 
     return hipGetLastError();
 }
 
-hipError_t launch_hist4(const uint32_t *in, uint64_t n, uint64_t *hist, hipStream_t s) {
+hipError_t launch_tile_counts(const uint32_t *in, uint64_t n, int shift, bool flip,
+                              uint32_t *tcounts, uint64_t *hist4, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    constexpr int B = 512;
-    const unsigned g = grid_for(n / 16 + 1, B, 1024);
-    auto *h = reinterpret_cast<unsigned long long *>(hist);
-    if ((reinterpret_cast<uintptr_t>(in) & 15) == 0)
-        k_hist4<B, true><<<g, B, 0, s>>>(in, n, h);
-    else
-        k_hist4<B, false><<<g, B, 0, s>>>(in, n, h);
+    constexpr int B = 256;
+    const uint32_t ntiles = (uint32_t)sweep_tiles(n);
+    const unsigned g = ntiles < 2048 ? ntiles : 2048;
+    const uint32_t fl = flip ? kFlip : 0u;
+    auto *h = reinterpret_cast<unsigned long long *>(hist4);
+    const bool vec = (reinterpret_cast<uintptr_t>(in) & 15) == 0;
+    if (hist4) {
+        if (shift != 0) return hipErrorInvalidValue;  // ALL4 counts tiles by digit 0
+        if (vec) k_tile_counts<B, true, true><<<g, B, 0, s>>>(in, n, 0, fl, tcounts, h, ntiles);
+        else k_tile_counts<B, true, false><<<g, B, 0, s>>>(in, n, 0, fl, tcounts, h, ntiles);
+    } else {
+        if (vec) k_tile_counts<B, false, true><<<g, B, 0, s>>>(in, n, shift, fl, tcounts, h, ntiles);
+        else k_tile_counts<B, false, false><<<g, B, 0, s>>>(in, n, shift, fl, tcounts, h, ntiles);
+    }
     return hipGetLastError();
 }
 
-hipError_t launch_onesweep(const uint32_t *in, uint32_t *out, uint64_t n, int shift,
-                           const uint64_t *base, uint64_t *status, uint32_t *tile_ctr,
-                           uint32_t *err, uint32_t epoch, bool flip_in, bool flip_out,
-                           hipStream_t s) {
+hipError_t launch_scan_tiles(uint32_t *tcounts, uint64_t n, uint64_t *gsum, uint64_t *totals,
+                             uint64_t *bases, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const uint32_t ntiles = (uint32_t)sweep_tiles(n);
+    const uint32_t ng = (uint32_t)scan_groups(n);
+    auto *gs = reinterpret_cast<unsigned long long *>(gsum);
+    auto *tot = reinterpret_cast<unsigned long long *>(totals);
+    k_scan_tiles<<<ng, kRadix, 0, s>>>(tcounts, ntiles, gs);
+    k_scan_groups<<<kRadix, 1024, 0, s>>>(gs, ng, tot);
+    k_scan_digits<<<1, kRadix, 0, s>>>(tot, reinterpret_cast<unsigned long long *>(bases));
+    return hipGetLastError();
+}
+
+hipError_t launch_scatter(const uint32_t *in, uint32_t *out, uint64_t n, int shift,
+                          const uint32_t *toff, const uint64_t *gpfx, const uint64_t *bases,
+                          bool flip_in, bool flip_out, hipStream_t s) {
     if (n == 0) return hipSuccess;
     const unsigned g = (unsigned)sweep_tiles(n);
-    auto *b = reinterpret_cast<const unsigned long long *>(base);
-    auto *st = reinterpret_cast<unsigned long long *>(status);
+    auto *gp = reinterpret_cast<const unsigned long long *>(gpfx);
+    auto *bs = reinterpret_cast<const unsigned long long *>(bases);
     constexpr int B = kSweepBlock, I = kSweepItems;
     if (flip_in && flip_out)
-        k_onesweep<B, I, true, true><<<g, B, 0, s>>>(in, out, n, shift, b, st, tile_ctr, err, epoch);
+        k_scatter<B, I, true, true><<<g, B, 0, s>>>(in, out, n, shift, toff, gp, bs);
     else if (flip_in)
-        k_onesweep<B, I, true, false><<<g, B, 0, s>>>(in, out, n, shift, b, st, tile_ctr, err, epoch);
+        k_scatter<B, I, true, false><<<g, B, 0, s>>>(in, out, n, shift, toff, gp, bs);
     else if (flip_out)
-        k_onesweep<B, I, false, true><<<g, B, 0, s>>>(in, out, n, shift, b, st, tile_ctr, err, epoch);
+        k_scatter<B, I, false, true><<<g, B, 0, s>>>(in, out, n, shift, toff, gp, bs);
     else
-        k_onesweep<B, I, false, false><<<g, B, 0, s>>>(in, out, n, shift, b, st, tile_ctr, err, epoch);
+        k_scatter<B, I, false, false><<<g, B, 0, s>>>(in, out, n, shift, toff, gp, bs);
     return hipGetLastError();
 }
 

@@ -26,11 +26,10 @@ struct gsort_group {
 namespace {
 
 enum Slot { S_TMP, S_OUT, S_CUR, S_SORTED, S_RECV, S_IN, S_STAGE, S_NSLOTS };
-enum Phase { PH_HIST, PH_PASS0, PH_PASS1, PH_PASS2, PH_PASS3, PH_EXCH, PH_PLACE, PH_SAMPLE,
+enum Phase { PH_COUNT, PH_PASS0, PH_PASS1, PH_PASS2, PH_PASS3, PH_EXCH, PH_PLACE, PH_SAMPLE,
              PH_MERGE, PH_TOTAL, PH_N };
 
 constexpr size_t kSmallBytes = 256 * 1024;  // device + pinned scratch for counts, plans
-constexpr int kMaxCounters = 64;           // tile counters per call
 
 struct DevBuf {
     void *p = nullptr;
@@ -45,11 +44,10 @@ struct gsort_ctx {
     Comm *comm = nullptr;
     std::string err;
     DevBuf slot[S_NSLOTS];
-    DevBuf status;
-    uint32_t epoch = 1;
-    int next_counter = 0;
-    // device small area: [0, 8K) hist4 (4x256 u64) | [8K, 16K) bases (4x256 u64) |
-    // [16K, 18K) next-digit hist | [18K, 18K+256) tile counters | [20K, 256K) plans/samples
+    DevBuf tcounts;  // K1/K2: per-tile digit counts -> in-group offsets (u32 [tiles][256])
+    DevBuf gsum;     // K2: per-group digit prefixes (u64 [groups][256])
+    // device small area: [0, 8K) hist4 (4x256 u64) | [8K, 10K) pass digit totals (256 u64) |
+    // [10K, 12K) pass digit bases (256 u64) | [20K, 256K) plans / samples / routing tables
     char *d_small = nullptr;
     char *h_small = nullptr;  // pinned mirror
     std::vector<int32_t> splitters;
@@ -64,8 +62,7 @@ struct gsort_ctx {
 
 namespace {
 
-constexpr size_t OFF_HIST = 0, OFF_BASE = 8192, OFF_NHIST = 16384, OFF_CTR = 18432,
-                 OFF_PLAN = 20480;
+constexpr size_t OFF_HIST = 0, OFF_TOT = 8192, OFF_BASES = 10240, OFF_PLAN = 20480;
 
 gsort_status set_err(gsort_ctx *c, gsort_status st, const std::string &msg) {
     if (c) c->err = msg;
@@ -142,7 +139,7 @@ void timing_finish(gsort_ctx *c, gsort_stats *st) {
         float ms = 0.f;
         if (hipEventElapsedTime(&ms, sp.a, sp.b) != hipSuccess) continue;
         switch (sp.phase) {
-            case PH_HIST: st->ms_hist += ms; st->ms_local_sort += ms; break;
+            case PH_COUNT: st->ms_hist += ms; st->ms_local_sort += ms; break;
             case PH_PASS0: case PH_PASS1: case PH_PASS2: case PH_PASS3:
                 st->ms_pass[sp.phase - PH_PASS0] += ms; st->ms_local_sort += ms; break;
             case PH_EXCH: st->ms_exchange += ms; break;
@@ -155,92 +152,74 @@ void timing_finish(gsort_ctx *c, gsort_stats *st) {
     c->timing = false;
 }
 
-// ---- onesweep pass with status/epoch bookkeeping ----------------------------------------
-gsort_status ensure_status(gsort_ctx *c, uint64_t n) {
-    const size_t need = (size_t)std::max<uint64_t>(sweep_tiles(n), 1) * kRadix * 8;
-    if (need > c->status.cap) {
-        ST_TRY(ensure(c, c->status, need));
-        HIP_TRY(c, hipMemsetAsync(c->status.p, 0, c->status.cap, c->stream));
-        c->epoch = 1;
-    }
+gsort_status ensure_pass_scratch(gsort_ctx *c, uint64_t n) {
+    ST_TRY(ensure(c, c->tcounts, (size_t)std::max<uint64_t>(sweep_tiles(n), 1) * kRadix * 4));
+    ST_TRY(ensure(c, c->gsum, (size_t)std::max<uint64_t>(scan_groups(n), 1) * kRadix * 8));
     return GSORT_OK;
 }
 
-gsort_status run_pass(gsort_ctx *c, const uint32_t *src, uint32_t *dst, uint64_t n, int digit,
-                      const uint64_t *d_base, bool flip_in, bool flip_out) {
-    if (c->next_counter >= kMaxCounters) return set_err(c, GSORT_EINVAL, "too many passes");
-    if (c->epoch >= 0xFFFF) {  // epochs tag the status words; re-zero once per 65k passes
-        HIP_TRY(c, hipMemsetAsync(c->status.p, 0, c->status.cap, c->stream));
-        c->epoch = 1;
-    }
-    uint32_t *ctrs = reinterpret_cast<uint32_t *>(c->d_small + OFF_CTR);
+uint32_t *d_tcounts(gsort_ctx *c) { return reinterpret_cast<uint32_t *>(c->tcounts.p); }
+uint64_t *d_gsum(gsort_ctx *c) { return reinterpret_cast<uint64_t *>(c->gsum.p); }
+
+// K1 (digit counts per tile) for digit p of src; skipped when the caller already has them.
+gsort_status count_tiles(gsort_ctx *c, const uint32_t *src, uint64_t n, int digit, bool flip) {
     hipEvent_t t = tic(c);
-    HIP_TRY(c, launch_onesweep(src, dst, n, 8 * digit, d_base,
-                               reinterpret_cast<uint64_t *>(c->status.p),
-                               ctrs + c->next_counter++, ctrs + kMaxCounters, c->epoch++,
-                               flip_in, flip_out, c->stream));
+    HIP_TRY(c, launch_tile_counts(src, n, 8 * digit, flip, d_tcounts(c), nullptr, c->stream));
+    toc(c, PH_COUNT, t);
+    return GSORT_OK;
+}
+
+// K2 + K3: one stable LSD pass src -> dst over `digit`, tile counts already in tcounts.
+// The pass's 256 digit counts are left in the small area at OFF_TOT (used for routing).
+gsort_status scan_and_scatter(gsort_ctx *c, const uint32_t *src, uint32_t *dst, uint64_t n,
+                              int digit, bool flip_in, bool flip_out) {
+    uint64_t *totals = reinterpret_cast<uint64_t *>(c->d_small + OFF_TOT);
+    uint64_t *bases = reinterpret_cast<uint64_t *>(c->d_small + OFF_BASES);
+    hipEvent_t t = tic(c);
+    HIP_TRY(c, launch_scan_tiles(d_tcounts(c), n, d_gsum(c), totals, bases, c->stream));
+    toc(c, PH_COUNT, t);
+    t = tic(c);
+    HIP_TRY(c, launch_scatter(src, dst, n, 8 * digit, d_tcounts(c), d_gsum(c), bases, flip_in,
+                              flip_out, c->stream));
     toc(c, PH_PASS0 + digit, t);
     return GSORT_OK;
 }
 
-// Exclusive scan of a 256-bin histogram into the pinned mirror at `hb`.
-void exclusive_256(const uint64_t *h, uint64_t *out) {
-    uint64_t s = 0;
-    for (int d = 0; d < kRadix; ++d) { out[d] = s; s += h[d]; }
-}
-
 gsort_status reset_call(gsort_ctx *c) {
-    c->next_counter = 0;
     HIP_TRY(c, hipSetDevice(c->device));
-    // tile counters + the lookback-timeout word behind them
-    HIP_TRY(c, hipMemsetAsync(c->d_small + OFF_CTR, 0, (kMaxCounters + 1) * 4, c->stream));
     return GSORT_OK;
 }
 
-// After the stream is synchronised: did any onesweep lookback give up?
-gsort_status check_kernel_err(gsort_ctx *c) {
-    uint32_t *h = reinterpret_cast<uint32_t *>(c->h_small + OFF_CTR);
-    HIP_TRY(c, hipMemcpyAsync(h, c->d_small + OFF_CTR + kMaxCounters * 4, 4,
-                              hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
-    if (*h) return set_err(c, GSORT_EHIP, "onesweep decoupled lookback timed out");
-    return GSORT_OK;
-}
-
-// ---- local sort: K1 + up to four K3 passes (in -> out, tmp as ping-pong) -----------------
+// ---- local sort: K1 (+ all four histograms) then per non-trivial digit K1/K2/K3 ---------
 // Reference: the per-key digit loop mpi_radix_sort.c:144-147 (there: base P, all passes
 // through rank 0) and the local qsort mpi_sample_sort.c:85 / :174.
 gsort_status local_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *out,
                         uint32_t *tmp, int *passes_run) {
     if (passes_run) *passes_run = 0;
     if (n == 0) return GSORT_OK;
-    ST_TRY(ensure_status(c, n));
+    ST_TRY(ensure_pass_scratch(c, n));
     uint64_t *d_hist = reinterpret_cast<uint64_t *>(c->d_small + OFF_HIST);
-    uint64_t *d_base = reinterpret_cast<uint64_t *>(c->d_small + OFF_BASE);
     uint64_t *h_hist = reinterpret_cast<uint64_t *>(c->h_small + OFF_HIST);
-    uint64_t *h_base = reinterpret_cast<uint64_t *>(c->h_small + OFF_BASE);
     HIP_TRY(c, hipMemsetAsync(d_hist, 0, 4 * kRadix * 8, c->stream));
     hipEvent_t t = tic(c);
-    HIP_TRY(c, launch_hist4(in, n, d_hist, c->stream));
-    toc(c, PH_HIST, t);
+    HIP_TRY(c, launch_tile_counts(in, n, 0, true, d_tcounts(c), d_hist, c->stream));
+    toc(c, PH_COUNT, t);
     HIP_TRY(c, hipMemcpyAsync(h_hist, d_hist, 4 * kRadix * 8, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     int active[4], k = 0;
     for (int p = 0; p < 4; ++p) {
         const uint64_t *h = h_hist + p * kRadix;
         if (*std::max_element(h, h + kRadix) < n) active[k++] = p;  // skip trivial digits
-        exclusive_256(h, h_base + p * kRadix);
     }
     if (k == 0) {
         HIP_TRY(c, launch_copy(in, out, n, c->stream));
         return GSORT_OK;
     }
-    HIP_TRY(c, hipMemcpyAsync(d_base, h_base, 4 * kRadix * 8, hipMemcpyHostToDevice, c->stream));
     const uint32_t *src = in;
     for (int i = 0; i < k; ++i) {
         uint32_t *dst = ((k - 1 - i) % 2 == 0) ? out : tmp;
-        ST_TRY(run_pass(c, src, dst, n, active[i], d_base + active[i] * kRadix, i == 0,
-                        i == k - 1));
+        if (!(i == 0 && active[0] == 0)) ST_TRY(count_tiles(c, src, n, active[i], i == 0));
+        ST_TRY(scan_and_scatter(c, src, dst, n, active[i], i == 0, i == k - 1));
         src = dst;
     }
     if (passes_run) *passes_run = k;
@@ -269,11 +248,11 @@ void block_of(uint64_t N, int P, int r, uint64_t *B, uint64_t *len) {
 }
 
 // ---- distributed LSD radix (P > 1) ------------------------------------------------------
-// Per non-trivial digit: local onesweep pass (stable by digit), all-gather per-rank digit
-// counts, route contiguous slices to the ranks owning their global positions (grouped
-// send/recv), then place received runs (K8) and histogram the next digit in the same sweep.
-// Keeps the reference's invariant that rank q holds positions [qB, (q+1)B) after each pass
-// (mpi_radix_sort.c:139,:192) without moving any key through rank 0.
+// Per non-trivial digit: local K1/K2 (tile counts; the digit totals of this rank), all-gather
+// of the P x 256 per-rank digit counts, local K3 (stable by digit), route contiguous slices to
+// the ranks owning their global positions (one grouped send/recv round), then place the
+// received runs (K8).  Keeps the reference's invariant that rank q holds positions
+// [qB, (q+1)B) after each pass (mpi_radix_sort.c:139,:192) without moving keys through rank 0.
 gsort_status radix_dist(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in, int32_t **d_out,
                         uint64_t *n_out, gsort_stats *stats) {
     const int P = c->nranks, me = c->rank;
@@ -285,19 +264,19 @@ gsort_status radix_dist(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in, int3
     block_of(N, P, me, &B, &mine);
     const uint64_t cap = std::max<uint64_t>(std::max(n_in, B), 1);
     for (Slot s : {S_CUR, S_SORTED, S_RECV, S_OUT}) ST_TRY(ensure(c, c->slot[s], cap * 4));
-    ST_TRY(ensure_status(c, cap));
+    ST_TRY(ensure_pass_scratch(c, cap));
     if (N == 0) { *d_out = slot_ptr<int32_t>(c, S_OUT); *n_out = 0; return GSORT_OK; }
 
-    // K1 on the input: all four digit histograms; all-gathered they give the global digit
-    // totals (invariant under the exchange), so every rank skips the same trivial digits.
+    // K1 on the input: tile counts of digit 0 + all four digit histograms; all-gathered they
+    // give the global digit totals (invariant under the exchange), so every rank skips the
+    // same trivial digits.
     uint64_t *d_hist = reinterpret_cast<uint64_t *>(c->d_small + OFF_HIST);
-    uint64_t *d_base = reinterpret_cast<uint64_t *>(c->d_small + OFF_BASE);
-    uint64_t *d_nhist = reinterpret_cast<uint64_t *>(c->d_small + OFF_NHIST);
-    uint64_t *h_base = reinterpret_cast<uint64_t *>(c->h_small + OFF_BASE);
+    uint64_t *d_tot = reinterpret_cast<uint64_t *>(c->d_small + OFF_TOT);
     HIP_TRY(c, hipMemsetAsync(d_hist, 0, 4 * kRadix * 8, c->stream));
     hipEvent_t t = tic(c);
-    HIP_TRY(c, launch_hist4(reinterpret_cast<const uint32_t *>(d_keys), n_in, d_hist, c->stream));
-    toc(c, PH_HIST, t);
+    HIP_TRY(c, launch_tile_counts(reinterpret_cast<const uint32_t *>(d_keys), n_in, 0, true,
+                                  d_tcounts(c), d_hist, c->stream));
+    toc(c, PH_COUNT, t);
     DevBuf &allh = c->slot[S_STAGE];
     ST_TRY(ensure(c, allh, (size_t)P * 4 * kRadix * 8));
     ST_TRY(comm_try(c, c->comm->allgather(d_hist, allh.p, 4 * kRadix * 8, c->stream)));
@@ -325,21 +304,16 @@ gsort_status radix_dist(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in, int3
     for (int i = 0; i < k; ++i) {
         const int p = active[i];
         const bool first = i == 0, last = i == k - 1;
-        // per-rank counts of digit p for the current distribution
-        if (first) {
-            for (int r = 0; r < P; ++r)
-                memcpy(&hp[(size_t)r * kRadix], &H[((size_t)r * 4 + p) * kRadix], kRadix * 8);
-        } else {
-            uint64_t *d_allnh = reinterpret_cast<uint64_t *>(allh.p);
-            ST_TRY(comm_try(c, c->comm->allgather(d_nhist, d_allnh, kRadix * 8, c->stream)));
-            HIP_TRY(c, hipMemcpyAsync(hp.data(), d_allnh, hp.size() * 8, hipMemcpyDeviceToHost,
-                                      c->stream));
-            HIP_TRY(c, hipStreamSynchronize(c->stream));
-        }
-        exclusive_256(&hp[(size_t)me * kRadix], h_base);
-        HIP_TRY(c, hipMemcpyAsync(d_base, h_base, kRadix * 8, hipMemcpyHostToDevice, c->stream));
+        // this rank's tile counts and totals of digit p, then everyone's totals
+        if (!(first && p == 0)) ST_TRY(count_tiles(c, src, n_src, p, first));
         uint32_t *sorted = slot_ptr<uint32_t>(c, S_SORTED);
-        ST_TRY(run_pass(c, src, sorted, n_src, p, d_base, first, false));
+        ST_TRY(scan_and_scatter(c, src, sorted, n_src, p, first, false));
+        if (n_src == 0) HIP_TRY(c, hipMemsetAsync(d_tot, 0, kRadix * 8, c->stream));
+        uint64_t *d_allt = reinterpret_cast<uint64_t *>(allh.p);
+        ST_TRY(comm_try(c, c->comm->allgather(d_tot, d_allt, kRadix * 8, c->stream)));
+        HIP_TRY(c, hipMemcpyAsync(hp.data(), d_allt, hp.size() * 8, hipMemcpyDeviceToHost,
+                                  c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
 
         size_t nseg = 0;
         ST_TRY(gsort_plan_radix_route(P, hp.data(), B, me, send.data(), recv.data(), seg.data(),
@@ -372,10 +346,8 @@ gsort_status radix_dist(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in, int3
         }
         HIP_TRY(c, hipMemcpyAsync(d_seg, h_seg, nseg * 24, hipMemcpyHostToDevice, c->stream));
         uint32_t *dst = last ? slot_ptr<uint32_t>(c, S_OUT) : placed[i & 1];
-        if (!last) HIP_TRY(c, hipMemsetAsync(d_nhist, 0, kRadix * 8, c->stream));
         t = tic(c);
-        HIP_TRY(c, launch_place(rbuf, dst, d_seg, (int)nseg, mine, last ? nullptr : d_nhist,
-                                last ? 0 : 8 * active[i + 1], last, c->stream));
+        HIP_TRY(c, launch_place(rbuf, dst, d_seg, (int)nseg, mine, nullptr, 0, last, c->stream));
         toc(c, PH_PLACE, t);
         src = dst;
         n_src = mine;
@@ -599,7 +571,8 @@ gsort_status gsort_destroy(gsort_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     delete c->comm;
     for (auto &b : c->slot) if (b.p) (void)hipFree(b.p);
-    if (c->status.p) (void)hipFree(c->status.p);
+    if (c->tcounts.p) (void)hipFree(c->tcounts.p);
+    if (c->gsum.p) (void)hipFree(c->gsum.p);
     if (c->d_small) (void)hipFree(c->d_small);
     if (c->h_small) (void)hipHostFree(c->h_small);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
@@ -615,7 +588,7 @@ gsort_status gsort_reserve(gsort_ctx *c, size_t n) {
     for (Slot s : {S_TMP, S_OUT}) ST_TRY(ensure(c, c->slot[s], cap));
     if (c->nranks > 1)
         for (Slot s : {S_CUR, S_SORTED, S_RECV}) ST_TRY(ensure(c, c->slot[s], cap));
-    ST_TRY(ensure_status(c, n));
+    ST_TRY(ensure_pass_scratch(c, n));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     return GSORT_OK;
 }
@@ -646,7 +619,6 @@ gsort_status gsort_radix(gsort_ctx *c, const int32_t *d_keys, size_t n_local, in
     if (st != GSORT_OK) return st;
     toc(c, PH_TOTAL, t0);
     HIP_TRY(c, hipStreamSynchronize(c->stream));
-    ST_TRY(check_kernel_err(c));
     *n_out = nout;
     if (stats) { stats->keys_local_in = n_local; stats->keys_local_out = nout; }
     timing_finish(c, stats);
@@ -680,7 +652,6 @@ gsort_status gsort_sample(gsort_ctx *c, const int32_t *d_keys, size_t n_local, i
     }
     toc(c, PH_TOTAL, t0);
     HIP_TRY(c, hipStreamSynchronize(c->stream));
-    ST_TRY(check_kernel_err(c));
     *n_out = nout;
     if (stats) { stats->keys_local_in = n_local; stats->keys_local_out = nout; }
     timing_finish(c, stats);
