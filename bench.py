@@ -12,8 +12,8 @@ canonical splitmix64 generator on device (K10), so the data is synthetic and ide
 the oracle and the reference CPU run see.
 
 The timed region is K steps bracketed by a barrier + torch.cuda.synchronize() on both sides;
-the slowest rank's time is reported.  `roofline` prices the dominant kernel (the onesweep pass,
-8 B/key algorithmic traffic) with its average duration measured live by HIP events recorded on
+the slowest rank's time is reported.  `roofline` prices the dominant kernel (K3, the rank +
+scatter of one LSD pass, 8 B/key algorithmic traffic) with its average duration measured live by HIP events recorded on
 libgsort's own stream around every launch; `traffic` is the HBM bytes per launch from the
 rocprofv3 PMC summary in profiles/ (FETCH_SIZE x 2 + WRITE_SIZE, gfx950 correction) when one
 exists for this configuration, else null.  `cpu_baseline` runs the reference radix_sort
@@ -39,7 +39,7 @@ for _p in (ROOT, PKG):
 METRIC = "sorted keys/sec (GKeys/s) at 1/2/4/8 GPUs + % HBM/xGMI roofline"
 HBM_PEAK_GBPS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level table)
 XGMI_LINK_GBPS = 153.0      # one xGMI link, per direction
-PASS_BYTES_PER_KEY = 8      # onesweep pass: read 4 B + write 4 B per key
+PASS_BYTES_PER_KEY = 8      # K3 pass: read 4 B + write 4 B per key
 
 
 def parse():
@@ -99,15 +99,24 @@ def cpu_baseline(dist, seed):
 
 
 def pmc_traffic(algo, n_local, n_gpus):
-    """HBM bytes per onesweep launch from the committed rocprofv3 PMC summary, if it was
-    collected for this exact configuration (tools/profile_pmc.sh writes it)."""
-    path = os.path.join(ROOT, "profiles", "pmc_onesweep.json")
-    try:
-        d = json.load(open(path))
-        if d.get("algo") == algo and d.get("n_local") == n_local and n_gpus == 1:
-            return d.get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
-        pass
+    """HBM bytes per K3 launch (FETCH_SIZE x 2 + WRITE_SIZE, MI355X_MICROARCH.md §HBM) from the
+    newest committed rocprofv3 PMC summary of this exact configuration
+    (mpi-test_amd/tools/profile_pmc.sh -> profiles/*_pmc_summary.json), else None."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json")),
+                       reverse=True):
+        try:
+            d = json.load(open(path))
+            cfg = d["bench"]["config"]
+            if cfg["algo"] != algo or cfg["keys_per_gpu"] != n_local or n_gpus != 1:
+                continue
+            k3 = [v["hbm_bytes"] for k, v in d["kernels"].items()
+                  if k.startswith("k_scatter") and "hbm_bytes" in v]
+            if k3:
+                return {"hbm_bytes_per_launch": round(sum(k3) / len(k3)),
+                        "source": os.path.relpath(path, ROOT)}
+        except (OSError, ValueError, KeyError):
+            continue
     return None
 
 
@@ -186,7 +195,7 @@ def main():
     ms_step = elapsed * 1e3 / a.steps
     value = n_total / (ms_step / 1e3) / 1e9
 
-    # dominant kernel: the onesweep pass (HIP events on libgsort's stream, every launch)
+    # dominant kernel: K3 (HIP events on libgsort's stream, every launch)
     passes = [st["ms_pass"] for st in stats]
     launches = sum(1 for p in passes for x in p if x > 0)
     pass_ms = sum(x for p in passes for x in p) / max(launches, 1)
@@ -195,7 +204,8 @@ def main():
     else:
         keys_per_launch = n_local  # first local sort; the merge re-sort sees ~n_local too
     achieved = keys_per_launch * PASS_BYTES_PER_KEY / (pass_ms * 1e-3) / 1e9
-    traffic = pmc_traffic(a.algo, n_local, world)
+    pmc = pmc_traffic(a.algo, n_local, world)
+    traffic = pmc["hbm_bytes_per_launch"] if pmc else None
     last = stats[-1]
     phases = {k: round(sum(s[k] for s in stats) / len(stats), 4)
               for k in ("ms_total", "ms_hist", "ms_local_sort", "ms_exchange", "ms_place",
@@ -222,11 +232,12 @@ def main():
             "keys_per_gpu": n_local, "total_keys": n_total, "algo": a.algo,
             "parallelism": f"dp{world}", "onesweep_tile": gsort.onesweep_tile(),
         },
-        "roofline": {"bound": "hbm", "kernel": "k_onesweep (one LSD pass)",
+        "roofline": {"bound": "hbm", "kernel": "k_scatter (K3: rank + stable scatter of one LSD pass)",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4),
                      "traffic": traffic,
                      "algorithmic_bytes_per_launch": keys_per_launch * PASS_BYTES_PER_KEY,
+                     "traffic_source": pmc["source"] if pmc else None,
                      "avg_launch_ms": round(pass_ms, 5), "launches_timed": launches},
         "cpu_baseline": cpu,
         "phases_ms_avg": phases,
