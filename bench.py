@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--dist", choices=["uniform", "zipf"], default="uniform")
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--local", choices=["msd", "lsd"], default="msd",
+                    help="local sort algorithm (DESIGN.md 5)")
     return ap.parse_args()
 
 
@@ -98,8 +100,41 @@ def cpu_baseline(dist, seed):
         shutil.rmtree(tmp, ignore_errors=True)
 
 
-def pmc_traffic(algo, n_local, n_gpus):
-    """HBM bytes per K3 launch (FETCH_SIZE x 2 + WRITE_SIZE, MI355X_MICROARCH.md §HBM) from the
+def kernel_rooflines(stats, n_local):
+    """Per kernel class: total device time over the timed steps (HIP events recorded on
+    libgsort's stream around every launch), launches, algorithmic bytes:
+    K3 / K3u read + write every key of the launch (8 B/key), K11 reads and writes every key of
+    its buckets once (8 B/key)."""
+    out = []
+
+    def add(kernel, prefixes, ms_list, keys_list, bpk):
+        launches = sum(1 for m in ms_list if m > 0)
+        tot_ms = sum(ms_list)
+        if not launches or tot_ms <= 0:
+            return
+        tot_bytes = sum(k * bpk for m, k in zip(ms_list, keys_list) if m > 0)
+        out.append({"kernel": kernel, "pmc_prefixes": prefixes, "total_ms": tot_ms,
+                    "launches": launches, "avg_launch_ms": round(tot_ms / launches, 5),
+                    "bytes_per_key": bpk,
+                    "bytes_per_launch": round(tot_bytes / launches),
+                    "achieved": round(tot_bytes / (tot_ms * 1e-3) / 1e9, 1)})
+
+    add("k_scatter (K3: rank + stable scatter of one LSD pass)", ("k_scatter",),
+        [x for s in stats for x in s["ms_pass"]],
+        [n_local for s in stats for x in s["ms_pass"]], PASS_BYTES_PER_KEY)
+    add("k_partition / k_seg_partition (K3u: unstable MSD partition of one level)",
+        ("k_partition", "k_seg_partition"),
+        [x for s in stats for x in s["ms_level"]],
+        [k for s in stats for k in s["keys_level"]], PASS_BYTES_PER_KEY)
+    add("k_local_sort (K11: in-LDS sort of the small buckets)", ("k_local_sort",),
+        [s["ms_bucket_sort"] for s in stats], [s["keys_bucket_sort"] for s in stats],
+        PASS_BYTES_PER_KEY)
+    return out
+
+
+def pmc_traffic(algo, n_local, n_gpus, prefixes=("k_scatter",)):
+    """HBM bytes per launch of the dominant kernel (FETCH_SIZE x 2 + WRITE_SIZE,
+    MI355X_MICROARCH.md §HBM) from the
     newest committed rocprofv3 PMC summary of this exact configuration
     (mpi-test_amd/tools/profile_pmc.sh -> profiles/*_pmc_summary.json), else None."""
     import glob
@@ -111,7 +146,7 @@ def pmc_traffic(algo, n_local, n_gpus):
             if cfg["algo"] != algo or cfg["keys_per_gpu"] != n_local or n_gpus != 1:
                 continue
             k3 = [v["hbm_bytes"] for k, v in d["kernels"].items()
-                  if k.startswith("k_scatter") and "hbm_bytes" in v]
+                  if k.startswith(tuple(prefixes)) and "hbm_bytes" in v]
             if k3:
                 return {"hbm_bytes_per_launch": round(sum(k3) / len(k3)),
                         "source": os.path.relpath(path, ROOT)}
@@ -159,6 +194,7 @@ def main():
     ctx.generate(gsort.UNIFORM if dist_name == "uniform" else gsort.ZIPF, a.seed,
                  rank * n_local, n_local, d_in)
     ctx.reserve(n_local)
+    ctx.set_local_algo(gsort.LOCAL_MSD if a.local == "msd" else gsort.LOCAL_LSD)
     fn = ctx.radix if a.algo == "radix" else ctx.sample
 
     for _ in range(a.warmup):
@@ -195,16 +231,9 @@ def main():
     ms_step = elapsed * 1e3 / a.steps
     value = n_total / (ms_step / 1e3) / 1e9
 
-    # dominant kernel: K3 (HIP events on libgsort's stream, every launch)
-    passes = [st["ms_pass"] for st in stats]
-    launches = sum(1 for p in passes for x in p if x > 0)
-    pass_ms = sum(x for p in passes for x in p) / max(launches, 1)
-    if a.algo == "radix":
-        keys_per_launch = n_local
-    else:
-        keys_per_launch = n_local  # first local sort; the merge re-sort sees ~n_local too
-    achieved = keys_per_launch * PASS_BYTES_PER_KEY / (pass_ms * 1e-3) / 1e9
-    pmc = pmc_traffic(a.algo, n_local, world)
+    rooflines = kernel_rooflines(stats, n_local)
+    dom = max(rooflines, key=lambda r: r["total_ms"])
+    pmc = pmc_traffic(a.algo, n_local, world, dom["pmc_prefixes"])
     traffic = pmc["hbm_bytes_per_launch"] if pmc else None
     last = stats[-1]
     phases = {k: round(sum(s[k] for s in stats) / len(stats), 4)
@@ -212,6 +241,9 @@ def main():
                         "ms_sample", "ms_merge")}
     phases["ms_pass"] = [round(sum(s["ms_pass"][i] for s in stats) / len(stats), 4)
                          for i in range(4)]
+    phases["ms_level"] = [round(sum(s["ms_level"][i] for s in stats) / len(stats), 4)
+                          for i in range(4)]
+    phases["ms_bucket_sort"] = round(sum(s["ms_bucket_sort"] for s in stats) / len(stats), 4)
     line = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -232,16 +264,20 @@ def main():
             "keys_per_gpu": n_local, "total_keys": n_total, "algo": a.algo,
             "parallelism": f"dp{world}", "onesweep_tile": gsort.onesweep_tile(),
         },
-        "roofline": {"bound": "hbm", "kernel": "k_scatter (K3: rank + stable scatter of one LSD pass)",
-                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBPS, 4),
+        "roofline": {"bound": "hbm", "kernel": dom["kernel"],
+                     "achieved": dom["achieved"], "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": round(dom["achieved"] / HBM_PEAK_GBPS, 4),
                      "traffic": traffic,
-                     "algorithmic_bytes_per_launch": keys_per_launch * PASS_BYTES_PER_KEY,
                      "traffic_source": pmc["source"] if pmc else None,
-                     "avg_launch_ms": round(pass_ms, 5), "launches_timed": launches},
+                     "algorithmic_bytes_per_launch": dom["bytes_per_launch"],
+                     "bytes_per_key": dom["bytes_per_key"],
+                     "avg_launch_ms": dom["avg_launch_ms"],
+                     "launches_timed": dom["launches"]},
+        "kernels": [{k: v for k, v in r.items() if k != "pmc_prefixes"} for r in rooflines],
         "cpu_baseline": cpu,
         "phases_ms_avg": phases,
         "passes_run": last["passes_run"],
+        "local_algo": "lsd" if last["local_algo"] == gsort.LOCAL_LSD else "msd",
         "verified": bool(ok),
     }
     if world > 1:

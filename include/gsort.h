@@ -48,7 +48,7 @@ typedef struct { char internal[128]; } gsort_uid;
 /* Per-call device-time breakdown (hipEvents on the context's stream), filled when non-NULL. */
 typedef struct {
     double ms_total;          /* whole call, device time                                    */
-    double ms_hist;           /* K1 digit histograms                                        */
+    double ms_hist;           /* K1 digit histograms (+ K2 scans, K12 plans in the MSD sort)  */
     double ms_pass[4];        /* K3 onesweep passes of the final local sort, by digit        */
     double ms_local_sort;     /* all local-sort kernels (K1+K3), every local sort in the call */
     double ms_exchange;       /* RCCL key exchange(s), all passes                           */
@@ -59,9 +59,20 @@ typedef struct {
     uint64_t keys_local_out;  /* keys this rank holds after the call                        */
     uint64_t bytes_sent;      /* key bytes this rank sent to OTHER ranks, all passes        */
     uint64_t max_pair_bytes;  /* largest single (this rank -> peer) message, bytes          */
-    int passes_run;           /* onesweep passes run by the final local sort (<= 4)         */
+    int passes_run;           /* LSD passes (or MSD levels) run by the final local sort     */
     int exchanges;            /* RCCL all-to-all rounds                                      */
+    double ms_level[4];       /* MSD: K3u partition of level 3..0 (its counts: ms_hist)      */
+    double ms_bucket_sort;    /* MSD: K11 in-LDS bucket sorts                                */
+    uint64_t keys_level[4];   /* MSD: keys partitioned at level 3..0                         */
+    uint64_t keys_bucket_sort;/* MSD: keys sorted by K11                                     */
+    uint64_t buckets_local;   /* MSD: buckets finished by K11                                */
+    int local_algo;           /* local sort used: GSORT_LOCAL_MSD or GSORT_LOCAL_LSD         */
 } gsort_stats;
+
+/* Local (one-GPU) sort algorithm.  MSD: unstable LDS-atomic partitions of the top digits and
+ * in-LDS bucket sorts (default).  LSD: four stable K1/K2/K3 passes (kept for comparison and
+ * as the path the distributed radix pass structure is built on). */
+enum { GSORT_LOCAL_MSD = 0, GSORT_LOCAL_LSD = 1 };
 
 /* ---- context -------------------------------------------------------------------------- */
 gsort_status gsort_get_uid(gsort_uid *out);
@@ -81,6 +92,8 @@ gsort_status gsort_create_in_group(gsort_ctx **ctx, gsort_group *grp, int rank, 
 gsort_status gsort_destroy(gsort_ctx *ctx);
 /* Pre-size device scratch for n_local keys (keeps hipMalloc out of timed regions). */
 gsort_status gsort_reserve(gsort_ctx *ctx, size_t n_local);
+/* Select the local sort algorithm (GSORT_LOCAL_MSD / GSORT_LOCAL_LSD) for later calls. */
+gsort_status gsort_set_local_algo(gsort_ctx *ctx, int algo);
 const char *gsort_strerror(gsort_status st);
 const char *gsort_last_error(const gsort_ctx *ctx);
 int gsort_rank(const gsort_ctx *ctx);

@@ -51,6 +51,62 @@ hipError_t launch_select_splitters(const int32_t *samples, int m, int k, int nsp
 // K6 bucket bounds on a sorted block: bounds[j] = #keys <= splitters[j] (j < nsplit).
 hipError_t launch_bucket_bounds(const int32_t *sorted, uint64_t n, const int32_t *splitters,
                                 int nsplit, uint64_t *bounds, hipStream_t s);
+// ---- MSD partition sort (gsort_kernels.hip, "MSD partition sort") -----------------------
+// K11 geometry: one 512-thread workgroup sorts a bucket of up to kLocalMax keys entirely in
+// LDS (32 keys per thread; 16 when every bucket of the launch has <= kLocalMax / 2 keys).
+constexpr int kLocalBlock = 512;
+constexpr uint64_t kLocalMax = 16384;
+
+// K3u, level 3: unstable partition of global tiles by digit shift/8 (offsets from K1/K2).
+hipError_t launch_partition(const uint32_t *in, uint32_t *out, uint64_t n, int shift,
+                            const uint32_t *toff, const uint64_t *gpfx, const uint64_t *bases,
+                            bool flip_in, hipStream_t s);
+// Work lists of child buckets: list[0] = next level (> lmax keys), list[1] = K11 with 16
+// keys per thread (1..small_max keys), list[2] = K11 with 32 keys per thread (small_max, lmax].
+// Each list is u64 pairs {start, len}; ctr[3*i .. 3*i+2] = {entries, keys, longest} of list i.
+// ctr == nullptr: no classification (the last level).
+struct WorkLists {
+    uint64_t *list[3];
+    uint64_t *ctr;
+    uint64_t small_max, lmax;
+};
+// The 256 level-3 buckets {bases[d], totals[d]} -> work lists.
+hipError_t launch_classify_buckets(const uint64_t *bases, const uint64_t *totals,
+                                   const WorkLists &wl, hipStream_t s);
+// One segmented level: partition every segment of `segs` by digit shift/8 (in -> out, same
+// positions), children classified into `lists`.  Device scratch sized by the caller for
+// max_tiles >= tiles of all segments and max_groups >= their scan groups.
+struct SegPass {
+    const uint32_t *in;
+    uint32_t *out;
+    const uint64_t *segs;
+    uint32_t nseg;
+    int shift;
+    bool flip_out;
+    uint32_t max_tiles, max_groups;
+    uint32_t *tpfx, *gpfx;         // nseg + 1 each
+    uint32_t *segmap, *groupmap;   // max_tiles / max_groups
+    uint32_t *tcounts;             // max_tiles x 256
+    uint64_t *gsum;                // max_groups x 256
+    uint64_t *cstart;              // nseg x 256
+    WorkLists lists;
+};
+// K12 + K1s + K2s: plan the tiles, count them, scan, child starts + classification.
+hipError_t launch_seg_count(const SegPass &sp, hipStream_t s);
+// K3u over the planned segment tiles (after launch_seg_count).
+hipError_t launch_seg_partition(const SegPass &sp, hipStream_t s);
+// K11: sort each listed bucket (all <= maxlen <= kLocalMax keys) on digits 0..ndigits-1 in
+// LDS, store as int32 into out (same positions; in == out allowed).  flip_in: the input is
+// int32 (else ordered u32).  A list counter is {entries, keys, longest entry}.
+// atomic_rank: stable ranks from LDS atomics (lane-order property, checked at context
+// creation by launch_lds_order_check), else from wave64 ballots.
+hipError_t launch_local_sort(const uint32_t *in, uint32_t *out, const uint64_t *list,
+                             uint32_t nlist, uint64_t maxlen, int ndigits, bool flip_in,
+                             bool atomic_rank, hipStream_t s);
+// Lane-order self-check: nblocks x 512 threads x 16 digits from `digits` (mod nbins);
+// bad[0] += violations (zeroed by the caller).
+hipError_t launch_lds_order_check(const uint32_t *digits, uint32_t nblocks, uint32_t nbins,
+                                  uint64_t *bad, hipStream_t s);
 // Plain device copy kernel (used when a sort has no non-trivial pass).
 hipError_t launch_copy(const uint32_t *in, uint32_t *out, uint64_t n, hipStream_t s);
 

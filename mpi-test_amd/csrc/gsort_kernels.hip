@@ -473,6 +473,512 @@ __global__ void k_copy(const uint32_t *__restrict__ in, uint32_t *__restrict__ o
         out[i] = in[i];
 }
 
+// =======================================================================================
+// MSD partition sort (keys only).  A keys-only sort does not need stable partitions: an MSD
+// pass only has to put every key into its digit's bucket, and the buckets are then sorted on
+// the remaining digits.  So the partition passes rank keys with one LDS atomic each (no ballot
+// matching), and buckets small enough for one workgroup (<= kLocalMax keys) are finished in
+// LDS by K11 -- one HBM read + one write for all their remaining digits.
+//   level 3: K1 + K2 (global tiles) + K3u  -> 256 buckets
+//   level L<3: K12 plan/map, K1s, K2s-a, K2s-b, K3u over the oversized buckets of level L+1
+//   K11: buckets <= kLocalMax keys, remaining digits sorted in LDS (first digit unstable by
+//        LDS atomics, the others stable by wave64 ballot ranks), written back flipped to int32
+// Segment descriptors are u64 pairs {start, len}.  Segment tile ranges are NOT padded: group
+// G of segment s covers its tiles [32 (G - gpfx[s]), +32) counted from the segment's first.
+// =======================================================================================
+
+// Block-strided tile load: k[i] = src[i * BLOCK] (src already offset by threadIdx.x) for the
+// first len keys of the tile, 0 beyond.  All loads are issued before any use: a per-key branch
+// around a load AND its use (e.g. the int32 flip) makes the compiler wait on every load.
+template <int BLOCK, int ITEMS, bool FIN>
+__device__ __forceinline__ void load_tile(const uint32_t *__restrict__ src, bool full,
+                                          uint32_t len, uint32_t (&k)[ITEMS]) {
+    if (full) {
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i) k[i] = src[i * BLOCK];
+    } else {
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i)
+            k[i] = (uint32_t)(i * BLOCK + threadIdx.x) < len ? src[i * BLOCK] : 0u;
+    }
+    if (FIN) {
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i) k[i] ^= kFlip;
+    }
+}
+
+// Shared K3u body: unstable partition of one tile [t0, t0 + len) of `in` by digit `shift`.
+// dst_base (tid < 256) = out + global start of this tile's digit-tid keys.
+template <int BLOCK, int ITEMS, bool FIN, bool FOUT>
+__device__ __forceinline__ void partition_tile(const uint32_t *__restrict__ in, uint64_t t0,
+                                               uint32_t len, int shift, uint32_t *dst_base,
+                                               uint32_t *s_keys, uint32_t *s_cur,
+                                               uint32_t **s_dst, uint32_t *s_wsum) {
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    constexpr int TILE = BLOCK * ITEMS;
+    const bool full = len == (uint32_t)TILE;
+    if (tid < kRadix) s_cur[tid] = 0;
+    uint32_t k[ITEMS];
+    load_tile<BLOCK, ITEMS, FIN>(in + t0 + tid, full, len, k);
+    __syncthreads();
+    uint32_t r[ITEMS];
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i)
+        if (full || (uint32_t)(i * BLOCK + tid) < len)
+            r[i] = atomicAdd(&s_cur[(k[i] >> shift) & 255u], 1u);
+    __syncthreads();
+    uint32_t c = 0, excl = 0;
+    if (tid < kRadix) {
+        c = s_cur[tid];
+        uint32_t v = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t t = __shfl_up(v, o);
+            if (lane >= o) v += t;
+        }
+        if (lane == 63) s_wsum[w] = v;
+        excl = v - c;
+    }
+    __syncthreads();
+    if (tid < kRadix) {
+        for (int ww = 0; ww < w; ++ww) excl += s_wsum[ww];
+        s_cur[tid] = excl;
+        s_dst[tid] = dst_base - excl;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i)
+        if (full || (uint32_t)(i * BLOCK + tid) < len)
+            s_keys[s_cur[(k[i] >> shift) & 255u] + r[i]] = k[i];
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+        const uint32_t j = (uint32_t)(i * BLOCK + tid);
+        if (full || j < len) {
+            const uint32_t key = s_keys[j];
+            s_dst[(key >> shift) & 255u][j] = FOUT ? (key ^ kFlip) : key;
+        }
+    }
+}
+
+// K3u (level 3, global tiles): offsets from K1/K2 exactly as K3.
+template <int BLOCK, int ITEMS, bool FIN>
+__global__ __launch_bounds__(BLOCK) void k_partition(const uint32_t *__restrict__ in,
+                                                     uint32_t *__restrict__ out, uint64_t n,
+                                                     int shift, const uint32_t *__restrict__ toff,
+                                                     const unsigned long long *__restrict__ gpfx,
+                                                     const unsigned long long *__restrict__ bases) {
+    constexpr int TILE = BLOCK * ITEMS;
+    static_assert(TILE == kSweepTile, "K1/K2 count tiles of kSweepTile keys");
+    __shared__ uint32_t s_keys[TILE];
+    __shared__ uint32_t s_cur[kRadix];
+    __shared__ uint32_t *s_dst[kRadix];
+    __shared__ uint32_t s_wsum[kRadix / 64];
+    const uint32_t tile = xcd_tile(blockIdx.x, gridDim.x);
+    const uint64_t t0 = (uint64_t)tile * TILE;
+    const uint32_t len = (uint32_t)(n - t0 < (uint64_t)TILE ? n - t0 : (uint64_t)TILE);
+    uint32_t *dst_base = nullptr;
+    if (threadIdx.x < kRadix)
+        dst_base = out + bases[threadIdx.x] +
+                   gpfx[(uint64_t)(tile / kScanGroup) * kRadix + threadIdx.x] +
+                   toff[(uint64_t)tile * kRadix + threadIdx.x];
+    partition_tile<BLOCK, ITEMS, FIN, false>(in, t0, len, shift, dst_base, s_keys, s_cur, s_dst,
+                                             s_wsum);
+}
+
+// Tile -> segment geometry of a segmented pass.
+struct SegTile {
+    uint32_t seg;    // segment index
+    uint32_t group;  // global scan-group index
+    uint64_t t0;     // first key
+    uint32_t len;    // keys in this tile (0: tile beyond the last segment)
+};
+__device__ __forceinline__ SegTile seg_tile(uint32_t t, const unsigned long long *segs,
+                                            const uint32_t *tpfx, const uint32_t *gpfx,
+                                            const uint32_t *segmap, uint32_t nseg) {
+    SegTile st{0, 0, 0, 0};
+    if (t >= tpfx[nseg]) return st;
+    const uint32_t s = segmap[t];
+    const uint32_t j = t - tpfx[s];
+    const uint64_t a = segs[2 * s] + (uint64_t)j * kSweepTile;
+    const uint64_t e = segs[2 * s] + segs[2 * s + 1];
+    st.seg = s;
+    st.group = gpfx[s] + j / kScanGroup;
+    st.t0 = a;
+    st.len = (uint32_t)(e - a < (uint64_t)kSweepTile ? e - a : (uint64_t)kSweepTile);
+    return st;
+}
+
+// K12a: tpfx[s] / gpfx[s] = tiles / scan groups before segment s (one 1024-thread block).
+__global__ __launch_bounds__(1024) void k_seg_plan(const unsigned long long *__restrict__ segs,
+                                                   uint32_t nseg, uint32_t *__restrict__ tpfx,
+                                                   uint32_t *__restrict__ gpfx) {
+    __shared__ uint32_t s_t[16], s_g[16];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint32_t per = (nseg + 1023) / 1024, s0 = tid * per;
+    uint32_t st = 0, sg = 0;
+    for (uint32_t j = 0; j < per && s0 + j < nseg; ++j) {
+        const uint32_t nt = (uint32_t)((segs[2 * (s0 + j) + 1] + kSweepTile - 1) / kSweepTile);
+        st += nt;
+        sg += (nt + kScanGroup - 1) / kScanGroup;
+    }
+    uint32_t vt = st, vg = sg;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t a = __shfl_up(vt, o), b = __shfl_up(vg, o);
+        if (lane >= o) { vt += a; vg += b; }
+    }
+    if (lane == 63) { s_t[w] = vt; s_g[w] = vg; }
+    __syncthreads();
+    uint32_t rt = vt - st, rg = vg - sg;
+    for (uint32_t ww = 0; ww < w; ++ww) { rt += s_t[ww]; rg += s_g[ww]; }
+    for (uint32_t j = 0; j < per && s0 + j < nseg; ++j) {
+        tpfx[s0 + j] = rt;
+        gpfx[s0 + j] = rg;
+        const uint32_t nt = (uint32_t)((segs[2 * (s0 + j) + 1] + kSweepTile - 1) / kSweepTile);
+        rt += nt;
+        rg += (nt + kScanGroup - 1) / kScanGroup;
+    }
+    if (tid == 1023) {
+        uint32_t tt = 0, tg = 0;
+        for (int ww = 0; ww < 16; ++ww) { tt += s_t[ww]; tg += s_g[ww]; }
+        tpfx[nseg] = tt;
+        gpfx[nseg] = tg;
+    }
+}
+
+// K12b: segmap[t] = segment of tile t, groupmap[G] = segment of scan group G (block = segment).
+__global__ __launch_bounds__(256) void k_seg_map(const uint32_t *__restrict__ tpfx,
+                                                 const uint32_t *__restrict__ gpfx,
+                                                 uint32_t *__restrict__ segmap,
+                                                 uint32_t *__restrict__ groupmap) {
+    const uint32_t s = blockIdx.x;
+    for (uint32_t t = tpfx[s] + threadIdx.x; t < tpfx[s + 1]; t += 256) segmap[t] = s;
+    for (uint32_t g = gpfx[s] + threadIdx.x; g < gpfx[s + 1]; g += 256) groupmap[g] = s;
+}
+
+// K1s: digit counts of every segment tile (one block per tile; grid may exceed the tiles).
+__global__ __launch_bounds__(256) void k_seg_counts(const uint32_t *__restrict__ in,
+                                                    const unsigned long long *__restrict__ segs,
+                                                    const uint32_t *__restrict__ tpfx,
+                                                    const uint32_t *__restrict__ gpfx,
+                                                    const uint32_t *__restrict__ segmap,
+                                                    uint32_t nseg, int shift,
+                                                    uint32_t *__restrict__ tcounts) {
+    __shared__ uint32_t s_h[kRadix];
+    const uint32_t t = blockIdx.x, tid = threadIdx.x;
+    const SegTile st = seg_tile(t, segs, tpfx, gpfx, segmap, nseg);
+    if (st.len == 0) return;
+    s_h[tid] = 0;
+    __syncthreads();
+    const uint32_t *src = in + st.t0;
+#pragma unroll 8
+    for (uint32_t i = tid; i < st.len; i += 256) atomicAdd(&s_h[(src[i] >> shift) & 255u], 1u);
+    __syncthreads();
+    tcounts[(uint64_t)t * kRadix + tid] = s_h[tid];
+}
+
+// K2s-a: group-local exclusive scan of the tile counts of each scan group (group = block).
+__global__ __launch_bounds__(kRadix) void k_seg_scan_tiles(uint32_t *__restrict__ tcounts,
+                                                           const uint32_t *__restrict__ tpfx,
+                                                           const uint32_t *__restrict__ gpfx,
+                                                           const uint32_t *__restrict__ groupmap,
+                                                           uint32_t nseg,
+                                                           unsigned long long *__restrict__ gsum) {
+    const uint32_t g = blockIdx.x, d = threadIdx.x;
+    if (g >= gpfx[nseg]) return;
+    const uint32_t s = groupmap[g];
+    const uint32_t t0 = tpfx[s] + (g - gpfx[s]) * kScanGroup;
+    const uint32_t nt = min((uint32_t)kScanGroup, tpfx[s + 1] - t0);
+    uint32_t c[kScanGroup];
+#pragma unroll
+    for (int j = 0; j < kScanGroup; ++j)
+        c[j] = (uint32_t)j < nt ? tcounts[(uint64_t)(t0 + j) * kRadix + d] : 0u;
+    uint32_t run = 0;
+#pragma unroll
+    for (int j = 0; j < kScanGroup; ++j) {
+        if ((uint32_t)j < nt) tcounts[(uint64_t)(t0 + j) * kRadix + d] = run;
+        run += c[j];
+    }
+    gsum[(uint64_t)g * kRadix + d] = run;
+}
+
+// Child buckets -> work lists (WorkLists, gsort_kernels.h): > lmax keys to the next level,
+// (small_max, lmax] keys and 1..small_max keys to K11's two geometries.  A list is u64 pairs
+// {start, len}; its counter {entries, keys, longest entry}.  Called by all kRadix threads of a
+// block (one child each): the block reserves its entries with one global atomic per list, so
+// the counters see a few atomics per block, not one per child.
+__device__ __forceinline__ void classify_block(uint64_t start, uint64_t len, const WorkLists &wl) {
+    __shared__ unsigned int s_n[3];
+    __shared__ unsigned long long s_keys[3], s_max[3], s_base[3];
+    const uint32_t tid = threadIdx.x;
+    if (tid < 3) { s_n[tid] = 0; s_keys[tid] = 0; s_max[tid] = 0; }
+    __syncthreads();
+    const int which = len > wl.lmax ? 0 : len > wl.small_max ? 2 : len > 0 ? 1 : -1;
+    unsigned int idx = 0;
+    if (which >= 0) {
+        idx = atomicAdd(&s_n[which], 1u);
+        atomicAdd(&s_keys[which], (unsigned long long)len);
+        atomicMax(&s_max[which], (unsigned long long)len);
+    }
+    __syncthreads();
+    if (tid < 3 && s_n[tid]) {
+        unsigned long long *ctr = reinterpret_cast<unsigned long long *>(wl.ctr) + 3 * tid;
+        s_base[tid] = atomicAdd(&ctr[0], (unsigned long long)s_n[tid]);
+        atomicAdd(&ctr[1], s_keys[tid]);
+        atomicMax(&ctr[2], s_max[tid]);
+    }
+    __syncthreads();
+    if (which >= 0) {
+        unsigned long long *list = reinterpret_cast<unsigned long long *>(wl.list[which]);
+        const unsigned long long i = s_base[which] + idx;
+        list[2 * i] = start;
+        list[2 * i + 1] = len;
+    }
+}
+
+// K2s-b: per segment (block) and digit (thread): exclusive scan over the segment's scan
+// groups (in place), then the child bucket starts; classify the children.
+__global__ __launch_bounds__(kRadix) void k_seg_scan_groups(
+    unsigned long long *__restrict__ gsum, const unsigned long long *__restrict__ segs,
+    const uint32_t *__restrict__ gpfx, unsigned long long *__restrict__ cstart, WorkLists wl) {
+    __shared__ unsigned long long s_w[kRadix / 64];
+    const uint32_t s = blockIdx.x, d = threadIdx.x, lane = d & 63, w = d >> 6;
+    const uint32_t g0 = gpfx[s], g1 = gpfx[s + 1];
+    unsigned long long run = 0;
+    for (uint32_t g = g0; g < g1; g += 16) {
+        unsigned long long v[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) v[j] = g + j < g1 ? gsum[(uint64_t)(g + j) * kRadix + d] : 0ull;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            if (g + j < g1) gsum[(uint64_t)(g + j) * kRadix + d] = run;
+            run += v[j];
+        }
+    }
+    unsigned long long x = run;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned long long t = __shfl_up(x, o);
+        if (lane >= o) x += t;
+    }
+    if (lane == 63) s_w[w] = x;
+    __syncthreads();
+    unsigned long long excl = x - run;
+    for (uint32_t ww = 0; ww < w; ++ww) excl += s_w[ww];
+    const uint64_t start = segs[2 * s] + excl;
+    cstart[(uint64_t)s * kRadix + d] = start;
+    if (wl.ctr) classify_block(start, run, wl);
+}
+
+// Level-3 children: the 256 buckets of the global pass.
+__global__ __launch_bounds__(kRadix) void k_classify_buckets(
+    const unsigned long long *__restrict__ bases, const unsigned long long *__restrict__ totals,
+    WorkLists wl) {
+    const uint32_t d = threadIdx.x;
+    classify_block(bases[d], totals[d], wl);
+}
+
+// K3u (segmented): one block per segment tile.
+template <int BLOCK, int ITEMS, bool FOUT>
+__global__ __launch_bounds__(BLOCK) void k_seg_partition(
+    const uint32_t *__restrict__ in, uint32_t *__restrict__ out, int shift,
+    const uint32_t *__restrict__ toff, const unsigned long long *__restrict__ gpfx64,
+    const unsigned long long *__restrict__ cstart, const unsigned long long *__restrict__ segs,
+    const uint32_t *__restrict__ tpfx, const uint32_t *__restrict__ gpfx,
+    const uint32_t *__restrict__ segmap, uint32_t nseg) {
+    constexpr int TILE = BLOCK * ITEMS;
+    static_assert(TILE == kSweepTile, "segment tiles are kSweepTile keys");
+    __shared__ uint32_t s_keys[TILE];
+    __shared__ uint32_t s_cur[kRadix];
+    __shared__ uint32_t *s_dst[kRadix];
+    __shared__ uint32_t s_wsum[kRadix / 64];
+    const uint32_t t = xcd_tile(blockIdx.x, gridDim.x);
+    const SegTile st = seg_tile(t, segs, tpfx, gpfx, segmap, nseg);
+    if (st.len == 0) return;
+    uint32_t *dst_base = nullptr;
+    if (threadIdx.x < kRadix)
+        dst_base = out + cstart[(uint64_t)st.seg * kRadix + threadIdx.x] +
+                   gpfx64[(uint64_t)st.group * kRadix + threadIdx.x] +
+                   toff[(uint64_t)t * kRadix + threadIdx.x];
+    partition_tile<BLOCK, ITEMS, false, FOUT>(in, st.t0, st.len, shift, dst_base, s_keys, s_cur,
+                                              s_dst, s_wsum);
+}
+
+// Stable wave-level rank of one round (64 keys, lane order = key order) against the wave's
+// running digit counters wc[256] (u32): returns #earlier keys of the wave with this digit.
+//   ATOMIC: one ds_add_rtn_u32 per lane.  The MI355X LDS serializes lanes of one instruction
+//           that hit the same address in ascending lane order, so the returned counts are the
+//           stable ranks (measured: tools/lds_order.hip; re-checked by gsort_create, which
+//           selects BALLOT if the check fails -- DESIGN.md 5).
+//   BALLOT: 8 ballots give each lane the mask of lanes sharing its digit (v_bfe, v_cmp, two
+//           v_bitop3 per bit); rank = running count + peers below; 36 VALU per round.
+template <bool ATOMIC>
+__device__ __forceinline__ uint32_t wave_rank(uint32_t *wc, uint32_t d, bool valid) {
+    if (ATOMIC) return valid ? atomicAdd(&wc[d], 1u) : 0u;
+    uint32_t plo = ~0u, phi = ~0u;
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int32_t)d, b, 1);
+        uint64_t bal;
+        asm("v_cmp_ne_u32_e64 %0, 0, %1" : "=s"(bal) : "v"(m));
+        plo = __builtin_amdgcn_bitop3_b32(plo, (uint32_t)bal, m, 0x90);
+        phi = __builtin_amdgcn_bitop3_b32(phi, (uint32_t)(bal >> 32), m, 0x90);
+    }
+    const uint64_t vm = __ballot(valid);  // invalid lanes neither rank nor count
+    plo &= (uint32_t)vm;
+    phi &= (uint32_t)(vm >> 32);
+    const uint32_t below = __builtin_amdgcn_mbcnt_hi(phi, __builtin_amdgcn_mbcnt_lo(plo, 0u));
+    const uint32_t prev = wc[d];
+    if (valid) wc[d] = prev + (uint32_t)(__popc(plo) + __popc(phi));  // same from all peers
+    return prev + below;
+}
+
+// K11: sort each listed bucket (<= BLOCK * ITEMS keys) on digits 0 .. ndigits-1 in LDS and
+// write it back flipped to int32 order.  Digit 0 is ranked by block-wide LDS atomics (an LSD
+// sort may order equal first digits arbitrarily); every later digit is ranked stably per wave
+// (wave_rank) in (wave, round, lane) order over wave-contiguous chunks, then offset by the
+// (digit, wave)-major exclusive scan of the per-wave counts.
+template <int BLOCK, int ITEMS, bool FIN, bool ATOMIC>
+__global__ __launch_bounds__(BLOCK) void k_local_sort(const uint32_t *__restrict__ in,
+                                                      uint32_t *__restrict__ out,
+                                                      const unsigned long long *__restrict__ list,
+                                                      int ndigits) {
+    constexpr int WAVES = BLOCK / 64;
+    constexpr int TILE = BLOCK * ITEMS;
+    static_assert(TILE <= 65536, "ranks are packed as 16 bits");
+    __shared__ uint32_t s_a[TILE];
+    __shared__ uint32_t s_wc[WAVES * kRadix];  // per-wave digit counts, then offsets
+    // the digit scans run while every key is in registers, so their 4 wave sums borrow the
+    // tail of s_a (40 KiB per workgroup instead of 40 KiB + 16 B: 4 workgroups per CU)
+    uint32_t *s_wsum = s_a + TILE - kRadix / 64;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint64_t start = list[2 * blockIdx.x];
+    const uint32_t len = (uint32_t)list[2 * blockIdx.x + 1];
+    uint32_t *cnt = s_wc;  // digit 0: block-wide counters, then digit starts
+
+    auto block_scan = [&](uint32_t c) -> uint32_t {  // tid < 256: exclusive scan over digits
+        uint32_t v = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t t = __shfl_up(v, o);
+            if (lane >= o) v += t;
+        }
+        if (lane == 63) s_wsum[w] = v;
+        return v - c;
+    };
+
+    // digit 0: unstable counting sort from global into s_a
+    {
+        if (tid < kRadix) cnt[tid] = 0;
+        uint32_t k[ITEMS], r[ITEMS];
+        load_tile<BLOCK, ITEMS, FIN>(in + start + tid, len == (uint32_t)TILE, len, k);
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i)
+            if ((uint32_t)(i * BLOCK + tid) < len) r[i] = atomicAdd(&cnt[k[i] & 255u], 1u);
+        __syncthreads();
+        uint32_t excl = 0;
+        if (tid < kRadix) excl = block_scan(cnt[tid]);
+        __syncthreads();
+        if (tid < kRadix) {
+            for (int ww = 0; ww < w; ++ww) excl += s_wsum[ww];
+            cnt[tid] = excl;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i)
+            if ((uint32_t)(i * BLOCK + tid) < len) s_a[cnt[k[i] & 255u] + r[i]] = k[i];
+        __syncthreads();
+    }
+
+    // digits 1 .. ndigits-1: stable, wave-chunked (wave w owns [w*64*R, (w+1)*64*R))
+    const uint32_t R = (len + 64 * WAVES - 1) / (64 * WAVES);
+    for (int p = 1; p < ndigits; ++p) {
+        const int shift = 8 * p;
+        uint32_t *wc = s_wc + w * kRadix;
+#pragma unroll
+        for (int j = 0; j < kRadix / 64; ++j) wc[j * 64 + lane] = 0;
+        uint32_t k[ITEMS];
+        const uint32_t base = (uint32_t)w * 64 * R + lane;
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i)
+            if ((uint32_t)i < R) k[i] = base + i * 64 < len ? s_a[base + i * 64] : 0u;
+        __syncthreads();
+        uint32_t rk[(ITEMS + 1) / 2];
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i) {
+            if ((uint32_t)i >= R) continue;
+            const uint32_t rr = wave_rank<ATOMIC>(wc, (k[i] >> shift) & 255u, base + i * 64 < len);
+            if (i & 1) rk[i >> 1] |= rr << 16; else rk[i >> 1] = rr;
+        }
+        __syncthreads();
+        uint32_t tcount = 0, excl = 0;
+        if (tid < kRadix) {
+#pragma unroll
+            for (int ww = 0; ww < WAVES; ++ww) tcount += s_wc[ww * kRadix + tid];
+            excl = block_scan(tcount);
+        }
+        __syncthreads();
+        if (tid < kRadix) {
+            uint32_t off = excl;
+            for (int ww = 0; ww < w; ++ww) off += s_wsum[ww];
+#pragma unroll
+            for (int ww = 0; ww < WAVES; ++ww) {
+                const uint32_t cw = s_wc[ww * kRadix + tid];
+                s_wc[ww * kRadix + tid] = off;
+                off += cw;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i) {
+            if ((uint32_t)i >= R || base + i * 64 >= len) continue;
+            const uint32_t rr = (i & 1) ? (rk[i >> 1] >> 16) : (rk[i >> 1] & 0xFFFFu);
+            s_a[wc[(k[i] >> shift) & 255u] + rr] = k[i];
+        }
+        __syncthreads();
+    }
+    uint32_t *dst = out + start;
+    for (uint32_t j = tid; j < len; j += BLOCK) dst[j] = s_a[j] ^ kFlip;
+}
+
+// Self-check of the LDS lane-order property wave_rank<true> relies on: every wave of a block
+// ranks 16 rounds of digits drawn from `digits` (nbins-valued) with ds_add_rtn and counts the
+// ranks that are not the wave's previous rank of that digit + 1.  bad[0] must stay 0.
+__global__ __launch_bounds__(512) void k_lds_order_check(const uint32_t *__restrict__ digits,
+                                                          uint32_t nbins,
+                                                          unsigned long long *bad) {
+    __shared__ uint32_t cnt[8 * kRadix];
+    __shared__ uint32_t last[8 * kRadix];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    for (int i = tid; i < 8 * kRadix; i += 512) { cnt[i] = 0; last[i] = 0xFFFFFFFFu; }
+    __syncthreads();
+    const uint64_t base = ((uint64_t)blockIdx.x * 8 + w) * 64 * 16;
+    uint32_t d[16], r[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) d[i] = digits[base + i * 64 + lane] % nbins;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) r[i] = atomicAdd(&cnt[w * kRadix + d[i]], 1u);
+    // lane order within a round: a lane's rank exceeds the rank of every lower lane with the
+    // same digit; across rounds: exceeds every rank of an earlier round
+    uint32_t nbad = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        for (int l = 0; l < 64; ++l) {
+            const uint32_t dl = __shfl(d[i], l), rl = __shfl(r[i], l);
+            if (l < lane && dl == d[i] && rl >= r[i]) ++nbad;
+        }
+        uint32_t *lw = last + w * kRadix;
+        // every lane of the round, in lane order, checks against the previous round's maximum
+        if (i > 0 && lw[d[i]] != 0xFFFFFFFFu && r[i] <= lw[d[i]]) ++nbad;
+        __syncthreads();
+        atomicMax(&lw[d[i]], r[i]);
+        __syncthreads();
+    }
+    if (nbad) atomicAdd(bad, (unsigned long long)nbad);
+}
+
 unsigned grid_for(uint64_t n, unsigned block, unsigned cap) {
     uint64_t g = (n + block - 1) / block;
     if (g < 1) g = 1;
@@ -577,6 +1083,89 @@ hipError_t launch_bucket_bounds(const int32_t *sorted, uint64_t n, const int32_t
     if (nsplit <= 0) return hipSuccess;
     k_bucket_bounds<<<nsplit, 64, 0, s>>>(sorted, n, splitters,
                                           reinterpret_cast<unsigned long long *>(bounds));
+    return hipGetLastError();
+}
+
+hipError_t launch_partition(const uint32_t *in, uint32_t *out, uint64_t n, int shift,
+                            const uint32_t *toff, const uint64_t *gpfx, const uint64_t *bases,
+                            bool flip_in, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const unsigned g = (unsigned)sweep_tiles(n);
+    auto *gp = reinterpret_cast<const unsigned long long *>(gpfx);
+    auto *bs = reinterpret_cast<const unsigned long long *>(bases);
+    constexpr int B = kSweepBlock, I = kSweepItems;
+    if (flip_in) k_partition<B, I, true><<<g, B, 0, s>>>(in, out, n, shift, toff, gp, bs);
+    else k_partition<B, I, false><<<g, B, 0, s>>>(in, out, n, shift, toff, gp, bs);
+    return hipGetLastError();
+}
+
+hipError_t launch_classify_buckets(const uint64_t *bases, const uint64_t *totals,
+                                   const WorkLists &wl, hipStream_t s) {
+    using ull = unsigned long long;
+    k_classify_buckets<<<1, kRadix, 0, s>>>(reinterpret_cast<const ull *>(bases),
+                                            reinterpret_cast<const ull *>(totals), wl);
+    return hipGetLastError();
+}
+
+hipError_t launch_seg_count(const SegPass &sp, hipStream_t s) {
+    using ull = unsigned long long;
+    if (sp.nseg == 0) return hipSuccess;
+    const ull *segs = reinterpret_cast<const ull *>(sp.segs);
+    ull *gsum = reinterpret_cast<ull *>(sp.gsum);
+    k_seg_plan<<<1, 1024, 0, s>>>(segs, sp.nseg, sp.tpfx, sp.gpfx);
+    k_seg_map<<<sp.nseg, 256, 0, s>>>(sp.tpfx, sp.gpfx, sp.segmap, sp.groupmap);
+    k_seg_counts<<<sp.max_tiles, 256, 0, s>>>(sp.in, segs, sp.tpfx, sp.gpfx, sp.segmap, sp.nseg,
+                                              sp.shift, sp.tcounts);
+    k_seg_scan_tiles<<<sp.max_groups, kRadix, 0, s>>>(sp.tcounts, sp.tpfx, sp.gpfx, sp.groupmap,
+                                                      sp.nseg, gsum);
+    k_seg_scan_groups<<<sp.nseg, kRadix, 0, s>>>(gsum, segs, sp.gpfx,
+                                                 reinterpret_cast<ull *>(sp.cstart), sp.lists);
+    return hipGetLastError();
+}
+
+hipError_t launch_seg_partition(const SegPass &sp, hipStream_t s) {
+    using ull = unsigned long long;
+    if (sp.nseg == 0) return hipSuccess;
+    const ull *segs = reinterpret_cast<const ull *>(sp.segs);
+    ull *gsum = reinterpret_cast<ull *>(sp.gsum);
+    constexpr int B = kSweepBlock, I = kSweepItems;
+    if (sp.flip_out)
+        k_seg_partition<B, I, true><<<sp.max_tiles, B, 0, s>>>(
+            sp.in, sp.out, sp.shift, sp.tcounts, gsum, reinterpret_cast<const ull *>(sp.cstart),
+            segs, sp.tpfx, sp.gpfx, sp.segmap, sp.nseg);
+    else
+        k_seg_partition<B, I, false><<<sp.max_tiles, B, 0, s>>>(
+            sp.in, sp.out, sp.shift, sp.tcounts, gsum, reinterpret_cast<const ull *>(sp.cstart),
+            segs, sp.tpfx, sp.gpfx, sp.segmap, sp.nseg);
+    return hipGetLastError();
+}
+
+hipError_t launch_local_sort(const uint32_t *in, uint32_t *out, const uint64_t *list,
+                             uint32_t nlist, uint64_t maxlen, int ndigits, bool flip_in,
+                             bool atomic_rank, hipStream_t s) {
+    if (nlist == 0) return hipSuccess;
+    if (ndigits < 1 || ndigits > 4) return hipErrorInvalidValue;
+    if (maxlen > kLocalMax) return hipErrorInvalidValue;
+    auto *l = reinterpret_cast<const unsigned long long *>(list);
+    constexpr int B = kLocalBlock;
+    // buckets <= kLocalMax / 2 keys: 16 keys per thread; larger: 32 (same workgroup size)
+#define GSORT_K11(I, FI, AT) k_local_sort<B, I, FI, AT><<<nlist, B, 0, s>>>(in, out, l, ndigits)
+    const bool small = maxlen <= (uint64_t)B * 16;
+    if (atomic_rank) {
+        if (small) { if (flip_in) GSORT_K11(16, true, true); else GSORT_K11(16, false, true); }
+        else { if (flip_in) GSORT_K11(32, true, true); else GSORT_K11(32, false, true); }
+    } else {
+        if (small) { if (flip_in) GSORT_K11(16, true, false); else GSORT_K11(16, false, false); }
+        else { if (flip_in) GSORT_K11(32, true, false); else GSORT_K11(32, false, false); }
+    }
+#undef GSORT_K11
+    return hipGetLastError();
+}
+
+hipError_t launch_lds_order_check(const uint32_t *digits, uint32_t nblocks, uint32_t nbins,
+                                  uint64_t *bad, hipStream_t s) {
+    k_lds_order_check<<<nblocks, 512, 0, s>>>(digits, nbins,
+                                              reinterpret_cast<unsigned long long *>(bad));
     return hipGetLastError();
 }
 

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -27,7 +28,7 @@ namespace {
 
 enum Slot { S_TMP, S_OUT, S_CUR, S_SORTED, S_RECV, S_IN, S_STAGE, S_NSLOTS };
 enum Phase { PH_COUNT, PH_PASS0, PH_PASS1, PH_PASS2, PH_PASS3, PH_EXCH, PH_PLACE, PH_SAMPLE,
-             PH_MERGE, PH_TOTAL, PH_N };
+             PH_MERGE, PH_TOTAL, PH_LEVEL3, PH_LEVEL2, PH_LEVEL1, PH_LEVEL0, PH_BUCKET, PH_N };
 
 constexpr size_t kSmallBytes = 256 * 1024;  // device + pinned scratch for counts, plans
 
@@ -46,6 +47,10 @@ struct gsort_ctx {
     DevBuf slot[S_NSLOTS];
     DevBuf tcounts;  // K1/K2: per-tile digit counts -> in-group offsets (u32 [tiles][256])
     DevBuf gsum;     // K2: per-group digit prefixes (u64 [groups][256])
+    int local_algo = GSORT_LOCAL_MSD;
+    bool atomic_rank = false;  // LDS lane-order property verified on this device (create)
+    // MSD scratch: segment plan/maps, child starts, work lists (u64 {start, len} pairs)
+    DevBuf m_tpfx, m_gpfx, m_segmap, m_groupmap, m_cstart, m_next[2], m_local[2];
     // device small area: [0, 8K) hist4 (4x256 u64) | [8K, 10K) pass digit totals (256 u64) |
     // [10K, 12K) pass digit bases (256 u64) | [20K, 256K) plans / samples / routing tables
     char *d_small = nullptr;
@@ -62,7 +67,10 @@ struct gsort_ctx {
 
 namespace {
 
-constexpr size_t OFF_HIST = 0, OFF_TOT = 8192, OFF_BASES = 10240, OFF_PLAN = 20480;
+// [12K, 12K+72): MSD work-list counters, {entries, keys, longest} for the next-level list and
+// the two K11 lists; [12K+128, 12K+144): a one-entry list for a single-bucket sort
+constexpr size_t OFF_HIST = 0, OFF_TOT = 8192, OFF_BASES = 10240, OFF_CTR = 12288,
+                 OFF_ONE = 12416, OFF_PLAN = 20480;
 
 gsort_status set_err(gsort_ctx *c, gsort_status st, const std::string &msg) {
     if (c) c->err = msg;
@@ -147,6 +155,9 @@ void timing_finish(gsort_ctx *c, gsort_stats *st) {
             case PH_SAMPLE: st->ms_sample += ms; break;
             case PH_MERGE: st->ms_merge += ms; break;
             case PH_TOTAL: st->ms_total += ms; break;
+            case PH_LEVEL3: case PH_LEVEL2: case PH_LEVEL1: case PH_LEVEL0:
+                st->ms_level[sp.phase - PH_LEVEL3] += ms; st->ms_local_sort += ms; break;
+            case PH_BUCKET: st->ms_bucket_sort += ms; st->ms_local_sort += ms; break;
         }
     }
     c->timing = false;
@@ -190,11 +201,11 @@ gsort_status reset_call(gsort_ctx *c) {
     return GSORT_OK;
 }
 
-// ---- local sort: K1 (+ all four histograms) then per non-trivial digit K1/K2/K3 ---------
+// ---- LSD local sort: K1 (+ all four histograms) then per non-trivial digit K1/K2/K3 -----
 // Reference: the per-key digit loop mpi_radix_sort.c:144-147 (there: base P, all passes
 // through rank 0) and the local qsort mpi_sample_sort.c:85 / :174.
-gsort_status local_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *out,
-                        uint32_t *tmp, int *passes_run) {
+gsort_status lsd_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *out,
+                      uint32_t *tmp, int *passes_run) {
     if (passes_run) *passes_run = 0;
     if (n == 0) return GSORT_OK;
     ST_TRY(ensure_pass_scratch(c, n));
@@ -223,6 +234,151 @@ gsort_status local_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *
         src = dst;
     }
     if (passes_run) *passes_run = k;
+    return GSORT_OK;
+}
+
+// ---- MSD local sort (gsort_kernels.hip, "MSD partition sort") --------------------------
+// Level 3 partitions the whole input by its top digit (K1 + K2 + K3u, in -> tmp); every later
+// level partitions the buckets still larger than kLocalMax by the next digit (alternating
+// tmp -> out -> tmp -> out, same positions); every bucket of <= kLocalMax keys is finished by
+// K11 in LDS and stored to out as int32.  The host reads two counters per level (a few us) to
+// size the next launches.  Same reference hot loops as lsd_sort.
+gsort_status ensure_list(gsort_ctx *c, DevBuf &b, uint64_t entries) {
+    return ensure(c, b, (size_t)std::max<uint64_t>(entries, 1) * 16);
+}
+
+gsort_status read_counters(gsort_ctx *c, uint64_t *h) {
+    HIP_TRY(c, hipMemcpyAsync(c->h_small + OFF_CTR, c->d_small + OFF_CTR, 72,
+                              hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    memcpy(h, c->h_small + OFF_CTR, 72);
+    return GSORT_OK;
+}
+
+gsort_status msd_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *out,
+                      uint32_t *tmp, gsort_stats *stats) {
+    if (n == 0) return GSORT_OK;
+    uint64_t *ctr = reinterpret_cast<uint64_t *>(c->d_small + OFF_CTR);
+    if (n <= kLocalMax) {  // one bucket: all four digits in LDS
+        uint64_t *h_one = reinterpret_cast<uint64_t *>(c->h_small + OFF_ONE);
+        uint64_t *d_one = reinterpret_cast<uint64_t *>(c->d_small + OFF_ONE);
+        HIP_TRY(c, hipStreamSynchronize(c->stream));  // h_one may feed an earlier copy
+        h_one[0] = 0;
+        h_one[1] = n;
+        HIP_TRY(c, hipMemcpyAsync(d_one, h_one, 16, hipMemcpyHostToDevice, c->stream));
+        hipEvent_t t = tic(c);
+        HIP_TRY(c, launch_local_sort(in, out, d_one, 1, n, 4, true, c->atomic_rank, c->stream));
+        toc(c, PH_BUCKET, t);
+        if (stats) { stats->buckets_local += 1; stats->keys_bucket_sort += n; }
+        return GSORT_OK;
+    }
+    ST_TRY(ensure_pass_scratch(c, n));
+    uint64_t *totals = reinterpret_cast<uint64_t *>(c->d_small + OFF_TOT);
+    uint64_t *bases = reinterpret_cast<uint64_t *>(c->d_small + OFF_BASES);
+    ST_TRY(ensure_list(c, c->m_next[0], kRadix));
+    ST_TRY(ensure_list(c, c->m_local[0], kRadix));
+    ST_TRY(ensure_list(c, c->m_local[1], kRadix));
+    auto lst = [](DevBuf &b) { return reinterpret_cast<uint64_t *>(b.p); };
+    auto lists = [&](int next) {
+        WorkLists wl;
+        wl.list[0] = lst(c->m_next[next]);
+        wl.list[1] = lst(c->m_local[0]);
+        wl.list[2] = lst(c->m_local[1]);
+        wl.ctr = ctr;
+        wl.small_max = kLocalMax / 2;
+        wl.lmax = kLocalMax;
+        return wl;
+    };
+
+    // level 3: global tiles
+    hipEvent_t t = tic(c);
+    HIP_TRY(c, launch_tile_counts(in, n, 24, true, d_tcounts(c), nullptr, c->stream));
+    HIP_TRY(c, launch_scan_tiles(d_tcounts(c), n, d_gsum(c), totals, bases, c->stream));
+    toc(c, PH_COUNT, t);
+    t = tic(c);
+    HIP_TRY(c, launch_partition(in, tmp, n, 24, d_tcounts(c), d_gsum(c), bases, true, c->stream));
+    toc(c, PH_LEVEL3, t);
+    if (stats) stats->keys_level[0] += n;
+    HIP_TRY(c, hipMemsetAsync(ctr, 0, 72, c->stream));
+    HIP_TRY(c, launch_classify_buckets(bases, totals, lists(0), c->stream));
+    uint64_t h[9];  // {entries, keys, longest} of: next level, K11 small, K11 large
+    ST_TRY(read_counters(c, h));
+    int levels = 1;
+    uint32_t *cur = tmp;
+    int cur_list = 0;
+    for (int L = 2;; --L) {
+        for (int k = 0; k < 2; ++k) {  // buckets finished in LDS: digits L..0 remain
+            const uint64_t *hk = h + 3 * (k + 1);
+            if (!hk[0]) continue;
+            t = tic(c);
+            HIP_TRY(c, launch_local_sort(cur, out, lst(c->m_local[k]), (uint32_t)hk[0], hk[2],
+                                         L + 1, false, c->atomic_rank, c->stream));
+            toc(c, PH_BUCKET, t);
+            if (stats) { stats->buckets_local += hk[0]; stats->keys_bucket_sort += hk[1]; }
+        }
+        const uint64_t nseg = h[0], keys = h[1];
+        if (nseg == 0 || L < 0) break;
+        uint32_t *dst = cur == tmp ? out : tmp;
+        const uint64_t max_tiles = sweep_tiles(keys) + nseg;
+        const uint64_t max_groups = (max_tiles + kScanGroup - 1) / kScanGroup + nseg;
+        ST_TRY(ensure(c, c->m_tpfx, (nseg + 1) * 4));
+        ST_TRY(ensure(c, c->m_gpfx, (nseg + 1) * 4));
+        ST_TRY(ensure(c, c->m_segmap, max_tiles * 4));
+        ST_TRY(ensure(c, c->m_groupmap, max_groups * 4));
+        ST_TRY(ensure(c, c->tcounts, max_tiles * kRadix * 4));
+        ST_TRY(ensure(c, c->gsum, max_groups * kRadix * 8));
+        ST_TRY(ensure(c, c->m_cstart, nseg * kRadix * 8));
+        const uint64_t child_cap = std::min<uint64_t>(nseg * kRadix, keys);
+        ST_TRY(ensure_list(c, c->m_next[cur_list ^ 1], std::min<uint64_t>(child_cap, keys / kLocalMax + 1)));
+        ST_TRY(ensure_list(c, c->m_local[0], child_cap));
+        ST_TRY(ensure_list(c, c->m_local[1], std::min<uint64_t>(child_cap, keys / (kLocalMax / 2) + 1)));
+        SegPass sp;
+        sp.in = cur;
+        sp.out = dst;
+        sp.segs = lst(c->m_next[cur_list]);
+        sp.nseg = (uint32_t)nseg;
+        sp.shift = 8 * L;
+        sp.flip_out = L == 0;
+        sp.max_tiles = (uint32_t)max_tiles;
+        sp.max_groups = (uint32_t)max_groups;
+        sp.tpfx = reinterpret_cast<uint32_t *>(c->m_tpfx.p);
+        sp.gpfx = reinterpret_cast<uint32_t *>(c->m_gpfx.p);
+        sp.segmap = reinterpret_cast<uint32_t *>(c->m_segmap.p);
+        sp.groupmap = reinterpret_cast<uint32_t *>(c->m_groupmap.p);
+        sp.tcounts = d_tcounts(c);
+        sp.gsum = d_gsum(c);
+        sp.cstart = reinterpret_cast<uint64_t *>(c->m_cstart.p);
+        sp.lists = lists(cur_list ^ 1);
+        if (L == 0) sp.lists.ctr = nullptr;  // digit 0: every child is a run of equal keys
+        t = tic(c);
+        HIP_TRY(c, hipMemsetAsync(ctr, 0, 72, c->stream));
+        HIP_TRY(c, launch_seg_count(sp, c->stream));
+        toc(c, PH_COUNT, t);
+        t = tic(c);
+        HIP_TRY(c, launch_seg_partition(sp, c->stream));
+        toc(c, PH_LEVEL3 + (3 - L), t);
+        if (stats) stats->keys_level[3 - L] += keys;
+        ++levels;
+        if (L == 0) break;
+        ST_TRY(read_counters(c, h));
+        cur = dst;
+        cur_list ^= 1;
+    }
+    if (stats) stats->passes_run = levels;
+    return GSORT_OK;
+}
+
+gsort_status local_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *out,
+                        uint32_t *tmp, int *passes_run, gsort_stats *stats = nullptr) {
+    if (stats) stats->local_algo = c->local_algo;
+    if (c->local_algo == GSORT_LOCAL_LSD) return lsd_sort(c, in, n, out, tmp, passes_run);
+    gsort_stats tmp_st;
+    memset(&tmp_st, 0, sizeof(tmp_st));
+    gsort_stats *st = stats ? stats : &tmp_st;
+    const int before = st->passes_run;
+    ST_TRY(msd_sort(c, in, n, out, tmp, st));
+    if (passes_run) *passes_run = st->passes_run;
+    if (stats) stats->passes_run = std::max(before, st->passes_run);
     return GSORT_OK;
 }
 
@@ -469,6 +625,31 @@ gsort_status check_input(gsort_ctx *c, const int32_t *d_keys) {
     return GSORT_OK;
 }
 
+// The stable ranks of K11 (and K3) may come from LDS atomics only if the device serializes
+// same-address lanes of one ds_add_rtn in lane order.  Check it once per context
+// on xorshift digits at four densities; on any violation the ballot ranks are used instead.
+gsort_status check_lds_order(gsort_ctx *c) {
+    constexpr uint32_t kBlocks = 64, kN = kBlocks * 512 * 16;
+    std::vector<uint32_t> h(kN);
+    uint64_t x = 0x9E3779B97F4A7C15ull;
+    for (auto &v : h) { x ^= x << 13; x ^= x >> 7; x ^= x << 17; v = (uint32_t)(x >> 32); }
+    uint32_t *d = nullptr;
+    HIP_TRY(c, hipMalloc(&d, kN * 4));
+    uint64_t *bad = reinterpret_cast<uint64_t *>(c->d_small + OFF_PLAN);
+    hipError_t e = hipMemcpyAsync(d, h.data(), kN * 4, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(bad, 0, 8, c->stream);
+    for (uint32_t bins : {1u, 3u, 17u, 256u})
+        if (e == hipSuccess) e = launch_lds_order_check(d, kBlocks, bins, bad, c->stream);
+    uint64_t nbad = 1;
+    if (e == hipSuccess) e = hipMemcpyAsync(&nbad, bad, 8, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    (void)hipFree(d);
+    if (e != hipSuccess) return set_err(c, GSORT_EHIP, std::string("lds order check: ") +
+                                                           hipGetErrorString(e));
+    c->atomic_rank = nbad == 0 && !getenv("GSORT_BALLOT_RANK");
+    return GSORT_OK;
+}
+
 gsort_status create_common(gsort_ctx *c, int hip_device) {
     if (hip_device < 0) {  // -1 - local_rank: pick the local rank's GPU
         int count = 0;
@@ -482,7 +663,7 @@ gsort_status create_common(gsort_ctx *c, int hip_device) {
     HIP_TRY(c, hipMalloc(&c->d_small, kSmallBytes));
     HIP_TRY(c, hipHostMalloc(&c->h_small, kSmallBytes, hipHostMallocDefault));
     HIP_TRY(c, hipMemset(c->d_small, 0, kSmallBytes));
-    return GSORT_OK;
+    return check_lds_order(c);
 }
 
 }  // namespace
@@ -573,6 +754,9 @@ gsort_status gsort_destroy(gsort_ctx *c) {
     for (auto &b : c->slot) if (b.p) (void)hipFree(b.p);
     if (c->tcounts.p) (void)hipFree(c->tcounts.p);
     if (c->gsum.p) (void)hipFree(c->gsum.p);
+    for (DevBuf *b : {&c->m_tpfx, &c->m_gpfx, &c->m_segmap, &c->m_groupmap, &c->m_cstart,
+                      &c->m_next[0], &c->m_next[1], &c->m_local[0], &c->m_local[1]})
+        if (b->p) (void)hipFree(b->p);
     if (c->d_small) (void)hipFree(c->d_small);
     if (c->h_small) (void)hipHostFree(c->h_small);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
@@ -593,6 +777,14 @@ gsort_status gsort_reserve(gsort_ctx *c, size_t n) {
     return GSORT_OK;
 }
 
+gsort_status gsort_set_local_algo(gsort_ctx *c, int algo) {
+    ST_TRY(check_ctx(c));
+    if (algo != GSORT_LOCAL_MSD && algo != GSORT_LOCAL_LSD)
+        return set_err(c, GSORT_EINVAL, "unknown local sort algorithm");
+    c->local_algo = algo;
+    return GSORT_OK;
+}
+
 gsort_status gsort_radix(gsort_ctx *c, const int32_t *d_keys, size_t n_local, int32_t **d_out,
                          size_t *n_out, gsort_stats *stats) {
     ST_TRY(check_ctx(c));
@@ -609,7 +801,7 @@ gsort_status gsort_radix(gsort_ctx *c, const int32_t *d_keys, size_t n_local, in
         ST_TRY(ensure(c, c->slot[S_OUT], cap));
         int pr = 0;
         st = local_sort(c, reinterpret_cast<const uint32_t *>(d_keys), n_local,
-                        slot_ptr<uint32_t>(c, S_OUT), slot_ptr<uint32_t>(c, S_TMP), &pr);
+                        slot_ptr<uint32_t>(c, S_OUT), slot_ptr<uint32_t>(c, S_TMP), &pr, stats);
         if (stats) stats->passes_run = pr;
         *d_out = slot_ptr<int32_t>(c, S_OUT);
         nout = n_local;
@@ -641,7 +833,7 @@ gsort_status gsort_sample(gsort_ctx *c, const int32_t *d_keys, size_t n_local, i
         ST_TRY(ensure(c, c->slot[S_OUT], cap));
         int pr = 0;
         ST_TRY(local_sort(c, reinterpret_cast<const uint32_t *>(d_keys), n_local,
-                          slot_ptr<uint32_t>(c, S_OUT), slot_ptr<uint32_t>(c, S_TMP), &pr));
+                          slot_ptr<uint32_t>(c, S_OUT), slot_ptr<uint32_t>(c, S_TMP), &pr, stats));
         if (stats) stats->passes_run = pr;
         c->splitters.clear();
         c->bucket_counts.assign(1, n_local);

@@ -19,6 +19,7 @@ LIB_PATH = os.path.join(PKG, "lib", "libgsort.so")
 
 OK, EINVAL, ENOMEM, EHIP, ERCCL, ENOSAMPLE, ECOMM = range(7)
 UNIFORM, ZIPF = 0, 1
+LOCAL_MSD, LOCAL_LSD = 0, 1
 
 
 class GsortError(RuntimeError):
@@ -34,11 +35,16 @@ class Stats(ctypes.Structure):
                 ("ms_sample", ctypes.c_double), ("ms_merge", ctypes.c_double),
                 ("keys_local_in", ctypes.c_uint64), ("keys_local_out", ctypes.c_uint64),
                 ("bytes_sent", ctypes.c_uint64), ("max_pair_bytes", ctypes.c_uint64),
-                ("passes_run", ctypes.c_int), ("exchanges", ctypes.c_int)]
+                ("passes_run", ctypes.c_int), ("exchanges", ctypes.c_int),
+                ("ms_level", ctypes.c_double * 4), ("ms_bucket_sort", ctypes.c_double),
+                ("keys_level", ctypes.c_uint64 * 4), ("keys_bucket_sort", ctypes.c_uint64),
+                ("buckets_local", ctypes.c_uint64), ("local_algo", ctypes.c_int)]
 
     def as_dict(self):
         d = {k: getattr(self, k) for k, _ in self._fields_}
         d["ms_pass"] = list(self.ms_pass)
+        d["ms_level"] = list(self.ms_level)
+        d["keys_level"] = list(self.keys_level)
         return d
 
 
@@ -48,7 +54,8 @@ class Uid(ctypes.Structure):
 
 EXPORTS = [
     "gsort_get_uid", "gsort_create", "gsort_group_create", "gsort_group_destroy",
-    "gsort_create_in_group", "gsort_destroy", "gsort_reserve", "gsort_strerror",
+    "gsort_create_in_group", "gsort_destroy", "gsort_reserve", "gsort_set_local_algo",
+    "gsort_strerror",
     "gsort_last_error", "gsort_rank", "gsort_nranks", "gsort_radix", "gsort_sample",
     "gsort_sample_info", "gsort_scatter_from_root", "gsort_gather_to_root", "gsort_generate",
     "gsort_fingerprint", "gsort_device_alloc", "gsort_device_free", "gsort_copy_to_host",
@@ -81,6 +88,7 @@ def lib():
     L.gsort_create_in_group.argtypes = [P(VP), VP, I, I]
     L.gsort_destroy.argtypes = [VP]
     L.gsort_reserve.argtypes = [VP, SZ]
+    L.gsort_set_local_algo.argtypes = [VP, I]
     L.gsort_strerror.argtypes = [I]
     L.gsort_last_error.argtypes = [VP]
     L.gsort_rank.argtypes = [VP]
@@ -169,6 +177,10 @@ class Context:
 
     def reserve(self, n):
         self._c(lib().gsort_reserve(self.h, n))
+
+    def set_local_algo(self, algo):
+        """LOCAL_MSD (default) or LOCAL_LSD for every later local sort of this context."""
+        self._c(lib().gsort_set_local_algo(self.h, algo))
 
     def _sort(self, fn, d_keys, n):
         out, nout, st = ctypes.c_void_p(), ctypes.c_size_t(), Stats()

@@ -17,9 +17,12 @@ from conftest import case_input, case_output
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module")
-def ctx(gsort):
+@pytest.fixture(scope="module", params=["msd", "lsd"])
+def ctx(gsort, request):
+    """Both local-sort algorithms (MSD partitions + in-LDS buckets, and stable LSD passes)."""
     c = gsort.Context()
+    c.set_local_algo(gsort.LOCAL_MSD if request.param == "msd" else gsort.LOCAL_LSD)
+    c.algo = request.param
     yield c
     c.close()
 
@@ -78,9 +81,47 @@ def test_radix_one_gpu_value_edge_cases(ctx, orc):
     for name, keys in cases.items():
         got, st = sort_on_gpu(ctx, keys)
         assert np.array_equal(got, np.sort(keys)), name
-    # a single non-trivial digit runs one pass
-    _, st = sort_on_gpu(ctx, cases["low_byte_only"])
-    assert st["passes_run"] == 1
+    if ctx.algo == "lsd":  # a single non-trivial digit runs one pass
+        _, st = sort_on_gpu(ctx, cases["low_byte_only"])
+        assert st["passes_run"] == 1
+
+
+def _msd_cases(orc):
+    rng = np.random.default_rng(7)
+    half = np.concatenate([np.full(1 << 19, 123456, dtype=np.int32),
+                           orc.gen(orc.UNIFORM, 9, 1 << 19)])
+    rng.shuffle(half)
+    return {
+        # one bucket / first level only
+        "n_localmax": orc.gen(orc.UNIFORM, 1, 16384),
+        "n_localmax_plus1": orc.gen(orc.UNIFORM, 2, 16385),
+        "n_half_localmax_plus1": orc.gen(orc.UNIFORM, 3, 8193),
+        "uniform31_2p26": orc.gen(orc.UNIFORM, 6, 1 << 26),
+        # top digits trivial: buckets stay oversized down to the last level (digit 0)
+        "below_2p16": rng.integers(0, 1 << 16, 1 << 20).astype(np.int32),
+        "below_2p24": rng.integers(0, 1 << 24, 1 << 21).astype(np.int32),
+        "all_equal_big": np.full(1 << 20, -77, dtype=np.int32),
+        "zipf_2p22": orc.gen(orc.ZIPF, 4, 1 << 22),
+        "uniform_2p24": orc.gen(orc.UNIFORM, 5, 1 << 24),
+        "one_hot_bucket": half,
+        "negatives_2p21": rng.integers(-2**31, 2**31, 1 << 21, dtype=np.int64).astype(np.int32),
+        "bucket_edges": np.repeat(np.arange(-600, 600, dtype=np.int32) * 65536, 8190),
+        "full32_2p24": rng.integers(-2**31, 2**31, 1 << 24, dtype=np.int64).astype(np.int32),
+    }
+
+
+MSD_CASES = ["n_localmax", "n_localmax_plus1", "n_half_localmax_plus1", "uniform31_2p26",
+             "below_2p16", "below_2p24", "all_equal_big",
+             "zipf_2p22", "uniform_2p24", "one_hot_bucket", "negatives_2p21", "bucket_edges", "full32_2p24"]
+
+
+@pytest.mark.parametrize("name", MSD_CASES)
+def test_radix_one_gpu_bucket_regimes(ctx, orc, name):
+    """MSD level structure: single-bucket sorts, all-local first level, oversized buckets down
+    to the digit-0 level, one huge bucket among normal ones, exact kLocalMax boundaries."""
+    keys = _msd_cases(orc)[name]
+    got, st = sort_on_gpu(ctx, keys)
+    assert np.array_equal(got, np.sort(keys)), name
 
 
 def test_radix_matches_reference_golden_outputs(ctx, orc, ref_cases, ref_outputs):
@@ -106,7 +147,9 @@ def test_radix_2p28_properties(ctx, gsort, orc):
         ctx.generate(gsort.UNIFORM, 42, 0, n, p)
         fin = ctx.fingerprint(p, n)
         out, nout, st = ctx.radix(p, n)
-        assert nout == n and st["passes_run"] == 4
+        # MSD: the canonical keys use 31 bits: level 3 gives 128 buckets of ~2^21 keys,
+        # level 2 buckets of ~8192 keys, all within kLocalMax = 16384 -> two levels
+        assert nout == n and st["passes_run"] == (4 if ctx.algo == "lsd" else 2)
         fout = ctx.fingerprint(out, n)
         assert fout["sorted"] and (fout["sum"], fout["xor"]) == (fin["sum"], fin["xor"])
         # spot-check a window against the oracle's sort of a generated slice bound
