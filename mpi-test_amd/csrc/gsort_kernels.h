@@ -10,6 +10,7 @@ constexpr int kSweepBlock = 512;
 constexpr int kSweepItems = 16;
 constexpr int kSweepTile = kSweepBlock * kSweepItems;  // 8192 keys per workgroup tile
 constexpr int kScanGroup = 32;                           // tiles per K2a scan group
+constexpr int kPartBlock = 1024;                         // K3u: 1024 threads x 8 keys per tile
 constexpr int kRadix = 256;
 
 inline uint64_t sweep_tiles(uint64_t n) { return (n + kSweepTile - 1) / kSweepTile; }
@@ -52,23 +53,32 @@ hipError_t launch_select_splitters(const int32_t *samples, int m, int k, int nsp
 hipError_t launch_bucket_bounds(const int32_t *sorted, uint64_t n, const int32_t *splitters,
                                 int nsplit, uint64_t *bounds, hipStream_t s);
 // ---- MSD partition sort (gsort_kernels.hip, "MSD partition sort") -----------------------
-// K11 geometry: one 512-thread workgroup sorts a bucket of up to kLocalMax keys entirely in
-// LDS (32 keys per thread; 16 when every bucket of the launch has <= kLocalMax / 2 keys).
-constexpr int kLocalBlock = 512;
-constexpr uint64_t kLocalMax = 16384;
+// K11 geometry: one workgroup sorts a bucket entirely in LDS.  A stable pass costs a wave
+// ~16 rounds of 64 keys best (measured, tools/kexp3.hip), so the workgroup size follows the
+// bucket size: class 1 = 256 threads x 18 keys, class 2 = 512 x 18, class 3 = 512 x 32.
+constexpr int kLocalClasses = 3;
+constexpr uint64_t kLocalCap[kLocalClasses + 1] = {0, 256 * 18, 512 * 18, 512 * 32};
+constexpr uint64_t kLocalMax = kLocalCap[kLocalClasses];
+inline int local_class(uint64_t len) {
+    for (int k = 1; k <= kLocalClasses; ++k)
+        if (len <= kLocalCap[k]) return k;
+    return 0;
+}
 
+// K1 without the all-digit histograms: one block per tile (tcounts as launch_tile_counts).
+hipError_t launch_tile_counts1(const uint32_t *in, uint64_t n, int shift, bool flip,
+                               uint32_t *tcounts, hipStream_t s);
 // K3u, level 3: unstable partition of global tiles by digit shift/8 (offsets from K1/K2).
 hipError_t launch_partition(const uint32_t *in, uint32_t *out, uint64_t n, int shift,
                             const uint32_t *toff, const uint64_t *gpfx, const uint64_t *bases,
                             bool flip_in, hipStream_t s);
-// Work lists of child buckets: list[0] = next level (> lmax keys), list[1] = K11 with 16
-// keys per thread (1..small_max keys), list[2] = K11 with 32 keys per thread (small_max, lmax].
-// Each list is u64 pairs {start, len}; ctr[3*i .. 3*i+2] = {entries, keys, longest} of list i.
-// ctr == nullptr: no classification (the last level).
+// Work lists of child buckets: list[0] = next level (> kLocalMax keys), list[k] = K11 class k
+// (kLocalCap[k-1] < len <= kLocalCap[k]).  Each list is u64 pairs {start, len};
+// ctr[3*i .. 3*i+2] = {entries, keys, longest} of list i.  ctr == nullptr: no classification
+// (the last level).
 struct WorkLists {
-    uint64_t *list[3];
+    uint64_t *list[kLocalClasses + 1];
     uint64_t *ctr;
-    uint64_t small_max, lmax;
 };
 // The 256 level-3 buckets {bases[d], totals[d]} -> work lists.
 hipError_t launch_classify_buckets(const uint64_t *bases, const uint64_t *totals,
@@ -95,13 +105,13 @@ struct SegPass {
 hipError_t launch_seg_count(const SegPass &sp, hipStream_t s);
 // K3u over the planned segment tiles (after launch_seg_count).
 hipError_t launch_seg_partition(const SegPass &sp, hipStream_t s);
-// K11: sort each listed bucket (all <= maxlen <= kLocalMax keys) on digits 0..ndigits-1 in
-// LDS, store as int32 into out (same positions; in == out allowed).  flip_in: the input is
-// int32 (else ordered u32).  A list counter is {entries, keys, longest entry}.
-// atomic_rank: stable ranks from LDS atomics (lane-order property, checked at context
-// creation by launch_lds_order_check), else from wave64 ballots.
+// K11: sort each listed bucket (all of class cls: <= kLocalCap[cls] keys) on digits
+// 0..ndigits-1 in LDS, store as int32 into out (same positions; in == out allowed).
+// flip_in: the input is int32 (else ordered u32).  atomic_rank: stable ranks from LDS atomics
+// (lane-order property, checked at context creation by launch_lds_order_check), else from
+// wave64 ballots.
 hipError_t launch_local_sort(const uint32_t *in, uint32_t *out, const uint64_t *list,
-                             uint32_t nlist, uint64_t maxlen, int ndigits, bool flip_in,
+                             uint32_t nlist, int cls, int ndigits, bool flip_in,
                              bool atomic_rank, hipStream_t s);
 // Lane-order self-check: nblocks x 512 threads x 16 digits from `digits` (mod nbins);
 // bad[0] += violations (zeroed by the caller).

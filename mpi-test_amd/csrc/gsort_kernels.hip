@@ -657,25 +657,41 @@ __global__ __launch_bounds__(256) void k_seg_map(const uint32_t *__restrict__ tp
     for (uint32_t g = gpfx[s] + threadIdx.x; g < gpfx[s + 1]; g += 256) groupmap[g] = s;
 }
 
-// K1s: digit counts of every segment tile (one block per tile; grid may exceed the tiles).
-__global__ __launch_bounds__(256) void k_seg_counts(const uint32_t *__restrict__ in,
-                                                    const unsigned long long *__restrict__ segs,
-                                                    const uint32_t *__restrict__ tpfx,
-                                                    const uint32_t *__restrict__ gpfx,
-                                                    const uint32_t *__restrict__ segmap,
-                                                    uint32_t nseg, int shift,
-                                                    uint32_t *__restrict__ tcounts) {
+// K1s: digit counts of one tile per block: SEG=false, global tile t = [t*kSweepTile, ...);
+// SEG=true, tile t of the segment plan (grid may exceed the tiles).  Block-strided dword
+// loads (segments start anywhere), all issued before the first LDS atomic.
+template <int BLOCK, bool SEG, bool FIN>
+__global__ __launch_bounds__(BLOCK) void k_seg_counts(const uint32_t *__restrict__ in,
+                                                      uint64_t n,
+                                                      const unsigned long long *__restrict__ segs,
+                                                      const uint32_t *__restrict__ tpfx,
+                                                      const uint32_t *__restrict__ gpfx,
+                                                      const uint32_t *__restrict__ segmap,
+                                                      uint32_t nseg, int shift,
+                                                      uint32_t *__restrict__ tcounts) {
+    constexpr int ITEMS = kSweepTile / BLOCK;
     __shared__ uint32_t s_h[kRadix];
     const uint32_t t = blockIdx.x, tid = threadIdx.x;
-    const SegTile st = seg_tile(t, segs, tpfx, gpfx, segmap, nseg);
-    if (st.len == 0) return;
-    s_h[tid] = 0;
+    uint64_t t0;
+    uint32_t len;
+    if (SEG) {
+        const SegTile st = seg_tile(t, segs, tpfx, gpfx, segmap, nseg);
+        if (st.len == 0) return;
+        t0 = st.t0;
+        len = st.len;
+    } else {
+        t0 = (uint64_t)t * kSweepTile;
+        len = (uint32_t)(n - t0 < (uint64_t)kSweepTile ? n - t0 : (uint64_t)kSweepTile);
+    }
+    for (uint32_t b = tid; b < kRadix; b += BLOCK) s_h[b] = 0;
+    uint32_t k[ITEMS];
+    load_tile<BLOCK, ITEMS, FIN>(in + t0 + tid, len == (uint32_t)kSweepTile, len, k);
     __syncthreads();
-    const uint32_t *src = in + st.t0;
-#pragma unroll 8
-    for (uint32_t i = tid; i < st.len; i += 256) atomicAdd(&s_h[(src[i] >> shift) & 255u], 1u);
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i)
+        if ((uint32_t)(i * BLOCK) + tid < len) atomicAdd(&s_h[(k[i] >> shift) & 255u], 1u);
     __syncthreads();
-    tcounts[(uint64_t)t * kRadix + tid] = s_h[tid];
+    for (uint32_t b = tid; b < kRadix; b += BLOCK) tcounts[(uint64_t)t * kRadix + b] = s_h[b];
 }
 
 // K2s-a: group-local exclusive scan of the tile counts of each scan group (group = block).
@@ -703,18 +719,23 @@ __global__ __launch_bounds__(kRadix) void k_seg_scan_tiles(uint32_t *__restrict_
     gsum[(uint64_t)g * kRadix + d] = run;
 }
 
-// Child buckets -> work lists (WorkLists, gsort_kernels.h): > lmax keys to the next level,
-// (small_max, lmax] keys and 1..small_max keys to K11's two geometries.  A list is u64 pairs
-// {start, len}; its counter {entries, keys, longest entry}.  Called by all kRadix threads of a
-// block (one child each): the block reserves its entries with one global atomic per list, so
-// the counters see a few atomics per block, not one per child.
+// Child buckets -> work lists (WorkLists, gsort_kernels.h): > kLocalMax keys to the next
+// level, the rest to K11's size classes.  Called by all kRadix threads of a block (one child
+// each): the block reserves its entries with one global atomic per list, so the counters see
+// a few atomics per block, not one per child.
 __device__ __forceinline__ void classify_block(uint64_t start, uint64_t len, const WorkLists &wl) {
-    __shared__ unsigned int s_n[3];
-    __shared__ unsigned long long s_keys[3], s_max[3], s_base[3];
+    constexpr int NL = kLocalClasses + 1;
+    __shared__ unsigned int s_n[NL];
+    __shared__ unsigned long long s_keys[NL], s_max[NL], s_base[NL];
     const uint32_t tid = threadIdx.x;
-    if (tid < 3) { s_n[tid] = 0; s_keys[tid] = 0; s_max[tid] = 0; }
+    if (tid < NL) { s_n[tid] = 0; s_keys[tid] = 0; s_max[tid] = 0; }
     __syncthreads();
-    const int which = len > wl.lmax ? 0 : len > wl.small_max ? 2 : len > 0 ? 1 : -1;
+    int which = -1;
+    if (len > 0) {
+        which = 0;
+        for (int k = 1; k < NL; ++k)
+            if (len <= kLocalCap[k]) { which = k; break; }
+    }
     unsigned int idx = 0;
     if (which >= 0) {
         idx = atomicAdd(&s_n[which], 1u);
@@ -722,7 +743,7 @@ __device__ __forceinline__ void classify_block(uint64_t start, uint64_t len, con
         atomicMax(&s_max[which], (unsigned long long)len);
     }
     __syncthreads();
-    if (tid < 3 && s_n[tid]) {
+    if (tid < NL && s_n[tid]) {
         unsigned long long *ctr = reinterpret_cast<unsigned long long *>(wl.ctr) + 3 * tid;
         s_base[tid] = atomicAdd(&ctr[0], (unsigned long long)s_n[tid]);
         atomicAdd(&ctr[1], s_keys[tid]);
@@ -847,6 +868,7 @@ __global__ __launch_bounds__(BLOCK) void k_local_sort(const uint32_t *__restrict
     constexpr int WAVES = BLOCK / 64;
     constexpr int TILE = BLOCK * ITEMS;
     static_assert(TILE <= 65536, "ranks are packed as 16 bits");
+    static_assert(BLOCK >= kRadix, "one thread per digit in the scans");
     __shared__ uint32_t s_a[TILE];
     __shared__ uint32_t s_wc[WAVES * kRadix];  // per-wave digit counts, then offsets
     // the digit scans run while every key is in registers, so their 4 wave sums borrow the
@@ -979,6 +1001,10 @@ __global__ __launch_bounds__(512) void k_lds_order_check(const uint32_t *__restr
     if (nbad) atomicAdd(bad, (unsigned long long)nbad);
 }
 
+constexpr int cls_of(int block, int items) {
+    return block == 256 ? 1 : items == 18 ? 2 : 3;
+}
+
 unsigned grid_for(uint64_t n, unsigned block, unsigned cap) {
     uint64_t g = (n + block - 1) / block;
     if (g < 1) g = 1;
@@ -1086,6 +1112,19 @@ hipError_t launch_bucket_bounds(const int32_t *sorted, uint64_t n, const int32_t
     return hipGetLastError();
 }
 
+hipError_t launch_tile_counts1(const uint32_t *in, uint64_t n, int shift, bool flip,
+                               uint32_t *tcounts, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const unsigned g = (unsigned)sweep_tiles(n);
+    if (flip)
+        k_seg_counts<512, false, true><<<g, 512, 0, s>>>(in, n, nullptr, nullptr, nullptr, nullptr,
+                                                         0, shift, tcounts);
+    else
+        k_seg_counts<512, false, false><<<g, 512, 0, s>>>(in, n, nullptr, nullptr, nullptr,
+                                                          nullptr, 0, shift, tcounts);
+    return hipGetLastError();
+}
+
 hipError_t launch_partition(const uint32_t *in, uint32_t *out, uint64_t n, int shift,
                             const uint32_t *toff, const uint64_t *gpfx, const uint64_t *bases,
                             bool flip_in, hipStream_t s) {
@@ -1093,7 +1132,7 @@ hipError_t launch_partition(const uint32_t *in, uint32_t *out, uint64_t n, int s
     const unsigned g = (unsigned)sweep_tiles(n);
     auto *gp = reinterpret_cast<const unsigned long long *>(gpfx);
     auto *bs = reinterpret_cast<const unsigned long long *>(bases);
-    constexpr int B = kSweepBlock, I = kSweepItems;
+    constexpr int B = kPartBlock, I = kSweepTile / kPartBlock;
     if (flip_in) k_partition<B, I, true><<<g, B, 0, s>>>(in, out, n, shift, toff, gp, bs);
     else k_partition<B, I, false><<<g, B, 0, s>>>(in, out, n, shift, toff, gp, bs);
     return hipGetLastError();
@@ -1114,8 +1153,8 @@ hipError_t launch_seg_count(const SegPass &sp, hipStream_t s) {
     ull *gsum = reinterpret_cast<ull *>(sp.gsum);
     k_seg_plan<<<1, 1024, 0, s>>>(segs, sp.nseg, sp.tpfx, sp.gpfx);
     k_seg_map<<<sp.nseg, 256, 0, s>>>(sp.tpfx, sp.gpfx, sp.segmap, sp.groupmap);
-    k_seg_counts<<<sp.max_tiles, 256, 0, s>>>(sp.in, segs, sp.tpfx, sp.gpfx, sp.segmap, sp.nseg,
-                                              sp.shift, sp.tcounts);
+    k_seg_counts<512, true, false><<<sp.max_tiles, 512, 0, s>>>(
+        sp.in, 0, segs, sp.tpfx, sp.gpfx, sp.segmap, sp.nseg, sp.shift, sp.tcounts);
     k_seg_scan_tiles<<<sp.max_groups, kRadix, 0, s>>>(sp.tcounts, sp.tpfx, sp.gpfx, sp.groupmap,
                                                       sp.nseg, gsum);
     k_seg_scan_groups<<<sp.nseg, kRadix, 0, s>>>(gsum, segs, sp.gpfx,
@@ -1128,7 +1167,7 @@ hipError_t launch_seg_partition(const SegPass &sp, hipStream_t s) {
     if (sp.nseg == 0) return hipSuccess;
     const ull *segs = reinterpret_cast<const ull *>(sp.segs);
     ull *gsum = reinterpret_cast<ull *>(sp.gsum);
-    constexpr int B = kSweepBlock, I = kSweepItems;
+    constexpr int B = kPartBlock, I = kSweepTile / kPartBlock;
     if (sp.flip_out)
         k_seg_partition<B, I, true><<<sp.max_tiles, B, 0, s>>>(
             sp.in, sp.out, sp.shift, sp.tcounts, gsum, reinterpret_cast<const ull *>(sp.cstart),
@@ -1141,22 +1180,26 @@ hipError_t launch_seg_partition(const SegPass &sp, hipStream_t s) {
 }
 
 hipError_t launch_local_sort(const uint32_t *in, uint32_t *out, const uint64_t *list,
-                             uint32_t nlist, uint64_t maxlen, int ndigits, bool flip_in,
+                             uint32_t nlist, int cls, int ndigits, bool flip_in,
                              bool atomic_rank, hipStream_t s) {
     if (nlist == 0) return hipSuccess;
-    if (ndigits < 1 || ndigits > 4) return hipErrorInvalidValue;
-    if (maxlen > kLocalMax) return hipErrorInvalidValue;
+    if (ndigits < 1 || ndigits > 4 || cls < 1 || cls > kLocalClasses) return hipErrorInvalidValue;
     auto *l = reinterpret_cast<const unsigned long long *>(list);
-    constexpr int B = kLocalBlock;
-    // buckets <= kLocalMax / 2 keys: 16 keys per thread; larger: 32 (same workgroup size)
-#define GSORT_K11(I, FI, AT) k_local_sort<B, I, FI, AT><<<nlist, B, 0, s>>>(in, out, l, ndigits)
-    const bool small = maxlen <= (uint64_t)B * 16;
-    if (atomic_rank) {
-        if (small) { if (flip_in) GSORT_K11(16, true, true); else GSORT_K11(16, false, true); }
-        else { if (flip_in) GSORT_K11(32, true, true); else GSORT_K11(32, false, true); }
-    } else {
-        if (small) { if (flip_in) GSORT_K11(16, true, false); else GSORT_K11(16, false, false); }
-        else { if (flip_in) GSORT_K11(32, true, false); else GSORT_K11(32, false, false); }
+#define GSORT_K11(B, I)                                                                        \
+    do {                                                                                       \
+        static_assert((uint64_t)B * I == kLocalCap[cls_of(B, I)], "class geometry");          \
+        if (atomic_rank) {                                                                     \
+            if (flip_in) k_local_sort<B, I, true, true><<<nlist, B, 0, s>>>(in, out, l, ndigits); \
+            else k_local_sort<B, I, false, true><<<nlist, B, 0, s>>>(in, out, l, ndigits);        \
+        } else {                                                                               \
+            if (flip_in) k_local_sort<B, I, true, false><<<nlist, B, 0, s>>>(in, out, l, ndigits); \
+            else k_local_sort<B, I, false, false><<<nlist, B, 0, s>>>(in, out, l, ndigits);       \
+        }                                                                                      \
+    } while (0)
+    switch (cls) {
+        case 1: GSORT_K11(256, 18); break;
+        case 2: GSORT_K11(512, 18); break;
+        default: GSORT_K11(512, 32); break;
     }
 #undef GSORT_K11
     return hipGetLastError();

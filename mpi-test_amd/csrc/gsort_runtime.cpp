@@ -50,7 +50,7 @@ struct gsort_ctx {
     int local_algo = GSORT_LOCAL_MSD;
     bool atomic_rank = false;  // LDS lane-order property verified on this device (create)
     // MSD scratch: segment plan/maps, child starts, work lists (u64 {start, len} pairs)
-    DevBuf m_tpfx, m_gpfx, m_segmap, m_groupmap, m_cstart, m_next[2], m_local[2];
+    DevBuf m_tpfx, m_gpfx, m_segmap, m_groupmap, m_cstart, m_next[2], m_local[kLocalClasses];
     // device small area: [0, 8K) hist4 (4x256 u64) | [8K, 10K) pass digit totals (256 u64) |
     // [10K, 12K) pass digit bases (256 u64) | [20K, 256K) plans / samples / routing tables
     char *d_small = nullptr;
@@ -67,8 +67,8 @@ struct gsort_ctx {
 
 namespace {
 
-// [12K, 12K+72): MSD work-list counters, {entries, keys, longest} for the next-level list and
-// the two K11 lists; [12K+128, 12K+144): a one-entry list for a single-bucket sort
+// [12K, 12K+96): MSD work-list counters, {entries, keys, longest} for the next-level list and
+// the K11 class lists; [12K+128, 12K+144): a one-entry list for a single-bucket sort
 constexpr size_t OFF_HIST = 0, OFF_TOT = 8192, OFF_BASES = 10240, OFF_CTR = 12288,
                  OFF_ONE = 12416, OFF_PLAN = 20480;
 
@@ -243,15 +243,18 @@ gsort_status lsd_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *ou
 // tmp -> out -> tmp -> out, same positions); every bucket of <= kLocalMax keys is finished by
 // K11 in LDS and stored to out as int32.  The host reads two counters per level (a few us) to
 // size the next launches.  Same reference hot loops as lsd_sort.
+constexpr size_t kCtrBytes = 3 * 8 * (kLocalClasses + 1);
+static_assert(OFF_CTR + kCtrBytes <= OFF_ONE, "counter area");
+
 gsort_status ensure_list(gsort_ctx *c, DevBuf &b, uint64_t entries) {
     return ensure(c, b, (size_t)std::max<uint64_t>(entries, 1) * 16);
 }
 
 gsort_status read_counters(gsort_ctx *c, uint64_t *h) {
-    HIP_TRY(c, hipMemcpyAsync(c->h_small + OFF_CTR, c->d_small + OFF_CTR, 72,
+    HIP_TRY(c, hipMemcpyAsync(c->h_small + OFF_CTR, c->d_small + OFF_CTR, kCtrBytes,
                               hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
-    memcpy(h, c->h_small + OFF_CTR, 72);
+    memcpy(h, c->h_small + OFF_CTR, kCtrBytes);
     return GSORT_OK;
 }
 
@@ -267,7 +270,8 @@ gsort_status msd_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *ou
         h_one[1] = n;
         HIP_TRY(c, hipMemcpyAsync(d_one, h_one, 16, hipMemcpyHostToDevice, c->stream));
         hipEvent_t t = tic(c);
-        HIP_TRY(c, launch_local_sort(in, out, d_one, 1, n, 4, true, c->atomic_rank, c->stream));
+        HIP_TRY(c, launch_local_sort(in, out, d_one, 1, local_class(n), 4, true, c->atomic_rank,
+                                     c->stream));
         toc(c, PH_BUCKET, t);
         if (stats) { stats->buckets_local += 1; stats->keys_bucket_sort += n; }
         return GSORT_OK;
@@ -276,42 +280,38 @@ gsort_status msd_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *ou
     uint64_t *totals = reinterpret_cast<uint64_t *>(c->d_small + OFF_TOT);
     uint64_t *bases = reinterpret_cast<uint64_t *>(c->d_small + OFF_BASES);
     ST_TRY(ensure_list(c, c->m_next[0], kRadix));
-    ST_TRY(ensure_list(c, c->m_local[0], kRadix));
-    ST_TRY(ensure_list(c, c->m_local[1], kRadix));
+    for (auto &b : c->m_local) ST_TRY(ensure_list(c, b, kRadix));
     auto lst = [](DevBuf &b) { return reinterpret_cast<uint64_t *>(b.p); };
     auto lists = [&](int next) {
         WorkLists wl;
         wl.list[0] = lst(c->m_next[next]);
-        wl.list[1] = lst(c->m_local[0]);
-        wl.list[2] = lst(c->m_local[1]);
+        for (int k = 0; k < kLocalClasses; ++k) wl.list[k + 1] = lst(c->m_local[k]);
         wl.ctr = ctr;
-        wl.small_max = kLocalMax / 2;
-        wl.lmax = kLocalMax;
         return wl;
     };
 
     // level 3: global tiles
     hipEvent_t t = tic(c);
-    HIP_TRY(c, launch_tile_counts(in, n, 24, true, d_tcounts(c), nullptr, c->stream));
+    HIP_TRY(c, launch_tile_counts1(in, n, 24, true, d_tcounts(c), c->stream));
     HIP_TRY(c, launch_scan_tiles(d_tcounts(c), n, d_gsum(c), totals, bases, c->stream));
     toc(c, PH_COUNT, t);
     t = tic(c);
     HIP_TRY(c, launch_partition(in, tmp, n, 24, d_tcounts(c), d_gsum(c), bases, true, c->stream));
     toc(c, PH_LEVEL3, t);
     if (stats) stats->keys_level[0] += n;
-    HIP_TRY(c, hipMemsetAsync(ctr, 0, 72, c->stream));
+    HIP_TRY(c, hipMemsetAsync(ctr, 0, kCtrBytes, c->stream));
     HIP_TRY(c, launch_classify_buckets(bases, totals, lists(0), c->stream));
-    uint64_t h[9];  // {entries, keys, longest} of: next level, K11 small, K11 large
+    uint64_t h[3 * (kLocalClasses + 1)];  // {entries, keys, longest}: next level, K11 classes
     ST_TRY(read_counters(c, h));
     int levels = 1;
     uint32_t *cur = tmp;
     int cur_list = 0;
     for (int L = 2;; --L) {
-        for (int k = 0; k < 2; ++k) {  // buckets finished in LDS: digits L..0 remain
+        for (int k = 0; k < kLocalClasses; ++k) {  // buckets finished in LDS: digits L..0 remain
             const uint64_t *hk = h + 3 * (k + 1);
             if (!hk[0]) continue;
             t = tic(c);
-            HIP_TRY(c, launch_local_sort(cur, out, lst(c->m_local[k]), (uint32_t)hk[0], hk[2],
+            HIP_TRY(c, launch_local_sort(cur, out, lst(c->m_local[k]), (uint32_t)hk[0], k + 1,
                                          L + 1, false, c->atomic_rank, c->stream));
             toc(c, PH_BUCKET, t);
             if (stats) { stats->buckets_local += hk[0]; stats->keys_bucket_sort += hk[1]; }
@@ -330,8 +330,9 @@ gsort_status msd_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *ou
         ST_TRY(ensure(c, c->m_cstart, nseg * kRadix * 8));
         const uint64_t child_cap = std::min<uint64_t>(nseg * kRadix, keys);
         ST_TRY(ensure_list(c, c->m_next[cur_list ^ 1], std::min<uint64_t>(child_cap, keys / kLocalMax + 1)));
-        ST_TRY(ensure_list(c, c->m_local[0], child_cap));
-        ST_TRY(ensure_list(c, c->m_local[1], std::min<uint64_t>(child_cap, keys / (kLocalMax / 2) + 1)));
+        for (int k = 0; k < kLocalClasses; ++k)
+            ST_TRY(ensure_list(c, c->m_local[k],
+                               std::min<uint64_t>(child_cap, keys / (kLocalCap[k] + 1) + 1)));
         SegPass sp;
         sp.in = cur;
         sp.out = dst;
@@ -351,7 +352,7 @@ gsort_status msd_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *ou
         sp.lists = lists(cur_list ^ 1);
         if (L == 0) sp.lists.ctr = nullptr;  // digit 0: every child is a run of equal keys
         t = tic(c);
-        HIP_TRY(c, hipMemsetAsync(ctr, 0, 72, c->stream));
+        HIP_TRY(c, hipMemsetAsync(ctr, 0, kCtrBytes, c->stream));
         HIP_TRY(c, launch_seg_count(sp, c->stream));
         toc(c, PH_COUNT, t);
         t = tic(c);
@@ -755,8 +756,10 @@ gsort_status gsort_destroy(gsort_ctx *c) {
     if (c->tcounts.p) (void)hipFree(c->tcounts.p);
     if (c->gsum.p) (void)hipFree(c->gsum.p);
     for (DevBuf *b : {&c->m_tpfx, &c->m_gpfx, &c->m_segmap, &c->m_groupmap, &c->m_cstart,
-                      &c->m_next[0], &c->m_next[1], &c->m_local[0], &c->m_local[1]})
+                      &c->m_next[0], &c->m_next[1]})
         if (b->p) (void)hipFree(b->p);
+    for (auto &b : c->m_local)
+        if (b.p) (void)hipFree(b.p);
     if (c->d_small) (void)hipFree(c->d_small);
     if (c->h_small) (void)hipHostFree(c->h_small);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);

@@ -36,44 +36,43 @@ int main(int argc, char **argv) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    for (uint64_t bsize : {4096ull, 8192ull, 16384ull}) {
-        const uint64_t nb = n / bsize;
+    struct Cfg { uint64_t bsize; int block, items; };
+    const Cfg cfgs[] = {{4096, 512, 16}, {4096, 256, 16}, {2048, 256, 16}, {2048, 256, 8},
+                        {8192, 512, 16}, {8192, 512, 18}, {9000, 512, 18}, {9000, 512, 32},
+                        {9000, 1024, 16}, {16384, 512, 32}, {16384, 1024, 16}};
+    for (const Cfg &cf : cfgs) {
+        const uint64_t bsize = cf.bsize, nb = n / bsize;
         std::vector<unsigned long long> hl(2 * nb);
         for (uint64_t b = 0; b < nb; ++b) { hl[2 * b] = b * bsize; hl[2 * b + 1] = bsize; }
         CK(hipMemcpy(list, hl.data(), nb * 16, hipMemcpyHostToDevice));
-        for (int nd = 1; nd <= 3; ++nd) {
-            for (int big = 0; big < 4; ++big) {  // bit 0: 32 keys/thread, bit 1: ballot ranks
-                if (!(big & 1) && bsize > 8192) continue;
-                std::vector<float> t;
-                for (int r = 0; r < rounds; ++r) {
-                    CK(hipEventRecord(e0, s));
-                    if (big == 0) k_local_sort<512, 16, true, true><<<nb, 512, 0, s>>>(in, out, list, nd);
-                    if (big == 1) k_local_sort<512, 32, true, true><<<nb, 512, 0, s>>>(in, out, list, nd);
-                    if (big == 2) k_local_sort<512, 16, true, false><<<nb, 512, 0, s>>>(in, out, list, nd);
-                    if (big == 3) k_local_sort<512, 32, true, false><<<nb, 512, 0, s>>>(in, out, list, nd);
-                    CK(hipEventRecord(e1, s));
-                    CK(hipEventSynchronize(e1));
-                    float m;
-                    CK(hipEventElapsedTime(&m, e0, e1));
-                    t.push_back(m);
-                }
-                CK(hipMemcpy(h_out.data(), out, n * 4, hipMemcpyDeviceToHost));
-                const uint32_t mask = nd >= 4 ? 0xFFFFFFFFu : ((1u << (8 * nd)) - 1);
-                for (uint64_t b = 0; b < nb; b += 97) {
-                    std::vector<uint32_t> a(h_in.begin() + b * bsize, h_in.begin() + (b + 1) * bsize);
-                    std::vector<uint32_t> o(h_out.begin() + b * bsize, h_out.begin() + (b + 1) * bsize);
-                    for (uint64_t i = 1; i < bsize; ++i)
-                        if ((o[i] & mask) < (o[i - 1] & mask)) { printf("UNSORTED b=%llu\n", (unsigned long long)b); return 1; }
-                    std::sort(a.begin(), a.end());
-                    std::sort(o.begin(), o.end());
-                    if (a != o) { printf("NOT A PERMUTATION b=%llu\n", (unsigned long long)b); return 1; }
-                }
-                std::sort(t.begin(), t.end());
-                const float m = t[t.size() / 2];
-                printf("{\"bucket\": %llu, \"digits\": %d, \"items\": %d, \"rank\": \"%s\", \"ms\": %.4f, \"GBps\": %.1f}\n",
-                       (unsigned long long)bsize, nd, (big & 1) ? 32 : 16, (big & 2) ? "ballot" : "atomic", m,
-                       n * 8.0 / (m * 1e-3) / 1e9);
+        for (int nd = 2; nd <= 3; ++nd) {
+            std::vector<float> t;
+            for (int r = 0; r < rounds; ++r) {
+                CK(hipEventRecord(e0, s));
+#define L(B, I) if (cf.block == B && cf.items == I) k_local_sort<B, I, true, true><<<nb, B, 0, s>>>(in, out, list, nd)
+                L(256, 8); L(256, 16); L(512, 16); L(512, 18); L(512, 32); L(1024, 16);
+#undef L
+                CK(hipEventRecord(e1, s));
+                CK(hipEventSynchronize(e1));
+                float m;
+                CK(hipEventElapsedTime(&m, e0, e1));
+                t.push_back(m);
             }
+            CK(hipMemcpy(h_out.data(), out, n * 4, hipMemcpyDeviceToHost));
+            const uint32_t mask = (1u << (8 * nd)) - 1;
+            for (uint64_t b = 0; b < nb; b += 97) {
+                std::vector<uint32_t> a(h_in.begin() + b * bsize, h_in.begin() + (b + 1) * bsize);
+                std::vector<uint32_t> o(h_out.begin() + b * bsize, h_out.begin() + (b + 1) * bsize);
+                for (uint64_t i = 1; i < bsize; ++i)
+                    if ((o[i] & mask) < (o[i - 1] & mask)) { printf("UNSORTED b=%llu\n", (unsigned long long)b); return 1; }
+                std::sort(a.begin(), a.end());
+                std::sort(o.begin(), o.end());
+                if (a != o) { printf("NOT A PERMUTATION b=%llu\n", (unsigned long long)b); return 1; }
+            }
+            std::sort(t.begin(), t.end());
+            const float m = t[t.size() / 2];
+            printf("{\"bucket\": %llu, \"digits\": %d, \"block\": %d, \"items\": %d, \"ms\": %.4f, \"GBps\": %.1f}\n",
+                   (unsigned long long)bsize, nd, cf.block, cf.items, m, nb * bsize * 8.0 / (m * 1e-3) / 1e9);
         }
     }
     return 0;

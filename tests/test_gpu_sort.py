@@ -93,9 +93,13 @@ def _msd_cases(orc):
     rng.shuffle(half)
     return {
         # one bucket / first level only
+        # K11 class caps (kLocalCap: 4608, 9216, 16384) and one past each
+        "n_cap1": orc.gen(orc.UNIFORM, 11, 4608),
+        "n_cap1_plus1": orc.gen(orc.UNIFORM, 12, 4609),
+        "n_cap2": orc.gen(orc.UNIFORM, 13, 9216),
+        "n_cap2_plus1": orc.gen(orc.UNIFORM, 14, 9217),
         "n_localmax": orc.gen(orc.UNIFORM, 1, 16384),
         "n_localmax_plus1": orc.gen(orc.UNIFORM, 2, 16385),
-        "n_half_localmax_plus1": orc.gen(orc.UNIFORM, 3, 8193),
         "uniform31_2p26": orc.gen(orc.UNIFORM, 6, 1 << 26),
         # top digits trivial: buckets stay oversized down to the last level (digit 0)
         "below_2p16": rng.integers(0, 1 << 16, 1 << 20).astype(np.int32),
@@ -110,7 +114,8 @@ def _msd_cases(orc):
     }
 
 
-MSD_CASES = ["n_localmax", "n_localmax_plus1", "n_half_localmax_plus1", "uniform31_2p26",
+MSD_CASES = ["n_cap1", "n_cap1_plus1", "n_cap2", "n_cap2_plus1", "n_localmax",
+             "n_localmax_plus1", "uniform31_2p26",
              "below_2p16", "below_2p24", "all_equal_big",
              "zipf_2p22", "uniform_2p24", "one_hot_bucket", "negatives_2p21", "bucket_edges", "full32_2p24"]
 
@@ -148,7 +153,7 @@ def test_radix_2p28_properties(ctx, gsort, orc):
         fin = ctx.fingerprint(p, n)
         out, nout, st = ctx.radix(p, n)
         # MSD: the canonical keys use 31 bits: level 3 gives 128 buckets of ~2^21 keys,
-        # level 2 buckets of ~8192 keys, all within kLocalMax = 16384 -> two levels
+        # level 2 buckets of ~8192 keys, all within kLocalMax -> two levels
         assert nout == n and st["passes_run"] == (4 if ctx.algo == "lsd" else 2)
         fout = ctx.fingerprint(out, n)
         assert fout["sorted"] and (fout["sum"], fout["xor"]) == (fin["sum"], fin["xor"])
