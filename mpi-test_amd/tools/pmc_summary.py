@@ -4,8 +4,9 @@
 For every kernel: dispatches, average duration (kernel trace) and the average of every PMC
 counter per dispatch.  HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE / WRITE_SIZE are
 KiB; on gfx950 FETCH_SIZE reports half the bytes of a coalesced streaming read, so the read
-side is FETCH_SIZE * 1024 * 2.  The factor is checked on k_tile_counts, which reads exactly
-4 B per key once (`fetch_check` = corrected bytes / known bytes, expected 1.00).
+side is FETCH_SIZE * 1024 * 2.  The factor is checked on the level-3 tile count (K1:
+k_seg_counts<.., false, ..> or k_tile_counts), which reads exactly 4 B per key once
+(`fetch_check` = corrected bytes / known bytes, expected 1.00).
 """
 import csv
 import glob
@@ -58,7 +59,8 @@ def main(root):
         pass
     cal = summary["fetch_calibration"] = 2.0
     for k, v in summary["kernels"].items():
-        if k.startswith("k_tile_counts") and n and v.get("FETCH_SIZE"):
+        if (k.startswith("k_tile_counts") or k.startswith("k_seg_counts<512, false")) \
+                and n and v.get("FETCH_SIZE"):
             summary["fetch_check"] = v["FETCH_SIZE"] * 1024 * cal / (n * 4)
     for k, v in summary["kernels"].items():
         if "FETCH_SIZE" in v and "WRITE_SIZE" in v and cal:
