@@ -171,6 +171,13 @@ gsort_status gsort_plan_radix_route(int P, const uint64_t *hist, uint64_t B, int
                                     uint64_t *send, uint64_t *recv, uint64_t *seg,
                                     size_t *nseg);
 gsort_status gsort_plan_splitters(int P, const int32_t *samples, int32_t *splitters);
+/* gsort_plan_split: the one exchange of the distributed radix sort (replaces the per-digit
+ * routing of mpi_radix_sort.c:139,150-192).  n_all[P] = keys per rank (each block sorted);
+ * lt / le = P x (P-1): keys of rank p < / <= v_q, the g_q = min(qB, N)-th smallest key of all
+ * (B = ceil(N/P)).  Copies of v_q are taken left of a boundary in rank order.  Outputs the
+ * keys rank `me` sends to / receives from every rank (contiguous, in rank order). */
+gsort_status gsort_plan_split(int P, const uint64_t *n_all, const uint64_t *lt,
+                              const uint64_t *le, int me, uint64_t *send, uint64_t *recv);
 
 #ifdef __cplusplus
 }

@@ -43,6 +43,9 @@ hipError_t launch_place(const uint32_t *recv, uint32_t *out, const uint64_t *seg
 // K9 fingerprint: acc[0] += sum mix64(key), acc[1] ^= xor, acc[2] += #descents; acc zeroed.
 hipError_t launch_fingerprint(const int32_t *keys, uint64_t n, unsigned long long *acc,
                               hipStream_t s);
+// K13: out[i] = #keys of the sorted int32 block whose ordered-u32 form is < xs[i] (i < m).
+hipError_t launch_count_below(const int32_t *sorted, uint64_t n, const uint64_t *xs, int m,
+                              uint64_t *out, hipStream_t s);
 // K4 regular sampling: out[i] = sorted[i * interval], i < k (caller checks bounds).
 hipError_t launch_regular_sample(const int32_t *sorted, uint64_t interval, int k,
                                  int32_t *out, hipStream_t s);

@@ -417,6 +417,23 @@ __global__ __launch_bounds__(256) void k_fingerprint(const int32_t *__restrict__
     }
 }
 
+// K13: out[i] = #keys of the sorted int32 block `a` whose ordered u32 form is < xs[i] (u64:
+// 2^32 counts every key).  One thread per threshold, binary search.  Radix select of the exact
+// global splitters of the distributed radix sort (gsort_runtime.cpp, radix_dist).
+__global__ __launch_bounds__(256) void k_count_below(const int32_t *__restrict__ a, uint64_t n,
+                                                     const unsigned long long *__restrict__ xs,
+                                                     int m, unsigned long long *__restrict__ out) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= m) return;
+    const uint64_t x = xs[i];
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if ((uint64_t)((uint32_t)a[mid] ^ kFlip) < x) lo = mid + 1; else hi = mid;
+    }
+    out[i] = lo;
+}
+
 // K4: regular samples of a sorted block.
 __global__ void k_regular_sample(const int32_t *sorted, uint64_t interval, int k, int32_t *out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1088,6 +1105,15 @@ hipError_t launch_fingerprint(const int32_t *keys, uint64_t n, unsigned long lon
                               hipStream_t s) {
     if (n == 0) return hipSuccess;
     k_fingerprint<<<grid_for(n, 256, 2048), 256, 0, s>>>(keys, n, acc);
+    return hipGetLastError();
+}
+
+hipError_t launch_count_below(const int32_t *sorted, uint64_t n, const uint64_t *xs, int m,
+                              uint64_t *out, hipStream_t s) {
+    if (m <= 0) return hipSuccess;
+    k_count_below<<<(m + 255) / 256, 256, 0, s>>>(sorted, n,
+                                                  reinterpret_cast<const unsigned long long *>(xs),
+                                                  m, reinterpret_cast<unsigned long long *>(out));
     return hipGetLastError();
 }
 

@@ -69,3 +69,55 @@ extern "C" gsort_status gsort_plan_splitters(int P, const int32_t *samples, int3
     for (int i = 0; i < P - 1; ++i) splitters[i] = s[(size_t)(i + 1) * k];
     return GSORT_OK;
 }
+
+// Exact split of P locally sorted blocks into the global balanced blocks [qB, (q+1)B).
+// For each inner boundary q (1..P-1) at global position g_q = min(qB, N), v_q is the g_q-th
+// smallest key (found on device by radix select, gsort_runtime.cpp), lt[p][q-1] / le[p][q-1]
+// = keys of rank p that are < / <= v_q.  Copies of v_q left of the boundary
+// (L_q = g_q - sum_p lt) are taken from the ranks in rank order, so rank p's block is cut at
+//   s_p(q) = lt_p(q) + clamp(L_q - sum_{p'<p} eq_{p'}(q), 0, eq_p(q)),   eq = le - lt,
+// with s_p(0) = 0, s_p(P) = n_p and s_p(q) = n_p when g_q >= N.  Rank me sends
+// [s_me(q), s_me(q+1)) to q and receives s_p(me+1) - s_p(me) keys from each p.
+// (Replaces the per-pass digit routing through rank 0, mpi_radix_sort.c:139,150-192: one
+// exchange instead of one per base-P digit.)
+extern "C" gsort_status gsort_plan_split(int P, const uint64_t *n_all, const uint64_t *lt,
+                                         const uint64_t *le, int me, uint64_t *send,
+                                         uint64_t *recv) {
+    if (P < 1 || !n_all || (P > 1 && (!lt || !le)) || !send || !recv || me < 0 || me >= P)
+        return GSORT_EINVAL;
+    uint64_t N = 0;
+    for (int p = 0; p < P; ++p) N += n_all[p];
+    const uint64_t B = (N + P - 1) / P;
+    // cut[p][q], q = 0..P
+    std::vector<uint64_t> cut((size_t)P * (P + 1), 0);
+    for (int p = 0; p < P; ++p) cut[(size_t)p * (P + 1) + P] = n_all[p];
+    for (int q = 1; q < P; ++q) {
+        const uint64_t g = std::min<uint64_t>((uint64_t)q * B, N);
+        uint64_t lt_all = 0, eq_before = 0;
+        for (int p = 0; p < P; ++p) lt_all += lt[(size_t)p * (P - 1) + (q - 1)];
+        if (g >= N) {
+            for (int p = 0; p < P; ++p) cut[(size_t)p * (P + 1) + q] = n_all[p];
+            continue;
+        }
+        if (lt_all > g) return GSORT_EINVAL;  // counts inconsistent with v_q
+        const uint64_t L = g - lt_all;
+        for (int p = 0; p < P; ++p) {
+            const uint64_t l = lt[(size_t)p * (P - 1) + (q - 1)];
+            const uint64_t e = le[(size_t)p * (P - 1) + (q - 1)];
+            if (e < l || e > n_all[p]) return GSORT_EINVAL;
+            const uint64_t eq = e - l;
+            const uint64_t want = L > eq_before ? L - eq_before : 0;
+            cut[(size_t)p * (P + 1) + q] = l + std::min(want, eq);
+            eq_before += eq;
+        }
+    }
+    for (int q = 0; q < P; ++q) {
+        const uint64_t a = cut[(size_t)me * (P + 1) + q], b = cut[(size_t)me * (P + 1) + q + 1];
+        if (b < a) return GSORT_EINVAL;
+        send[q] = b - a;
+        const uint64_t ra = cut[(size_t)q * (P + 1) + me], rb = cut[(size_t)q * (P + 1) + me + 1];
+        if (rb < ra) return GSORT_EINVAL;
+        recv[q] = rb - ra;
+    }
+    return GSORT_OK;
+}

@@ -51,6 +51,7 @@ struct gsort_ctx {
     bool atomic_rank = false;  // LDS lane-order property verified on this device (create)
     // MSD scratch: segment plan/maps, child starts, work lists (u64 {start, len} pairs)
     DevBuf m_tpfx, m_gpfx, m_segmap, m_groupmap, m_cstart, m_next[2], m_local[kLocalClasses];
+    DevBuf m_split;  // radix select thresholds + counts of the distributed radix
     // device small area: [0, 8K) hist4 (4x256 u64) | [8K, 10K) pass digit totals (256 u64) |
     // [10K, 12K) pass digit bases (256 u64) | [20K, 256K) plans / samples / routing tables
     char *d_small = nullptr;
@@ -404,7 +405,110 @@ void block_of(uint64_t N, int P, int r, uint64_t *B, uint64_t *len) {
     *len = lo >= N ? 0 : std::min(*B, N - lo);
 }
 
-// ---- distributed LSD radix (P > 1) ------------------------------------------------------
+// ---- distributed radix (P > 1): local sort, exact splitters, ONE exchange, local sort ------
+// The reference keeps rank q on global positions [qB, (q+1)B) by routing every key through
+// rank 0 on each of its base-P passes (mpi_radix_sort.c:139 Scatter, :150-173 all-to-all,
+// :180-192 Gatherv).  Here: (1) each rank sorts its block (MSD local sort); (2) radix select of
+// the exact boundary keys: 4 rounds of 8 bits, each counting the keys below 257 thresholds per
+// boundary by binary search on the sorted blocks (K13) and all-gathering the counts; (3) the
+// cut of every block (gsort_plan_split: copies of a boundary key go left in rank order); (4) one
+// grouped send/recv of contiguous runs; (5) the received runs are sorted again locally.
+gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in,
+                              int32_t **d_out, uint64_t *n_out, gsort_stats *stats) {
+    const int P = c->nranks, me = c->rank;
+    std::vector<uint64_t> n_all;
+    ST_TRY(allgather_u64(c, n_in, n_all));
+    uint64_t N = 0;
+    for (uint64_t v : n_all) N += v;
+    uint64_t B, mine;
+    block_of(N, P, me, &B, &mine);
+    const uint64_t cap = std::max<uint64_t>(std::max(n_in, mine), 1);
+    ST_TRY(ensure(c, c->slot[S_SORTED], std::max<uint64_t>(n_in, 1) * 4));
+    ST_TRY(ensure(c, c->slot[S_TMP], cap * 4));
+    ST_TRY(ensure(c, c->slot[S_RECV], std::max<uint64_t>(mine, 1) * 4));
+    ST_TRY(ensure(c, c->slot[S_OUT], std::max<uint64_t>(mine, 1) * 4));
+    int32_t *sorted = slot_ptr<int32_t>(c, S_SORTED);
+    int pr = 0;
+    ST_TRY(local_sort(c, reinterpret_cast<const uint32_t *>(d_keys), n_in,
+                      reinterpret_cast<uint32_t *>(sorted), slot_ptr<uint32_t>(c, S_TMP), &pr,
+                      stats));
+
+    // (2) radix select of v_q, the g_q-th smallest key, for the P-1 inner boundaries
+    const int nb = P - 1, M = 257;
+    std::vector<uint64_t> g(nb), prefix(nb, 0), hx((size_t)nb * M), all((size_t)P * nb * M);
+    std::vector<int> dsel(nb, 0);
+    for (int q = 0; q < nb; ++q) g[q] = std::min<uint64_t>((uint64_t)(q + 1) * B, N);
+    ST_TRY(ensure(c, c->m_split, (size_t)nb * M * 16));
+    ST_TRY(ensure(c, c->slot[S_STAGE], (size_t)P * nb * M * 8));
+    uint64_t *d_xs = reinterpret_cast<uint64_t *>(c->m_split.p);
+    uint64_t *d_cnt = d_xs + (size_t)nb * M;
+    hipEvent_t t = tic(c);
+    for (int k = 0; k < 4; ++k) {
+        const int shift = 24 - 8 * k;
+        for (int q = 0; q < nb; ++q)
+            for (int d = 0; d < M; ++d) hx[(size_t)q * M + d] = prefix[q] + ((uint64_t)d << shift);
+        HIP_TRY(c, hipMemcpyAsync(d_xs, hx.data(), hx.size() * 8, hipMemcpyHostToDevice,
+                                  c->stream));
+        HIP_TRY(c, launch_count_below(sorted, n_in, d_xs, nb * M, d_cnt, c->stream));
+        ST_TRY(comm_try(c, c->comm->allgather(d_cnt, c->slot[S_STAGE].p, (size_t)nb * M * 8,
+                                              c->stream)));
+        HIP_TRY(c, hipMemcpyAsync(all.data(), c->slot[S_STAGE].p, all.size() * 8,
+                                  hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        for (int q = 0; q < nb; ++q) {
+            if (g[q] >= N) continue;  // boundary at the end: every key goes left
+            int best = 0;
+            for (int d = 0; d < 256; ++d) {
+                uint64_t below = 0;
+                for (int p = 0; p < P; ++p) below += all[((size_t)p * nb + q) * M + d];
+                if (below <= g[q]) best = d; else break;
+            }
+            dsel[q] = best;
+            prefix[q] += (uint64_t)best << shift;
+        }
+    }
+    toc(c, PH_SAMPLE, t);
+    // (3) cut points from the last round: lt = count(< v_q), le = count(< v_q + 1)
+    std::vector<uint64_t> lt((size_t)P * nb), le((size_t)P * nb), send(P), recv(P);
+    for (int p = 0; p < P; ++p)
+        for (int q = 0; q < nb; ++q) {
+            const uint64_t *row = &all[((size_t)p * nb + q) * M];
+            lt[(size_t)p * nb + q] = g[q] >= N ? n_all[p] : row[dsel[q]];
+            le[(size_t)p * nb + q] = g[q] >= N ? n_all[p] : row[dsel[q] + 1];
+        }
+    gsort_status ps = gsort_plan_split(P, n_all.data(), lt.data(), le.data(), me, send.data(),
+                                       recv.data());
+    if (ps != GSORT_OK) return set_err(c, ps, "inconsistent splitter counts");
+    // (4) one exchange
+    std::vector<size_t> sc(P), sd(P), rc(P), rd(P);
+    size_t so = 0, ro = 0;
+    for (int q = 0; q < P; ++q) {
+        sc[q] = send[q] * 4; sd[q] = so; so += sc[q];
+        rc[q] = recv[q] * 4; rd[q] = ro; ro += rc[q];
+        if (stats && q != me) {
+            stats->bytes_sent += sc[q];
+            stats->max_pair_bytes = std::max<uint64_t>(stats->max_pair_bytes, sc[q]);
+        }
+    }
+    if (ro != mine * 4) return set_err(c, GSORT_EINVAL, "exchange plan does not fill the block");
+    int32_t *rbuf = slot_ptr<int32_t>(c, S_RECV);
+    t = tic(c);
+    ST_TRY(comm_try(c, c->comm->alltoallv(sorted, sc.data(), sd.data(), rbuf, rc.data(),
+                                          rd.data(), c->stream)));
+    toc(c, PH_EXCH, t);
+    if (stats) stats->exchanges = 1;
+    // (5) the P received runs are sorted again (a P-way merge is DESIGN.md 9 work)
+    t = tic(c);
+    ST_TRY(local_sort(c, reinterpret_cast<const uint32_t *>(rbuf), mine,
+                      slot_ptr<uint32_t>(c, S_OUT), slot_ptr<uint32_t>(c, S_TMP), &pr, stats));
+    toc(c, PH_MERGE, t);
+    if (stats) stats->passes_run = pr;
+    *d_out = slot_ptr<int32_t>(c, S_OUT);
+    *n_out = mine;
+    return GSORT_OK;
+}
+
+// ---- distributed LSD radix (P > 1, GSORT_LOCAL_LSD) ----------------------------------------
 // Per non-trivial digit: local K1/K2 (tile counts; the digit totals of this rank), all-gather
 // of the P x 256 per-rank digit counts, local K3 (stable by digit), route contiguous slices to
 // the ranks owning their global positions (one grouped send/recv round), then place the
@@ -756,7 +860,7 @@ gsort_status gsort_destroy(gsort_ctx *c) {
     if (c->tcounts.p) (void)hipFree(c->tcounts.p);
     if (c->gsum.p) (void)hipFree(c->gsum.p);
     for (DevBuf *b : {&c->m_tpfx, &c->m_gpfx, &c->m_segmap, &c->m_groupmap, &c->m_cstart,
-                      &c->m_next[0], &c->m_next[1]})
+                      &c->m_next[0], &c->m_next[1], &c->m_split})
         if (b->p) (void)hipFree(b->p);
     for (auto &b : c->m_local)
         if (b.p) (void)hipFree(b.p);
@@ -808,8 +912,10 @@ gsort_status gsort_radix(gsort_ctx *c, const int32_t *d_keys, size_t n_local, in
         if (stats) stats->passes_run = pr;
         *d_out = slot_ptr<int32_t>(c, S_OUT);
         nout = n_local;
-    } else {
+    } else if (c->local_algo == GSORT_LOCAL_LSD) {
         st = radix_dist(c, d_keys, n_local, d_out, &nout, stats);
+    } else {
+        st = radix_dist_exact(c, d_keys, n_local, d_out, &nout, stats);
     }
     if (st != GSORT_OK) return st;
     toc(c, PH_TOTAL, t0);

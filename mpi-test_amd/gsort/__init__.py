@@ -60,7 +60,7 @@ EXPORTS = [
     "gsort_sample_info", "gsort_scatter_from_root", "gsort_gather_to_root", "gsort_generate",
     "gsort_fingerprint", "gsort_device_alloc", "gsort_device_free", "gsort_copy_to_host",
     "gsort_copy_to_device", "gsort_onesweep_tile", "gsort_plan_radix_route",
-    "gsort_plan_splitters", "gsort_parse_text",
+    "gsort_plan_splitters", "gsort_plan_split", "gsort_parse_text",
 ]
 
 _lib = None
@@ -107,6 +107,7 @@ def lib():
     L.gsort_copy_to_device.argtypes = [VP, VP, VP, SZ]
     L.gsort_plan_radix_route.argtypes = [I, VP, U64, I, VP, VP, VP, P(SZ)]
     L.gsort_plan_splitters.argtypes = [I, VP, VP]
+    L.gsort_plan_split.argtypes = [I, VP, VP, VP, I, VP, VP]
     L.gsort_parse_text.argtypes = [ctypes.c_char_p, SZ, VP, SZ, I]
     L.gsort_parse_text.restype = ctypes.c_longlong
     _lib = L
@@ -273,6 +274,20 @@ def plan_radix_route(hist, B, me):
                                         recv.ctypes.data, seg.ctypes.data, ctypes.byref(n)),
            None)
     return send, recv, seg[: 4 * n.value].reshape(-1, 4)
+
+
+def plan_split(n_all, lt, le, me):
+    """Host-only exact split of the distributed radix (gsort_plan_split): (send, recv)."""
+    import numpy as np
+    n_all = np.ascontiguousarray(n_all, dtype=np.uint64)
+    P = n_all.size
+    lt = np.ascontiguousarray(lt, dtype=np.uint64).reshape(P, max(P - 1, 0))
+    le = np.ascontiguousarray(le, dtype=np.uint64).reshape(P, max(P - 1, 0))
+    send = np.zeros(P, dtype=np.uint64)
+    recv = np.zeros(P, dtype=np.uint64)
+    _check(lib().gsort_plan_split(P, n_all.ctypes.data, lt.ctypes.data, le.ctypes.data, me,
+                                  send.ctypes.data, recv.ctypes.data), None)
+    return send, recv
 
 
 def plan_splitters(samples, P):

@@ -45,6 +45,53 @@ def test_radix_route_matches_oracle(gsort, orc):
                 assert np.array_equal(g1, g2), (P, trial, me)
 
 
+def _split_case(rng, P, kind):
+    n_all = rng.integers(0, 3000, P)
+    if kind == "empty_ranks":
+        n_all[rng.integers(0, P, max(1, P // 2))] = 0
+    if kind == "tiny":
+        n_all = rng.integers(0, 2, P)
+    hi = {"uniform": 2**31, "dups": 5, "one_value": 1, "empty_ranks": 100, "tiny": 3}[kind]
+    blocks = [np.sort(rng.integers(-hi, hi, int(k)).astype(np.int32)) for k in n_all]
+    return [int(k) for k in n_all], blocks
+
+
+@pytest.mark.parametrize("kind", ["uniform", "dups", "one_value", "empty_ranks", "tiny"])
+def test_plan_split_yields_the_global_blocks(gsort, kind):
+    """gsort_plan_split (the distributed radix's one exchange): with lt/le taken at the exact
+    boundary keys, the runs every rank receives concatenate to its global block
+    [qB, (q+1)B) of the sorted multiset -- including duplicate-heavy and empty ranks."""
+    rng = np.random.default_rng(sum(map(ord, kind)))
+    for P in (2, 3, 4, 5, 8):
+        for trial in range(6):
+            n_all, blocks = _split_case(rng, P, kind)
+            allk = np.sort(np.concatenate(blocks)) if sum(n_all) else np.zeros(0, np.int32)
+            N = allk.size
+            B = -(-N // P) if N else 0
+            lt = np.zeros((P, P - 1), np.uint64)
+            le = np.zeros((P, P - 1), np.uint64)
+            for q in range(1, P):
+                g = min(q * B, N)
+                for p in range(P):
+                    if g >= N:
+                        lt[p, q - 1] = le[p, q - 1] = n_all[p]
+                    else:
+                        v = allk[g]
+                        lt[p, q - 1] = np.searchsorted(blocks[p], v, "left")
+                        le[p, q - 1] = np.searchsorted(blocks[p], v, "right")
+            sends = [gsort.plan_split(n_all, lt, le, me) for me in range(P)]
+            for q in range(P):
+                # rank q receives, in rank order, the slice each p sends to q
+                parts = []
+                for p in range(P):
+                    s_p = sends[p][0]
+                    a = int(s_p[:q].sum())
+                    parts.append(blocks[p][a:a + int(s_p[q])])
+                    assert sends[q][1][p] == s_p[q]
+                got = np.sort(np.concatenate(parts))
+                assert np.array_equal(got, allk[q * B:(q + 1) * B]), (P, trial, q)
+
+
 def test_splitters_match_reference_fixtures(gsort, orc, ref_cases):
     n = 0
     for c in ref_cases:

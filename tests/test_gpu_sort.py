@@ -178,7 +178,7 @@ def test_fingerprint_matches_oracle(ctx, orc):
 # ---------------------------------------------------------------------------------------
 # multi-rank on one GPU (in-process rank group)
 # ---------------------------------------------------------------------------------------
-def run_group(gsort, blocks, algo):
+def run_group(gsort, blocks, algo, local="msd"):
     P = len(blocks)
     grp = gsort.Group(P)
     res, errs = [None] * P, []
@@ -186,6 +186,7 @@ def run_group(gsort, blocks, algo):
     def worker(r):
         try:
             with gsort.Context(rank=r, group=grp) as c:
+                c.set_local_algo(gsort.LOCAL_MSD if local == "msd" else gsort.LOCAL_LSD)
                 p = c.alloc(max(blocks[r].size, 1) * 4)
                 c.to_device(blocks[r], p)
                 fn = c.radix if algo == "radix" else c.sample
@@ -207,26 +208,57 @@ def run_group(gsort, blocks, algo):
     return res
 
 
+@pytest.mark.parametrize("local", ["msd", "lsd"])
 @pytest.mark.parametrize("P", [2, 3, 4, 8])
-def test_radix_multirank_balanced_blocks(gsort, orc, P):
+def test_radix_multirank_balanced_blocks(gsort, orc, P, local):
+    """msd: exact splitters + one exchange; lsd: one exchange per digit (the reference's pass
+    structure).  Both must leave rank q with global positions [qB, (q+1)B)."""
     for dist, n in ((orc.UNIFORM, 200003), (orc.ZIPF, 150000)):
         keys = orc.gen(dist, P, n)
         B = -(-n // P)
         blocks = [keys[r * B:(r + 1) * B] for r in range(P)]
-        res = run_group(gsort, blocks, "radix")
+        res = run_group(gsort, blocks, "radix", local)
         ref = np.sort(keys)
         for q in range(P):
             assert np.array_equal(res[q][0], ref[q * B:(q + 1) * B]), (P, dist, q)
+        if local == "msd":
+            assert all(r[1]["exchanges"] == 1 for r in res)
 
 
-def test_radix_multirank_uneven_and_empty_inputs(gsort, orc):
+@pytest.mark.parametrize("local", ["msd", "lsd"])
+def test_radix_multirank_uneven_and_empty_inputs(gsort, orc, local):
     keys = orc.gen(orc.UNIFORM, 9, 50000) - (1 << 30)
     blocks = [keys[:0], keys[:31000], keys[31000:31001], keys[31001:]]
-    res = run_group(gsort, blocks, "radix")
+    res = run_group(gsort, blocks, "radix", local)
     ref = np.sort(keys)
     B = -(-keys.size // 4)
     for q in range(4):
         assert np.array_equal(res[q][0], ref[q * B:(q + 1) * B])
+
+
+@pytest.mark.parametrize("case", ["all_equal", "two_values", "boundary_dups", "tiny",
+                                  "extremes", "big_uniform"])
+def test_radix_multirank_splitter_edges(gsort, orc, case):
+    """Exact splitters where a boundary key repeats across ranks and blocks (copies split in
+    rank order), fewer keys than ranks, INT_MIN/INT_MAX keys, and a 2^22-key sort."""
+    rng = np.random.default_rng(sum(map(ord, case)))
+    P = 5
+    keys = {
+        "all_equal": np.full(40003, 7, dtype=np.int32),
+        "two_values": rng.choice(np.array([-3, 9], dtype=np.int32), 30011),
+        "boundary_dups": np.repeat(np.arange(-4, 5, dtype=np.int32), 7777),
+        "tiny": np.array([5, -1, 5], dtype=np.int32),
+        "extremes": rng.choice(np.array([-2**31, 2**31 - 1, 0, -1], dtype=np.int32), 12345),
+        "big_uniform": orc.gen(orc.UNIFORM, 77, 1 << 22),
+    }[case]
+    rng.shuffle(keys)
+    cuts = np.sort(rng.integers(0, keys.size + 1, P - 1))
+    blocks = np.split(keys, cuts)
+    res = run_group(gsort, blocks, "radix")
+    ref = np.sort(keys)
+    B = -(-keys.size // P)
+    for q in range(P):
+        assert np.array_equal(res[q][0], ref[q * B:(q + 1) * B]), (case, q)
 
 
 @pytest.mark.parametrize("P", [2, 4, 8])
