@@ -116,6 +116,23 @@ hipError_t launch_seg_partition(const SegPass &sp, hipStream_t s);
 hipError_t launch_local_sort(const uint32_t *in, uint32_t *out, const uint64_t *list,
                              uint32_t nlist, int cls, int ndigits, bool flip_in,
                              bool atomic_rank, hipStream_t s);
+// ---- receive side of the distributed sorts: P sorted runs -> one sorted block -----------
+constexpr uint32_t kBuckets16 = 65536;  // buckets by the top 16 bits (ordered u32)
+// pos[p][h] (P x 65537 u64) = keys of run p (recv[roff[p] .. +rlen[p]), int32, sorted) below
+// bucket h; bsize / bstart (65536 u64) = bucket sizes and their exclusive scan; buckets are
+// classified into wl (next level: {bstart, len} segments; K11g classes: {h, len}).
+hipError_t launch_recv_plan(const int32_t *recv, const uint64_t *roff, const uint64_t *rlen, int P,
+                            uint64_t *pos, uint64_t *bsize, uint64_t *bstart, const WorkLists &wl,
+                            hipStream_t s);
+// K11g: gather the P pieces of every listed bucket, sort its low 16 bits in LDS, store int32
+// at out[bstart[h] ..).
+hipError_t launch_gather_sort(const int32_t *recv, const uint64_t *pos, const uint64_t *roff,
+                              int P, const uint64_t *bstart, const uint64_t *list, uint32_t nlist,
+                              int cls, bool atomic_rank, uint32_t *out, hipStream_t s);
+// Copy the pieces of every bucket > kLocalMax keys to out[bstart[h] ..) as ordered u32.
+hipError_t launch_gather_copy(const int32_t *recv, const uint64_t *pos, const uint64_t *roff,
+                              int P, const uint64_t *bsize, const uint64_t *bstart, uint32_t *out,
+                              hipStream_t s);
 // Lane-order self-check: nblocks x 512 threads x 16 digits from `digits` (mod nbins);
 // bad[0] += violations (zeroed by the caller).
 hipError_t launch_lds_order_check(const uint32_t *digits, uint32_t nblocks, uint32_t nbins,

@@ -872,28 +872,24 @@ __device__ __forceinline__ uint32_t wave_rank(uint32_t *wc, uint32_t d, bool val
     return prev + below;
 }
 
-// K11: sort each listed bucket (<= BLOCK * ITEMS keys) on digits 0 .. ndigits-1 in LDS and
-// write it back flipped to int32 order.  Digit 0 is ranked by block-wide LDS atomics (an LSD
-// sort may order equal first digits arbitrarily); every later digit is ranked stably per wave
+// Body of K11: the bucket's keys are in registers (k[i] = key i*BLOCK + threadIdx.x, ordered
+// u32, valid below len); sort them on digits 0 .. ndigits-1 in LDS and store them flipped to
+// int32 order at dst[0 .. len).  Digit 0 is ranked by block-wide LDS atomics (an LSD sort may
+// order equal first digits arbitrarily); every later digit is ranked stably per wave
 // (wave_rank) in (wave, round, lane) order over wave-contiguous chunks, then offset by the
 // (digit, wave)-major exclusive scan of the per-wave counts.
-template <int BLOCK, int ITEMS, bool FIN, bool ATOMIC>
-__global__ __launch_bounds__(BLOCK) void k_local_sort(const uint32_t *__restrict__ in,
-                                                      uint32_t *__restrict__ out,
-                                                      const unsigned long long *__restrict__ list,
-                                                      int ndigits) {
+template <int BLOCK, int ITEMS, bool ATOMIC>
+__device__ __forceinline__ void sort_bucket(uint32_t (&k)[ITEMS], uint32_t len, int ndigits,
+                                            uint32_t *__restrict__ dst, uint32_t *s_a,
+                                            uint32_t *s_wc) {
     constexpr int WAVES = BLOCK / 64;
     constexpr int TILE = BLOCK * ITEMS;
     static_assert(TILE <= 65536, "ranks are packed as 16 bits");
     static_assert(BLOCK >= kRadix, "one thread per digit in the scans");
-    __shared__ uint32_t s_a[TILE];
-    __shared__ uint32_t s_wc[WAVES * kRadix];  // per-wave digit counts, then offsets
     // the digit scans run while every key is in registers, so their 4 wave sums borrow the
     // tail of s_a (40 KiB per workgroup instead of 40 KiB + 16 B: 4 workgroups per CU)
     uint32_t *s_wsum = s_a + TILE - kRadix / 64;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const uint64_t start = list[2 * blockIdx.x];
-    const uint32_t len = (uint32_t)list[2 * blockIdx.x + 1];
     uint32_t *cnt = s_wc;  // digit 0: block-wide counters, then digit starts
 
     auto block_scan = [&](uint32_t c) -> uint32_t {  // tid < 256: exclusive scan over digits
@@ -907,12 +903,9 @@ __global__ __launch_bounds__(BLOCK) void k_local_sort(const uint32_t *__restrict
         return v - c;
     };
 
-    // digit 0: unstable counting sort from global into s_a
+    // digit 0: unstable counting sort into s_a (cnt zeroed by the caller before its barrier)
     {
-        if (tid < kRadix) cnt[tid] = 0;
-        uint32_t k[ITEMS], r[ITEMS];
-        load_tile<BLOCK, ITEMS, FIN>(in + start + tid, len == (uint32_t)TILE, len, k);
-        __syncthreads();
+        uint32_t r[ITEMS];
 #pragma unroll
         for (int i = 0; i < ITEMS; ++i)
             if ((uint32_t)(i * BLOCK + tid) < len) r[i] = atomicAdd(&cnt[k[i] & 255u], 1u);
@@ -938,7 +931,6 @@ __global__ __launch_bounds__(BLOCK) void k_local_sort(const uint32_t *__restrict
         uint32_t *wc = s_wc + w * kRadix;
 #pragma unroll
         for (int j = 0; j < kRadix / 64; ++j) wc[j * 64 + lane] = 0;
-        uint32_t k[ITEMS];
         const uint32_t base = (uint32_t)w * 64 * R + lane;
 #pragma unroll
         for (int i = 0; i < ITEMS; ++i)
@@ -978,8 +970,163 @@ __global__ __launch_bounds__(BLOCK) void k_local_sort(const uint32_t *__restrict
         }
         __syncthreads();
     }
-    uint32_t *dst = out + start;
     for (uint32_t j = tid; j < len; j += BLOCK) dst[j] = s_a[j] ^ kFlip;
+}
+
+// K11: sort each listed bucket {start, len} (<= BLOCK * ITEMS keys) of `in` on digits
+// 0 .. ndigits-1 in LDS and write it back flipped to int32 order at the same position of out.
+template <int BLOCK, int ITEMS, bool FIN, bool ATOMIC>
+__global__ __launch_bounds__(BLOCK) void k_local_sort(const uint32_t *__restrict__ in,
+                                                      uint32_t *__restrict__ out,
+                                                      const unsigned long long *__restrict__ list,
+                                                      int ndigits) {
+    constexpr int WAVES = BLOCK / 64;
+    constexpr int TILE = BLOCK * ITEMS;
+    __shared__ uint32_t s_a[TILE];
+    __shared__ uint32_t s_wc[WAVES * kRadix];  // per-wave digit counts, then offsets
+    const uint64_t start = list[2 * blockIdx.x];
+    const uint32_t len = (uint32_t)list[2 * blockIdx.x + 1];
+    if (threadIdx.x < kRadix) s_wc[threadIdx.x] = 0;
+    uint32_t k[ITEMS];
+    load_tile<BLOCK, ITEMS, FIN>(in + start + threadIdx.x, len == (uint32_t)TILE, len, k);
+    __syncthreads();
+    sort_bucket<BLOCK, ITEMS, ATOMIC>(k, len, ndigits, out + start, s_a, s_wc);
+}
+
+// K11g (receive side of the distributed sorts): bucket h of the 2^16 top-16-bit buckets of
+// the P received sorted runs.  Its keys are the P pieces recv[roff[p] + pos[p][h] ..
+// roff[p] + pos[p][h+1]) (int32); they are gathered, sorted on the low 16 bits in LDS and
+// stored at out[bstart[h] ..).  List entries are {h, len}.
+template <int BLOCK, int ITEMS, bool ATOMIC>
+__global__ __launch_bounds__(BLOCK) void k_gather_sort(const int32_t *__restrict__ recv,
+                                                       const unsigned long long *__restrict__ pos,
+                                                       const unsigned long long *__restrict__ roff,
+                                                       int P,
+                                                       const unsigned long long *__restrict__ bstart,
+                                                       const unsigned long long *__restrict__ list,
+                                                       uint32_t *__restrict__ out) {
+    constexpr int WAVES = BLOCK / 64;
+    constexpr int TILE = BLOCK * ITEMS;
+    constexpr int MAXP = 64;
+    __shared__ uint32_t s_a[TILE];
+    __shared__ uint32_t s_wc[WAVES * kRadix];
+    __shared__ uint64_t s_src[MAXP];  // piece p: first key in recv
+    __shared__ uint32_t s_cum[MAXP + 1];
+    const int tid = threadIdx.x;
+    const uint64_t h = list[2 * blockIdx.x];
+    const uint32_t len = (uint32_t)list[2 * blockIdx.x + 1];
+    if (tid < kRadix) s_wc[tid] = 0;
+    if (tid == 0) {
+        uint32_t cum = 0;
+        for (int p = 0; p < P; ++p) {
+            const uint64_t a = pos[(uint64_t)p * (kBuckets16 + 1) + h];
+            const uint64_t b = pos[(uint64_t)p * (kBuckets16 + 1) + h + 1];
+            s_src[p] = roff[p] + a;
+            s_cum[p] = cum;
+            cum += (uint32_t)(b - a);
+        }
+        s_cum[P] = cum;
+    }
+    __syncthreads();
+    uint32_t k[ITEMS];
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+        const uint32_t j = (uint32_t)(i * BLOCK + tid);
+        k[i] = 0;
+        if (j < len) {
+            int p = 0;
+            while (p + 1 < P && s_cum[p + 1] <= j) ++p;
+            k[i] = (uint32_t)recv[s_src[p] + (j - s_cum[p])] ^ kFlip;
+        }
+    }
+    __syncthreads();
+    sort_bucket<BLOCK, ITEMS, ATOMIC>(k, len, 2, out + bstart[h], s_a, s_wc);
+}
+
+// Receive side, K11g bookkeeping.  pos[p][h] = keys of sorted run p whose top 16 bits (ordered
+// u32) are < h, h = 0 .. 2^16 (binary search; one thread per (p, h)).
+__global__ __launch_bounds__(256) void k_run_bounds(const int32_t *__restrict__ recv,
+                                                    const unsigned long long *__restrict__ roff,
+                                                    const unsigned long long *__restrict__ rlen,
+                                                    int P, unsigned long long *__restrict__ pos) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (uint64_t)P * (kBuckets16 + 1)) return;
+    const uint32_t p = (uint32_t)(i / (kBuckets16 + 1)), h = (uint32_t)(i % (kBuckets16 + 1));
+    const int32_t *a = recv + roff[p];
+    const uint64_t x = (uint64_t)h << 16;
+    uint64_t lo = 0, hi = rlen[p];
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if ((uint64_t)((uint32_t)a[mid] ^ kFlip) < x) lo = mid + 1; else hi = mid;
+    }
+    pos[i] = lo;
+}
+
+// bsize[h] = sum_p pos[p][h+1] - pos[p][h]; bstart = exclusive scan (one 1024-thread block);
+// then classify the buckets (one 256-thread block per 256 buckets, classify_block): the
+// next-level list gets {bstart, len} (segments), the K11g lists get {h, len}.
+__global__ __launch_bounds__(1024) void k_bucket_scan(const unsigned long long *__restrict__ pos,
+                                                      int P, unsigned long long *__restrict__ bsize,
+                                                      unsigned long long *__restrict__ bstart) {
+    __shared__ unsigned long long s_w[16];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    constexpr uint32_t PER = kBuckets16 / 1024;
+    unsigned long long loc[PER], sum = 0;
+#pragma unroll 4
+    for (uint32_t j = 0; j < PER; ++j) {
+        const uint32_t h = tid * PER + j;
+        unsigned long long c = 0;
+        for (int p = 0; p < P; ++p)
+            c += pos[(uint64_t)p * (kBuckets16 + 1) + h + 1] - pos[(uint64_t)p * (kBuckets16 + 1) + h];
+        loc[j] = c;
+        sum += c;
+    }
+    unsigned long long v = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned long long t = __shfl_up(v, o);
+        if (lane >= o) v += t;
+    }
+    if (lane == 63) s_w[w] = v;
+    __syncthreads();
+    unsigned long long run = v - sum;
+    for (uint32_t ww = 0; ww < w; ++ww) run += s_w[ww];
+    for (uint32_t j = 0; j < PER; ++j) {
+        const uint32_t h = tid * PER + j;
+        bsize[h] = loc[j];
+        bstart[h] = run;
+        run += loc[j];
+    }
+}
+
+__global__ __launch_bounds__(kRadix) void k_classify_gather(
+    const unsigned long long *__restrict__ bsize, const unsigned long long *__restrict__ bstart,
+    WorkLists wl) {
+    const uint32_t h = blockIdx.x * kRadix + threadIdx.x;
+    const uint64_t len = bsize[h];
+    // next level: a segment of out; K11g: the bucket id
+    classify_block(len > kLocalMax ? bstart[h] : h, len, wl);
+}
+
+// Oversized receive buckets: gather their pieces into out[bstart[h] ..) as ordered u32 (they
+// continue through the MSD levels 1 and 0).  One block per bucket; others exit.
+__global__ __launch_bounds__(256) void k_gather_copy(const int32_t *__restrict__ recv,
+                                                     const unsigned long long *__restrict__ pos,
+                                                     const unsigned long long *__restrict__ roff,
+                                                     int P,
+                                                     const unsigned long long *__restrict__ bsize,
+                                                     const unsigned long long *__restrict__ bstart,
+                                                     uint32_t *__restrict__ out) {
+    const uint32_t h = blockIdx.x;
+    if (bsize[h] <= kLocalMax) return;
+    uint32_t *dst = out + bstart[h];
+    for (int p = 0; p < P; ++p) {
+        const uint64_t a = pos[(uint64_t)p * (kBuckets16 + 1) + h];
+        const uint64_t b = pos[(uint64_t)p * (kBuckets16 + 1) + h + 1];
+        const int32_t *src = recv + roff[p] + a;
+        for (uint64_t j = threadIdx.x; j < b - a; j += 256) dst[j] = (uint32_t)src[j] ^ kFlip;
+        dst += b - a;
+    }
 }
 
 // Self-check of the LDS lane-order property wave_rank<true> relies on: every wave of a block
@@ -1228,6 +1375,57 @@ hipError_t launch_local_sort(const uint32_t *in, uint32_t *out, const uint64_t *
         default: GSORT_K11(512, 32); break;
     }
 #undef GSORT_K11
+    return hipGetLastError();
+}
+
+hipError_t launch_recv_plan(const int32_t *recv, const uint64_t *roff, const uint64_t *rlen, int P,
+                            uint64_t *pos, uint64_t *bsize, uint64_t *bstart, const WorkLists &wl,
+                            hipStream_t s) {
+    using ull = unsigned long long;
+    if (P < 1 || P > 64) return hipErrorInvalidValue;
+    const uint64_t m = (uint64_t)P * (kBuckets16 + 1);
+    k_run_bounds<<<(unsigned)((m + 255) / 256), 256, 0, s>>>(
+        recv, reinterpret_cast<const ull *>(roff), reinterpret_cast<const ull *>(rlen), P,
+        reinterpret_cast<ull *>(pos));
+    k_bucket_scan<<<1, 1024, 0, s>>>(reinterpret_cast<const ull *>(pos), P,
+                                     reinterpret_cast<ull *>(bsize),
+                                     reinterpret_cast<ull *>(bstart));
+    k_classify_gather<<<kBuckets16 / kRadix, kRadix, 0, s>>>(
+        reinterpret_cast<const ull *>(bsize), reinterpret_cast<const ull *>(bstart), wl);
+    return hipGetLastError();
+}
+
+hipError_t launch_gather_sort(const int32_t *recv, const uint64_t *pos, const uint64_t *roff,
+                              int P, const uint64_t *bstart, const uint64_t *list, uint32_t nlist,
+                              int cls, bool atomic_rank, uint32_t *out, hipStream_t s) {
+    using ull = unsigned long long;
+    if (nlist == 0) return hipSuccess;
+    if (cls < 1 || cls > kLocalClasses || P < 1 || P > 64) return hipErrorInvalidValue;
+    auto *ps = reinterpret_cast<const ull *>(pos);
+    auto *ro = reinterpret_cast<const ull *>(roff);
+    auto *bs = reinterpret_cast<const ull *>(bstart);
+    auto *l = reinterpret_cast<const ull *>(list);
+#define GSORT_K11G(B, I)                                                                       \
+    do {                                                                                       \
+        if (atomic_rank) k_gather_sort<B, I, true><<<nlist, B, 0, s>>>(recv, ps, ro, P, bs, l, out); \
+        else k_gather_sort<B, I, false><<<nlist, B, 0, s>>>(recv, ps, ro, P, bs, l, out);       \
+    } while (0)
+    switch (cls) {
+        case 1: GSORT_K11G(256, 18); break;
+        case 2: GSORT_K11G(512, 18); break;
+        default: GSORT_K11G(512, 32); break;
+    }
+#undef GSORT_K11G
+    return hipGetLastError();
+}
+
+hipError_t launch_gather_copy(const int32_t *recv, const uint64_t *pos, const uint64_t *roff,
+                              int P, const uint64_t *bsize, const uint64_t *bstart, uint32_t *out,
+                              hipStream_t s) {
+    using ull = unsigned long long;
+    k_gather_copy<<<kBuckets16, 256, 0, s>>>(
+        recv, reinterpret_cast<const ull *>(pos), reinterpret_cast<const ull *>(roff), P,
+        reinterpret_cast<const ull *>(bsize), reinterpret_cast<const ull *>(bstart), out);
     return hipGetLastError();
 }
 

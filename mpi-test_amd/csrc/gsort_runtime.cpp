@@ -52,6 +52,7 @@ struct gsort_ctx {
     // MSD scratch: segment plan/maps, child starts, work lists (u64 {start, len} pairs)
     DevBuf m_tpfx, m_gpfx, m_segmap, m_groupmap, m_cstart, m_next[2], m_local[kLocalClasses];
     DevBuf m_split;  // radix select thresholds + counts of the distributed radix
+    DevBuf m_rpos, m_bsize;  // receive side: run bucket bounds (P x 65537), bucket size/start
     // device small area: [0, 8K) hist4 (4x256 u64) | [8K, 10K) pass digit totals (256 u64) |
     // [10K, 12K) pass digit bases (256 u64) | [20K, 256K) plans / samples / routing tables
     char *d_small = nullptr;
@@ -259,55 +260,27 @@ gsort_status read_counters(gsort_ctx *c, uint64_t *h) {
     return GSORT_OK;
 }
 
-gsort_status msd_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *out,
-                      uint32_t *tmp, gsort_stats *stats) {
-    if (n == 0) return GSORT_OK;
-    uint64_t *ctr = reinterpret_cast<uint64_t *>(c->d_small + OFF_CTR);
-    if (n <= kLocalMax) {  // one bucket: all four digits in LDS
-        uint64_t *h_one = reinterpret_cast<uint64_t *>(c->h_small + OFF_ONE);
-        uint64_t *d_one = reinterpret_cast<uint64_t *>(c->d_small + OFF_ONE);
-        HIP_TRY(c, hipStreamSynchronize(c->stream));  // h_one may feed an earlier copy
-        h_one[0] = 0;
-        h_one[1] = n;
-        HIP_TRY(c, hipMemcpyAsync(d_one, h_one, 16, hipMemcpyHostToDevice, c->stream));
-        hipEvent_t t = tic(c);
-        HIP_TRY(c, launch_local_sort(in, out, d_one, 1, local_class(n), 4, true, c->atomic_rank,
-                                     c->stream));
-        toc(c, PH_BUCKET, t);
-        if (stats) { stats->buckets_local += 1; stats->keys_bucket_sort += n; }
-        return GSORT_OK;
-    }
-    ST_TRY(ensure_pass_scratch(c, n));
-    uint64_t *totals = reinterpret_cast<uint64_t *>(c->d_small + OFF_TOT);
-    uint64_t *bases = reinterpret_cast<uint64_t *>(c->d_small + OFF_BASES);
-    ST_TRY(ensure_list(c, c->m_next[0], kRadix));
-    for (auto &b : c->m_local) ST_TRY(ensure_list(c, b, kRadix));
-    auto lst = [](DevBuf &b) { return reinterpret_cast<uint64_t *>(b.p); };
-    auto lists = [&](int next) {
-        WorkLists wl;
-        wl.list[0] = lst(c->m_next[next]);
-        for (int k = 0; k < kLocalClasses; ++k) wl.list[k + 1] = lst(c->m_local[k]);
-        wl.ctr = ctr;
-        return wl;
-    };
+WorkLists work_lists(gsort_ctx *c, int next) {
+    WorkLists wl;
+    wl.list[0] = reinterpret_cast<uint64_t *>(c->m_next[next].p);
+    for (int k = 0; k < kLocalClasses; ++k)
+        wl.list[k + 1] = reinterpret_cast<uint64_t *>(c->m_local[k].p);
+    wl.ctr = reinterpret_cast<uint64_t *>(c->d_small + OFF_CTR);
+    return wl;
+}
 
-    // level 3: global tiles
-    hipEvent_t t = tic(c);
-    HIP_TRY(c, launch_tile_counts1(in, n, 24, true, d_tcounts(c), c->stream));
-    HIP_TRY(c, launch_scan_tiles(d_tcounts(c), n, d_gsum(c), totals, bases, c->stream));
-    toc(c, PH_COUNT, t);
-    t = tic(c);
-    HIP_TRY(c, launch_partition(in, tmp, n, 24, d_tcounts(c), d_gsum(c), bases, true, c->stream));
-    toc(c, PH_LEVEL3, t);
-    if (stats) stats->keys_level[0] += n;
-    HIP_TRY(c, hipMemsetAsync(ctr, 0, kCtrBytes, c->stream));
-    HIP_TRY(c, launch_classify_buckets(bases, totals, lists(0), c->stream));
-    uint64_t h[3 * (kLocalClasses + 1)];  // {entries, keys, longest}: next level, K11 classes
-    ST_TRY(read_counters(c, h));
-    int levels = 1;
-    uint32_t *cur = tmp;
-    int cur_list = 0;
-    for (int L = 2;; --L) {
+// The MSD levels L, L-1, .. 0 (gsort_kernels.hip, "MSD partition sort").  On entry h holds
+// the counters of the work lists filled by level L+1: m_next[cur_list] (buckets still larger
+// than kLocalMax, ordered u32 in `cur`) and m_local[k] (K11 buckets of `cur`, digits L..0
+// left).  Level L partitions cur -> the other buffer (tmp <-> out); level 0 stores int32 into
+// out, as does K11.
+gsort_status msd_levels(gsort_ctx *c, int L, uint32_t *cur, uint32_t *out, uint32_t *tmp,
+                        int cur_list, uint64_t *h, gsort_stats *stats, int *levels) {
+    auto lst = [](DevBuf &b) { return reinterpret_cast<uint64_t *>(b.p); };
+    uint64_t *ctr = reinterpret_cast<uint64_t *>(c->d_small + OFF_CTR);
+    auto lists = [&](int next) { return work_lists(c, next); };
+    hipEvent_t t;
+    for (;; --L) {
         for (int k = 0; k < kLocalClasses; ++k) {  // buckets finished in LDS: digits L..0 remain
             const uint64_t *hk = h + 3 * (k + 1);
             if (!hk[0]) continue;
@@ -360,12 +333,56 @@ gsort_status msd_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *ou
         HIP_TRY(c, launch_seg_partition(sp, c->stream));
         toc(c, PH_LEVEL3 + (3 - L), t);
         if (stats) stats->keys_level[3 - L] += keys;
-        ++levels;
+        ++*levels;
         if (L == 0) break;
         ST_TRY(read_counters(c, h));
         cur = dst;
         cur_list ^= 1;
     }
+    return GSORT_OK;
+}
+
+
+gsort_status msd_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *out,
+                      uint32_t *tmp, gsort_stats *stats) {
+    if (n == 0) return GSORT_OK;
+    uint64_t *ctr = reinterpret_cast<uint64_t *>(c->d_small + OFF_CTR);
+    if (n <= kLocalMax) {  // one bucket: all four digits in LDS
+        uint64_t *h_one = reinterpret_cast<uint64_t *>(c->h_small + OFF_ONE);
+        uint64_t *d_one = reinterpret_cast<uint64_t *>(c->d_small + OFF_ONE);
+        HIP_TRY(c, hipStreamSynchronize(c->stream));  // h_one may feed an earlier copy
+        h_one[0] = 0;
+        h_one[1] = n;
+        HIP_TRY(c, hipMemcpyAsync(d_one, h_one, 16, hipMemcpyHostToDevice, c->stream));
+        hipEvent_t t = tic(c);
+        HIP_TRY(c, launch_local_sort(in, out, d_one, 1, local_class(n), 4, true, c->atomic_rank,
+                                     c->stream));
+        toc(c, PH_BUCKET, t);
+        if (stats) { stats->buckets_local += 1; stats->keys_bucket_sort += n; }
+        return GSORT_OK;
+    }
+    ST_TRY(ensure_pass_scratch(c, n));
+    uint64_t *totals = reinterpret_cast<uint64_t *>(c->d_small + OFF_TOT);
+    uint64_t *bases = reinterpret_cast<uint64_t *>(c->d_small + OFF_BASES);
+    ST_TRY(ensure_list(c, c->m_next[0], kRadix));
+    for (auto &b : c->m_local) ST_TRY(ensure_list(c, b, kRadix));
+    auto lists = [&](int next) { return work_lists(c, next); };
+
+    // level 3: global tiles
+    hipEvent_t t = tic(c);
+    HIP_TRY(c, launch_tile_counts1(in, n, 24, true, d_tcounts(c), c->stream));
+    HIP_TRY(c, launch_scan_tiles(d_tcounts(c), n, d_gsum(c), totals, bases, c->stream));
+    toc(c, PH_COUNT, t);
+    t = tic(c);
+    HIP_TRY(c, launch_partition(in, tmp, n, 24, d_tcounts(c), d_gsum(c), bases, true, c->stream));
+    toc(c, PH_LEVEL3, t);
+    if (stats) stats->keys_level[0] += n;
+    HIP_TRY(c, hipMemsetAsync(ctr, 0, kCtrBytes, c->stream));
+    HIP_TRY(c, launch_classify_buckets(bases, totals, lists(0), c->stream));
+    uint64_t h[3 * (kLocalClasses + 1)];  // {entries, keys, longest}: next level, K11 classes
+    ST_TRY(read_counters(c, h));
+    int levels = 1;
+    ST_TRY(msd_levels(c, 2, tmp, out, tmp, 0, h, stats, &levels));
     if (stats) stats->passes_run = levels;
     return GSORT_OK;
 }
@@ -381,6 +398,59 @@ gsort_status local_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *
     ST_TRY(msd_sort(c, in, n, out, tmp, st));
     if (passes_run) *passes_run = st->passes_run;
     if (stats) stats->passes_run = std::max(before, st->passes_run);
+    return GSORT_OK;
+}
+
+// ---- receive side: P sorted runs (after an exchange) -> one sorted block ---------------------
+// Replaces the re-sort of the received keys (the reference's final qsort, mpi_sample_sort.c:174;
+// for the radix path the last pass's placement, mpi_radix_sort.c:185-192).  The runs are
+// bucketed by their top 16 bits with binary searches (no pass over the keys), and K11g sorts
+// every bucket's low 16 bits straight from the P pieces: one read + one write per key.  Buckets
+// larger than kLocalMax are gathered into place and finish through the MSD levels 1 and 0.
+gsort_status recv_sort(gsort_ctx *c, const int32_t *recv, const std::vector<uint64_t> &rlen,
+                       uint64_t n, uint32_t *out, uint32_t *tmp, gsort_stats *stats) {
+    const int P = (int)rlen.size();
+    if (n == 0) return GSORT_OK;
+    if (P > 64 || c->local_algo == GSORT_LOCAL_LSD) {  // K11g holds at most 64 pieces
+        int pr = 0;
+        return local_sort(c, reinterpret_cast<const uint32_t *>(recv), n, out, tmp, &pr, stats);
+    }
+    hipEvent_t t = tic(c);
+    ST_TRY(ensure(c, c->m_rpos, (size_t)P * (kBuckets16 + 1) * 8));
+    ST_TRY(ensure(c, c->m_bsize, (size_t)kBuckets16 * 16));
+    ST_TRY(ensure_list(c, c->m_next[0], kBuckets16));
+    for (auto &b : c->m_local) ST_TRY(ensure_list(c, b, kBuckets16));
+    uint64_t *h_r = reinterpret_cast<uint64_t *>(c->h_small + OFF_PLAN);
+    uint64_t *d_r = reinterpret_cast<uint64_t *>(c->d_small + OFF_PLAN);
+    HIP_TRY(c, hipStreamSynchronize(c->stream));  // h_r may still feed an earlier copy
+    uint64_t off = 0;
+    for (int p = 0; p < P; ++p) { h_r[p] = off; h_r[P + p] = rlen[p]; off += rlen[p]; }
+    HIP_TRY(c, hipMemcpyAsync(d_r, h_r, (size_t)2 * P * 8, hipMemcpyHostToDevice, c->stream));
+    uint64_t *pos = reinterpret_cast<uint64_t *>(c->m_rpos.p);
+    uint64_t *bsize = reinterpret_cast<uint64_t *>(c->m_bsize.p), *bstart = bsize + kBuckets16;
+    uint64_t *ctr = reinterpret_cast<uint64_t *>(c->d_small + OFF_CTR);
+    HIP_TRY(c, hipMemsetAsync(ctr, 0, kCtrBytes, c->stream));
+    HIP_TRY(c, launch_recv_plan(recv, d_r, d_r + P, P, pos, bsize, bstart, work_lists(c, 0),
+                                c->stream));
+    toc(c, PH_COUNT, t);
+    uint64_t h[3 * (kLocalClasses + 1)];
+    ST_TRY(read_counters(c, h));
+    for (int k = 0; k < kLocalClasses; ++k) {
+        const uint64_t *hk = h + 3 * (k + 1);
+        if (!hk[0]) continue;
+        t = tic(c);
+        HIP_TRY(c, launch_gather_sort(recv, pos, d_r, P, bstart,
+                                      reinterpret_cast<uint64_t *>(c->m_local[k].p),
+                                      (uint32_t)hk[0], k + 1, c->atomic_rank, out, c->stream));
+        toc(c, PH_BUCKET, t);
+        if (stats) { stats->buckets_local += hk[0]; stats->keys_bucket_sort += hk[1]; }
+    }
+    if (h[0]) {  // oversized buckets: into place, then levels 1 and 0
+        HIP_TRY(c, launch_gather_copy(recv, pos, d_r, P, bsize, bstart, out, c->stream));
+        for (int k = 3; k < 3 * (kLocalClasses + 1); ++k) h[k] = 0;
+        int levels = 0;
+        ST_TRY(msd_levels(c, 1, out, out, tmp, 0, h, stats, &levels));
+    }
     return GSORT_OK;
 }
 
@@ -412,7 +482,8 @@ void block_of(uint64_t N, int P, int r, uint64_t *B, uint64_t *len) {
 // the exact boundary keys: 4 rounds of 8 bits, each counting the keys below 257 thresholds per
 // boundary by binary search on the sorted blocks (K13) and all-gathering the counts; (3) the
 // cut of every block (gsort_plan_split: copies of a boundary key go left in rank order); (4) one
-// grouped send/recv of contiguous runs; (5) the received runs are sorted again locally.
+// grouped send/recv of contiguous runs; (5) the received sorted runs are bucketed by their top
+// 16 bits and every bucket is finished in LDS (recv_sort).
 gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in,
                               int32_t **d_out, uint64_t *n_out, gsort_stats *stats) {
     const int P = c->nranks, me = c->rank;
@@ -497,10 +568,10 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
                                           rd.data(), c->stream)));
     toc(c, PH_EXCH, t);
     if (stats) stats->exchanges = 1;
-    // (5) the P received runs are sorted again (a P-way merge is DESIGN.md 9 work)
+    // (5) the P received sorted runs -> one sorted block (recv_sort)
     t = tic(c);
-    ST_TRY(local_sort(c, reinterpret_cast<const uint32_t *>(rbuf), mine,
-                      slot_ptr<uint32_t>(c, S_OUT), slot_ptr<uint32_t>(c, S_TMP), &pr, stats));
+    ST_TRY(recv_sort(c, rbuf, recv, mine, slot_ptr<uint32_t>(c, S_OUT),
+                     slot_ptr<uint32_t>(c, S_TMP), stats));
     toc(c, PH_MERGE, t);
     if (stats) stats->passes_run = pr;
     *d_out = slot_ptr<int32_t>(c, S_OUT);
@@ -709,10 +780,13 @@ gsort_status sample_dist(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in, int
                                           rd.data(), c->stream)));
     toc(c, PH_EXCH, t);
     if (stats) stats->exchanges = 1;
-    // final local order of the received bucket (mpi_sample_sort.c:174): re-sort the P runs
+    // final local order of the received bucket (mpi_sample_sort.c:174): the P received runs
+    // are sorted slices of the senders' sorted blocks -> recv_sort
+    std::vector<uint64_t> rlen(P);
+    for (int q = 0; q < P; ++q) rlen[q] = M[(size_t)q * P + me];
     t = tic(c);
-    ST_TRY(local_sort(c, reinterpret_cast<const uint32_t *>(rbuf), total,
-                      slot_ptr<uint32_t>(c, S_OUT), slot_ptr<uint32_t>(c, S_TMP), &pr));
+    ST_TRY(recv_sort(c, rbuf, rlen, total, slot_ptr<uint32_t>(c, S_OUT),
+                     slot_ptr<uint32_t>(c, S_TMP), stats));
     toc(c, PH_MERGE, t);
     if (stats) stats->passes_run = pr;
     *d_out = slot_ptr<int32_t>(c, S_OUT);
@@ -860,7 +934,7 @@ gsort_status gsort_destroy(gsort_ctx *c) {
     if (c->tcounts.p) (void)hipFree(c->tcounts.p);
     if (c->gsum.p) (void)hipFree(c->gsum.p);
     for (DevBuf *b : {&c->m_tpfx, &c->m_gpfx, &c->m_segmap, &c->m_groupmap, &c->m_cstart,
-                      &c->m_next[0], &c->m_next[1], &c->m_split})
+                      &c->m_next[0], &c->m_next[1], &c->m_split, &c->m_rpos, &c->m_bsize})
         if (b->p) (void)hipFree(b->p);
     for (auto &b : c->m_local)
         if (b.p) (void)hipFree(b.p);
