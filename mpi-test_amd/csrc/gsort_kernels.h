@@ -82,6 +82,7 @@ hipError_t launch_partition(const uint32_t *in, uint32_t *out, uint64_t n, int s
 struct WorkLists {
     uint64_t *list[kLocalClasses + 1];
     uint64_t *ctr;
+    bool force_next;  // every non-empty child to list[0]
 };
 // The 256 level-3 buckets {bases[d], totals[d]} -> work lists.
 hipError_t launch_classify_buckets(const uint64_t *bases, const uint64_t *totals,

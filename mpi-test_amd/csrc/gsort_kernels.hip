@@ -750,8 +750,9 @@ __device__ __forceinline__ void classify_block(uint64_t start, uint64_t len, con
     int which = -1;
     if (len > 0) {
         which = 0;
-        for (int k = 1; k < NL; ++k)
-            if (len <= kLocalCap[k]) { which = k; break; }
+        if (!wl.force_next)
+            for (int k = 1; k < NL; ++k)
+                if (len <= kLocalCap[k]) { which = k; break; }
     }
     unsigned int idx = 0;
     if (which >= 0) {
@@ -1016,28 +1017,53 @@ __global__ __launch_bounds__(BLOCK) void k_gather_sort(const int32_t *__restrict
     const uint64_t h = list[2 * blockIdx.x];
     const uint32_t len = (uint32_t)list[2 * blockIdx.x + 1];
     if (tid < kRadix) s_wc[tid] = 0;
-    if (tid == 0) {
-        uint32_t cum = 0;
-        for (int p = 0; p < P; ++p) {
-            const uint64_t a = pos[(uint64_t)p * (kBuckets16 + 1) + h];
-            const uint64_t b = pos[(uint64_t)p * (kBuckets16 + 1) + h + 1];
-            s_src[p] = roff[p] + a;
-            s_cum[p] = cum;
-            cum += (uint32_t)(b - a);
+    if (tid < 64) {  // lane p: piece p; wave scan of the piece lengths
+        uint64_t a = 0, b = 0;
+        if (tid < P) {
+            a = pos[(uint64_t)tid * (kBuckets16 + 1) + h];
+            b = pos[(uint64_t)tid * (kBuckets16 + 1) + h + 1];
         }
-        s_cum[P] = cum;
+        const uint32_t l = (uint32_t)(b - a);
+        uint32_t v = l;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t t = __shfl_up(v, o);
+            if (tid >= o) v += t;
+        }
+        if (tid < P) {
+            s_src[tid] = roff[tid] + a;
+            s_cum[tid] = v - l;
+        }
+        if (tid == P - 1) s_cum[P] = v;
+    }
+    __syncthreads();
+    // gather the pieces into s_a (coalesced per piece, 8 loads in flight per thread), then
+    // take the keys block-strided
+#pragma unroll 1
+    for (int p = 0; p < P; ++p) {
+        const int32_t *src = recv + s_src[p];
+        const uint32_t c0 = s_cum[p], c1 = s_cum[p + 1];
+#pragma unroll 1
+        for (uint32_t b = c0; b < c1; b += 8 * BLOCK) {
+            uint32_t v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const uint32_t j = b + u * BLOCK + tid;
+                v[u] = j < c1 ? (uint32_t)src[j - c0] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const uint32_t j = b + u * BLOCK + tid;
+                if (j < c1) s_a[j] = v[u] ^ kFlip;
+            }
+        }
     }
     __syncthreads();
     uint32_t k[ITEMS];
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
         const uint32_t j = (uint32_t)(i * BLOCK + tid);
-        k[i] = 0;
-        if (j < len) {
-            int p = 0;
-            while (p + 1 < P && s_cum[p + 1] <= j) ++p;
-            k[i] = (uint32_t)recv[s_src[p] + (j - s_cum[p])] ^ kFlip;
-        }
+        k[i] = j < len ? s_a[j] : 0u;
     }
     __syncthreads();
     sort_bucket<BLOCK, ITEMS, ATOMIC>(k, len, 2, out + bstart[h], s_a, s_wc);
@@ -1062,25 +1088,29 @@ __global__ __launch_bounds__(256) void k_run_bounds(const int32_t *__restrict__ 
     pos[i] = lo;
 }
 
-// bsize[h] = sum_p pos[p][h+1] - pos[p][h]; bstart = exclusive scan (one 1024-thread block);
-// then classify the buckets (one 256-thread block per 256 buckets, classify_block): the
-// next-level list gets {bstart, len} (segments), the K11g lists get {h, len}.
-__global__ __launch_bounds__(1024) void k_bucket_scan(const unsigned long long *__restrict__ pos,
-                                                      int P, unsigned long long *__restrict__ bsize,
+// bsize[h] = sum_p pos[p][h+1] - pos[p][h] (one thread per bucket); then bstart = exclusive
+// scan of bsize (one 1024-thread block, 64 buckets per thread); then the buckets are
+// classified (one 256-thread block per 256 buckets, classify_block): the next-level list gets
+// {bstart, len} (segments), the K11g lists get {h, len}.
+__global__ __launch_bounds__(256) void k_bucket_sizes(const unsigned long long *__restrict__ pos,
+                                                      int P,
+                                                      unsigned long long *__restrict__ bsize) {
+    const uint32_t h = blockIdx.x * 256 + threadIdx.x;
+    unsigned long long c = 0;
+    for (int p = 0; p < P; ++p)
+        c += pos[(uint64_t)p * (kBuckets16 + 1) + h + 1] - pos[(uint64_t)p * (kBuckets16 + 1) + h];
+    bsize[h] = c;
+}
+
+__global__ __launch_bounds__(1024) void k_bucket_scan(const unsigned long long *__restrict__ bsize,
                                                       unsigned long long *__restrict__ bstart) {
     __shared__ unsigned long long s_w[16];
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     constexpr uint32_t PER = kBuckets16 / 1024;
-    unsigned long long loc[PER], sum = 0;
-#pragma unroll 4
-    for (uint32_t j = 0; j < PER; ++j) {
-        const uint32_t h = tid * PER + j;
-        unsigned long long c = 0;
-        for (int p = 0; p < P; ++p)
-            c += pos[(uint64_t)p * (kBuckets16 + 1) + h + 1] - pos[(uint64_t)p * (kBuckets16 + 1) + h];
-        loc[j] = c;
-        sum += c;
-    }
+    const unsigned long long *b = bsize + tid * PER;
+    unsigned long long sum = 0;
+#pragma unroll 16
+    for (uint32_t j = 0; j < PER; ++j) sum += b[j];
     unsigned long long v = sum;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -1091,11 +1121,10 @@ __global__ __launch_bounds__(1024) void k_bucket_scan(const unsigned long long *
     __syncthreads();
     unsigned long long run = v - sum;
     for (uint32_t ww = 0; ww < w; ++ww) run += s_w[ww];
+#pragma unroll 16
     for (uint32_t j = 0; j < PER; ++j) {
-        const uint32_t h = tid * PER + j;
-        bsize[h] = loc[j];
-        bstart[h] = run;
-        run += loc[j];
+        bstart[tid * PER + j] = run;
+        run += b[j];
     }
 }
 
@@ -1387,8 +1416,9 @@ hipError_t launch_recv_plan(const int32_t *recv, const uint64_t *roff, const uin
     k_run_bounds<<<(unsigned)((m + 255) / 256), 256, 0, s>>>(
         recv, reinterpret_cast<const ull *>(roff), reinterpret_cast<const ull *>(rlen), P,
         reinterpret_cast<ull *>(pos));
-    k_bucket_scan<<<1, 1024, 0, s>>>(reinterpret_cast<const ull *>(pos), P,
-                                     reinterpret_cast<ull *>(bsize),
+    k_bucket_sizes<<<kBuckets16 / 256, 256, 0, s>>>(reinterpret_cast<const ull *>(pos), P,
+                                                     reinterpret_cast<ull *>(bsize));
+    k_bucket_scan<<<1, 1024, 0, s>>>(reinterpret_cast<const ull *>(bsize),
                                      reinterpret_cast<ull *>(bstart));
     k_classify_gather<<<kBuckets16 / kRadix, kRadix, 0, s>>>(
         reinterpret_cast<const ull *>(bsize), reinterpret_cast<const ull *>(bstart), wl);

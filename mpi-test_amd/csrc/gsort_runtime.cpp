@@ -53,6 +53,7 @@ struct gsort_ctx {
     DevBuf m_tpfx, m_gpfx, m_segmap, m_groupmap, m_cstart, m_next[2], m_local[kLocalClasses];
     DevBuf m_split;  // radix select thresholds + counts of the distributed radix
     DevBuf m_rpos, m_bsize;  // receive side: run bucket bounds (P x 65537), bucket size/start
+    DevBuf m_bseg, m_blist;  // boundary groups of the distributed radix: scratch, K11 list
     // device small area: [0, 8K) hist4 (4x256 u64) | [8K, 10K) pass digit totals (256 u64) |
     // [10K, 12K) pass digit bases (256 u64) | [20K, 256K) plans / samples / routing tables
     char *d_small = nullptr;
@@ -266,6 +267,7 @@ WorkLists work_lists(gsort_ctx *c, int next) {
     for (int k = 0; k < kLocalClasses; ++k)
         wl.list[k + 1] = reinterpret_cast<uint64_t *>(c->m_local[k].p);
     wl.ctr = reinterpret_cast<uint64_t *>(c->d_small + OFF_CTR);
+    wl.force_next = false;
     return wl;
 }
 
@@ -275,7 +277,8 @@ WorkLists work_lists(gsort_ctx *c, int next) {
 // left).  Level L partitions cur -> the other buffer (tmp <-> out); level 0 stores int32 into
 // out, as does K11.
 gsort_status msd_levels(gsort_ctx *c, int L, uint32_t *cur, uint32_t *out, uint32_t *tmp,
-                        int cur_list, uint64_t *h, gsort_stats *stats, int *levels) {
+                        int cur_list, uint64_t *h, gsort_stats *stats, int *levels,
+                        int last_level = 0) {
     auto lst = [](DevBuf &b) { return reinterpret_cast<uint64_t *>(b.p); };
     uint64_t *ctr = reinterpret_cast<uint64_t *>(c->d_small + OFF_CTR);
     auto lists = [&](int next) { return work_lists(c, next); };
@@ -313,7 +316,7 @@ gsort_status msd_levels(gsort_ctx *c, int L, uint32_t *cur, uint32_t *out, uint3
         sp.segs = lst(c->m_next[cur_list]);
         sp.nseg = (uint32_t)nseg;
         sp.shift = 8 * L;
-        sp.flip_out = L == 0;
+        sp.flip_out = L == last_level;
         sp.max_tiles = (uint32_t)max_tiles;
         sp.max_groups = (uint32_t)max_groups;
         sp.tpfx = reinterpret_cast<uint32_t *>(c->m_tpfx.p);
@@ -324,7 +327,8 @@ gsort_status msd_levels(gsort_ctx *c, int L, uint32_t *cur, uint32_t *out, uint3
         sp.gsum = d_gsum(c);
         sp.cstart = reinterpret_cast<uint64_t *>(c->m_cstart.p);
         sp.lists = lists(cur_list ^ 1);
-        if (L == 0) sp.lists.ctr = nullptr;  // digit 0: every child is a run of equal keys
+        // digit 0: every child is a run of equal keys; a partition-only sort stops here too
+        if (L == last_level) sp.lists.ctr = nullptr;
         t = tic(c);
         HIP_TRY(c, hipMemsetAsync(ctr, 0, kCtrBytes, c->stream));
         HIP_TRY(c, launch_seg_count(sp, c->stream));
@@ -334,7 +338,7 @@ gsort_status msd_levels(gsort_ctx *c, int L, uint32_t *cur, uint32_t *out, uint3
         toc(c, PH_LEVEL3 + (3 - L), t);
         if (stats) stats->keys_level[3 - L] += keys;
         ++*levels;
-        if (L == 0) break;
+        if (L == last_level) break;
         ST_TRY(read_counters(c, h));
         cur = dst;
         cur_list ^= 1;
@@ -343,8 +347,10 @@ gsort_status msd_levels(gsort_ctx *c, int L, uint32_t *cur, uint32_t *out, uint3
 }
 
 
+// group16: stop after level 2 -- out holds the keys (int32) grouped by their top 16 bits
+// (ordered u32) but not sorted inside a group (the sender side of the distributed radix).
 gsort_status msd_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *out,
-                      uint32_t *tmp, gsort_stats *stats) {
+                      uint32_t *tmp, gsort_stats *stats, bool group16 = false) {
     if (n == 0) return GSORT_OK;
     uint64_t *ctr = reinterpret_cast<uint64_t *>(c->d_small + OFF_CTR);
     if (n <= kLocalMax) {  // one bucket: all four digits in LDS
@@ -378,11 +384,13 @@ gsort_status msd_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *ou
     toc(c, PH_LEVEL3, t);
     if (stats) stats->keys_level[0] += n;
     HIP_TRY(c, hipMemsetAsync(ctr, 0, kCtrBytes, c->stream));
-    HIP_TRY(c, launch_classify_buckets(bases, totals, lists(0), c->stream));
+    WorkLists wl3 = lists(0);
+    wl3.force_next = group16;  // every level-3 bucket goes through level 2
+    HIP_TRY(c, launch_classify_buckets(bases, totals, wl3, c->stream));
     uint64_t h[3 * (kLocalClasses + 1)];  // {entries, keys, longest}: next level, K11 classes
     ST_TRY(read_counters(c, h));
     int levels = 1;
-    ST_TRY(msd_levels(c, 2, tmp, out, tmp, 0, h, stats, &levels));
+    ST_TRY(msd_levels(c, 2, tmp, out, tmp, 0, h, stats, &levels, group16 ? 2 : 0));
     if (stats) stats->passes_run = levels;
     return GSORT_OK;
 }
@@ -475,6 +483,40 @@ void block_of(uint64_t N, int P, int r, uint64_t *B, uint64_t *len) {
     *len = lo >= N ? 0 : std::min(*B, N - lo);
 }
 
+// Sort the listed groups {start, len} of an int32 block in place on their low 16 bits (their
+// top 16 bits are equal): K11 for groups of <= kLocalMax keys, the LSD passes otherwise.
+gsort_status sort_groups(gsort_ctx *c, int32_t *a,
+                         const std::vector<std::pair<uint64_t, uint64_t>> &groups) {
+    std::vector<uint64_t> small[kLocalClasses];
+    for (const auto &gr : groups) {
+        const int k = local_class(gr.second);
+        if (k) {
+            small[k - 1].push_back(gr.first);
+            small[k - 1].push_back(gr.second);
+            continue;
+        }
+        ST_TRY(ensure(c, c->m_bseg, gr.second * 8));
+        uint32_t *t0 = reinterpret_cast<uint32_t *>(c->m_bseg.p), *t1 = t0 + gr.second;
+        int pr = 0;  // lsd_sort leaves its result in its `out` (t0)
+        ST_TRY(lsd_sort(c, reinterpret_cast<const uint32_t *>(a + gr.first), gr.second, t0, t1,
+                        &pr));
+        HIP_TRY(c, hipMemcpyAsync(a + gr.first, t0, gr.second * 4, hipMemcpyDeviceToDevice,
+                                  c->stream));
+    }
+    for (int k = 0; k < kLocalClasses; ++k) {
+        if (small[k].empty()) continue;
+        ST_TRY(ensure(c, c->m_blist, small[k].size() * 8));
+        HIP_TRY(c, hipMemcpyAsync(c->m_blist.p, small[k].data(), small[k].size() * 8,
+                                  hipMemcpyHostToDevice, c->stream));
+        uint32_t *ab = reinterpret_cast<uint32_t *>(a);
+        HIP_TRY(c, launch_local_sort(ab, ab, reinterpret_cast<uint64_t *>(c->m_blist.p),
+                                     (uint32_t)(small[k].size() / 2), k + 1, 2, true,
+                                     c->atomic_rank, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));  // small[k] is host memory
+    }
+    return GSORT_OK;
+}
+
 // ---- distributed radix (P > 1): local sort, exact splitters, ONE exchange, local sort ------
 // The reference keeps rank q on global positions [qB, (q+1)B) by routing every key through
 // rank 0 on each of its base-P passes (mpi_radix_sort.c:139 Scatter, :150-173 all-to-all,
@@ -498,11 +540,18 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
     ST_TRY(ensure(c, c->slot[S_TMP], cap * 4));
     ST_TRY(ensure(c, c->slot[S_RECV], std::max<uint64_t>(mine, 1) * 4));
     ST_TRY(ensure(c, c->slot[S_OUT], std::max<uint64_t>(mine, 1) * 4));
+    // (1) group the block by its top 16 bits (MSD levels 3 and 2 only: the receivers sort the
+    // low 16 bits anyway); only the groups holding a boundary key get sorted, below
     int32_t *sorted = slot_ptr<int32_t>(c, S_SORTED);
-    int pr = 0;
-    ST_TRY(local_sort(c, reinterpret_cast<const uint32_t *>(d_keys), n_in,
-                      reinterpret_cast<uint32_t *>(sorted), slot_ptr<uint32_t>(c, S_TMP), &pr,
-                      stats));
+    if (stats) stats->local_algo = c->local_algo;
+    {
+        gsort_stats tmp_st;
+        memset(&tmp_st, 0, sizeof(tmp_st));
+        ST_TRY(msd_sort(c, reinterpret_cast<const uint32_t *>(d_keys), n_in,
+                        reinterpret_cast<uint32_t *>(sorted), slot_ptr<uint32_t>(c, S_TMP),
+                        stats ? stats : &tmp_st, true));
+    }
+    int pr = stats ? stats->passes_run : 0;
 
     // (2) radix select of v_q, the g_q-th smallest key, for the P-1 inner boundaries
     const int nb = P - 1, M = 257;
@@ -536,6 +585,18 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
             }
             dsel[q] = best;
             prefix[q] += (uint64_t)best << shift;
+        }
+        if (k == 1) {  // the 16-bit group of every boundary is known: sort it on this rank
+            std::vector<std::pair<uint64_t, uint64_t>> groups;
+            for (int q = 0; q < nb; ++q) {
+                if (g[q] >= N) continue;
+                const uint64_t *row = &all[((size_t)me * nb + q) * M];
+                if (row[dsel[q] + 1] > row[dsel[q]])
+                    groups.push_back({row[dsel[q]], row[dsel[q] + 1] - row[dsel[q]]});
+            }
+            std::sort(groups.begin(), groups.end());
+            groups.erase(std::unique(groups.begin(), groups.end()), groups.end());
+            ST_TRY(sort_groups(c, sorted, groups));
         }
     }
     toc(c, PH_SAMPLE, t);
@@ -934,7 +995,8 @@ gsort_status gsort_destroy(gsort_ctx *c) {
     if (c->tcounts.p) (void)hipFree(c->tcounts.p);
     if (c->gsum.p) (void)hipFree(c->gsum.p);
     for (DevBuf *b : {&c->m_tpfx, &c->m_gpfx, &c->m_segmap, &c->m_groupmap, &c->m_cstart,
-                      &c->m_next[0], &c->m_next[1], &c->m_split, &c->m_rpos, &c->m_bsize})
+                      &c->m_next[0], &c->m_next[1], &c->m_split, &c->m_rpos, &c->m_bsize,
+                      &c->m_bseg, &c->m_blist})
         if (b->p) (void)hipFree(b->p);
     for (auto &b : c->m_local)
         if (b.p) (void)hipFree(b.p);
