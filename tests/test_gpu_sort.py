@@ -237,7 +237,7 @@ def test_radix_multirank_uneven_and_empty_inputs(gsort, orc, local):
 
 
 @pytest.mark.parametrize("case", ["all_equal", "two_values", "boundary_dups", "tiny",
-                                  "extremes", "big_uniform"])
+                                  "extremes", "big_uniform", "big_groups"])
 def test_radix_multirank_splitter_edges(gsort, orc, case):
     """Exact splitters where a boundary key repeats across ranks and blocks (copies split in
     rank order), fewer keys than ranks, INT_MIN/INT_MAX keys, and a 2^22-key sort."""
@@ -250,6 +250,10 @@ def test_radix_multirank_splitter_edges(gsort, orc, case):
         "tiny": np.array([5, -1, 5], dtype=np.int32),
         "extremes": rng.choice(np.array([-2**31, 2**31 - 1, 0, -1], dtype=np.int32), 12345),
         "big_uniform": orc.gen(orc.UNIFORM, 77, 1 << 22),
+        # three 16-bit groups of 60000 keys each: boundary groups larger than kLocalMax on the
+        # sender (LSD group sort) and receive buckets larger than kLocalMax (gather + levels)
+        "big_groups": (np.repeat(np.array([-5, 0, 7], dtype=np.int64) << 16, 60000) +
+                       rng.integers(0, 1 << 16, 180000)).astype(np.int32),
     }[case]
     rng.shuffle(keys)
     cuts = np.sort(rng.integers(0, keys.size + 1, P - 1))
