@@ -119,20 +119,32 @@ hipError_t launch_local_sort(const uint32_t *in, uint32_t *out, const uint64_t *
                              bool atomic_rank, hipStream_t s);
 // ---- receive side of the distributed sorts: P sorted runs -> one sorted block -----------
 constexpr uint32_t kBuckets16 = 65536;  // buckets by the top 16 bits (ordered u32)
-// pos[p][h] (P x 65537 u64) = keys of run p (recv[roff[p] .. +rlen[p]), int32, sorted) below
-// bucket h; bsize / bstart (65536 u64) = bucket sizes and their exclusive scan; buckets are
-// classified into wl (next level: {bstart, len} segments; K11g classes: {h, len}).
-hipError_t launch_recv_plan(const int32_t *recv, const uint64_t *roff, const uint64_t *rlen, int P,
-                            uint64_t *pos, uint64_t *bsize, uint64_t *bstart, const WorkLists &wl,
-                            hipStream_t s);
-// K11g: gather the P pieces of every listed bucket, sort its low 16 bits in LDS, store int32
-// at out[bstart[h] ..).
-hipError_t launch_gather_sort(const int32_t *recv, const uint64_t *pos, const uint64_t *roff,
-                              int P, const uint64_t *bstart, const uint64_t *list, uint32_t nlist,
-                              int cls, bool atomic_rank, uint32_t *out, hipStream_t s);
+// pos[p][h] (P x 65537 u64) = keys of run p (recv[roff[p] .. +rlen[p]), int32, grouped by
+// the top 16 bits) below bucket h, by binary search.
+hipError_t launch_run_bounds(const int32_t *recv, const uint64_t *roff, const uint64_t *rlen,
+                             int P, uint64_t *pos, hipStream_t s);
+// pos[p][h] from source p's counts of buckets [h_lo, h_lo + nh) at meta + moff[p]
+// (moff[p] = ~0: nothing received from p) -- the packed exchange.
+hipError_t launch_pos_from_meta(const uint32_t *meta, const uint64_t *moff, uint32_t h_lo,
+                                uint32_t nh, int P, uint64_t *pos, hipStream_t s);
+// bsize / bstart (65536 u64) = bucket sizes and their exclusive scan; buckets classified into
+// wl (next level: {bstart, len} segments; K11g classes: {h, len}).
+hipError_t launch_recv_classify(const uint64_t *pos, int P, uint64_t *bsize, uint64_t *bstart,
+                                const WorkLists &wl, hipStream_t s);
+// K11g: gather the P pieces of every listed bucket (int32 keys, or packed16: the low 16 bits),
+// sort its low 16 bits in LDS, store int32 at out[bstart[h] ..).
+hipError_t launch_gather_sort(const void *recv, bool packed16, const uint64_t *pos,
+                              const uint64_t *roff, int P, const uint64_t *bstart,
+                              const uint64_t *list, uint32_t nlist, int cls, bool atomic_rank,
+                              uint32_t *out, hipStream_t s);
 // Copy the pieces of every bucket > kLocalMax keys to out[bstart[h] ..) as ordered u32.
-hipError_t launch_gather_copy(const int32_t *recv, const uint64_t *pos, const uint64_t *roff,
-                              int P, const uint64_t *bsize, const uint64_t *bstart, uint32_t *out,
+hipError_t launch_gather_copy(const void *recv, bool packed16, const uint64_t *pos,
+                              const uint64_t *roff, int P, const uint64_t *bsize,
+                              const uint64_t *bstart, uint32_t *out, hipStream_t s);
+// Sender of the packed exchange: out[i] = low 16 bits of a[i]; meta counts per destination
+// range (rng: nrng x {a, b, h_lo, nh, out_off}; gb = 65537 bucket bounds of the block).
+hipError_t launch_pack16(const int32_t *a, uint64_t n, uint16_t *out, hipStream_t s);
+hipError_t launch_meta_counts(const uint64_t *gb, const uint64_t *rng, int nrng, uint32_t *meta,
                               hipStream_t s);
 // Lane-order self-check: nblocks x 512 threads x 16 digits from `digits` (mod nbins);
 // bad[0] += violations (zeroed by the caller).

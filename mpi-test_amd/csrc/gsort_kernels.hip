@@ -998,8 +998,13 @@ __global__ __launch_bounds__(BLOCK) void k_local_sort(const uint32_t *__restrict
 // the P received sorted runs.  Its keys are the P pieces recv[roff[p] + pos[p][h] ..
 // roff[p] + pos[p][h+1]) (int32); they are gathered, sorted on the low 16 bits in LDS and
 // stored at out[bstart[h] ..).  List entries are {h, len}.
-template <int BLOCK, int ITEMS, bool ATOMIC>
-__global__ __launch_bounds__(BLOCK) void k_gather_sort(const int32_t *__restrict__ recv,
+// A received key in ordered-u32 form: int32 payload (flip), or the low 16 bits of a key whose
+// top 16 bits are the bucket h (the packed exchange of the distributed radix).
+__device__ __forceinline__ uint32_t recv_key(int32_t x, uint32_t) { return (uint32_t)x ^ kFlip; }
+__device__ __forceinline__ uint32_t recv_key(uint16_t x, uint32_t h) { return (h << 16) | x; }
+
+template <int BLOCK, int ITEMS, bool ATOMIC, typename T>
+__global__ __launch_bounds__(BLOCK) void k_gather_sort(const T *__restrict__ recv,
                                                        const unsigned long long *__restrict__ pos,
                                                        const unsigned long long *__restrict__ roff,
                                                        int P,
@@ -1041,20 +1046,20 @@ __global__ __launch_bounds__(BLOCK) void k_gather_sort(const int32_t *__restrict
     // take the keys block-strided
 #pragma unroll 1
     for (int p = 0; p < P; ++p) {
-        const int32_t *src = recv + s_src[p];
+        const T *src = recv + s_src[p];
         const uint32_t c0 = s_cum[p], c1 = s_cum[p + 1];
 #pragma unroll 1
         for (uint32_t b = c0; b < c1; b += 8 * BLOCK) {
-            uint32_t v[8];
+            T v[8];
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
                 const uint32_t j = b + u * BLOCK + tid;
-                v[u] = j < c1 ? (uint32_t)src[j - c0] : 0u;
+                v[u] = j < c1 ? src[j - c0] : T(0);
             }
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
                 const uint32_t j = b + u * BLOCK + tid;
-                if (j < c1) s_a[j] = v[u] ^ kFlip;
+                if (j < c1) s_a[j] = recv_key(v[u], (uint32_t)h);
             }
         }
     }
@@ -1139,7 +1144,8 @@ __global__ __launch_bounds__(kRadix) void k_classify_gather(
 
 // Oversized receive buckets: gather their pieces into out[bstart[h] ..) as ordered u32 (they
 // continue through the MSD levels 1 and 0).  One block per bucket; others exit.
-__global__ __launch_bounds__(256) void k_gather_copy(const int32_t *__restrict__ recv,
+template <typename T>
+__global__ __launch_bounds__(256) void k_gather_copy(const T *__restrict__ recv,
                                                      const unsigned long long *__restrict__ pos,
                                                      const unsigned long long *__restrict__ roff,
                                                      int P,
@@ -1152,10 +1158,66 @@ __global__ __launch_bounds__(256) void k_gather_copy(const int32_t *__restrict__
     for (int p = 0; p < P; ++p) {
         const uint64_t a = pos[(uint64_t)p * (kBuckets16 + 1) + h];
         const uint64_t b = pos[(uint64_t)p * (kBuckets16 + 1) + h + 1];
-        const int32_t *src = recv + roff[p] + a;
-        for (uint64_t j = threadIdx.x; j < b - a; j += 256) dst[j] = (uint32_t)src[j] ^ kFlip;
+        const T *src = recv + roff[p] + a;
+        for (uint64_t j = threadIdx.x; j < b - a; j += 256) dst[j] = recv_key(src[j], h);
         dst += b - a;
     }
+}
+
+// Packed exchange of the distributed radix (sender): the low 16 bits of every key (the top 16
+// are implied by the bucket each piece belongs to, sent as counts).
+__global__ __launch_bounds__(256) void k_pack16(const int32_t *__restrict__ a, uint64_t n,
+                                                uint16_t *__restrict__ out) {
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride)
+        out[i] = (uint16_t)(uint32_t)a[i];
+}
+
+// Sender: for destination block q (rng[5q..] = {a, b, h_lo, nh, out_off}), meta[out_off + i] =
+// keys of this rank's cut [a, b) in bucket h_lo + i (gb = bucket bounds of the grouped block).
+__global__ __launch_bounds__(256) void k_meta_counts(const unsigned long long *__restrict__ gb,
+                                                     const unsigned long long *__restrict__ rng,
+                                                     uint32_t *__restrict__ meta) {
+    const unsigned long long *r = rng + 5 * blockIdx.x;
+    const uint64_t a = r[0], b = r[1], h0 = r[2], nh = r[3], off = r[4];
+    for (uint64_t i = threadIdx.x; i < nh; i += 256) {
+        const uint64_t x = gb[h0 + i], y = gb[h0 + i + 1];
+        const uint64_t lo = x > a ? x : a, hi = y < b ? y : b;
+        meta[off + i] = (uint32_t)(hi > lo ? hi - lo : 0);
+    }
+}
+
+// Receiver: pos[p][h] (h = 0 .. 2^16) from source p's bucket counts for buckets
+// [h_lo, h_lo + nh) at meta + moff[p] (moff[p] = ~0: nothing from p).  One block per source.
+__global__ __launch_bounds__(1024) void k_pos_from_meta(const uint32_t *__restrict__ meta,
+                                                        const unsigned long long *__restrict__ moff,
+                                                        uint32_t h_lo, uint32_t nh,
+                                                        unsigned long long *__restrict__ pos) {
+    __shared__ unsigned long long s_w[16];
+    const uint32_t p = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const unsigned long long mo = moff[p];
+    constexpr uint32_t PER = kBuckets16 / 1024;
+    auto cnt = [&](uint32_t h) -> unsigned long long {
+        return (mo != ~0ull && h >= h_lo && h - h_lo < nh) ? meta[mo + (h - h_lo)] : 0ull;
+    };
+    unsigned long long sum = 0;
+    for (uint32_t j = 0; j < PER; ++j) sum += cnt(tid * PER + j);
+    unsigned long long v = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned long long t = __shfl_up(v, o);
+        if (lane >= o) v += t;
+    }
+    if (lane == 63) s_w[w] = v;
+    __syncthreads();
+    unsigned long long run = v - sum;
+    for (uint32_t ww = 0; ww < w; ++ww) run += s_w[ww];
+    unsigned long long *pp = pos + (uint64_t)p * (kBuckets16 + 1);
+    for (uint32_t j = 0; j < PER; ++j) {
+        pp[tid * PER + j] = run;
+        run += cnt(tid * PER + j);
+    }
+    if (tid == 1023) pp[kBuckets16] = run;
 }
 
 // Self-check of the LDS lane-order property wave_rank<true> relies on: every wave of a block
@@ -1407,15 +1469,29 @@ hipError_t launch_local_sort(const uint32_t *in, uint32_t *out, const uint64_t *
     return hipGetLastError();
 }
 
-hipError_t launch_recv_plan(const int32_t *recv, const uint64_t *roff, const uint64_t *rlen, int P,
-                            uint64_t *pos, uint64_t *bsize, uint64_t *bstart, const WorkLists &wl,
-                            hipStream_t s) {
+hipError_t launch_run_bounds(const int32_t *recv, const uint64_t *roff, const uint64_t *rlen,
+                             int P, uint64_t *pos, hipStream_t s) {
     using ull = unsigned long long;
     if (P < 1 || P > 64) return hipErrorInvalidValue;
     const uint64_t m = (uint64_t)P * (kBuckets16 + 1);
     k_run_bounds<<<(unsigned)((m + 255) / 256), 256, 0, s>>>(
         recv, reinterpret_cast<const ull *>(roff), reinterpret_cast<const ull *>(rlen), P,
         reinterpret_cast<ull *>(pos));
+    return hipGetLastError();
+}
+
+hipError_t launch_pos_from_meta(const uint32_t *meta, const uint64_t *moff, uint32_t h_lo,
+                                uint32_t nh, int P, uint64_t *pos, hipStream_t s) {
+    using ull = unsigned long long;
+    if (P < 1 || P > 64) return hipErrorInvalidValue;
+    k_pos_from_meta<<<P, 1024, 0, s>>>(meta, reinterpret_cast<const ull *>(moff), h_lo, nh,
+                                       reinterpret_cast<ull *>(pos));
+    return hipGetLastError();
+}
+
+hipError_t launch_recv_classify(const uint64_t *pos, int P, uint64_t *bsize, uint64_t *bstart,
+                                const WorkLists &wl, hipStream_t s) {
+    using ull = unsigned long long;
     k_bucket_sizes<<<kBuckets16 / 256, 256, 0, s>>>(reinterpret_cast<const ull *>(pos), P,
                                                      reinterpret_cast<ull *>(bsize));
     k_bucket_scan<<<1, 1024, 0, s>>>(reinterpret_cast<const ull *>(bsize),
@@ -1425,9 +1501,10 @@ hipError_t launch_recv_plan(const int32_t *recv, const uint64_t *roff, const uin
     return hipGetLastError();
 }
 
-hipError_t launch_gather_sort(const int32_t *recv, const uint64_t *pos, const uint64_t *roff,
-                              int P, const uint64_t *bstart, const uint64_t *list, uint32_t nlist,
-                              int cls, bool atomic_rank, uint32_t *out, hipStream_t s) {
+hipError_t launch_gather_sort(const void *recv, bool packed16, const uint64_t *pos,
+                              const uint64_t *roff, int P, const uint64_t *bstart,
+                              const uint64_t *list, uint32_t nlist, int cls, bool atomic_rank,
+                              uint32_t *out, hipStream_t s) {
     using ull = unsigned long long;
     if (nlist == 0) return hipSuccess;
     if (cls < 1 || cls > kLocalClasses || P < 1 || P > 64) return hipErrorInvalidValue;
@@ -1435,27 +1512,50 @@ hipError_t launch_gather_sort(const int32_t *recv, const uint64_t *pos, const ui
     auto *ro = reinterpret_cast<const ull *>(roff);
     auto *bs = reinterpret_cast<const ull *>(bstart);
     auto *l = reinterpret_cast<const ull *>(list);
-#define GSORT_K11G(B, I)                                                                       \
+    auto *r32 = reinterpret_cast<const int32_t *>(recv);
+    auto *r16 = reinterpret_cast<const uint16_t *>(recv);
+#define GSORT_K11G(B, I, AT)                                                                   \
     do {                                                                                       \
-        if (atomic_rank) k_gather_sort<B, I, true><<<nlist, B, 0, s>>>(recv, ps, ro, P, bs, l, out); \
-        else k_gather_sort<B, I, false><<<nlist, B, 0, s>>>(recv, ps, ro, P, bs, l, out);       \
+        if (packed16) k_gather_sort<B, I, AT><<<nlist, B, 0, s>>>(r16, ps, ro, P, bs, l, out); \
+        else k_gather_sort<B, I, AT><<<nlist, B, 0, s>>>(r32, ps, ro, P, bs, l, out);          \
     } while (0)
     switch (cls) {
-        case 1: GSORT_K11G(256, 18); break;
-        case 2: GSORT_K11G(512, 18); break;
-        default: GSORT_K11G(512, 32); break;
+        case 1: if (atomic_rank) GSORT_K11G(256, 18, true); else GSORT_K11G(256, 18, false); break;
+        case 2: if (atomic_rank) GSORT_K11G(512, 18, true); else GSORT_K11G(512, 18, false); break;
+        default: if (atomic_rank) GSORT_K11G(512, 32, true); else GSORT_K11G(512, 32, false); break;
     }
 #undef GSORT_K11G
     return hipGetLastError();
 }
 
-hipError_t launch_gather_copy(const int32_t *recv, const uint64_t *pos, const uint64_t *roff,
-                              int P, const uint64_t *bsize, const uint64_t *bstart, uint32_t *out,
-                              hipStream_t s) {
+hipError_t launch_gather_copy(const void *recv, bool packed16, const uint64_t *pos,
+                              const uint64_t *roff, int P, const uint64_t *bsize,
+                              const uint64_t *bstart, uint32_t *out, hipStream_t s) {
     using ull = unsigned long long;
-    k_gather_copy<<<kBuckets16, 256, 0, s>>>(
-        recv, reinterpret_cast<const ull *>(pos), reinterpret_cast<const ull *>(roff), P,
-        reinterpret_cast<const ull *>(bsize), reinterpret_cast<const ull *>(bstart), out);
+    auto *ps = reinterpret_cast<const ull *>(pos);
+    auto *ro = reinterpret_cast<const ull *>(roff);
+    auto *bz = reinterpret_cast<const ull *>(bsize);
+    auto *bs = reinterpret_cast<const ull *>(bstart);
+    if (packed16)
+        k_gather_copy<<<kBuckets16, 256, 0, s>>>(reinterpret_cast<const uint16_t *>(recv), ps, ro,
+                                                 P, bz, bs, out);
+    else
+        k_gather_copy<<<kBuckets16, 256, 0, s>>>(reinterpret_cast<const int32_t *>(recv), ps, ro,
+                                                 P, bz, bs, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_pack16(const int32_t *a, uint64_t n, uint16_t *out, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    k_pack16<<<grid_for(n, 256, 8192), 256, 0, s>>>(a, n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_meta_counts(const uint64_t *gb, const uint64_t *rng, int nrng, uint32_t *meta,
+                              hipStream_t s) {
+    if (nrng <= 0) return hipSuccess;
+    k_meta_counts<<<nrng, 256, 0, s>>>(reinterpret_cast<const unsigned long long *>(gb),
+                                       reinterpret_cast<const unsigned long long *>(rng), meta);
     return hipGetLastError();
 }
 

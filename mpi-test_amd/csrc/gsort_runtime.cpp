@@ -54,6 +54,7 @@ struct gsort_ctx {
     DevBuf m_split;  // radix select thresholds + counts of the distributed radix
     DevBuf m_rpos, m_bsize;  // receive side: run bucket bounds (P x 65537), bucket size/start
     DevBuf m_bseg, m_blist;  // boundary groups of the distributed radix: scratch, K11 list
+    DevBuf m_gb, m_pack, m_meta;  // packed exchange: bucket bounds, low 16 bits, counts
     // device small area: [0, 8K) hist4 (4x256 u64) | [8K, 10K) pass digit totals (256 u64) |
     // [10K, 12K) pass digit bases (256 u64) | [20K, 256K) plans / samples / routing tables
     char *d_small = nullptr;
@@ -415,14 +416,19 @@ gsort_status local_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *
 // bucketed by their top 16 bits with binary searches (no pass over the keys), and K11g sorts
 // every bucket's low 16 bits straight from the P pieces: one read + one write per key.  Buckets
 // larger than kLocalMax are gathered into place and finish through the MSD levels 1 and 0.
-gsort_status recv_sort(gsort_ctx *c, const int32_t *recv, const std::vector<uint64_t> &rlen,
-                       uint64_t n, uint32_t *out, uint32_t *tmp, gsort_stats *stats) {
+// recv holds the P runs back to back (run p has rlen[p] keys), each grouped by the top 16 bits
+// (ordered u32): int32 keys, or with packed16 only their low 16 bits, in which case the caller
+// has already filled c->m_rpos (pos[p][h], launch_pos_from_meta).
+gsort_status recv_sort(gsort_ctx *c, const void *recv, bool packed16,
+                       const std::vector<uint64_t> &rlen, uint64_t n, uint32_t *out,
+                       uint32_t *tmp, gsort_stats *stats) {
     const int P = (int)rlen.size();
     if (n == 0) return GSORT_OK;
-    if (P > 64 || c->local_algo == GSORT_LOCAL_LSD) {  // K11g holds at most 64 pieces
+    if (!packed16 && (P > 64 || c->local_algo == GSORT_LOCAL_LSD)) {  // K11g: <= 64 pieces
         int pr = 0;
         return local_sort(c, reinterpret_cast<const uint32_t *>(recv), n, out, tmp, &pr, stats);
     }
+    if (P > 64) return set_err(c, GSORT_EINVAL, "packed exchange supports at most 64 ranks");
     hipEvent_t t = tic(c);
     ST_TRY(ensure(c, c->m_rpos, (size_t)P * (kBuckets16 + 1) * 8));
     ST_TRY(ensure(c, c->m_bsize, (size_t)kBuckets16 * 16));
@@ -438,8 +444,10 @@ gsort_status recv_sort(gsort_ctx *c, const int32_t *recv, const std::vector<uint
     uint64_t *bsize = reinterpret_cast<uint64_t *>(c->m_bsize.p), *bstart = bsize + kBuckets16;
     uint64_t *ctr = reinterpret_cast<uint64_t *>(c->d_small + OFF_CTR);
     HIP_TRY(c, hipMemsetAsync(ctr, 0, kCtrBytes, c->stream));
-    HIP_TRY(c, launch_recv_plan(recv, d_r, d_r + P, P, pos, bsize, bstart, work_lists(c, 0),
-                                c->stream));
+    if (!packed16)
+        HIP_TRY(c, launch_run_bounds(reinterpret_cast<const int32_t *>(recv), d_r, d_r + P, P, pos,
+                                     c->stream));
+    HIP_TRY(c, launch_recv_classify(pos, P, bsize, bstart, work_lists(c, 0), c->stream));
     toc(c, PH_COUNT, t);
     uint64_t h[3 * (kLocalClasses + 1)];
     ST_TRY(read_counters(c, h));
@@ -447,14 +455,14 @@ gsort_status recv_sort(gsort_ctx *c, const int32_t *recv, const std::vector<uint
         const uint64_t *hk = h + 3 * (k + 1);
         if (!hk[0]) continue;
         t = tic(c);
-        HIP_TRY(c, launch_gather_sort(recv, pos, d_r, P, bstart,
+        HIP_TRY(c, launch_gather_sort(recv, packed16, pos, d_r, P, bstart,
                                       reinterpret_cast<uint64_t *>(c->m_local[k].p),
                                       (uint32_t)hk[0], k + 1, c->atomic_rank, out, c->stream));
         toc(c, PH_BUCKET, t);
         if (stats) { stats->buckets_local += hk[0]; stats->keys_bucket_sort += hk[1]; }
     }
     if (h[0]) {  // oversized buckets: into place, then levels 1 and 0
-        HIP_TRY(c, launch_gather_copy(recv, pos, d_r, P, bsize, bstart, out, c->stream));
+        HIP_TRY(c, launch_gather_copy(recv, packed16, pos, d_r, P, bsize, bstart, out, c->stream));
         for (int k = 3; k < 3 * (kLocalClasses + 1); ++k) h[k] = 0;
         int levels = 0;
         ST_TRY(msd_levels(c, 1, out, out, tmp, 0, h, stats, &levels));
@@ -611,27 +619,86 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
     gsort_status ps = gsort_plan_split(P, n_all.data(), lt.data(), le.data(), me, send.data(),
                                        recv.data());
     if (ps != GSORT_OK) return set_err(c, ps, "inconsistent splitter counts");
-    // (4) one exchange
-    std::vector<size_t> sc(P), sd(P), rc(P), rd(P);
+    // (4) one exchange of the keys' low 16 bits: every destination block's keys lie in a known
+    // range of 16-bit buckets (from the boundary keys), so the top 16 bits travel as one count
+    // per (destination, bucket) instead of 2 bytes per key
+    std::vector<uint64_t> hlo(P), nh(P), cut(P + 1, 0);
+    for (int q = 0; q < P; ++q) {
+        const uint64_t lo = q == 0 ? 0 : (g[q - 1] >= N ? 0xFFFFFFFFull : prefix[q - 1]);
+        const uint64_t hi = q == P - 1 ? 0xFFFFFFFFull : (g[q] >= N ? 0xFFFFFFFFull : prefix[q]);
+        hlo[q] = lo >> 16;
+        nh[q] = (hi >> 16) - hlo[q] + 1;
+        cut[q + 1] = cut[q] + send[q];
+    }
+    ST_TRY(ensure(c, c->m_gb, (size_t)(kBuckets16 + 1) * 8));
+    ST_TRY(ensure(c, c->m_pack, std::max<uint64_t>(n_in, 1) * 2));
+    uint64_t meta_n = 0;
+    std::vector<uint64_t> rng;
+    for (int q = 0; q < P; ++q)
+        if (send[q]) {
+            rng.insert(rng.end(), {cut[q], cut[q + 1], hlo[q], nh[q], meta_n});
+            meta_n += nh[q];
+        }
+    uint64_t nsrc = 0;
+    for (int p = 0; p < P; ++p) nsrc += recv[p] ? 1 : 0;
+    ST_TRY(ensure(c, c->m_meta, (std::max<uint64_t>(meta_n, 1) + nsrc * nh[me] + 1) * 4 +
+                                    (rng.size() + 2 * P + 2) * 8));
+    uint32_t *meta_s = reinterpret_cast<uint32_t *>(c->m_meta.p);
+    uint32_t *meta_r = meta_s + std::max<uint64_t>(meta_n, 1);
+    uint64_t *d_tab = reinterpret_cast<uint64_t *>(
+        reinterpret_cast<char *>(c->m_meta.p) +
+        (((std::max<uint64_t>(meta_n, 1) + nsrc * nh[me] + 1) * 4 + 7) & ~size_t(7)));
+    std::vector<uint64_t> tab(rng);
+    std::vector<uint64_t> moff(P, ~0ull);
+    {
+        uint64_t k = 0;
+        for (int p = 0; p < P; ++p)
+            if (recv[p]) moff[p] = (k++) * nh[me];
+    }
+    tab.insert(tab.end(), moff.begin(), moff.end());
+    tab.insert(tab.end(), {0ull, n_in});  // this rank's block as one run (bucket bounds)
+    HIP_TRY(c, hipMemcpyAsync(d_tab, tab.data(), tab.size() * 8, hipMemcpyHostToDevice,
+                              c->stream));
+    const uint64_t *d_rng = d_tab, *d_moff = d_tab + rng.size(), *d_one = d_moff + P;
+    uint64_t *gb = reinterpret_cast<uint64_t *>(c->m_gb.p);
+    uint16_t *pack = reinterpret_cast<uint16_t *>(c->m_pack.p);
+    t = tic(c);
+    HIP_TRY(c, launch_run_bounds(sorted, d_one, d_one + 1, 1, gb, c->stream));
+    HIP_TRY(c, launch_meta_counts(gb, d_rng, (int)(rng.size() / 5), meta_s, c->stream));
+    HIP_TRY(c, launch_pack16(sorted, n_in, pack, c->stream));
+    toc(c, PH_PLACE, t);
+    std::vector<size_t> sc(P, 0), sd(P, 0), rc(P, 0), rd(P, 0);
+    {
+        uint64_t mo = 0, ro = 0;
+        for (int q = 0; q < P; ++q) {
+            if (send[q]) { sc[q] = nh[q] * 4; sd[q] = mo * 4; mo += nh[q]; }
+            if (recv[q]) { rc[q] = nh[me] * 4; rd[q] = ro * 4; ro += nh[me]; }
+        }
+    }
+    t = tic(c);
+    ST_TRY(comm_try(c, c->comm->alltoallv(meta_s, sc.data(), sd.data(), meta_r, rc.data(),
+                                          rd.data(), c->stream)));
     size_t so = 0, ro = 0;
     for (int q = 0; q < P; ++q) {
-        sc[q] = send[q] * 4; sd[q] = so; so += sc[q];
-        rc[q] = recv[q] * 4; rd[q] = ro; ro += rc[q];
+        sc[q] = send[q] * 2; sd[q] = so; so += sc[q];
+        rc[q] = recv[q] * 2; rd[q] = ro; ro += rc[q];
         if (stats && q != me) {
             stats->bytes_sent += sc[q];
             stats->max_pair_bytes = std::max<uint64_t>(stats->max_pair_bytes, sc[q]);
         }
     }
-    if (ro != mine * 4) return set_err(c, GSORT_EINVAL, "exchange plan does not fill the block");
-    int32_t *rbuf = slot_ptr<int32_t>(c, S_RECV);
-    t = tic(c);
-    ST_TRY(comm_try(c, c->comm->alltoallv(sorted, sc.data(), sd.data(), rbuf, rc.data(),
+    if (ro != mine * 2) return set_err(c, GSORT_EINVAL, "exchange plan does not fill the block");
+    uint16_t *rbuf = slot_ptr<uint16_t>(c, S_RECV);
+    ST_TRY(comm_try(c, c->comm->alltoallv(pack, sc.data(), sd.data(), rbuf, rc.data(),
                                           rd.data(), c->stream)));
     toc(c, PH_EXCH, t);
     if (stats) stats->exchanges = 1;
-    // (5) the P received sorted runs -> one sorted block (recv_sort)
+    // (5) the P received runs -> one sorted block (recv_sort), their bucket bounds from the counts
     t = tic(c);
-    ST_TRY(recv_sort(c, rbuf, recv, mine, slot_ptr<uint32_t>(c, S_OUT),
+    ST_TRY(ensure(c, c->m_rpos, (size_t)P * (kBuckets16 + 1) * 8));
+    HIP_TRY(c, launch_pos_from_meta(meta_r, d_moff, (uint32_t)hlo[me], (uint32_t)nh[me], P,
+                                    reinterpret_cast<uint64_t *>(c->m_rpos.p), c->stream));
+    ST_TRY(recv_sort(c, rbuf, true, recv, mine, slot_ptr<uint32_t>(c, S_OUT),
                      slot_ptr<uint32_t>(c, S_TMP), stats));
     toc(c, PH_MERGE, t);
     if (stats) stats->passes_run = pr;
@@ -846,7 +913,7 @@ gsort_status sample_dist(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in, int
     std::vector<uint64_t> rlen(P);
     for (int q = 0; q < P; ++q) rlen[q] = M[(size_t)q * P + me];
     t = tic(c);
-    ST_TRY(recv_sort(c, rbuf, rlen, total, slot_ptr<uint32_t>(c, S_OUT),
+    ST_TRY(recv_sort(c, rbuf, false, rlen, total, slot_ptr<uint32_t>(c, S_OUT),
                      slot_ptr<uint32_t>(c, S_TMP), stats));
     toc(c, PH_MERGE, t);
     if (stats) stats->passes_run = pr;
@@ -996,7 +1063,7 @@ gsort_status gsort_destroy(gsort_ctx *c) {
     if (c->gsum.p) (void)hipFree(c->gsum.p);
     for (DevBuf *b : {&c->m_tpfx, &c->m_gpfx, &c->m_segmap, &c->m_groupmap, &c->m_cstart,
                       &c->m_next[0], &c->m_next[1], &c->m_split, &c->m_rpos, &c->m_bsize,
-                      &c->m_bseg, &c->m_blist})
+                      &c->m_bseg, &c->m_blist, &c->m_gb, &c->m_pack, &c->m_meta})
         if (b->p) (void)hipFree(b->p);
     for (auto &b : c->m_local)
         if (b.p) (void)hipFree(b.p);
