@@ -524,6 +524,26 @@ __device__ __forceinline__ void load_tile(const uint32_t *__restrict__ src, bool
     }
 }
 
+// Buffer descriptor over n_bytes at p (wave-uniform p and n_bytes): loads past the end return
+// 0 and stores past it are dropped, so partial buckets need no per-key bound.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t bucket_rsrc(const void *p, uint32_t n_bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, (int)n_bytes, 0x00020000);
+}
+
+// K11 bucket load: k[i] = src[i * BLOCK + threadIdx.x] below len, 0 past it.
+template <int BLOCK, int ITEMS, bool FIN>
+__device__ __forceinline__ void load_bucket(const uint32_t *src, uint32_t len,
+                                            uint32_t (&k)[ITEMS]) {
+    const __amdgpu_buffer_rsrc_t rs = bucket_rsrc(src, len * 4u);
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i)
+        k[i] = __builtin_amdgcn_raw_buffer_load_b32(rs, (i * BLOCK + (int)threadIdx.x) * 4, 0, 0);
+    if (FIN) {
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i) k[i] ^= kFlip;
+    }
+}
+
 // Shared K3u body: unstable partition of one tile [t0, t0 + len) of `in` by digit `shift`.
 // dst_base (tid < 256) = out + global start of this tile's digit-tid keys.
 template <int BLOCK, int ITEMS, bool FIN, bool FOUT>
@@ -879,19 +899,26 @@ __device__ __forceinline__ uint32_t wave_rank(uint32_t *wc, uint32_t d, bool val
 // order equal first digits arbitrarily); every later digit is ranked stably per wave
 // (wave_rank) in (wave, round, lane) order over wave-contiguous chunks, then offset by the
 // (digit, wave)-major exclusive scan of the per-wave counts.
+// Keys past len are neither counted nor placed (a lane-level mask on wave-uniform bounds; a
+// padding key per empty slot would put every such lane on one LDS counter, serialized).
+// The caller zeroes s_wc[0 .. 255] before its barrier.
 template <int BLOCK, int ITEMS, bool ATOMIC>
 __device__ __forceinline__ void sort_bucket(uint32_t (&k)[ITEMS], uint32_t len, int ndigits,
                                             uint32_t *__restrict__ dst, uint32_t *s_a,
                                             uint32_t *s_wc) {
     constexpr int WAVES = BLOCK / 64;
     constexpr int TILE = BLOCK * ITEMS;
-    static_assert(TILE <= 65536, "ranks are packed as 16 bits");
+    static_assert(TILE <= 65536, "ranks fit 16 bits");
     static_assert(BLOCK >= kRadix, "one thread per digit in the scans");
     // the digit scans run while every key is in registers, so their 4 wave sums borrow the
-    // tail of s_a (40 KiB per workgroup instead of 40 KiB + 16 B: 4 workgroups per CU)
+    // tail of s_a
     uint32_t *s_wsum = s_a + TILE - kRadix / 64;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     uint32_t *cnt = s_wc;  // digit 0: block-wide counters, then digit starts
+    // keys of item i are valid for tid < lim(i) (a wave-uniform bound)
+    auto lim = [&](int i) -> uint32_t {
+        return len > (uint32_t)(i * BLOCK) ? len - (uint32_t)(i * BLOCK) : 0u;
+    };
 
     auto block_scan = [&](uint32_t c) -> uint32_t {  // tid < 256: exclusive scan over digits
         uint32_t v = c;
@@ -904,12 +931,12 @@ __device__ __forceinline__ void sort_bucket(uint32_t (&k)[ITEMS], uint32_t len, 
         return v - c;
     };
 
-    // digit 0: unstable counting sort into s_a (cnt zeroed by the caller before its barrier)
+    // digit 0: unstable counting sort into s_a
     {
         uint32_t r[ITEMS];
 #pragma unroll
         for (int i = 0; i < ITEMS; ++i)
-            if ((uint32_t)(i * BLOCK + tid) < len) r[i] = atomicAdd(&cnt[k[i] & 255u], 1u);
+            if ((uint32_t)tid < lim(i)) r[i] = atomicAdd(&cnt[k[i] & 255u], 1u);
         __syncthreads();
         uint32_t excl = 0;
         if (tid < kRadix) excl = block_scan(cnt[tid]);
@@ -921,7 +948,7 @@ __device__ __forceinline__ void sort_bucket(uint32_t (&k)[ITEMS], uint32_t len, 
         __syncthreads();
 #pragma unroll
         for (int i = 0; i < ITEMS; ++i)
-            if ((uint32_t)(i * BLOCK + tid) < len) s_a[cnt[k[i] & 255u] + r[i]] = k[i];
+            if ((uint32_t)tid < lim(i)) s_a[cnt[k[i] & 255u] + r[i]] = k[i];
         __syncthreads();
     }
 
@@ -932,18 +959,18 @@ __device__ __forceinline__ void sort_bucket(uint32_t (&k)[ITEMS], uint32_t len, 
         uint32_t *wc = s_wc + w * kRadix;
 #pragma unroll
         for (int j = 0; j < kRadix / 64; ++j) wc[j * 64 + lane] = 0;
-        const uint32_t base = (uint32_t)w * 64 * R + lane;
+        const uint32_t base = (uint32_t)w * 64 * R;  // wave-uniform
+        const uint32_t wlen = len > base ? len - base : 0u;  // keys of this wave's chunk
 #pragma unroll
         for (int i = 0; i < ITEMS; ++i)
-            if ((uint32_t)i < R) k[i] = base + i * 64 < len ? s_a[base + i * 64] : 0u;
+            if ((uint32_t)i < R && (uint32_t)(i * 64 + lane) < wlen)
+                k[i] = s_a[base + i * 64 + lane];
         __syncthreads();
-        uint32_t rk[(ITEMS + 1) / 2];
+        uint32_t rk[ITEMS];
 #pragma unroll
-        for (int i = 0; i < ITEMS; ++i) {
-            if ((uint32_t)i >= R) continue;
-            const uint32_t rr = wave_rank<ATOMIC>(wc, (k[i] >> shift) & 255u, base + i * 64 < len);
-            if (i & 1) rk[i >> 1] |= rr << 16; else rk[i >> 1] = rr;
-        }
+        for (int i = 0; i < ITEMS; ++i)
+            if ((uint32_t)i < R)
+                rk[i] = wave_rank<ATOMIC>(wc, (k[i] >> shift) & 255u, (uint32_t)(i * 64 + lane) < wlen);
         __syncthreads();
         uint32_t tcount = 0, excl = 0;
         if (tid < kRadix) {
@@ -964,14 +991,17 @@ __device__ __forceinline__ void sort_bucket(uint32_t (&k)[ITEMS], uint32_t len, 
         }
         __syncthreads();
 #pragma unroll
-        for (int i = 0; i < ITEMS; ++i) {
-            if ((uint32_t)i >= R || base + i * 64 >= len) continue;
-            const uint32_t rr = (i & 1) ? (rk[i >> 1] >> 16) : (rk[i >> 1] & 0xFFFFu);
-            s_a[wc[(k[i] >> shift) & 255u] + rr] = k[i];
-        }
+        for (int i = 0; i < ITEMS; ++i)
+            if ((uint32_t)i < R && (uint32_t)(i * 64 + lane) < wlen)
+                s_a[wc[(k[i] >> shift) & 255u] + rk[i]] = k[i];
         __syncthreads();
     }
-    for (uint32_t j = tid; j < len; j += BLOCK) dst[j] = s_a[j] ^ kFlip;
+    const __amdgpu_buffer_rsrc_t rs = bucket_rsrc(dst, len * 4u);  // stores past len dropped
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+        const uint32_t j = (uint32_t)(i * BLOCK + tid);
+        __builtin_amdgcn_raw_buffer_store_b32(s_a[j] ^ kFlip, rs, (int)(j * 4u), 0, 0);
+    }
 }
 
 // K11: sort each listed bucket {start, len} (<= BLOCK * ITEMS keys) of `in` on digits
@@ -989,7 +1019,7 @@ __global__ __launch_bounds__(BLOCK) void k_local_sort(const uint32_t *__restrict
     const uint32_t len = (uint32_t)list[2 * blockIdx.x + 1];
     if (threadIdx.x < kRadix) s_wc[threadIdx.x] = 0;
     uint32_t k[ITEMS];
-    load_tile<BLOCK, ITEMS, FIN>(in + start + threadIdx.x, len == (uint32_t)TILE, len, k);
+    load_bucket<BLOCK, ITEMS, FIN>(in + start, len, k);
     __syncthreads();
     sort_bucket<BLOCK, ITEMS, ATOMIC>(k, len, ndigits, out + start, s_a, s_wc);
 }
