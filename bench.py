@@ -12,13 +12,17 @@ canonical splitmix64 generator on device (K10), so the data is synthetic and ide
 the oracle and the reference CPU run see.
 
 The timed region is K steps bracketed by a barrier + torch.cuda.synchronize() on both sides;
-the slowest rank's time is reported.  `roofline` prices the dominant kernel (K3, the rank +
-scatter of one LSD pass, 8 B/key algorithmic traffic) with its average duration measured live by HIP events recorded on
-libgsort's own stream around every launch; `traffic` is the HBM bytes per launch from the
-rocprofv3 PMC summary in profiles/ (FETCH_SIZE x 2 + WRITE_SIZE, gfx950 correction) when one
-exists for this configuration, else null.  `cpu_baseline` runs the reference radix_sort
-(oracle/_ref, built unchanged from its source) under mpirun on a bounded 2^24-key sample of the
-same stream on the host's cores (rank 0, N = 1 only), before the GPU is touched.
+the slowest rank's time is reported.  `roofline` prices the dominant kernel class (by total
+device time: K3u partition, K11 bucket sort or K3 LSD pass, 8 B/key algorithmic traffic each)
+with its average duration measured live by HIP events recorded on libgsort's own stream
+around every launch; `traffic` is the HBM bytes per launch from the rocprofv3 PMC summary in
+profiles/ (FETCH_SIZE x 2 + WRITE_SIZE, gfx950 correction) when one exists for this
+configuration, else null; `copy_ceiling` is a device-to-device copy of the same 2^k keys
+timed on this GPU (the practical ceiling of a read + write pass).  `drop_in` (N = 1) times
+the reference's own timer span -- rank-0 host array -> GPU -> sorted -> rank-0 host array --
+PCIe included; it is reported beside `value`, never as it.  `cpu_baseline` runs the reference
+radix_sort (oracle/_ref, built unchanged from its source) under mpirun on a bounded 2^24-key
+sample of the same stream on the host's cores (rank 0, N = 1 only), before the GPU is touched.
 """
 import argparse
 import json
@@ -155,6 +159,49 @@ def pmc_traffic(algo, n_local, n_gpus, prefixes=("k_scatter",)):
     return None
 
 
+def copy_ceiling(n_local, reps=10):
+    """Device-to-device copy of n_local int32 keys (torch copy_ = hipMemcpyAsync D2D), timed
+    with events on torch's stream: the practical HBM ceiling of one read + write pass."""
+    import torch
+    x = torch.empty(n_local, dtype=torch.int32, device="cuda")
+    y = torch.empty_like(x)
+    y.copy_(x)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ts = []
+    for _ in range(reps):
+        e0.record()
+        y.copy_(x)
+        e1.record()
+        e1.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    ts.sort()
+    ms = ts[len(ts) // 2]
+    del x, y
+    torch.cuda.empty_cache()
+    return {"ms": round(ms, 4), "GBps": round(n_local * 8 / (ms * 1e-3) / 1e9, 1),
+            "how": "torch copy_ (hipMemcpyAsync D2D) of the same keys, median of 10"}
+
+
+def drop_in_e2e(ctx, fn, d_in, n, reps=3):
+    """The reference's timer span at N = 1: pageable rank-0 host int32 array -> GPU
+    (gsort_scatter_from_root) -> gsort_radix -> rank-0 host array (gsort_gather_to_root)."""
+    import numpy as np
+    h = ctx.to_host(d_in, n)
+    ts, out = [], None
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        d, m = ctx.scatter_from_root(h, n)
+        d_out, n_out, _ = fn(d, m)
+        out = ctx.gather_to_root(d_out, n_out, n)
+        ts.append(time.perf_counter() - t0)
+    ok = bool(out.size == n and np.all(out[1:] >= out[:-1]))
+    ts.sort()
+    ms = ts[len(ts) // 2] * 1e3
+    return {"ms": round(ms, 2), "GKeys_s": round(n / (ms * 1e-3) / 1e9, 3), "sorted": ok,
+            "note": "pageable host array -> GPU -> sorted -> host (PCIe included), "
+                    "median of 3; not the headline value"}
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -231,6 +278,9 @@ def main():
     ms_step = elapsed * 1e3 / a.steps
     value = n_total / (ms_step / 1e3) / 1e9
 
+    ceiling = copy_ceiling(n_local) if rank == 0 else None
+    drop_in = drop_in_e2e(ctx, fn, d_in, n_local) if world == 1 else None
+
     rooflines = kernel_rooflines(stats, n_local)
     dom = max(rooflines, key=lambda r: r["total_ms"])
     pmc = pmc_traffic(a.algo, n_local, world, dom["pmc_prefixes"])
@@ -272,9 +322,14 @@ def main():
                      "algorithmic_bytes_per_launch": dom["bytes_per_launch"],
                      "bytes_per_key": dom["bytes_per_key"],
                      "avg_launch_ms": dom["avg_launch_ms"],
-                     "launches_timed": dom["launches"]},
+                     "launches_timed": dom["launches"],
+                     "copy_ceiling_GBps": ceiling["GBps"] if ceiling else None,
+                     "frac_of_copy": (round(dom["achieved"] / ceiling["GBps"], 4)
+                                      if ceiling else None)},
         "kernels": [{k: v for k, v in r.items() if k != "pmc_prefixes"} for r in rooflines],
         "cpu_baseline": cpu,
+        "copy_ceiling": ceiling,
+        "drop_in": drop_in,
         "phases_ms_avg": phases,
         "passes_run": last["passes_run"],
         "local_algo": "lsd" if last["local_algo"] == gsort.LOCAL_LSD else "msd",
