@@ -203,6 +203,11 @@ def drop_in_e2e(ctx, fn, d_in, n, reps=3):
 
 
 def main():
+    # stdout carries the one JSON line only: native libraries (RCCL prints a version banner
+    # at communicator init) write to fd 1, so point it at stderr and keep the real stdout
+    json_fd = os.dup(1)
+    sys.stdout.flush()
+    os.dup2(2, 1)
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -224,11 +229,14 @@ def main():
     if world > 1:
         dist.init_process_group("gloo")  # bootstrap only: uid broadcast, barrier, max-time
     uid = None
-    if world > 1:
+    # GSORT_FORCE_DIST=1 (test hook, tests/test_gpu_rccl.py): one rank still runs the
+    # distributed algorithm over a one-rank RCCL communicator
+    if world > 1 or os.environ.get("GSORT_FORCE_DIST") == "1":
         buf = torch.zeros(128, dtype=torch.uint8)
         if rank == 0:
             buf = torch.tensor(list(gsort.get_uid()), dtype=torch.uint8)
-        dist.broadcast(buf, 0)
+        if world > 1:
+            dist.broadcast(buf, 0)
         uid = bytes(buf.tolist())
 
     def barrier():
@@ -335,7 +343,7 @@ def main():
         "local_algo": "lsd" if last["local_algo"] == gsort.LOCAL_LSD else "msd",
         "verified": bool(ok),
     }
-    if world > 1:
+    if last["exchanges"]:
         ex = sum(s["ms_exchange"] for s in stats) / len(stats) / max(last["exchanges"], 1)
         pair = last["max_pair_bytes"]
         line["exchange"] = {"bound": "xgmi", "per_exchange_ms": round(ex, 4),
@@ -344,7 +352,7 @@ def main():
                             "peak_link_GBps": XGMI_LINK_GBPS,
                             "frac": round(pair / (ex * 1e-3) / 1e9 / XGMI_LINK_GBPS, 4) if ex else None}
     if rank == 0:
-        print(json.dumps(line), flush=True)
+        os.write(json_fd, (json.dumps(line) + "\n").encode())
     ctx.free(d_in)
     ctx.close()
     if world > 1:

@@ -2,6 +2,7 @@
 #include "gsort_comm.h"
 
 #include <rccl/rccl.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <chrono>
@@ -55,8 +56,17 @@ class RcclComm : public Comm {
     ncclComm_t comm_;
 };
 
+// RCCL's bootstrap (the uid's listening socket and the ranks' connections to it) runs over
+// TCP on an interface RCCL picks itself; on these single-node boxes the picked interface
+// refused the connection (measured: ncclCommInitRank "remote process exited or there was a
+// network error" after 35 retries).  Every rank of a gsort job is on one node, so the
+// bootstrap goes over loopback unless the caller chose an interface.  The key exchange itself
+// is GPU-to-GPU (xGMI), not sockets.
+static void bootstrap_on_loopback() { setenv("NCCL_SOCKET_IFNAME", "lo", 0); }
+
 gsort_status rccl_get_uid(gsort_uid *out) {
     static_assert(sizeof(ncclUniqueId) == sizeof(gsort_uid), "uid size");
+    bootstrap_on_loopback();
     ncclUniqueId id;
     if (ncclGetUniqueId(&id) != ncclSuccess) return GSORT_ERCCL;
     memcpy(out, &id, sizeof(id));
@@ -64,6 +74,7 @@ gsort_status rccl_get_uid(gsort_uid *out) {
 }
 
 Comm *make_rccl_comm(int rank, int nranks, const gsort_uid *uid, std::string *err) {
+    bootstrap_on_loopback();
     ncclUniqueId id;
     memcpy(&id, uid, sizeof(id));
     ncclComm_t c;

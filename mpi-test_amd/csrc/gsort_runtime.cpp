@@ -998,6 +998,15 @@ int gsort_rank(const gsort_ctx *ctx) { return ctx ? ctx->rank : -1; }
 int gsort_nranks(const gsort_ctx *ctx) { return ctx ? ctx->nranks : -1; }
 size_t gsort_onesweep_tile(void) { return kSweepTile; }
 
+// GSORT_FORCE_DIST=1: a one-rank context created with a uid (or in a group) still gets a
+// communicator and runs the distributed algorithms -- the only way to drive the RCCL calls
+// (init, all-gather, grouped send/recv to self, broadcast) on a one-GPU machine, since RCCL
+// refuses two ranks on one device.  Test hook; the drop-in never sets it.
+static bool force_dist() {
+    const char *v = getenv("GSORT_FORCE_DIST");
+    return v && v[0] == '1';
+}
+
 gsort_status gsort_get_uid(gsort_uid *out) {
     if (!out) return GSORT_EINVAL;
     return rccl_get_uid(out);
@@ -1012,7 +1021,7 @@ gsort_status gsort_create(gsort_ctx **ctx, int rank, int nranks, int hip_device,
     c->rank = rank;
     c->nranks = nranks;
     gsort_status st = create_common(c, hip_device);
-    if (st == GSORT_OK && nranks > 1) {
+    if (st == GSORT_OK && (nranks > 1 || (force_dist() && uid))) {
         std::string e;
         c->comm = make_rccl_comm(rank, nranks, uid, &e);
         if (!c->comm) st = set_err(c, GSORT_ERCCL, e);
@@ -1047,7 +1056,7 @@ gsort_status gsort_create_in_group(gsort_ctx **ctx, gsort_group *grp, int rank, 
     c->nranks = group_state_size(grp->st);
     gsort_status st = create_common(c, hip_device);
     if (st != GSORT_OK) { gsort_destroy(c); return st; }
-    if (c->nranks > 1) c->comm = make_group_comm(grp->st, rank);
+    if (c->nranks > 1 || force_dist()) c->comm = make_group_comm(grp->st, rank);
     *ctx = c;
     return GSORT_OK;
 }
@@ -1105,7 +1114,7 @@ gsort_status gsort_radix(gsort_ctx *c, const int32_t *d_keys, size_t n_local, in
     hipEvent_t t0 = tic(c);
     gsort_status st;
     uint64_t nout = 0;
-    if (c->nranks == 1) {
+    if (!c->comm) {
         const size_t cap = std::max<size_t>(n_local, 1) * 4;
         ST_TRY(ensure(c, c->slot[S_TMP], cap));
         ST_TRY(ensure(c, c->slot[S_OUT], cap));
@@ -1138,7 +1147,7 @@ gsort_status gsort_sample(gsort_ctx *c, const int32_t *d_keys, size_t n_local, i
     timing_begin(c, stats);
     hipEvent_t t0 = tic(c);
     uint64_t nout = 0;
-    if (c->nranks == 1) {
+    if (!c->comm) {
         // one rank: no splitters, one bucket (the reference reads splitters[-1] here, Q10)
         const size_t cap = std::max<size_t>(n_local, 1) * 4;
         ST_TRY(ensure(c, c->slot[S_TMP], cap));

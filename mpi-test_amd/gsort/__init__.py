@@ -49,7 +49,20 @@ class Stats(ctypes.Structure):
 
 
 class Uid(ctypes.Structure):
-    _fields_ = [("internal", ctypes.c_char * 128)]
+    # raw bytes: a c_char array field would cut the id at its first NUL on read and write
+    _fields_ = [("internal", ctypes.c_ubyte * 128)]
+
+    @classmethod
+    def from_bytes(cls, b):
+        b = bytes(b)
+        if len(b) != 128:
+            raise ValueError(f"a gsort uid is 128 bytes, got {len(b)}")
+        u = cls()
+        ctypes.memmove(ctypes.addressof(u), b, 128)
+        return u
+
+    def to_bytes(self):
+        return ctypes.string_at(ctypes.addressof(self), 128)
 
 
 EXPORTS = [
@@ -117,7 +130,7 @@ def lib():
 def get_uid():
     u = Uid()
     _check(lib().gsort_get_uid(ctypes.byref(u)), None)
-    return bytes(u.internal)
+    return u.to_bytes()
 
 
 def _check(st, ctx):
@@ -154,10 +167,7 @@ class Context:
         if group is not None:
             _check(L.gsort_create_in_group(ctypes.byref(self.h), group.h, rank, device), None)
         else:
-            u = None
-            if uid is not None:
-                u = Uid()
-                u.internal = uid
+            u = Uid.from_bytes(uid) if uid is not None else None
             _check(L.gsort_create(ctypes.byref(self.h), rank, nranks, device,
                                   ctypes.byref(u) if u is not None else None), None)
         self.rank, self.nranks, self.device = rank, (group.nranks if group else nranks), device

@@ -165,3 +165,12 @@ def test_cli_contract_without_gpu(tmp_path):
     r = subprocess.run([os.path.join(ROOT, "mpi-test_amd", "bin", "sample_sort"), str(bad)],
                        capture_output=True, text=True, timeout=60)
     assert r.returncode != 0 and "is not a valid file for read." in r.stderr
+
+
+def test_uid_bytes_survive_marshalling(gsort):
+    """An RCCL unique id holds NUL bytes (socket address, port): the ctypes struct must carry
+    all 128 bytes both ways (a c_char array field stops at the first NUL)."""
+    raw = bytes([2, 0, 0x1F, 0x90, 127, 0, 0, 1] + [0] * 56 + list(range(1, 65)))
+    u = gsort.Uid.from_bytes(raw)
+    assert u.to_bytes() == raw
+    assert bytes(u.internal) == raw
