@@ -104,6 +104,7 @@ struct SegPass {
     uint64_t *gsum;                // max_groups x 256
     uint64_t *cstart;              // nseg x 256
     WorkLists lists;
+    uint16_t *out16 = nullptr;     // set: K3u stores the low 16 bits of every key here
 };
 // K12 + K1s + K2s: plan the tiles, count them, scan, child starts + classification.
 hipError_t launch_seg_count(const SegPass &sp, hipStream_t s);
@@ -117,6 +118,28 @@ hipError_t launch_seg_partition(const SegPass &sp, hipStream_t s);
 hipError_t launch_local_sort(const uint32_t *in, uint32_t *out, const uint64_t *list,
                              uint32_t nlist, int cls, int ndigits, bool flip_in,
                              bool atomic_rank, hipStream_t s);
+// K18: receive buckets of kLocalMax < len <= kHxMax keys (list {h, len}), a counting sort of
+// their low 16 bits written straight from the counts, int32 at out[bstart[h] ..).
+constexpr uint64_t kHxMax = 1u << 20;
+hipError_t launch_hist_expand(const void *recv, bool packed16, const uint64_t *pos,
+                              const uint64_t *roff, int P, const uint64_t *bstart,
+                              const uint64_t *list, uint32_t nlist, uint32_t *out,
+                              hipStream_t s);
+// {h, len} list entries -> {bstart[h], len}.
+hipError_t launch_list_to_segments(uint64_t *list, uint32_t n, const uint64_t *bstart,
+                                   hipStream_t s);
+// ---- packed send buffer of the distributed radix (low 16 bits, grouped by the top 16) -----
+// out[i] = int32 key of bucket h from its low 16 bits in[i].
+hipError_t launch_unpack16(const uint16_t *in, uint64_t n, uint32_t h, int32_t *out,
+                           hipStream_t s);
+// gb[h] (65537 u64) = first position of 16-bit bucket h, from level 3's bases / totals and
+// level 2's segments (list0) and child starts.
+hipError_t launch_gb_from_plan(const uint64_t *bases, const uint64_t *totals,
+                               const uint64_t *segs, uint32_t nseg, const uint64_t *cstart,
+                               uint64_t n, uint64_t *gb, hipStream_t s);
+// K13 on the packed buffer (bucket bounds gb): out[i] = #keys < xs[i] (ordered u32).
+hipError_t launch_count_below16(const uint16_t *a, const uint64_t *gb, const uint64_t *xs,
+                                int m, uint64_t *out, hipStream_t s);
 // ---- receive side of the distributed sorts: P sorted runs -> one sorted block -----------
 constexpr uint32_t kBuckets16 = 65536;  // buckets by the top 16 bits (ordered u32)
 // pos[p][h] (P x 65537 u64) = keys of run p (recv[roff[p] .. +rlen[p]), int32, grouped by
@@ -125,12 +148,14 @@ hipError_t launch_run_bounds(const int32_t *recv, const uint64_t *roff, const ui
                              int P, uint64_t *pos, hipStream_t s);
 // pos[p][h] from source p's counts of buckets [h_lo, h_lo + nh) at meta + moff[p]
 // (moff[p] = ~0: nothing received from p) -- the packed exchange.
+// scratch: 64 x P u64.
 hipError_t launch_pos_from_meta(const uint32_t *meta, const uint64_t *moff, uint32_t h_lo,
-                                uint32_t nh, int P, uint64_t *pos, hipStream_t s);
+                                uint32_t nh, int P, uint64_t *pos, uint64_t *scratch,
+                                hipStream_t s);
 // bsize / bstart (65536 u64) = bucket sizes and their exclusive scan; buckets classified into
 // wl (next level: {bstart, len} segments; K11g classes: {h, len}).
 hipError_t launch_recv_classify(const uint64_t *pos, int P, uint64_t *bsize, uint64_t *bstart,
-                                const WorkLists &wl, hipStream_t s);
+                                const WorkLists &wl, uint64_t *scratch, hipStream_t s);
 // K11g: gather the P pieces of every listed bucket (int32 keys, or packed16: the low 16 bits),
 // sort its low 16 bits in LDS, store int32 at out[bstart[h] ..).
 hipError_t launch_gather_sort(const void *recv, bool packed16, const uint64_t *pos,

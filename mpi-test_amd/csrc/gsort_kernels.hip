@@ -546,11 +546,13 @@ __device__ __forceinline__ void load_bucket(const uint32_t *src, uint32_t len,
 
 // Shared K3u body: unstable partition of one tile [t0, t0 + len) of `in` by digit `shift`.
 // dst_base (tid < 256) = out + global start of this tile's digit-tid keys.
-template <int BLOCK, int ITEMS, bool FIN, bool FOUT>
+// OT = uint16_t stores only the low 16 bits of every key (the packed send buffer of the
+// distributed radix, whose groups are the top 16 bits).
+template <int BLOCK, int ITEMS, bool FIN, bool FOUT, typename OT = uint32_t>
 __device__ __forceinline__ void partition_tile(const uint32_t *__restrict__ in, uint64_t t0,
-                                               uint32_t len, int shift, uint32_t *dst_base,
+                                               uint32_t len, int shift, OT *dst_base,
                                                uint32_t *s_keys, uint32_t *s_cur,
-                                               uint32_t **s_dst, uint32_t *s_wsum) {
+                                               OT **s_dst, uint32_t *s_wsum) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     constexpr int TILE = BLOCK * ITEMS;
     const bool full = len == (uint32_t)TILE;
@@ -593,7 +595,7 @@ __device__ __forceinline__ void partition_tile(const uint32_t *__restrict__ in, 
         const uint32_t j = (uint32_t)(i * BLOCK + tid);
         if (full || j < len) {
             const uint32_t key = s_keys[j];
-            s_dst[(key >> shift) & 255u][j] = FOUT ? (key ^ kFlip) : key;
+            s_dst[(key >> shift) & 255u][j] = (OT)(FOUT ? (key ^ kFlip) : key);
         }
     }
 }
@@ -839,9 +841,9 @@ __global__ __launch_bounds__(kRadix) void k_classify_buckets(
 }
 
 // K3u (segmented): one block per segment tile.
-template <int BLOCK, int ITEMS, bool FOUT>
+template <int BLOCK, int ITEMS, bool FOUT, typename OT = uint32_t>
 __global__ __launch_bounds__(BLOCK) void k_seg_partition(
-    const uint32_t *__restrict__ in, uint32_t *__restrict__ out, int shift,
+    const uint32_t *__restrict__ in, OT *__restrict__ out, int shift,
     const uint32_t *__restrict__ toff, const unsigned long long *__restrict__ gpfx64,
     const unsigned long long *__restrict__ cstart, const unsigned long long *__restrict__ segs,
     const uint32_t *__restrict__ tpfx, const uint32_t *__restrict__ gpfx,
@@ -850,17 +852,17 @@ __global__ __launch_bounds__(BLOCK) void k_seg_partition(
     static_assert(TILE == kSweepTile, "segment tiles are kSweepTile keys");
     __shared__ uint32_t s_keys[TILE];
     __shared__ uint32_t s_cur[kRadix];
-    __shared__ uint32_t *s_dst[kRadix];
+    __shared__ OT *s_dst[kRadix];
     __shared__ uint32_t s_wsum[kRadix / 64];
     const uint32_t t = xcd_tile(blockIdx.x, gridDim.x);
     const SegTile st = seg_tile(t, segs, tpfx, gpfx, segmap, nseg);
     if (st.len == 0) return;
-    uint32_t *dst_base = nullptr;
+    OT *dst_base = nullptr;
     if (threadIdx.x < kRadix)
         dst_base = out + cstart[(uint64_t)st.seg * kRadix + threadIdx.x] +
                    gpfx64[(uint64_t)st.group * kRadix + threadIdx.x] +
                    toff[(uint64_t)t * kRadix + threadIdx.x];
-    partition_tile<BLOCK, ITEMS, false, FOUT>(in, st.t0, st.len, shift, dst_base, s_keys, s_cur,
+    partition_tile<BLOCK, ITEMS, false, FOUT, OT>(in, st.t0, st.len, shift, dst_base, s_keys, s_cur,
                                               s_dst, s_wsum);
 }
 
@@ -1137,39 +1139,108 @@ __global__ __launch_bounds__(256) void k_bucket_sizes(const unsigned long long *
     bsize[h] = c;
 }
 
-__global__ __launch_bounds__(1024) void k_bucket_scan(const unsigned long long *__restrict__ bsize,
-                                                      unsigned long long *__restrict__ bstart) {
-    __shared__ unsigned long long s_w[16];
-    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    constexpr uint32_t PER = kBuckets16 / 1024;
-    const unsigned long long *b = bsize + tid * PER;
-    unsigned long long sum = 0;
-#pragma unroll 16
-    for (uint32_t j = 0; j < PER; ++j) sum += b[j];
-    unsigned long long v = sum;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const unsigned long long t = __shfl_up(v, o);
-        if (lane >= o) v += t;
-    }
-    if (lane == 63) s_w[w] = v;
-    __syncthreads();
-    unsigned long long run = v - sum;
-    for (uint32_t ww = 0; ww < w; ++ww) run += s_w[ww];
-#pragma unroll 16
-    for (uint32_t j = 0; j < PER; ++j) {
-        bstart[tid * PER + j] = run;
-        run += b[j];
-    }
-}
-
 __global__ __launch_bounds__(kRadix) void k_classify_gather(
     const unsigned long long *__restrict__ bsize, const unsigned long long *__restrict__ bstart,
     WorkLists wl) {
     const uint32_t h = blockIdx.x * kRadix + threadIdx.x;
     const uint64_t len = bsize[h];
-    // next level: a segment of out; K11g: the bucket id
-    classify_block(len > kLocalMax ? bstart[h] : h, len, wl);
+    // {bucket id, len}: K11g classes, and list 0 (K18 or, past kHxMax, the MSD levels)
+    classify_block(h, len, wl);
+}
+
+// K18 (receive side, buckets of kLocalMax < len <= kHxMax keys): a counting sort of the
+// bucket's low 16 bits -- keys carry no payload, so the output is written straight from the
+// counts.  Two halves of the value range, 32768 u32 counters in LDS each (one pad word per 32
+// so that a thread's 32 consecutive counters sit in distinct banks during the scan):
+// histogram the P pieces, scan, then bin b writes its count copies of key (h, b) at the
+// running position; consecutive lanes take consecutive bins, so the stores coalesce.
+template <typename T>
+__global__ __launch_bounds__(1024) void k_hist_expand(const T *__restrict__ recv,
+                                                      const unsigned long long *__restrict__ pos,
+                                                      const unsigned long long *__restrict__ roff,
+                                                      int P,
+                                                      const unsigned long long *__restrict__ bstart,
+                                                      const unsigned long long *__restrict__ list,
+                                                      uint32_t *__restrict__ out) {
+    constexpr uint32_t HB = 32768, NT = 1024, PER = HB / NT;
+    __shared__ uint32_t s_c[HB + HB / 32];
+    __shared__ uint64_t s_src[64];
+    __shared__ uint32_t s_len[64];
+    __shared__ uint32_t s_w[NT / 64];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint32_t h = (uint32_t)list[2 * blockIdx.x];
+    if ((int)tid < P) {
+        const uint64_t a = pos[(uint64_t)tid * (kBuckets16 + 1) + h];
+        const uint64_t b = pos[(uint64_t)tid * (kBuckets16 + 1) + h + 1];
+        s_src[tid] = roff[tid] + a;
+        s_len[tid] = (uint32_t)(b - a);
+    }
+    uint32_t *dst = out + bstart[h];
+    uint32_t base = 0;  // keys of the lower half
+    auto pad = [](uint32_t b) { return b + (b >> 5); };
+    for (uint32_t half = 0; half < 2; ++half) {
+        for (uint32_t i = tid; i < HB + HB / 32; i += NT) s_c[i] = 0;
+        __syncthreads();
+#pragma unroll 1
+        for (int p = 0; p < P; ++p) {
+            const T *src = recv + s_src[p];
+            const uint32_t np = s_len[p];
+#pragma unroll 1
+            for (uint32_t j0 = 0; j0 < np; j0 += 8 * NT) {
+                uint32_t v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const uint32_t j = j0 + u * NT + tid;
+                    v[u] = j < np ? (recv_key(src[j], h) & 0xFFFFu) : 0x10000u;
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if ((v[u] >> 15) == half) atomicAdd(&s_c[pad(v[u] & (HB - 1))], 1u);
+            }
+        }
+        __syncthreads();
+        // exclusive scan: thread t owns bins [PER t, PER (t + 1))
+        uint32_t c[PER], sum = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < PER; ++j) { c[j] = s_c[pad(tid * PER + j)]; sum += c[j]; }
+        uint32_t x = sum;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t t = __shfl_up(x, o);
+            if ((int)lane >= o) x += t;
+        }
+        if (lane == 63) s_w[w] = x;
+        __syncthreads();
+        uint32_t run = base + x - sum, total = 0;
+        for (uint32_t ww = 0; ww < NT / 64; ++ww) {
+            const uint32_t sw = s_w[ww];
+            if (ww < w) run += sw;
+            total += sw;
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < PER; ++j) { s_c[pad(tid * PER + j)] = run; run += c[j]; }
+        __syncthreads();
+        // expand: bin b = j * NT + tid holds [s_c[b], s_c[b + 1]) (the last: base + total)
+        const uint32_t end_all = base + total;
+#pragma unroll 1
+        for (uint32_t j = 0; j < PER; ++j) {
+            const uint32_t b = j * NT + tid;
+            const uint32_t st = s_c[pad(b)];
+            const uint32_t en = b + 1 < HB ? s_c[pad(b + 1)] : end_all;
+            const uint32_t key = ((h << 16) | (half << 15) | b) ^ kFlip;
+            for (uint32_t q = st; q < en; ++q) dst[q] = key;
+        }
+        base = end_all;
+        __syncthreads();
+    }
+}
+
+// list 0 of the receive side, {h, len} -> {bstart[h], len} (segments of out for the MSD levels).
+__global__ __launch_bounds__(256) void k_list_to_segments(unsigned long long *__restrict__ list,
+                                                          uint32_t n,
+                                                          const unsigned long long *__restrict__ bstart) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) list[2 * i] = bstart[list[2 * i]];
 }
 
 // Oversized receive buckets: gather their pieces into out[bstart[h] ..) as ordered u32 (they
@@ -1203,51 +1274,141 @@ __global__ __launch_bounds__(256) void k_pack16(const int32_t *__restrict__ a, u
         out[i] = (uint16_t)(uint32_t)a[i];
 }
 
+// Packed sender: out[i] = key of bucket h from its low 16 bits (int32), i < n.
+__global__ __launch_bounds__(256) void k_unpack16(const uint16_t *__restrict__ in, uint64_t n,
+                                                  uint32_t h, int32_t *__restrict__ out) {
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride)
+        out[i] = (int32_t)(((h << 16) | in[i]) ^ kFlip);
+}
+
+// Packed sender, bucket bounds from the MSD plan instead of the keys: block s (level-3 bucket
+// s, bases / totals of level 3) finds its level-2 segment (list0 entry starting at bases[s];
+// every non-empty level-3 bucket is one) and copies the 256 child starts; an empty bucket's
+// children all start at bases[s].  gb[65536] = n.
+__global__ __launch_bounds__(kRadix) void k_gb_from_plan(
+    const unsigned long long *__restrict__ bases, const unsigned long long *__restrict__ totals,
+    const unsigned long long *__restrict__ segs, uint32_t nseg,
+    const unsigned long long *__restrict__ cstart, uint64_t n,
+    unsigned long long *__restrict__ gb) {
+    __shared__ int s_j;
+    const uint32_t sb = blockIdx.x, d = threadIdx.x;
+    if (d == 0) s_j = -1;
+    __syncthreads();
+    const uint64_t b = bases[sb];
+    const bool empty = totals[sb] == 0;
+    if (!empty)
+        for (uint32_t j = d; j < nseg; j += kRadix)
+            if (segs[2 * j] == b && segs[2 * j + 1] != 0) s_j = (int)j;
+    __syncthreads();
+    const int j = s_j;
+    gb[(uint64_t)sb * kRadix + d] = (empty || j < 0) ? b : cstart[(uint64_t)j * kRadix + d];
+    if (sb == 0 && d == 0) gb[kBuckets16] = n;
+}
+
+// K13 on the packed send buffer: out[i] = #keys (ordered u32) < xs[i], from the bucket bounds
+// for whole buckets and a binary search of the low 16 bits inside bucket xs[i] >> 16 (which
+// the caller has sorted whenever xs[i] is not a bucket start).
+__global__ __launch_bounds__(256) void k_count_below16(const uint16_t *__restrict__ a,
+                                                       const unsigned long long *__restrict__ gb,
+                                                       const unsigned long long *__restrict__ xs,
+                                                       int m, unsigned long long *__restrict__ out) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= m) return;
+    const uint64_t x = xs[i];
+    const uint64_t h = x >> 16;
+    if (h >= kBuckets16) { out[i] = gb[kBuckets16]; return; }
+    const uint32_t lo16 = (uint32_t)(x & 0xFFFFu);
+    uint64_t lo = gb[h], hi = gb[h + 1];
+    if (lo16 == 0) { out[i] = lo; return; }
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if ((uint32_t)a[mid] < lo16) lo = mid + 1; else hi = mid;
+    }
+    out[i] = lo;
+}
+
 // Sender: for destination block q (rng[5q..] = {a, b, h_lo, nh, out_off}), meta[out_off + i] =
 // keys of this rank's cut [a, b) in bucket h_lo + i (gb = bucket bounds of the grouped block).
 __global__ __launch_bounds__(256) void k_meta_counts(const unsigned long long *__restrict__ gb,
                                                      const unsigned long long *__restrict__ rng,
                                                      uint32_t *__restrict__ meta) {
-    const unsigned long long *r = rng + 5 * blockIdx.x;
+    const unsigned long long *r = rng + 5 * blockIdx.y;
     const uint64_t a = r[0], b = r[1], h0 = r[2], nh = r[3], off = r[4];
-    for (uint64_t i = threadIdx.x; i < nh; i += 256) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < nh;
+         i += (uint64_t)gridDim.x * 256) {
         const uint64_t x = gb[h0 + i], y = gb[h0 + i + 1];
         const uint64_t lo = x > a ? x : a, hi = y < b ? y : b;
         meta[off + i] = (uint32_t)(hi > lo ? hi - lo : 0);
     }
 }
 
-// Receiver: pos[p][h] (h = 0 .. 2^16) from source p's bucket counts for buckets
-// [h_lo, h_lo + nh) at meta + moff[p] (moff[p] = ~0: nothing from p).  One block per source.
-__global__ __launch_bounds__(1024) void k_pos_from_meta(const uint32_t *__restrict__ meta,
-                                                        const unsigned long long *__restrict__ moff,
-                                                        uint32_t h_lo, uint32_t nh,
-                                                        unsigned long long *__restrict__ pos) {
-    __shared__ unsigned long long s_w[16];
-    const uint32_t p = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const unsigned long long mo = moff[p];
-    constexpr uint32_t PER = kBuckets16 / 1024;
-    auto cnt = [&](uint32_t h) -> unsigned long long {
+// Row-wise exclusive scans over the 2^16 buckets (one row per source, or the bucket sizes):
+// 64 blocks per row each reduce 1024 consecutive values (coalesced), then each block scans
+// its 1024 values on top of the reduced prefix of the blocks before it; out[row][65536] =
+// the row total.  Value sources: per-source bucket counts of the packed exchange, or sizes.
+struct MetaCounts {  // source p's count of bucket h (0 outside [h_lo, h_lo + nh))
+    const uint32_t *meta;
+    const unsigned long long *moff;
+    uint32_t h_lo, nh;
+    __device__ unsigned long long operator()(uint32_t p, uint32_t h) const {
+        const unsigned long long mo = moff[p];
         return (mo != ~0ull && h >= h_lo && h - h_lo < nh) ? meta[mo + (h - h_lo)] : 0ull;
-    };
-    unsigned long long sum = 0;
-    for (uint32_t j = 0; j < PER; ++j) sum += cnt(tid * PER + j);
-    unsigned long long v = sum;
+    }
+};
+struct RowValues {  // v[h] (one row)
+    const unsigned long long *v;
+    __device__ unsigned long long operator()(uint32_t, uint32_t h) const { return v[h]; }
+};
+constexpr uint32_t kScanBlocks = kBuckets16 / 1024;  // 64
+
+template <typename Gen>
+__global__ __launch_bounds__(1024) void k_rowscan_reduce(Gen gen,
+                                                         unsigned long long *__restrict__ part) {
+    __shared__ unsigned long long s_w[16];
+    const uint32_t row = blockIdx.y, b = blockIdx.x, tid = threadIdx.x, lane = tid & 63,
+                   w = tid >> 6;
+    unsigned long long x = gen(row, b * 1024 + tid);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+    if (lane == 0) s_w[w] = x;
+    __syncthreads();
+    if (tid == 0) {
+        unsigned long long t = 0;
+        for (int i = 0; i < 16; ++i) t += s_w[i];
+        part[row * kScanBlocks + b] = t;
+    }
+}
+
+template <typename Gen>
+__global__ __launch_bounds__(1024) void k_rowscan_apply(Gen gen,
+                                                        const unsigned long long *__restrict__ part,
+                                                        unsigned long long *__restrict__ out,
+                                                        uint64_t row_stride) {
+    __shared__ unsigned long long s_w[16];
+    __shared__ unsigned long long s_pre;
+    const uint32_t row = blockIdx.y, b = blockIdx.x, tid = threadIdx.x, lane = tid & 63,
+                   w = tid >> 6;
+    if (tid < 64) {  // prefix of the earlier blocks of this row (b < 64 partials)
+        unsigned long long v = tid < b ? part[row * kScanBlocks + tid] : 0ull;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        if (tid == 0) s_pre = v;
+    }
+    const unsigned long long c = gen(row, b * 1024 + tid);
+    unsigned long long x = c;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-        const unsigned long long t = __shfl_up(v, o);
-        if (lane >= o) v += t;
+        const unsigned long long t = __shfl_up(x, o);
+        if ((int)lane >= o) x += t;
     }
-    if (lane == 63) s_w[w] = v;
+    if (lane == 63) s_w[w] = x;
     __syncthreads();
-    unsigned long long run = v - sum;
+    unsigned long long run = s_pre + x - c;
     for (uint32_t ww = 0; ww < w; ++ww) run += s_w[ww];
-    unsigned long long *pp = pos + (uint64_t)p * (kBuckets16 + 1);
-    for (uint32_t j = 0; j < PER; ++j) {
-        pp[tid * PER + j] = run;
-        run += cnt(tid * PER + j);
-    }
-    if (tid == 1023) pp[kBuckets16] = run;
+    unsigned long long *o = out + row * row_stride;
+    o[b * 1024 + tid] = run;
+    if (b == kScanBlocks - 1 && tid == 1023) o[kBuckets16] = run + c;
 }
 
 // Self-check of the LDS lane-order property wave_rank<true> relies on: every wave of a block
@@ -1462,7 +1623,11 @@ hipError_t launch_seg_partition(const SegPass &sp, hipStream_t s) {
     const ull *segs = reinterpret_cast<const ull *>(sp.segs);
     ull *gsum = reinterpret_cast<ull *>(sp.gsum);
     constexpr int B = kPartBlock, I = kSweepTile / kPartBlock;
-    if (sp.flip_out)
+    if (sp.out16)
+        k_seg_partition<B, I, false, uint16_t><<<sp.max_tiles, B, 0, s>>>(
+            sp.in, sp.out16, sp.shift, sp.tcounts, gsum, reinterpret_cast<const ull *>(sp.cstart),
+            segs, sp.tpfx, sp.gpfx, sp.segmap, sp.nseg);
+    else if (sp.flip_out)
         k_seg_partition<B, I, true><<<sp.max_tiles, B, 0, s>>>(
             sp.in, sp.out, sp.shift, sp.tcounts, gsum, reinterpret_cast<const ull *>(sp.cstart),
             segs, sp.tpfx, sp.gpfx, sp.segmap, sp.nseg);
@@ -1470,6 +1635,34 @@ hipError_t launch_seg_partition(const SegPass &sp, hipStream_t s) {
         k_seg_partition<B, I, false><<<sp.max_tiles, B, 0, s>>>(
             sp.in, sp.out, sp.shift, sp.tcounts, gsum, reinterpret_cast<const ull *>(sp.cstart),
             segs, sp.tpfx, sp.gpfx, sp.segmap, sp.nseg);
+    return hipGetLastError();
+}
+
+hipError_t launch_unpack16(const uint16_t *in, uint64_t n, uint32_t h, int32_t *out,
+                           hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    k_unpack16<<<grid_for(n, 256, 4096), 256, 0, s>>>(in, n, h, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_gb_from_plan(const uint64_t *bases, const uint64_t *totals,
+                               const uint64_t *segs, uint32_t nseg, const uint64_t *cstart,
+                               uint64_t n, uint64_t *gb, hipStream_t s) {
+    using ull = unsigned long long;
+    k_gb_from_plan<<<kRadix, kRadix, 0, s>>>(
+        reinterpret_cast<const ull *>(bases), reinterpret_cast<const ull *>(totals),
+        reinterpret_cast<const ull *>(segs), nseg, reinterpret_cast<const ull *>(cstart), n,
+        reinterpret_cast<ull *>(gb));
+    return hipGetLastError();
+}
+
+hipError_t launch_count_below16(const uint16_t *a, const uint64_t *gb, const uint64_t *xs,
+                                int m, uint64_t *out, hipStream_t s) {
+    using ull = unsigned long long;
+    if (m <= 0) return hipSuccess;
+    k_count_below16<<<(m + 255) / 256, 256, 0, s>>>(a, reinterpret_cast<const ull *>(gb),
+                                                    reinterpret_cast<const ull *>(xs), m,
+                                                    reinterpret_cast<ull *>(out));
     return hipGetLastError();
 }
 
@@ -1511,21 +1704,28 @@ hipError_t launch_run_bounds(const int32_t *recv, const uint64_t *roff, const ui
 }
 
 hipError_t launch_pos_from_meta(const uint32_t *meta, const uint64_t *moff, uint32_t h_lo,
-                                uint32_t nh, int P, uint64_t *pos, hipStream_t s) {
+                                uint32_t nh, int P, uint64_t *pos, uint64_t *scratch,
+                                hipStream_t s) {
     using ull = unsigned long long;
     if (P < 1 || P > 64) return hipErrorInvalidValue;
-    k_pos_from_meta<<<P, 1024, 0, s>>>(meta, reinterpret_cast<const ull *>(moff), h_lo, nh,
-                                       reinterpret_cast<ull *>(pos));
+    const MetaCounts gen{meta, reinterpret_cast<const ull *>(moff), h_lo, nh};
+    ull *part = reinterpret_cast<ull *>(scratch);
+    k_rowscan_reduce<<<dim3(kScanBlocks, P), 1024, 0, s>>>(gen, part);
+    k_rowscan_apply<<<dim3(kScanBlocks, P), 1024, 0, s>>>(gen, part, reinterpret_cast<ull *>(pos),
+                                                          kBuckets16 + 1);
     return hipGetLastError();
 }
 
 hipError_t launch_recv_classify(const uint64_t *pos, int P, uint64_t *bsize, uint64_t *bstart,
-                                const WorkLists &wl, hipStream_t s) {
+                                const WorkLists &wl, uint64_t *scratch, hipStream_t s) {
     using ull = unsigned long long;
     k_bucket_sizes<<<kBuckets16 / 256, 256, 0, s>>>(reinterpret_cast<const ull *>(pos), P,
                                                      reinterpret_cast<ull *>(bsize));
-    k_bucket_scan<<<1, 1024, 0, s>>>(reinterpret_cast<const ull *>(bsize),
-                                     reinterpret_cast<ull *>(bstart));
+    const RowValues gen{reinterpret_cast<const ull *>(bsize)};
+    ull *part = reinterpret_cast<ull *>(scratch);
+    k_rowscan_reduce<<<dim3(kScanBlocks, 1), 1024, 0, s>>>(gen, part);
+    k_rowscan_apply<<<dim3(kScanBlocks, 1), 1024, 0, s>>>(gen, part, reinterpret_cast<ull *>(bstart),
+                                                          kBuckets16 + 1);
     k_classify_gather<<<kBuckets16 / kRadix, kRadix, 0, s>>>(
         reinterpret_cast<const ull *>(bsize), reinterpret_cast<const ull *>(bstart), wl);
     return hipGetLastError();
@@ -1575,6 +1775,35 @@ hipError_t launch_gather_copy(const void *recv, bool packed16, const uint64_t *p
     return hipGetLastError();
 }
 
+hipError_t launch_hist_expand(const void *recv, bool packed16, const uint64_t *pos,
+                              const uint64_t *roff, int P, const uint64_t *bstart,
+                              const uint64_t *list, uint32_t nlist, uint32_t *out,
+                              hipStream_t s) {
+    using ull = unsigned long long;
+    if (nlist == 0) return hipSuccess;
+    if (P < 1 || P > 64) return hipErrorInvalidValue;
+    auto *ps = reinterpret_cast<const ull *>(pos);
+    auto *ro = reinterpret_cast<const ull *>(roff);
+    auto *bs = reinterpret_cast<const ull *>(bstart);
+    auto *l = reinterpret_cast<const ull *>(list);
+    if (packed16)
+        k_hist_expand<<<nlist, 1024, 0, s>>>(reinterpret_cast<const uint16_t *>(recv), ps, ro, P,
+                                             bs, l, out);
+    else
+        k_hist_expand<<<nlist, 1024, 0, s>>>(reinterpret_cast<const int32_t *>(recv), ps, ro, P,
+                                             bs, l, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_list_to_segments(uint64_t *list, uint32_t n, const uint64_t *bstart,
+                                   hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    k_list_to_segments<<<(n + 255) / 256, 256, 0, s>>>(
+        reinterpret_cast<unsigned long long *>(list), n,
+        reinterpret_cast<const unsigned long long *>(bstart));
+    return hipGetLastError();
+}
+
 hipError_t launch_pack16(const int32_t *a, uint64_t n, uint16_t *out, hipStream_t s) {
     if (n == 0) return hipSuccess;
     k_pack16<<<grid_for(n, 256, 8192), 256, 0, s>>>(a, n, out);
@@ -1584,8 +1813,9 @@ hipError_t launch_pack16(const int32_t *a, uint64_t n, uint16_t *out, hipStream_
 hipError_t launch_meta_counts(const uint64_t *gb, const uint64_t *rng, int nrng, uint32_t *meta,
                               hipStream_t s) {
     if (nrng <= 0) return hipSuccess;
-    k_meta_counts<<<nrng, 256, 0, s>>>(reinterpret_cast<const unsigned long long *>(gb),
-                                       reinterpret_cast<const unsigned long long *>(rng), meta);
+    k_meta_counts<<<dim3(kBuckets16 / 256, nrng), 256, 0, s>>>(
+        reinterpret_cast<const unsigned long long *>(gb),
+        reinterpret_cast<const unsigned long long *>(rng), meta);
     return hipGetLastError();
 }
 

@@ -51,10 +51,11 @@ struct gsort_ctx {
     bool atomic_rank = false;  // LDS lane-order property verified on this device (create)
     // MSD scratch: segment plan/maps, child starts, work lists (u64 {start, len} pairs)
     DevBuf m_tpfx, m_gpfx, m_segmap, m_groupmap, m_cstart, m_next[2], m_local[kLocalClasses];
+    uint64_t group16_nseg = 0;  // msd_sort(group16): level-2 segments (list m_next[0])
     DevBuf m_split;  // radix select thresholds + counts of the distributed radix
     DevBuf m_rpos, m_bsize;  // receive side: run bucket bounds (P x 65537), bucket size/start
     DevBuf m_bseg, m_blist;  // boundary groups of the distributed radix: scratch, K11 list
-    DevBuf m_gb, m_pack, m_meta;  // packed exchange: bucket bounds, low 16 bits, counts
+    DevBuf m_gb, m_pack, m_meta, m_g16;  // packed exchange: bucket bounds, low 16 bits, counts
     // device small area: [0, 8K) hist4 (4x256 u64) | [8K, 10K) pass digit totals (256 u64) |
     // [10K, 12K) pass digit bases (256 u64) | [20K, 256K) plans / samples / routing tables
     char *d_small = nullptr;
@@ -279,7 +280,7 @@ WorkLists work_lists(gsort_ctx *c, int next) {
 // out, as does K11.
 gsort_status msd_levels(gsort_ctx *c, int L, uint32_t *cur, uint32_t *out, uint32_t *tmp,
                         int cur_list, uint64_t *h, gsort_stats *stats, int *levels,
-                        int last_level = 0) {
+                        int last_level = 0, uint16_t *out16 = nullptr) {
     auto lst = [](DevBuf &b) { return reinterpret_cast<uint64_t *>(b.p); };
     uint64_t *ctr = reinterpret_cast<uint64_t *>(c->d_small + OFF_CTR);
     auto lists = [&](int next) { return work_lists(c, next); };
@@ -330,6 +331,7 @@ gsort_status msd_levels(gsort_ctx *c, int L, uint32_t *cur, uint32_t *out, uint3
         sp.lists = lists(cur_list ^ 1);
         // digit 0: every child is a run of equal keys; a partition-only sort stops here too
         if (L == last_level) sp.lists.ctr = nullptr;
+        if (L == last_level) sp.out16 = out16;
         t = tic(c);
         HIP_TRY(c, hipMemsetAsync(ctr, 0, kCtrBytes, c->stream));
         HIP_TRY(c, launch_seg_count(sp, c->stream));
@@ -349,9 +351,11 @@ gsort_status msd_levels(gsort_ctx *c, int L, uint32_t *cur, uint32_t *out, uint3
 
 
 // group16: stop after level 2 -- out holds the keys (int32) grouped by their top 16 bits
-// (ordered u32) but not sorted inside a group (the sender side of the distributed radix).
+// (ordered u32) but not sorted inside a group (the sender side of the distributed radix);
+// with out16 and n > kLocalMax, level 2 stores only the low 16 bits of every key, at out16.
 gsort_status msd_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *out,
-                      uint32_t *tmp, gsort_stats *stats, bool group16 = false) {
+                      uint32_t *tmp, gsort_stats *stats, bool group16 = false,
+                      uint16_t *out16 = nullptr) {
     if (n == 0) return GSORT_OK;
     uint64_t *ctr = reinterpret_cast<uint64_t *>(c->d_small + OFF_CTR);
     if (n <= kLocalMax) {  // one bucket: all four digits in LDS
@@ -390,8 +394,10 @@ gsort_status msd_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *ou
     HIP_TRY(c, launch_classify_buckets(bases, totals, wl3, c->stream));
     uint64_t h[3 * (kLocalClasses + 1)];  // {entries, keys, longest}: next level, K11 classes
     ST_TRY(read_counters(c, h));
+    c->group16_nseg = h[0];
     int levels = 1;
-    ST_TRY(msd_levels(c, 2, tmp, out, tmp, 0, h, stats, &levels, group16 ? 2 : 0));
+    ST_TRY(msd_levels(c, 2, tmp, out, tmp, 0, h, stats, &levels, group16 ? 2 : 0,
+                      group16 ? out16 : nullptr));
     if (stats) stats->passes_run = levels;
     return GSORT_OK;
 }
@@ -419,6 +425,9 @@ gsort_status local_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *
 // recv holds the P runs back to back (run p has rlen[p] keys), each grouped by the top 16 bits
 // (ordered u32): int32 keys, or with packed16 only their low 16 bits, in which case the caller
 // has already filled c->m_rpos (pos[p][h], launch_pos_from_meta).
+// bucket sizes (65536) + starts (65537) + row-scan partials (64 x 64), u64
+constexpr size_t kBsizeBytes = ((size_t)2 * kBuckets16 + 1 + 64 * 64) * 8;
+
 gsort_status recv_sort(gsort_ctx *c, const void *recv, bool packed16,
                        const std::vector<uint64_t> &rlen, uint64_t n, uint32_t *out,
                        uint32_t *tmp, gsort_stats *stats) {
@@ -431,7 +440,7 @@ gsort_status recv_sort(gsort_ctx *c, const void *recv, bool packed16,
     if (P > 64) return set_err(c, GSORT_EINVAL, "packed exchange supports at most 64 ranks");
     hipEvent_t t = tic(c);
     ST_TRY(ensure(c, c->m_rpos, (size_t)P * (kBuckets16 + 1) * 8));
-    ST_TRY(ensure(c, c->m_bsize, (size_t)kBuckets16 * 16));
+    ST_TRY(ensure(c, c->m_bsize, kBsizeBytes));
     ST_TRY(ensure_list(c, c->m_next[0], kBuckets16));
     for (auto &b : c->m_local) ST_TRY(ensure_list(c, b, kBuckets16));
     uint64_t *h_r = reinterpret_cast<uint64_t *>(c->h_small + OFF_PLAN);
@@ -447,7 +456,8 @@ gsort_status recv_sort(gsort_ctx *c, const void *recv, bool packed16,
     if (!packed16)
         HIP_TRY(c, launch_run_bounds(reinterpret_cast<const int32_t *>(recv), d_r, d_r + P, P, pos,
                                      c->stream));
-    HIP_TRY(c, launch_recv_classify(pos, P, bsize, bstart, work_lists(c, 0), c->stream));
+    HIP_TRY(c, launch_recv_classify(pos, P, bsize, bstart, work_lists(c, 0),
+                                    bstart + kBuckets16 + 1, c->stream));
     toc(c, PH_COUNT, t);
     uint64_t h[3 * (kLocalClasses + 1)];
     ST_TRY(read_counters(c, h));
@@ -461,7 +471,16 @@ gsort_status recv_sort(gsort_ctx *c, const void *recv, bool packed16,
         toc(c, PH_BUCKET, t);
         if (stats) { stats->buckets_local += hk[0]; stats->keys_bucket_sort += hk[1]; }
     }
-    if (h[0]) {  // oversized buckets: into place, then levels 1 and 0
+    if (h[0] && h[2] <= kHxMax) {  // buckets past LDS size: K18 counting sort
+        t = tic(c);
+        HIP_TRY(c, launch_hist_expand(recv, packed16, pos, d_r, P, bstart,
+                                      reinterpret_cast<uint64_t *>(c->m_next[0].p),
+                                      (uint32_t)h[0], out, c->stream));
+        toc(c, PH_BUCKET, t);
+        if (stats) { stats->buckets_local += h[0]; stats->keys_bucket_sort += h[1]; }
+    } else if (h[0]) {  // a bucket past kHxMax: all of list 0 into place, then levels 1 and 0
+        HIP_TRY(c, launch_list_to_segments(reinterpret_cast<uint64_t *>(c->m_next[0].p),
+                                           (uint32_t)h[0], bstart, c->stream));
         HIP_TRY(c, launch_gather_copy(recv, packed16, pos, d_r, P, bsize, bstart, out, c->stream));
         for (int k = 3; k < 3 * (kLocalClasses + 1); ++k) h[k] = 0;
         int levels = 0;
@@ -525,6 +544,32 @@ gsort_status sort_groups(gsort_ctx *c, int32_t *a,
     return GSORT_OK;
 }
 
+// The same on the packed send buffer: groups = {16-bit bucket h, first position}, ends[i] =
+// the group's end (gb[h + 1]).  Each group is rebuilt as int32 keys in scratch, sorted by
+// sort_groups (K11 or LSD passes by size), and packed back in place.
+gsort_status sort_groups16(gsort_ctx *c, uint16_t *pack,
+                           const std::vector<std::pair<uint64_t, uint64_t>> &groups,
+                           const std::vector<uint64_t> &ends) {
+    uint64_t total = 0;
+    for (size_t i = 0; i < groups.size(); ++i) total += ends[i] - groups[i].second;
+    ST_TRY(ensure(c, c->m_g16, std::max<uint64_t>(total, 1) * 4));
+    int32_t *scr = reinterpret_cast<int32_t *>(c->m_g16.p);
+    std::vector<std::pair<uint64_t, uint64_t>> local;
+    uint64_t off = 0;
+    for (size_t i = 0; i < groups.size(); ++i) {
+        const uint64_t a = groups[i].second, len = ends[i] - a;
+        HIP_TRY(c, launch_unpack16(pack + a, len, (uint32_t)groups[i].first, scr + off,
+                                   c->stream));
+        local.push_back({off, len});
+        off += len;
+    }
+    ST_TRY(sort_groups(c, scr, local));
+    for (size_t i = 0; i < groups.size(); ++i)
+        HIP_TRY(c, launch_pack16(scr + local[i].first, local[i].second, pack + groups[i].second,
+                                 c->stream));
+    return GSORT_OK;
+}
+
 // ---- distributed radix (P > 1): local sort, exact splitters, ONE exchange, local sort ------
 // The reference keeps rank q on global positions [qB, (q+1)B) by routing every key through
 // rank 0 on each of its base-P passes (mpi_radix_sort.c:139 Scatter, :150-173 all-to-all,
@@ -544,20 +589,50 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
     uint64_t B, mine;
     block_of(N, P, me, &B, &mine);
     const uint64_t cap = std::max<uint64_t>(std::max(n_in, mine), 1);
-    ST_TRY(ensure(c, c->slot[S_SORTED], std::max<uint64_t>(n_in, 1) * 4));
     ST_TRY(ensure(c, c->slot[S_TMP], cap * 4));
     ST_TRY(ensure(c, c->slot[S_RECV], std::max<uint64_t>(mine, 1) * 4));
     ST_TRY(ensure(c, c->slot[S_OUT], std::max<uint64_t>(mine, 1) * 4));
+    ST_TRY(ensure(c, c->m_gb, (size_t)(kBuckets16 + 1) * 8));
+    ST_TRY(ensure(c, c->m_pack, std::max<uint64_t>(n_in, 1) * 2));
+    uint64_t *gb = reinterpret_cast<uint64_t *>(c->m_gb.p);
+    uint16_t *pack = reinterpret_cast<uint16_t *>(c->m_pack.p);
     // (1) group the block by its top 16 bits (MSD levels 3 and 2 only: the receivers sort the
-    // low 16 bits anyway); only the groups holding a boundary key get sorted, below
-    int32_t *sorted = slot_ptr<int32_t>(c, S_SORTED);
+    // low 16 bits anyway).  Level 2 stores just the low 16 bits of every key -- the packed send
+    // buffer -- and the 16-bit bucket bounds gb come from the MSD plan (K17), not the keys.  A
+    // block of <= kLocalMax keys is sorted whole in LDS instead, then bounded and packed.
     if (stats) stats->local_algo = c->local_algo;
+    const bool packed_msd = n_in > kLocalMax;
+    hipEvent_t t;
     {
         gsort_stats tmp_st;
         memset(&tmp_st, 0, sizeof(tmp_st));
+        int32_t *sorted = nullptr;
+        if (!packed_msd) {
+            ST_TRY(ensure(c, c->slot[S_SORTED], std::max<uint64_t>(n_in, 1) * 4));
+            sorted = slot_ptr<int32_t>(c, S_SORTED);
+        }
         ST_TRY(msd_sort(c, reinterpret_cast<const uint32_t *>(d_keys), n_in,
                         reinterpret_cast<uint32_t *>(sorted), slot_ptr<uint32_t>(c, S_TMP),
-                        stats ? stats : &tmp_st, true));
+                        stats ? stats : &tmp_st, true, packed_msd ? pack : nullptr));
+        t = tic(c);
+        if (packed_msd) {
+            HIP_TRY(c, launch_gb_from_plan(reinterpret_cast<uint64_t *>(c->d_small + OFF_BASES),
+                                           reinterpret_cast<uint64_t *>(c->d_small + OFF_TOT),
+                                           reinterpret_cast<uint64_t *>(c->m_next[0].p),
+                                           (uint32_t)c->group16_nseg,
+                                           reinterpret_cast<uint64_t *>(c->m_cstart.p), n_in,
+                                           gb, c->stream));
+        } else {
+            uint64_t *h_one = reinterpret_cast<uint64_t *>(c->h_small + OFF_ONE);
+            uint64_t *d_one = reinterpret_cast<uint64_t *>(c->d_small + OFF_ONE);
+            HIP_TRY(c, hipStreamSynchronize(c->stream));  // h_one may feed an earlier copy
+            h_one[0] = 0;
+            h_one[1] = n_in;
+            HIP_TRY(c, hipMemcpyAsync(d_one, h_one, 16, hipMemcpyHostToDevice, c->stream));
+            HIP_TRY(c, launch_run_bounds(sorted, d_one, d_one + 1, 1, gb, c->stream));
+            HIP_TRY(c, launch_pack16(sorted, n_in, pack, c->stream));
+        }
+        toc(c, PH_PLACE, t);
     }
     int pr = stats ? stats->passes_run : 0;
 
@@ -566,18 +641,18 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
     std::vector<uint64_t> g(nb), prefix(nb, 0), hx((size_t)nb * M), all((size_t)P * nb * M);
     std::vector<int> dsel(nb, 0);
     for (int q = 0; q < nb; ++q) g[q] = std::min<uint64_t>((uint64_t)(q + 1) * B, N);
-    ST_TRY(ensure(c, c->m_split, (size_t)nb * M * 16));
-    ST_TRY(ensure(c, c->slot[S_STAGE], (size_t)P * nb * M * 8));
+    ST_TRY(ensure(c, c->m_split, (size_t)std::max(nb, 1) * M * 16));
+    ST_TRY(ensure(c, c->slot[S_STAGE], (size_t)P * std::max(nb, 1) * M * 8));
     uint64_t *d_xs = reinterpret_cast<uint64_t *>(c->m_split.p);
     uint64_t *d_cnt = d_xs + (size_t)nb * M;
-    hipEvent_t t = tic(c);
+    t = tic(c);
     for (int k = 0; k < 4; ++k) {
         const int shift = 24 - 8 * k;
         for (int q = 0; q < nb; ++q)
             for (int d = 0; d < M; ++d) hx[(size_t)q * M + d] = prefix[q] + ((uint64_t)d << shift);
         HIP_TRY(c, hipMemcpyAsync(d_xs, hx.data(), hx.size() * 8, hipMemcpyHostToDevice,
                                   c->stream));
-        HIP_TRY(c, launch_count_below(sorted, n_in, d_xs, nb * M, d_cnt, c->stream));
+        HIP_TRY(c, launch_count_below16(pack, gb, d_xs, nb * M, d_cnt, c->stream));
         ST_TRY(comm_try(c, c->comm->allgather(d_cnt, c->slot[S_STAGE].p, (size_t)nb * M * 8,
                                               c->stream)));
         HIP_TRY(c, hipMemcpyAsync(all.data(), c->slot[S_STAGE].p, all.size() * 8,
@@ -595,16 +670,25 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
             prefix[q] += (uint64_t)best << shift;
         }
         if (k == 1) {  // the 16-bit group of every boundary is known: sort it on this rank
-            std::vector<std::pair<uint64_t, uint64_t>> groups;
+            std::vector<std::pair<uint64_t, uint64_t>> groups;  // {h, first position}
+            std::vector<uint64_t> glen;
             for (int q = 0; q < nb; ++q) {
                 if (g[q] >= N) continue;
                 const uint64_t *row = &all[((size_t)me * nb + q) * M];
                 if (row[dsel[q] + 1] > row[dsel[q]])
-                    groups.push_back({row[dsel[q]], row[dsel[q] + 1] - row[dsel[q]]});
+                    groups.push_back({prefix[q] >> 16, row[dsel[q]]});
             }
             std::sort(groups.begin(), groups.end());
             groups.erase(std::unique(groups.begin(), groups.end()), groups.end());
-            ST_TRY(sort_groups(c, sorted, groups));
+            if (!groups.empty()) {
+                // group lengths: the next bucket's start (gb) on the host for these few groups
+                std::vector<uint64_t> h_gb(groups.size());
+                for (size_t i = 0; i < groups.size(); ++i)
+                    HIP_TRY(c, hipMemcpyAsync(&h_gb[i], gb + groups[i].first + 1, 8,
+                                              hipMemcpyDeviceToHost, c->stream));
+                HIP_TRY(c, hipStreamSynchronize(c->stream));
+                ST_TRY(sort_groups16(c, pack, groups, h_gb));
+            }
         }
     }
     toc(c, PH_SAMPLE, t);
@@ -630,8 +714,6 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
         nh[q] = (hi >> 16) - hlo[q] + 1;
         cut[q + 1] = cut[q] + send[q];
     }
-    ST_TRY(ensure(c, c->m_gb, (size_t)(kBuckets16 + 1) * 8));
-    ST_TRY(ensure(c, c->m_pack, std::max<uint64_t>(n_in, 1) * 2));
     uint64_t meta_n = 0;
     std::vector<uint64_t> rng;
     for (int q = 0; q < P; ++q)
@@ -642,7 +724,7 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
     uint64_t nsrc = 0;
     for (int p = 0; p < P; ++p) nsrc += recv[p] ? 1 : 0;
     ST_TRY(ensure(c, c->m_meta, (std::max<uint64_t>(meta_n, 1) + nsrc * nh[me] + 1) * 4 +
-                                    (rng.size() + 2 * P + 2) * 8));
+                                    (rng.size() + P + 2) * 8));
     uint32_t *meta_s = reinterpret_cast<uint32_t *>(c->m_meta.p);
     uint32_t *meta_r = meta_s + std::max<uint64_t>(meta_n, 1);
     uint64_t *d_tab = reinterpret_cast<uint64_t *>(
@@ -656,16 +738,11 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
             if (recv[p]) moff[p] = (k++) * nh[me];
     }
     tab.insert(tab.end(), moff.begin(), moff.end());
-    tab.insert(tab.end(), {0ull, n_in});  // this rank's block as one run (bucket bounds)
     HIP_TRY(c, hipMemcpyAsync(d_tab, tab.data(), tab.size() * 8, hipMemcpyHostToDevice,
                               c->stream));
-    const uint64_t *d_rng = d_tab, *d_moff = d_tab + rng.size(), *d_one = d_moff + P;
-    uint64_t *gb = reinterpret_cast<uint64_t *>(c->m_gb.p);
-    uint16_t *pack = reinterpret_cast<uint16_t *>(c->m_pack.p);
+    const uint64_t *d_rng = d_tab, *d_moff = d_tab + rng.size();
     t = tic(c);
-    HIP_TRY(c, launch_run_bounds(sorted, d_one, d_one + 1, 1, gb, c->stream));
     HIP_TRY(c, launch_meta_counts(gb, d_rng, (int)(rng.size() / 5), meta_s, c->stream));
-    HIP_TRY(c, launch_pack16(sorted, n_in, pack, c->stream));
     toc(c, PH_PLACE, t);
     std::vector<size_t> sc(P, 0), sd(P, 0), rc(P, 0), rd(P, 0);
     {
@@ -696,8 +773,11 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
     // (5) the P received runs -> one sorted block (recv_sort), their bucket bounds from the counts
     t = tic(c);
     ST_TRY(ensure(c, c->m_rpos, (size_t)P * (kBuckets16 + 1) * 8));
+    ST_TRY(ensure(c, c->m_bsize, kBsizeBytes));
     HIP_TRY(c, launch_pos_from_meta(meta_r, d_moff, (uint32_t)hlo[me], (uint32_t)nh[me], P,
-                                    reinterpret_cast<uint64_t *>(c->m_rpos.p), c->stream));
+                                    reinterpret_cast<uint64_t *>(c->m_rpos.p),
+                                    reinterpret_cast<uint64_t *>(c->m_bsize.p) + 2 * kBuckets16 + 1,
+                                    c->stream));
     ST_TRY(recv_sort(c, rbuf, true, recv, mine, slot_ptr<uint32_t>(c, S_OUT),
                      slot_ptr<uint32_t>(c, S_TMP), stats));
     toc(c, PH_MERGE, t);
@@ -1072,7 +1152,8 @@ gsort_status gsort_destroy(gsort_ctx *c) {
     if (c->gsum.p) (void)hipFree(c->gsum.p);
     for (DevBuf *b : {&c->m_tpfx, &c->m_gpfx, &c->m_segmap, &c->m_groupmap, &c->m_cstart,
                       &c->m_next[0], &c->m_next[1], &c->m_split, &c->m_rpos, &c->m_bsize,
-                      &c->m_bseg, &c->m_blist, &c->m_gb, &c->m_pack, &c->m_meta})
+                      &c->m_bseg, &c->m_blist, &c->m_gb, &c->m_pack, &c->m_meta,
+                      &c->m_g16})
         if (b->p) (void)hipFree(b->p);
     for (auto &b : c->m_local)
         if (b.p) (void)hipFree(b.p);

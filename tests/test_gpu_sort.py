@@ -237,7 +237,7 @@ def test_radix_multirank_uneven_and_empty_inputs(gsort, orc, local):
 
 
 @pytest.mark.parametrize("case", ["all_equal", "two_values", "boundary_dups", "tiny",
-                                  "extremes", "big_uniform", "big_groups"])
+                                  "extremes", "big_uniform", "big_groups", "wide_buckets"])
 def test_radix_multirank_splitter_edges(gsort, orc, case):
     """Exact splitters where a boundary key repeats across ranks and blocks (copies split in
     rank order), fewer keys than ranks, INT_MIN/INT_MAX keys, and a 2^22-key sort."""
@@ -254,6 +254,9 @@ def test_radix_multirank_splitter_edges(gsort, orc, case):
         # sender (LSD group sort) and receive buckets larger than kLocalMax (gather + levels)
         "big_groups": (np.repeat(np.array([-5, 0, 7], dtype=np.int64) << 16, 60000) +
                        rng.integers(0, 1 << 16, 180000)).astype(np.int32),
+        # 64 received 16-bit buckets of ~13000 keys per rank at P = 5 (the weak-scaling shape
+        # of 2^28 keys per GPU at P = 8: receive buckets past kLocalMax, sorted by K18)
+        "wide_buckets": rng.integers(0, 1 << 22, 1 << 22).astype(np.int32),
     }[case]
     rng.shuffle(keys)
     cuts = np.sort(rng.integers(0, keys.size + 1, P - 1))
@@ -307,3 +310,23 @@ def test_sample_multirank_zipf_skew(gsort, orc):
     got = np.concatenate([res[r][0] for r in range(P)])
     assert np.array_equal(got, np.sort(keys))
     assert max(res[r][0].size for r in range(P)) > 0.25 * n
+
+
+@pytest.mark.parametrize("algo", ["radix", "sample"])
+@pytest.mark.parametrize("P,span,n", [(2, 1 << 22, 1 << 22), (4, 1 << 21, (1 << 22) + 3),
+                                      (2, 1 << 16, (1 << 22) + 5), (3, 1 << 17, 3 << 20)])
+def test_multirank_large_receive_buckets(gsort, P, span, n, algo):
+    """Receive-side 16-bit buckets past kLocalMax: K18's counting sort from the pieces
+    (<= kHxMax keys) and, for a bucket past kHxMax (span 2^16 at P = 2: one bucket of ~2M keys
+    per rank), the gather + MSD levels fallback."""
+    rng = np.random.default_rng(P * 1000 + span % 977 + n % 13)
+    keys = (rng.integers(0, span, n) - span // 2).astype(np.int32)
+    B = -(-n // P)
+    blocks = [keys[r * B:(r + 1) * B] for r in range(P)]
+    res = run_group(gsort, blocks, algo)
+    got = np.concatenate([res[r][0] for r in range(P)])
+    assert np.array_equal(got, np.sort(keys))
+    if algo == "radix":
+        ref = np.sort(keys)
+        for q in range(P):
+            assert np.array_equal(res[q][0], ref[q * B:(q + 1) * B]), q
