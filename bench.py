@@ -126,10 +126,21 @@ def kernel_rooflines(stats, n_local):
     add("k_scatter (K3: rank + stable scatter of one LSD pass)", ("k_scatter",),
         [x for s in stats for x in s["ms_pass"]],
         [n_local for s in stats for x in s["ms_pass"]], PASS_BYTES_PER_KEY)
-    add("k_partition / k_seg_partition (K3u: unstable MSD partition of one level)",
-        ("k_partition", "k_seg_partition"),
-        [x for s in stats for x in s["ms_level"]],
-        [k for s in stats for k in s["keys_level"]], PASS_BYTES_PER_KEY)
+    # MSD levels: ms_level[0] = level 3 (K3u k_partition); with the two-level plan (default,
+    # GSORT_PLAN16 != 0) ms_level[1] = level 2 (K3a k_partition_h16, runs reserved by atomics);
+    # every other level is a segmented K3u (k_seg_partition)
+    plan16 = os.environ.get("GSORT_PLAN16", "1") != "0"
+    seg_from = 2 if plan16 else 1
+    add("k_partition (K3u: level 3, unstable MSD partition of the whole block)",
+        ("k_partition<",), [s["ms_level"][0] for s in stats],
+        [s["keys_level"][0] for s in stats], PASS_BYTES_PER_KEY)
+    if plan16:
+        add("k_partition_h16 (K3a: level 2, runs reserved by atomics on the K12h cursors)",
+            ("k_partition_h16",), [s["ms_level"][1] for s in stats],
+            [s["keys_level"][1] for s in stats], PASS_BYTES_PER_KEY)
+    add("k_seg_partition (K3u: segmented MSD level)", ("k_seg_partition",),
+        [x for s in stats for x in s["ms_level"][seg_from:]],
+        [k for s in stats for k in s["keys_level"][seg_from:]], PASS_BYTES_PER_KEY)
     add("k_local_sort (K11: in-LDS sort of the small buckets)", ("k_local_sort",),
         [s["ms_bucket_sort"] for s in stats], [s["keys_bucket_sort"] for s in stats],
         PASS_BYTES_PER_KEY)

@@ -548,11 +548,17 @@ __device__ __forceinline__ void load_bucket(const uint32_t *src, uint32_t len,
 // dst_base (tid < 256) = out + global start of this tile's digit-tid keys.
 // OT = uint16_t stores only the low 16 bits of every key (the packed send buffer of the
 // distributed radix, whose groups are the top 16 bits).
+// resv != nullptr (K3a): the tile reserves its digit runs instead, one returning device-scope
+// atomicAdd on resv[digit] (a u32 cursor into out, relative to out) per non-empty digit, issued
+// as soon as the tile's counts are known and consumed only after the LDS scatter; dst_base is
+// then ignored.
 template <int BLOCK, int ITEMS, bool FIN, bool FOUT, typename OT = uint32_t>
 __device__ __forceinline__ void partition_tile(const uint32_t *__restrict__ in, uint64_t t0,
                                                uint32_t len, int shift, OT *dst_base,
                                                uint32_t *s_keys, uint32_t *s_cur,
-                                               OT **s_dst, uint32_t *s_wsum) {
+                                               OT **s_dst, uint32_t *s_wsum,
+                                               uint32_t *resv = nullptr,
+                                               OT *out = nullptr) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     constexpr int TILE = BLOCK * ITEMS;
     const bool full = len == (uint32_t)TILE;
@@ -567,8 +573,10 @@ __device__ __forceinline__ void partition_tile(const uint32_t *__restrict__ in, 
             r[i] = atomicAdd(&s_cur[(k[i] >> shift) & 255u], 1u);
     __syncthreads();
     uint32_t c = 0, excl = 0;
+    unsigned long long pos = 0;
     if (tid < kRadix) {
         c = s_cur[tid];
+        if (resv && c) pos = atomicAdd(&resv[tid], c);
         uint32_t v = c;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
@@ -582,13 +590,13 @@ __device__ __forceinline__ void partition_tile(const uint32_t *__restrict__ in, 
     if (tid < kRadix) {
         for (int ww = 0; ww < w; ++ww) excl += s_wsum[ww];
         s_cur[tid] = excl;
-        s_dst[tid] = dst_base - excl;
     }
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i)
         if (full || (uint32_t)(i * BLOCK + tid) < len)
             s_keys[s_cur[(k[i] >> shift) & 255u] + r[i]] = k[i];
+    if (tid < kRadix) s_dst[tid] = (resv ? out + pos : dst_base) - excl;
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
@@ -864,6 +872,227 @@ __global__ __launch_bounds__(BLOCK) void k_seg_partition(
                    toff[(uint64_t)t * kRadix + threadIdx.x];
     partition_tile<BLOCK, ITEMS, false, FOUT, OT>(in, st.t0, st.len, shift, dst_base, s_keys, s_cur,
                                               s_dst, s_wsum);
+}
+
+// =======================================================================================
+// Two-level plan (default MSD front end): level 2 without its own counting pass.
+//   K1h  level-3 tile counts (as K1) + a histogram of the top 16 bits, in the same read
+//   K2   scan of the level-3 tile counts (unchanged)
+//   K12h from the 16-bit histogram: every level-2 child's count and start, the level-2
+//        cursors, the work lists and the level-2 tile plan -- all before level 3 runs
+//   K3u  level 3 (unchanged)
+//   K3a  level 2: K3u whose tiles reserve their digit runs with one atomicAdd per digit on the
+//        child's cursor (an MSD level needs every key in its child, not a stable order)
+// Level 2 then costs 8 B/key instead of 12 (no K1s re-read, no K2s scans), and the host reads
+// the work-list counters while levels 3 and 2 run instead of between them.
+// =======================================================================================
+
+// K1h: tcounts[tile][256] = top-digit counts of every kSweepTile tile (exactly as K1), and per
+// workgroup a histogram of the top 16 bits (ordered u32) kept in LDS as packed u16 pairs
+// (32768 words, 128 KiB: one workgroup per CU, striding over the tiles; the next tile's loads
+// are in flight while the current one is counted).  At the end each workgroup stores its words
+// to part[blockIdx.x][.].  A u16 half that wraps is repaired through fix[] (u64, zeroed by the
+// caller): every wrap is seen by exactly one thread, whose atomic returned 0xffff in that half.
+// A wrapped low half lost 65536 and carried one into the high half; a carry out of the whole
+// word (a high half wrapping, or a low add on 0xffffffff) lost 65536 of the high bin.  Hence
+// count[h] = sum_b half_h(part[b]) + fix[h] (mod 2^64).
+__device__ __forceinline__ void h16_wrap(unsigned long long *fix, uint32_t b, uint32_t old) {
+    atomicAdd(&fix[b], 65536ull);
+    if (!(b & 1u)) {
+        atomicAdd(&fix[b | 1u], ~0ull);  // -1: the carry into the high half
+        if (old == 0xffffffffu) atomicAdd(&fix[b | 1u], 65536ull);
+    }
+}
+
+template <int BLOCK, bool FIN>
+__global__ __launch_bounds__(BLOCK) void k_counts_h16(const uint32_t *__restrict__ in, uint64_t n,
+                                                      uint32_t *__restrict__ tcounts,
+                                                      uint32_t *__restrict__ part,
+                                                      unsigned long long *__restrict__ fix) {
+    constexpr int ITEMS = kSweepTile / BLOCK;
+    constexpr uint32_t kWords = kBuckets16 / 2;
+    __shared__ uint32_t s_h[kWords];
+    __shared__ uint32_t s_t[kRadix];
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t i = tid; i < kWords; i += BLOCK) s_h[i] = 0;
+    if (tid < kRadix) s_t[tid] = 0;
+    const uint64_t ntiles = (n + kSweepTile - 1) / kSweepTile;
+    uint32_t k[ITEMS];
+    if (blockIdx.x < ntiles) {
+        const uint64_t t0 = (uint64_t)blockIdx.x * kSweepTile;
+        const uint32_t len = (uint32_t)min(n - t0, (uint64_t)kSweepTile);
+        load_tile<BLOCK, ITEMS, FIN>(in + t0 + tid, len == (uint32_t)kSweepTile, len, k);
+    }
+    for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        __syncthreads();  // zeroing / the previous tile's count store done
+        const uint32_t len = (uint32_t)min(n - t * kSweepTile, (uint64_t)kSweepTile);
+        const uint64_t tn = t + gridDim.x;
+        uint32_t kn[ITEMS];
+        if (tn < ntiles) {
+            const uint64_t t0 = tn * kSweepTile;
+            const uint32_t lenn = (uint32_t)min(n - t0, (uint64_t)kSweepTile);
+            load_tile<BLOCK, ITEMS, FIN>(in + t0 + tid, lenn == (uint32_t)kSweepTile, lenn, kn);
+        }
+        // all 8 returning atomics in flight before the first wrap test (measured: a test per
+        // atomic waits out each LDS round trip, 0.31 vs 0.30 ms at 2^28)
+        uint32_t old[ITEMS];
+        bool wrap = false;
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i) {
+            old[i] = 0;
+            if ((uint32_t)(i * BLOCK) + tid < len) {
+                atomicAdd(&s_t[k[i] >> 24], 1u);
+                const uint32_t b = k[i] >> 16;
+                old[i] = atomicAdd(&s_h[b >> 1], 1u << ((b & 1u) << 4));
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i)
+            wrap |= (uint32_t)(i * BLOCK) + tid < len &&
+                    ((old[i] >> (((k[i] >> 16) & 1u) << 4)) & 0xffffu) == 0xffffu;
+        if (wrap) {
+#pragma unroll
+            for (int i = 0; i < ITEMS; ++i) {
+                const uint32_t b = k[i] >> 16;
+                if ((uint32_t)(i * BLOCK) + tid < len &&
+                    ((old[i] >> ((b & 1u) << 4)) & 0xffffu) == 0xffffu)
+                    h16_wrap(fix, b, old[i]);
+            }
+        }
+        __syncthreads();
+        if (tid < kRadix) {
+            tcounts[t * kRadix + tid] = s_t[tid];
+            s_t[tid] = 0;
+        }
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i) k[i] = kn[i];
+    }
+    __syncthreads();
+    uint32_t *dst = part + (uint64_t)blockIdx.x * kWords;
+    for (uint32_t i = tid; i < kWords; i += BLOCK) dst[i] = s_h[i];
+}
+
+// Level-3 bucket s goes through level 2 (K3a) when it is too large for K11, or -- force, the
+// grouping of the distributed sender -- whenever it is non-empty.
+__device__ __forceinline__ bool level2_bucket(unsigned long long tot, int force) {
+    return force ? tot > 0 : tot > kLocalMax;
+}
+
+// Block-wide (kRadix threads) exclusive scan of one u64 per thread; *total = the sum.
+__device__ __forceinline__ unsigned long long block_excl_scan(unsigned long long v,
+                                                              unsigned long long *s_w,
+                                                              unsigned long long *total) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    unsigned long long x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned long long t = __shfl_up(x, o);
+        if (lane >= o) x += t;
+    }
+    __syncthreads();
+    if (lane == 63) s_w[w] = x;
+    __syncthreads();
+    unsigned long long excl = x - v, all = 0;
+    for (uint32_t ww = 0; ww < kRadix / 64; ++ww) {
+        if (ww < w) excl += s_w[ww];
+        all += s_w[ww];
+    }
+    *total = all;
+    return excl;
+}
+
+// K12h: block s = level-3 digit, thread e = level-2 digit.  c = the child's key count (the
+// K1h partials of nblk workgroups + fix), cstart[s*256+e] = its first position (bases[s] + the
+// exclusive scan over e: the 65536 bucket bounds of the top 16 bits, cstart[65536] = n), and
+// for a level-2 bucket the K3a cursor cur[.] (u32, from the bucket start) and the child classified into wl2 (K11
+// classes / next level); any other non-empty bucket s goes whole to wl3 (K11 on three digits).
+// Block 0 also writes tpfx[0..256], the K3a tiles before each level-2 bucket.
+__global__ __launch_bounds__(kRadix) void k_plan_h16(
+    const uint32_t *__restrict__ part, uint32_t nblk, const unsigned long long *__restrict__ fix,
+    const unsigned long long *__restrict__ bases, const unsigned long long *__restrict__ totals,
+    uint64_t n, int force, unsigned long long *__restrict__ cstart,
+    uint32_t *__restrict__ cur, uint32_t *__restrict__ tpfx, WorkLists wl2,
+    WorkLists wl3) {
+    constexpr uint32_t kWords = kBuckets16 / 2;
+    __shared__ uint32_t s_lo[kRadix], s_hi[kRadix];
+    __shared__ unsigned long long s_w[kRadix / 64];
+    const uint32_t s = blockIdx.x, e = threadIdx.x;
+    // thread e sums word s*128 + (e & 127) (children 2j, 2j+1) over every other partial
+    const uint32_t word = s * (kRadix / 2) + (e & 127u);
+    uint32_t lo = 0, hi = 0;
+    uint32_t b = e >> 7;
+    for (; b + 14 < nblk; b += 16) {
+        uint32_t v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = part[(uint64_t)(b + 2 * j) * kWords + word];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { lo += v[j] & 0xffffu; hi += v[j] >> 16; }
+    }
+    for (; b < nblk; b += 2) {
+        const uint32_t v = part[(uint64_t)b * kWords + word];
+        lo += v & 0xffffu;
+        hi += v >> 16;
+    }
+    s_lo[e] = lo;
+    s_hi[e] = hi;
+    __syncthreads();
+    const uint32_t j = e >> 1;
+    const unsigned long long c =
+        (unsigned long long)((e & 1u) ? s_hi[j] + s_hi[j + 128] : s_lo[j] + s_lo[j + 128]) +
+        fix[s * kRadix + e];
+    unsigned long long sum;
+    const unsigned long long excl = block_excl_scan(c, s_w, &sum);
+    const unsigned long long tot = totals[s], st = bases[s] + excl;
+    cstart[s * kRadix + e] = st;
+    if (s == 0 && e == 0) cstart[kBuckets16] = n;
+    if (level2_bucket(tot, force)) {
+        cur[s * kRadix + e] = (uint32_t)excl;  // relative to the bucket start
+        if (wl2.ctr) classify_block(st, c, wl2);
+    } else if (wl3.ctr) {
+        classify_block(e == 0 ? bases[s] : 0ull, e == 0 ? tot : 0ull, wl3);
+    }
+    if (s == 0) {
+        const unsigned long long te = totals[e];
+        const unsigned long long nt =
+            level2_bucket(te, force) ? (te + kSweepTile - 1) / kSweepTile : 0ull;
+        unsigned long long all;
+        const unsigned long long tx = block_excl_scan(nt, s_w, &all);
+        tpfx[e] = (uint32_t)tx;
+        if (e == 0) tpfx[kRadix] = (uint32_t)all;
+    }
+}
+
+// K3a: level 2 over the level-2 buckets' tiles (grid >= tpfx[256]; surplus blocks exit).
+// Tile t belongs to bucket s with tpfx[s] <= t < tpfx[s+1] (binary search in LDS); its runs are
+// reserved on cur[s][.] (K12h).  Input: level 3's output (ordered u32).
+template <int BLOCK, int ITEMS, typename OT = uint32_t>
+__global__ __launch_bounds__(BLOCK) void k_partition_h16(
+    const uint32_t *__restrict__ in, OT *__restrict__ out, const uint32_t *__restrict__ tpfx,
+    const unsigned long long *__restrict__ bases, const unsigned long long *__restrict__ totals,
+    uint32_t *__restrict__ cur) {
+    constexpr int TILE = BLOCK * ITEMS;
+    static_assert(TILE == kSweepTile, "level-2 tiles are kSweepTile keys");
+    __shared__ uint32_t s_keys[TILE];
+    __shared__ uint32_t s_cur[kRadix];
+    __shared__ OT *s_dst[kRadix];
+    __shared__ uint32_t s_wsum[kRadix / 64];
+    __shared__ uint32_t s_tp[kRadix + 1];
+    const uint32_t tid = threadIdx.x;
+    if (tid <= kRadix) s_tp[tid] = tpfx[tid];
+    __syncthreads();
+    const uint32_t t = xcd_tile(blockIdx.x, gridDim.x);
+    if (t >= s_tp[kRadix]) return;
+    uint32_t lo = 0, hi = kRadix;  // s_tp[lo] <= t < s_tp[hi]
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (s_tp[mid] <= t) lo = mid;
+        else hi = mid;
+    }
+    const uint64_t b0 = bases[lo], end = b0 + totals[lo];
+    const uint64_t t0 = b0 + (uint64_t)(t - s_tp[lo]) * TILE;
+    const uint32_t len = (uint32_t)(end - t0 < (uint64_t)TILE ? end - t0 : (uint64_t)TILE);
+    partition_tile<BLOCK, ITEMS, false, false, OT>(in, t0, len, 16, nullptr, s_keys, s_cur, s_dst,
+                                                   s_wsum, cur + (uint64_t)lo * kRadix, out + b0);
 }
 
 // Stable wave-level rank of one round (64 keys, lane order = key order) against the wave's
@@ -1635,6 +1864,44 @@ hipError_t launch_seg_partition(const SegPass &sp, hipStream_t s) {
         k_seg_partition<B, I, false><<<sp.max_tiles, B, 0, s>>>(
             sp.in, sp.out, sp.shift, sp.tcounts, gsum, reinterpret_cast<const ull *>(sp.cstart),
             segs, sp.tpfx, sp.gpfx, sp.segmap, sp.nseg);
+    return hipGetLastError();
+}
+
+hipError_t launch_counts_h16(const uint32_t *in, uint64_t n, bool flip, uint32_t *tcounts,
+                             uint32_t *part, uint64_t *fix, uint32_t *nblk, hipStream_t s) {
+    const uint64_t tiles = sweep_tiles(n);
+    const uint32_t g = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(tiles, 1), kH16Blocks);
+    *nblk = g;
+    auto *fx = reinterpret_cast<unsigned long long *>(fix);
+    if (flip) k_counts_h16<1024, true><<<g, 1024, 0, s>>>(in, n, tcounts, part, fx);
+    else k_counts_h16<1024, false><<<g, 1024, 0, s>>>(in, n, tcounts, part, fx);
+    return hipGetLastError();
+}
+
+hipError_t launch_plan_h16(const uint32_t *part, uint32_t nblk, const uint64_t *fix,
+                           const uint64_t *bases, const uint64_t *totals, uint64_t n, bool force,
+                           uint64_t *cstart, uint32_t *cur, uint32_t *tpfx, const WorkLists &wl2,
+                           const WorkLists &wl3, hipStream_t s) {
+    using ull = unsigned long long;
+    k_plan_h16<<<kRadix, kRadix, 0, s>>>(
+        part, nblk, reinterpret_cast<const ull *>(fix), reinterpret_cast<const ull *>(bases),
+        reinterpret_cast<const ull *>(totals), n, force ? 1 : 0, reinterpret_cast<ull *>(cstart),
+        cur, tpfx, wl2, wl3);
+    return hipGetLastError();
+}
+
+hipError_t launch_partition_h16(const uint32_t *in, uint32_t *out, uint16_t *out16, uint64_t n,
+                                const uint32_t *tpfx, const uint64_t *bases,
+                                const uint64_t *totals, uint32_t *cur, hipStream_t s) {
+    using ull = unsigned long long;
+    if (n == 0) return hipSuccess;
+    const unsigned g = (unsigned)(sweep_tiles(n) + kRadix);  // >= the level-2 tiles
+    constexpr int B = kPartBlock, I = kSweepTile / kPartBlock;
+    const ull *bs = reinterpret_cast<const ull *>(bases);
+    const ull *tt = reinterpret_cast<const ull *>(totals);
+    uint32_t *cu = cur;
+    if (out16) k_partition_h16<B, I, uint16_t><<<g, B, 0, s>>>(in, out16, tpfx, bs, tt, cu);
+    else k_partition_h16<B, I><<<g, B, 0, s>>>(in, out, tpfx, bs, tt, cu);
     return hipGetLastError();
 }
 

@@ -52,6 +52,11 @@ struct gsort_ctx {
     // MSD scratch: segment plan/maps, child starts, work lists (u64 {start, len} pairs)
     DevBuf m_tpfx, m_gpfx, m_segmap, m_groupmap, m_cstart, m_next[2], m_local[kLocalClasses];
     uint64_t group16_nseg = 0;  // msd_sort(group16): level-2 segments (list m_next[0])
+    // two-level plan front end (K1h / K12h / K3a): 16-bit histogram partials, wrap repairs,
+    // level-2 cursors, K11 lists of the level-3 buckets; counters read while levels 3/2 run
+    bool plan16 = true;
+    DevBuf m_part, m_fix, m_cur, m_local3[kLocalClasses];
+    hipEvent_t ev_ctr = nullptr;
     DevBuf m_split;  // radix select thresholds + counts of the distributed radix
     DevBuf m_rpos, m_bsize;  // receive side: run bucket bounds (P x 65537), bucket size/start
     DevBuf m_bseg, m_blist;  // boundary groups of the distributed radix: scratch, K11 list
@@ -73,9 +78,10 @@ struct gsort_ctx {
 namespace {
 
 // [12K, 12K+96): MSD work-list counters, {entries, keys, longest} for the next-level list and
-// the K11 class lists; [12K+128, 12K+144): a one-entry list for a single-bucket sort
+// the K11 class lists; [12K+128, 12K+144): a one-entry list for a single-bucket sort;
+// [12K+256, 12K+352): the counters of the level-3 K11 lists of the two-level plan
 constexpr size_t OFF_HIST = 0, OFF_TOT = 8192, OFF_BASES = 10240, OFF_CTR = 12288,
-                 OFF_ONE = 12416, OFF_PLAN = 20480;
+                 OFF_ONE = 12416, OFF_CTR3 = 12544, OFF_PLAN = 20480;
 
 gsort_status set_err(gsort_ctx *c, gsort_status st, const std::string &msg) {
     if (c) c->err = msg;
@@ -350,12 +356,104 @@ gsort_status msd_levels(gsort_ctx *c, int L, uint32_t *cur, uint32_t *out, uint3
 }
 
 
+// Levels 3 and 2 through the two-level plan (gsort_kernels.hip, "Two-level plan"): K1h + K2
+// + K12h, then K3u (level 3, in -> tmp) and K3a (level 2, tmp -> out, or the low 16 bits ->
+// out16 with group16).  The work-list counters are copied to the host right after K12h and read
+// once levels 3 and 2 are queued, so the GPU never waits on the host in the common case.  Then
+// K11 for the small level-3 buckets (three digits, tmp -> out) and for the level-2 children
+// (two digits, in place in out); children still larger than kLocalMax go on through
+// msd_levels from level 1.  cstart (65537 u64) receives the 16-bit bucket bounds.
+gsort_status msd_sort_h16(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *out,
+                          uint32_t *tmp, gsort_stats *stats, bool group16, uint16_t *out16,
+                          uint64_t *cstart) {
+    uint64_t *totals = reinterpret_cast<uint64_t *>(c->d_small + OFF_TOT);
+    uint64_t *bases = reinterpret_cast<uint64_t *>(c->d_small + OFF_BASES);
+    uint64_t *ctr = reinterpret_cast<uint64_t *>(c->d_small + OFF_CTR);
+    uint64_t *ctr3 = reinterpret_cast<uint64_t *>(c->d_small + OFF_CTR3);
+    ST_TRY(ensure(c, c->m_part, (size_t)kH16Blocks * kH16PartWords * 4));
+    ST_TRY(ensure(c, c->m_fix, (size_t)kBuckets16 * 8));
+    ST_TRY(ensure(c, c->m_cur, (size_t)kBuckets16 * 4));
+    ST_TRY(ensure(c, c->m_tpfx, (kRadix + 1) * 4));
+    if (!cstart) {
+        ST_TRY(ensure(c, c->m_cstart, (size_t)(kBuckets16 + 1) * 8));
+        cstart = reinterpret_cast<uint64_t *>(c->m_cstart.p);
+    }
+    const uint64_t nchild = std::min<uint64_t>(kBuckets16, n);
+    WorkLists wl2 = work_lists(c, 0), wl3 = work_lists(c, 1);
+    if (!group16) {
+        ST_TRY(ensure_list(c, c->m_next[0], std::min<uint64_t>(nchild, n / kLocalMax + 1)));
+        ST_TRY(ensure_list(c, c->m_next[1], 1));
+        for (int k = 0; k < kLocalClasses; ++k) {
+            ST_TRY(ensure_list(c, c->m_local[k],
+                               std::min<uint64_t>(nchild, n / (kLocalCap[k] + 1) + 1)));
+            ST_TRY(ensure_list(c, c->m_local3[k], kRadix));
+        }
+        wl2 = work_lists(c, 0);
+        wl3 = work_lists(c, 1);
+        for (int k = 0; k < kLocalClasses; ++k)
+            wl3.list[k + 1] = reinterpret_cast<uint64_t *>(c->m_local3[k].p);
+        wl3.ctr = ctr3;
+    } else {
+        wl2.ctr = nullptr;
+        wl3.ctr = nullptr;
+    }
+    uint32_t *tpfx = reinterpret_cast<uint32_t *>(c->m_tpfx.p);
+    uint32_t *cur = reinterpret_cast<uint32_t *>(c->m_cur.p);
+    uint32_t nblk = 0;
+    hipEvent_t t = tic(c);
+    HIP_TRY(c, hipMemsetAsync(c->m_fix.p, 0, (size_t)kBuckets16 * 8, c->stream));
+    if (!group16) HIP_TRY(c, hipMemsetAsync(ctr, 0, OFF_CTR3 + kCtrBytes - OFF_CTR, c->stream));
+    HIP_TRY(c, launch_counts_h16(in, n, true, d_tcounts(c), reinterpret_cast<uint32_t *>(c->m_part.p),
+                                 reinterpret_cast<uint64_t *>(c->m_fix.p), &nblk, c->stream));
+    HIP_TRY(c, launch_scan_tiles(d_tcounts(c), n, d_gsum(c), totals, bases, c->stream));
+    HIP_TRY(c, launch_plan_h16(reinterpret_cast<uint32_t *>(c->m_part.p), nblk,
+                               reinterpret_cast<uint64_t *>(c->m_fix.p), bases, totals, n, group16,
+                               cstart, cur, tpfx, wl2, wl3, c->stream));
+    toc(c, PH_COUNT, t);
+    if (!group16) {
+        HIP_TRY(c, hipMemcpyAsync(c->h_small + OFF_CTR, c->d_small + OFF_CTR,
+                                  OFF_CTR3 + kCtrBytes - OFF_CTR, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipEventRecord(c->ev_ctr, c->stream));
+    }
+    t = tic(c);
+    HIP_TRY(c, launch_partition(in, tmp, n, 24, d_tcounts(c), d_gsum(c), bases, true, c->stream));
+    toc(c, PH_LEVEL3, t);
+    t = tic(c);
+    HIP_TRY(c, launch_partition_h16(tmp, out, group16 ? out16 : nullptr, n, tpfx, bases, totals,
+                                    cur, c->stream));
+    toc(c, PH_LEVEL2, t);
+    if (stats) { stats->keys_level[0] += n; stats->keys_level[1] += n; }
+    int levels = 2;
+    if (!group16) {
+        HIP_TRY(c, hipEventSynchronize(c->ev_ctr));
+        uint64_t h[3 * (kLocalClasses + 1)], h3[3 * (kLocalClasses + 1)];
+        memcpy(h, c->h_small + OFF_CTR, kCtrBytes);
+        memcpy(h3, c->h_small + OFF_CTR3, kCtrBytes);
+        if (stats) stats->keys_level[1] -= h3[1] + h3[4] + h3[7];  // K11'd at level 3
+        for (int k = 0; k < kLocalClasses; ++k) {
+            const uint64_t *hk = h3 + 3 * (k + 1);
+            if (!hk[0]) continue;
+            t = tic(c);
+            HIP_TRY(c, launch_local_sort(tmp, out, reinterpret_cast<uint64_t *>(c->m_local3[k].p),
+                                         (uint32_t)hk[0], k + 1, 3, false, c->atomic_rank,
+                                         c->stream));
+            toc(c, PH_BUCKET, t);
+            if (stats) { stats->buckets_local += hk[0]; stats->keys_bucket_sort += hk[1]; }
+        }
+        ST_TRY(msd_levels(c, 1, out, out, tmp, 0, h, stats, &levels));
+    }
+    if (stats) stats->passes_run = levels;
+    return GSORT_OK;
+}
+
 // group16: stop after level 2 -- out holds the keys (int32) grouped by their top 16 bits
 // (ordered u32) but not sorted inside a group (the sender side of the distributed radix);
 // with out16 and n > kLocalMax, level 2 stores only the low 16 bits of every key, at out16.
+// With the two-level plan (c->plan16) and group16, gb (65537 u64) receives the 16-bit bucket
+// bounds of the grouped block.
 gsort_status msd_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *out,
                       uint32_t *tmp, gsort_stats *stats, bool group16 = false,
-                      uint16_t *out16 = nullptr) {
+                      uint16_t *out16 = nullptr, uint64_t *gb = nullptr) {
     if (n == 0) return GSORT_OK;
     uint64_t *ctr = reinterpret_cast<uint64_t *>(c->d_small + OFF_CTR);
     if (n <= kLocalMax) {  // one bucket: all four digits in LDS
@@ -373,6 +471,8 @@ gsort_status msd_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *ou
         return GSORT_OK;
     }
     ST_TRY(ensure_pass_scratch(c, n));
+    if (c->plan16 && (!group16 || out16) && n < (1ull << 32))
+        return msd_sort_h16(c, in, n, out, tmp, stats, group16, out16, group16 ? gb : nullptr);
     uint64_t *totals = reinterpret_cast<uint64_t *>(c->d_small + OFF_TOT);
     uint64_t *bases = reinterpret_cast<uint64_t *>(c->d_small + OFF_BASES);
     ST_TRY(ensure_list(c, c->m_next[0], kRadix));
@@ -613,9 +713,11 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
         }
         ST_TRY(msd_sort(c, reinterpret_cast<const uint32_t *>(d_keys), n_in,
                         reinterpret_cast<uint32_t *>(sorted), slot_ptr<uint32_t>(c, S_TMP),
-                        stats ? stats : &tmp_st, true, packed_msd ? pack : nullptr));
+                        stats ? stats : &tmp_st, true, packed_msd ? pack : nullptr, gb));
         t = tic(c);
-        if (packed_msd) {
+        if (packed_msd && c->plan16) {
+            // gb written by the two-level plan
+        } else if (packed_msd) {
             HIP_TRY(c, launch_gb_from_plan(reinterpret_cast<uint64_t *>(c->d_small + OFF_BASES),
                                            reinterpret_cast<uint64_t *>(c->d_small + OFF_TOT),
                                            reinterpret_cast<uint64_t *>(c->m_next[0].p),
@@ -1050,6 +1152,8 @@ gsort_status create_common(gsort_ctx *c, int hip_device) {
     HIP_TRY(c, hipMalloc(&c->d_small, kSmallBytes));
     HIP_TRY(c, hipHostMalloc(&c->h_small, kSmallBytes, hipHostMallocDefault));
     HIP_TRY(c, hipMemset(c->d_small, 0, kSmallBytes));
+    HIP_TRY(c, hipEventCreateWithFlags(&c->ev_ctr, hipEventDisableTiming));
+    if (const char *e = getenv("GSORT_PLAN16")) c->plan16 = atoi(e) != 0;
     return check_lds_order(c);
 }
 
@@ -1153,10 +1257,13 @@ gsort_status gsort_destroy(gsort_ctx *c) {
     for (DevBuf *b : {&c->m_tpfx, &c->m_gpfx, &c->m_segmap, &c->m_groupmap, &c->m_cstart,
                       &c->m_next[0], &c->m_next[1], &c->m_split, &c->m_rpos, &c->m_bsize,
                       &c->m_bseg, &c->m_blist, &c->m_gb, &c->m_pack, &c->m_meta,
-                      &c->m_g16})
+                      &c->m_g16, &c->m_part, &c->m_fix, &c->m_cur})
         if (b->p) (void)hipFree(b->p);
     for (auto &b : c->m_local)
         if (b.p) (void)hipFree(b.p);
+    for (auto &b : c->m_local3)
+        if (b.p) (void)hipFree(b.p);
+    if (c->ev_ctr) (void)hipEventDestroy(c->ev_ctr);
     if (c->d_small) (void)hipFree(c->d_small);
     if (c->h_small) (void)hipHostFree(c->h_small);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);

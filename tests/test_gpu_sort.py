@@ -7,6 +7,7 @@ Multi-rank cases run the distributed algorithm with P ranks on ONE GPU through t
 in-process rank group (gsort_create_in_group): same kernels, same routing, device copies in
 place of RCCL transfers.
 """
+import os
 import threading
 
 import numpy as np
@@ -17,12 +18,22 @@ from conftest import case_input, case_output
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module", params=["msd", "lsd"])
+@pytest.fixture(scope="module", params=["msd", "msd_segplan", "lsd"])
 def ctx(gsort, request):
-    """Both local-sort algorithms (MSD partitions + in-LDS buckets, and stable LSD passes)."""
-    c = gsort.Context()
-    c.set_local_algo(gsort.LOCAL_MSD if request.param == "msd" else gsort.LOCAL_LSD)
-    c.algo = request.param
+    """Both local-sort algorithms (MSD partitions + in-LDS buckets, and stable LSD passes); the
+    MSD sort with its default two-level plan front end (K1h/K12h/K3a) and with the segmented
+    level-2 plan (K12/K1s/K2s, GSORT_PLAN16=0) that levels 1 and 0 always use."""
+    old = os.environ.get("GSORT_PLAN16")
+    os.environ["GSORT_PLAN16"] = "0" if request.param == "msd_segplan" else "1"
+    try:
+        c = gsort.Context()
+    finally:
+        if old is None:
+            os.environ.pop("GSORT_PLAN16")
+        else:
+            os.environ["GSORT_PLAN16"] = old
+    c.set_local_algo(gsort.LOCAL_LSD if request.param == "lsd" else gsort.LOCAL_MSD)
+    c.algo = "lsd" if request.param == "lsd" else "msd"
     yield c
     c.close()
 
@@ -86,45 +97,64 @@ def test_radix_one_gpu_value_edge_cases(ctx, orc):
         assert st["passes_run"] == 1
 
 
-def _msd_cases(orc):
+def _one_hot_bucket(orc):
     rng = np.random.default_rng(7)
     half = np.concatenate([np.full(1 << 19, 123456, dtype=np.int32),
                            orc.gen(orc.UNIFORM, 9, 1 << 19)])
     rng.shuffle(half)
+    return half
+
+
+def _h16_wrap_pair(orc):
+    """Two keys whose top 16 bits (ordered) share one packed K1h word, as its low (even) and
+    high (odd) half, 2^25 copies each: every K1h workgroup counts > 65535 of both, so both
+    halves wrap (and the word carries out) -- the repairs through fix[] must be exact."""
+    rng = np.random.default_rng(8)
+    a = np.int32(0x12340000)                   # ordered prefix 0x9234 (even)
+    b = np.int32(0x12350005)                   # ordered prefix 0x9235 (odd)
+    keys = np.where(rng.random(1 << 26) < 0.5, a, b).astype(np.int32)
+    keys[::1009] = rng.integers(-2**31, 2**31, keys[::1009].size, dtype=np.int64)
+    return keys
+
+
+def _msd_cases(orc):
+    rng = lambda s: np.random.default_rng(s)  # noqa: E731
     return {
         # one bucket / first level only
         # K11 class caps (kLocalCap: 4608, 9216, 16384) and one past each
-        "n_cap1": orc.gen(orc.UNIFORM, 11, 4608),
-        "n_cap1_plus1": orc.gen(orc.UNIFORM, 12, 4609),
-        "n_cap2": orc.gen(orc.UNIFORM, 13, 9216),
-        "n_cap2_plus1": orc.gen(orc.UNIFORM, 14, 9217),
-        "n_localmax": orc.gen(orc.UNIFORM, 1, 16384),
-        "n_localmax_plus1": orc.gen(orc.UNIFORM, 2, 16385),
-        "uniform31_2p26": orc.gen(orc.UNIFORM, 6, 1 << 26),
+        "n_cap1": lambda: orc.gen(orc.UNIFORM, 11, 4608),
+        "n_cap1_plus1": lambda: orc.gen(orc.UNIFORM, 12, 4609),
+        "n_cap2": lambda: orc.gen(orc.UNIFORM, 13, 9216),
+        "n_cap2_plus1": lambda: orc.gen(orc.UNIFORM, 14, 9217),
+        "n_localmax": lambda: orc.gen(orc.UNIFORM, 1, 16384),
+        "n_localmax_plus1": lambda: orc.gen(orc.UNIFORM, 2, 16385),
+        "uniform31_2p26": lambda: orc.gen(orc.UNIFORM, 6, 1 << 26),
         # top digits trivial: buckets stay oversized down to the last level (digit 0)
-        "below_2p16": rng.integers(0, 1 << 16, 1 << 20).astype(np.int32),
-        "below_2p24": rng.integers(0, 1 << 24, 1 << 21).astype(np.int32),
-        "all_equal_big": np.full(1 << 20, -77, dtype=np.int32),
-        "zipf_2p22": orc.gen(orc.ZIPF, 4, 1 << 22),
-        "uniform_2p24": orc.gen(orc.UNIFORM, 5, 1 << 24),
-        "one_hot_bucket": half,
-        "negatives_2p21": rng.integers(-2**31, 2**31, 1 << 21, dtype=np.int64).astype(np.int32),
-        "bucket_edges": np.repeat(np.arange(-600, 600, dtype=np.int32) * 65536, 8190),
-        "full32_2p24": rng.integers(-2**31, 2**31, 1 << 24, dtype=np.int64).astype(np.int32),
+        "below_2p16": lambda: rng(7).integers(0, 1 << 16, 1 << 20).astype(np.int32),
+        "below_2p24": lambda: rng(7).integers(0, 1 << 24, 1 << 21).astype(np.int32),
+        "all_equal_big": lambda: np.full(1 << 20, -77, dtype=np.int32),
+        # K1h: > 65535 equal 16-bit prefixes per workgroup (u16 wrap repairs)
+        "all_equal_2p25": lambda: np.full(1 << 25, 1 << 20, dtype=np.int32),
+        "h16_wrap_pair": lambda: _h16_wrap_pair(orc),
+        "zipf_2p22": lambda: orc.gen(orc.ZIPF, 4, 1 << 22),
+        "uniform_2p24": lambda: orc.gen(orc.UNIFORM, 5, 1 << 24),
+        "one_hot_bucket": lambda: _one_hot_bucket(orc),
+        "negatives_2p21": lambda: rng(7).integers(-2**31, 2**31, 1 << 21,
+                                                  dtype=np.int64).astype(np.int32),
+        "bucket_edges": lambda: np.repeat(np.arange(-600, 600, dtype=np.int32) * 65536, 8190),
+        "full32_2p24": lambda: rng(7).integers(-2**31, 2**31, 1 << 24,
+                                               dtype=np.int64).astype(np.int32),
     }
 
 
-MSD_CASES = ["n_cap1", "n_cap1_plus1", "n_cap2", "n_cap2_plus1", "n_localmax",
-             "n_localmax_plus1", "uniform31_2p26",
-             "below_2p16", "below_2p24", "all_equal_big",
-             "zipf_2p22", "uniform_2p24", "one_hot_bucket", "negatives_2p21", "bucket_edges", "full32_2p24"]
+MSD_CASES = list(_msd_cases(None))
 
 
 @pytest.mark.parametrize("name", MSD_CASES)
 def test_radix_one_gpu_bucket_regimes(ctx, orc, name):
     """MSD level structure: single-bucket sorts, all-local first level, oversized buckets down
     to the digit-0 level, one huge bucket among normal ones, exact kLocalMax boundaries."""
-    keys = _msd_cases(orc)[name]
+    keys = _msd_cases(orc)[name]()
     got, st = sort_on_gpu(ctx, keys)
     assert np.array_equal(got, np.sort(keys)), name
 
@@ -330,3 +360,20 @@ def test_multirank_large_receive_buckets(gsort, P, span, n, algo):
         ref = np.sort(keys)
         for q in range(P):
             assert np.array_equal(res[q][0], ref[q * B:(q + 1) * B]), q
+
+
+def test_radix_multirank_h16_wraps(gsort, orc):
+    """The distributed sender groups its block through the two-level plan (K1h 16-bit counts
+    -> bucket bounds gb and the packed low-16 send buffer): a key repeated > 65535 times per
+    K1h workgroup wraps its u16 counter; the bounds (and so the exchange) must stay exact."""
+    P, n = 2, 1 << 26
+    rng = np.random.default_rng(21)
+    u = rng.random(n)
+    keys = np.where(u < 0.7, np.int32(0x12340000),
+                    np.where(u < 0.9, np.int32(0x12350005),
+                             rng.integers(-2**31, 2**31, n, dtype=np.int64))).astype(np.int32)
+    B = n // P
+    res = run_group(gsort, [keys[r * B:(r + 1) * B] for r in range(P)], "radix")
+    got = np.concatenate([res[r][0] for r in range(P)])
+    assert all(res[r][0].size == B for r in range(P))
+    assert np.array_equal(got, np.sort(keys))
