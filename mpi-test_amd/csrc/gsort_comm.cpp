@@ -117,7 +117,8 @@ class GroupComm : public Comm {
   public:
     GroupComm(GroupState *g, int rank) : g_(g) { rank_ = rank; size_ = g->n; }
 
-    // generation barrier with a generous timeout so a dead peer cannot hang the process
+    // generation barrier with a timeout so a dead peer cannot hang the process (60 s: far above
+    // any collective here, short enough that a failed rank surfaces as an error, not a hang)
     bool barrier() {
         std::unique_lock<std::mutex> lk(g_->m);
         if (g_->broken) return false;
@@ -128,7 +129,7 @@ class GroupComm : public Comm {
             g_->cv.notify_all();
             return true;
         }
-        const bool ok = g_->cv.wait_for(lk, std::chrono::seconds(300),
+        const bool ok = g_->cv.wait_for(lk, std::chrono::seconds(60),
                                         [&] { return g_->generation != gen || g_->broken; });
         if (!ok || g_->broken) {
             g_->broken = true;

@@ -1095,6 +1095,107 @@ __global__ __launch_bounds__(BLOCK) void k_partition_h16(
                                                    s_wsum, cur + (uint64_t)lo * kRadix, out + b0);
 }
 
+// K3a2: K3a over PAIRS of level-2 tiles (2p, 2p+1 of the tile plan; grid >= ceil(tiles/2)).
+// Both tiles are ranked before either reservation is needed, so the two atomics are in flight
+// together and their round trip hides behind twice the scan + LDS scatter work; LDS holds both
+// tiles (2 x 32 KiB: still two 1024-thread workgroups per CU).
+template <int BLOCK, int ITEMS, typename OT = uint32_t>
+__global__ __launch_bounds__(BLOCK) void k_partition2_h16(
+    const uint32_t *__restrict__ in, OT *__restrict__ out, const uint32_t *__restrict__ tpfx,
+    const unsigned long long *__restrict__ bases, const unsigned long long *__restrict__ totals,
+    uint32_t *__restrict__ cur) {
+    constexpr int TILE = BLOCK * ITEMS, shift = 16;
+    static_assert(TILE == kSweepTile, "level-2 tiles are kSweepTile keys");
+    __shared__ uint32_t s_keys[2][TILE];
+    __shared__ uint32_t s_cur[2][kRadix];
+    __shared__ OT *s_dst[2][kRadix];
+    __shared__ uint32_t s_wsum[2][kRadix / 64];
+    __shared__ uint32_t s_tp[kRadix + 1];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (tid <= kRadix) s_tp[tid] = tpfx[tid];
+    if (tid < kRadix) { s_cur[0][tid] = 0; s_cur[1][tid] = 0; }
+    __syncthreads();
+    const uint32_t pr = xcd_tile(blockIdx.x, gridDim.x), ntile = s_tp[kRadix];
+    if (2 * pr >= ntile) return;
+    uint32_t seg[2], len[2];
+    uint64_t t0[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const uint32_t t = 2 * pr + h;
+        seg[h] = 0; len[h] = 0; t0[h] = 0;
+        if (t < ntile) {
+            uint32_t lo = 0, hi = kRadix;  // s_tp[lo] <= t < s_tp[hi]
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (s_tp[mid] <= t) lo = mid;
+                else hi = mid;
+            }
+            const uint64_t b0 = bases[lo], end = b0 + totals[lo];
+            seg[h] = lo;
+            t0[h] = b0 + (uint64_t)(t - s_tp[lo]) * TILE;
+            len[h] = (uint32_t)(end - t0[h] < (uint64_t)TILE ? end - t0[h] : (uint64_t)TILE);
+        }
+    }
+    uint32_t k[2][ITEMS], r[2][ITEMS];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+        load_tile<BLOCK, ITEMS, false>(in + t0[h] + tid, len[h] == (uint32_t)TILE, len[h], k[h]);
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i)
+            if ((uint32_t)(i * BLOCK) + tid < len[h])
+                r[h][i] = atomicAdd(&s_cur[h][(k[h][i] >> shift) & 255u], 1u);
+    __syncthreads();
+    uint32_t excl[2] = {0, 0}, pos[2] = {0, 0};
+    if (tid < kRadix) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t c = s_cur[h][tid];
+            if (c) pos[h] = atomicAdd(&cur[seg[h] * kRadix + tid], c);
+            uint32_t v = c;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t t = __shfl_up(v, o);
+                if (lane >= o) v += t;
+            }
+            if (lane == 63) s_wsum[h][w] = v;
+            excl[h] = v - c;
+        }
+    }
+    __syncthreads();
+    if (tid < kRadix) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            for (uint32_t ww = 0; ww < w; ++ww) excl[h] += s_wsum[h][ww];
+            s_cur[h][tid] = excl[h];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i)
+            if ((uint32_t)(i * BLOCK) + tid < len[h])
+                s_keys[h][s_cur[h][(k[h][i] >> shift) & 255u] + r[h][i]] = k[h][i];
+    if (tid < kRadix) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+            s_dst[h][tid] = out + (bases[seg[h]] + pos[h]) - excl[h];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i) {
+            const uint32_t j = (uint32_t)(i * BLOCK) + tid;
+            if (j < len[h]) {
+                const uint32_t key = s_keys[h][j];
+                s_dst[h][(key >> shift) & 255u][j] = (OT)key;
+            }
+        }
+}
+
 // Stable wave-level rank of one round (64 keys, lane order = key order) against the wave's
 // running digit counters wc[256] (u32): returns #earlier keys of the wave with this digit.
 //   ATOMIC: one ds_add_rtn_u32 per lane.  The MI355X LDS serializes lanes of one instruction
@@ -1900,8 +2001,19 @@ hipError_t launch_partition_h16(const uint32_t *in, uint32_t *out, uint16_t *out
     const ull *bs = reinterpret_cast<const ull *>(bases);
     const ull *tt = reinterpret_cast<const ull *>(totals);
     uint32_t *cu = cur;
-    if (out16) k_partition_h16<B, I, uint16_t><<<g, B, 0, s>>>(in, out16, tpfx, bs, tt, cu);
-    else k_partition_h16<B, I><<<g, B, 0, s>>>(in, out, tpfx, bs, tt, cu);
+    static const int pairs = [] {
+        const char *e = getenv("GSORT_K3A_PAIRS");
+        return e ? atoi(e) : 1;
+    }();
+    if (pairs) {
+        const unsigned g2 = (g + 1) / 2;
+        if (out16) k_partition2_h16<B, I, uint16_t><<<g2, B, 0, s>>>(in, out16, tpfx, bs, tt, cu);
+        else k_partition2_h16<B, I><<<g2, B, 0, s>>>(in, out, tpfx, bs, tt, cu);
+    } else if (out16) {
+        k_partition_h16<B, I, uint16_t><<<g, B, 0, s>>>(in, out16, tpfx, bs, tt, cu);
+    } else {
+        k_partition_h16<B, I><<<g, B, 0, s>>>(in, out, tpfx, bs, tt, cu);
+    }
     return hipGetLastError();
 }
 
