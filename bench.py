@@ -131,12 +131,16 @@ def kernel_rooflines(stats, n_local):
     # every other level is a segmented K3u (k_seg_partition)
     plan16 = os.environ.get("GSORT_PLAN16", "1") != "0"
     seg_from = 2 if plan16 else 1
+    if plan16:  # K1h reads every key once (4 B/key); the phase also holds K2 + K12h (~25 us)
+        add("k_counts_h16 (K1h: level-3 tile counts + 16-bit histogram; with K2 + K12h)",
+            ("k_counts_h16",), [s["ms_hist"] if s["ms_level"][1] > 0 else 0.0 for s in stats],
+            [n_local for s in stats], 4)
     add("k_partition (K3u: level 3, unstable MSD partition of the whole block)",
         ("k_partition<",), [s["ms_level"][0] for s in stats],
         [s["keys_level"][0] for s in stats], PASS_BYTES_PER_KEY)
     if plan16:
         add("k_partition_h16 (K3a: level 2, runs reserved by atomics on the K12h cursors)",
-            ("k_partition_h16",), [s["ms_level"][1] for s in stats],
+            ("k_partition_h16", "k_partition2_h16"), [s["ms_level"][1] for s in stats],
             [s["keys_level"][1] for s in stats], PASS_BYTES_PER_KEY)
     add("k_seg_partition (K3u: segmented MSD level)", ("k_seg_partition",),
         [x for s in stats for x in s["ms_level"][seg_from:]],
