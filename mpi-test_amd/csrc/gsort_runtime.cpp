@@ -11,7 +11,9 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "gsort.h"
@@ -73,6 +75,10 @@ struct gsort_ctx {
     size_t ev_used = 0;
     struct Span { int phase; hipEvent_t a, b; };
     std::vector<Span> spans;
+    // host staging of the drop-in path (gsort_scatter_from_root / gsort_gather_to_root):
+    // kStageBufs pinned chunks, allocated on first use
+    char *h_stage[4] = {nullptr, nullptr, nullptr, nullptr};
+    hipEvent_t ev_stage[4] = {nullptr, nullptr, nullptr, nullptr};
 };
 
 namespace {
@@ -1264,6 +1270,10 @@ gsort_status gsort_destroy(gsort_ctx *c) {
     for (auto &b : c->m_local3)
         if (b.p) (void)hipFree(b.p);
     if (c->ev_ctr) (void)hipEventDestroy(c->ev_ctr);
+    for (int b = 0; b < 4; ++b) {
+        if (c->h_stage[b]) (void)hipHostFree(c->h_stage[b]);
+        if (c->ev_stage[b]) (void)hipEventDestroy(c->ev_stage[b]);
+    }
     if (c->d_small) (void)hipFree(c->d_small);
     if (c->h_small) (void)hipHostFree(c->h_small);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
@@ -1366,6 +1376,95 @@ gsort_status gsort_sample_info(const gsort_ctx *c, int32_t *splitters, uint64_t 
     return GSORT_OK;
 }
 
+namespace {
+
+// Pageable host <-> device copies of the drop-in path (the reference's rank-0 int_buf,
+// radix:139,192 / sample:82,195) through kStageBufs pinned chunks: kStageThreads host threads
+// copy chunk i between the caller's pageable array and a pinned buffer while the DMA engine
+// moves chunk i-1 over PCIe, instead of the runtime's own pageable path.  Small copies go
+// directly.
+constexpr int kStageBufs = 4, kStageThreads = 16;  // 16: the GPU box's CPU share
+constexpr size_t kStageChunk = 32u << 20, kStageMin = 16u << 20;
+
+gsort_status stage_init(gsort_ctx *c) {
+    for (int b = 0; b < kStageBufs; ++b) {
+        if (!c->h_stage[b] &&
+            hipHostMalloc(reinterpret_cast<void **>(&c->h_stage[b]), kStageChunk) != hipSuccess) {
+            (void)hipGetLastError();
+            c->h_stage[b] = nullptr;
+            return set_err(c, GSORT_ENOMEM, "hipHostMalloc of a staging chunk failed");
+        }
+        if (!c->ev_stage[b])
+            HIP_TRY(c, hipEventCreateWithFlags(&c->ev_stage[b], hipEventDisableTiming));
+    }
+    return GSORT_OK;
+}
+
+// host memcpy of len bytes split over kStageThreads threads (the calling thread takes a share;
+// GSORT_STAGE_THREADS overrides the count)
+void par_memcpy(char *dst, const char *src, size_t len) {
+    static const int nt = getenv("GSORT_STAGE_THREADS")
+                              ? std::max(1, std::min(64, atoi(getenv("GSORT_STAGE_THREADS"))))
+                              : kStageThreads;
+    const size_t share = ((len + nt - 1) / nt + 4095) & ~(size_t)4095;
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) {
+        const size_t a = (size_t)t * share;
+        if (a >= len) break;
+        th.emplace_back([=] { memcpy(dst + a, src + a, std::min(share, len - a)); });
+    }
+    memcpy(dst, src, std::min(share, len));
+    for (auto &x : th) x.join();
+}
+
+gsort_status staged_h2d(gsort_ctx *c, void *d_dst, const void *h_src, size_t bytes) {
+    if (bytes < kStageMin) {
+        HIP_TRY(c, hipMemcpyAsync(d_dst, h_src, bytes, hipMemcpyHostToDevice, c->stream));
+        return GSORT_OK;
+    }
+    ST_TRY(stage_init(c));
+    const size_t nch = (bytes + kStageChunk - 1) / kStageChunk;
+    for (size_t i = 0; i < nch; ++i) {
+        const int b = (int)(i % kStageBufs);
+        const size_t off = i * kStageChunk, len = std::min(kStageChunk, bytes - off);
+        if (i >= (size_t)kStageBufs) HIP_TRY(c, hipEventSynchronize(c->ev_stage[b]));
+        par_memcpy(c->h_stage[b], static_cast<const char *>(h_src) + off, len);
+        HIP_TRY(c, hipMemcpyAsync(static_cast<char *>(d_dst) + off, c->h_stage[b], len,
+                                  hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(c, hipEventRecord(c->ev_stage[b], c->stream));
+    }
+    return GSORT_OK;
+}
+
+gsort_status staged_d2h(gsort_ctx *c, void *h_dst, const void *d_src, size_t bytes) {
+    if (bytes < kStageMin) {
+        HIP_TRY(c, hipMemcpyAsync(h_dst, d_src, bytes, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        return GSORT_OK;
+    }
+    ST_TRY(stage_init(c));
+    const size_t nch = (bytes + kStageChunk - 1) / kStageChunk;
+    auto issue = [&](size_t i) -> gsort_status {
+        const int b = (int)(i % kStageBufs);
+        const size_t off = i * kStageChunk, len = std::min(kStageChunk, bytes - off);
+        HIP_TRY(c, hipMemcpyAsync(c->h_stage[b], static_cast<const char *>(d_src) + off, len,
+                                  hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipEventRecord(c->ev_stage[b], c->stream));
+        return GSORT_OK;
+    };
+    for (size_t i = 0; i < nch && i < (size_t)kStageBufs; ++i) ST_TRY(issue(i));
+    for (size_t i = 0; i < nch; ++i) {
+        const int b = (int)(i % kStageBufs);
+        const size_t off = i * kStageChunk, len = std::min(kStageChunk, bytes - off);
+        HIP_TRY(c, hipEventSynchronize(c->ev_stage[b]));
+        par_memcpy(static_cast<char *>(h_dst) + off, c->h_stage[b], len);
+        if (i + kStageBufs < nch) ST_TRY(issue(i + kStageBufs));
+    }
+    return GSORT_OK;
+}
+
+}  // namespace
+
 gsort_status gsort_scatter_from_root(gsort_ctx *c, const int32_t *h_root, size_t n_total,
                                      int32_t **d_keys, size_t *n_local) {
     ST_TRY(check_ctx(c));
@@ -1378,15 +1477,14 @@ gsort_status gsort_scatter_from_root(gsort_ctx *c, const int32_t *h_root, size_t
     int32_t *d_in = slot_ptr<int32_t>(c, S_IN);
     if (P == 1) {
         if (n_total)
-            HIP_TRY(c, hipMemcpyAsync(d_in, h_root, n_total * 4, hipMemcpyHostToDevice, c->stream));
+            ST_TRY(staged_h2d(c, d_in, h_root, n_total * 4));
     } else {
         std::vector<size_t> sc(P, 0), sd(P, 0), rc(P, 0), rd(P, 0);
         const void *src = nullptr;
         if (c->rank == 0) {
             ST_TRY(ensure(c, c->slot[S_STAGE], std::max<size_t>(n_total, 1) * 4));
             if (n_total)
-                HIP_TRY(c, hipMemcpyAsync(c->slot[S_STAGE].p, h_root, n_total * 4,
-                                          hipMemcpyHostToDevice, c->stream));
+                ST_TRY(staged_h2d(c, c->slot[S_STAGE].p, h_root, n_total * 4));
             for (int q = 0; q < P; ++q) {
                 uint64_t bq, lq;
                 block_of(n_total, P, q, &bq, &lq);
@@ -1412,8 +1510,7 @@ gsort_status gsort_gather_to_root(gsort_ctx *c, const int32_t *d_out, size_t n_o
     ST_TRY(reset_call(c));
     const int P = c->nranks;
     if (P == 1) {
-        if (n_out)
-            HIP_TRY(c, hipMemcpyAsync(h_root, d_out, n_out * 4, hipMemcpyDeviceToHost, c->stream));
+        if (n_out) ST_TRY(staged_d2h(c, h_root, d_out, n_out * 4));
         HIP_TRY(c, hipStreamSynchronize(c->stream));
         return GSORT_OK;
     }
@@ -1433,8 +1530,7 @@ gsort_status gsort_gather_to_root(gsort_ctx *c, const int32_t *d_out, size_t n_o
     }
     ST_TRY(comm_try(c, c->comm->alltoallv(d_out, sc.data(), sd.data(), dst, rc.data(), rd.data(),
                                           c->stream)));
-    if (c->rank == 0 && total)
-        HIP_TRY(c, hipMemcpyAsync(h_root, dst, total * 4, hipMemcpyDeviceToHost, c->stream));
+    if (c->rank == 0 && total) ST_TRY(staged_d2h(c, h_root, dst, total * 4));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     return GSORT_OK;
 }

@@ -377,3 +377,24 @@ def test_radix_multirank_h16_wraps(gsort, orc):
     got = np.concatenate([res[r][0] for r in range(P)])
     assert all(res[r][0].size == B for r in range(P))
     assert np.array_equal(got, np.sort(keys))
+
+
+@pytest.mark.parametrize("n", [0, 1000, 1 << 22, (40 << 20) + 3])
+def test_drop_in_staged_round_trip(gsort, n):
+    """The drop-in host path: pageable rank-0 array -> GPU (gsort_scatter_from_root, through
+    the pinned staging chunks from 16 MiB on: exactly 16 MiB, and 160 MiB + 12 B, which ends
+    in a partial chunk) -> gsort_radix -> host (gsort_gather_to_root, staged the same way)."""
+    c = gsort.Context()
+    try:
+        rng = np.random.default_rng(n + 7)
+        h = rng.integers(-(1 << 31), (1 << 31) - 1, size=n, dtype=np.int64).astype(np.int32)
+        d, m = c.scatter_from_root(h, n)
+        assert m == n
+        if n:
+            np.testing.assert_array_equal(c.to_host(d, n), h)  # the H2D half alone
+        out, n_out, _ = c.radix(d, m)
+        assert n_out == n
+        back = c.gather_to_root(out, n_out, n)
+        np.testing.assert_array_equal(back, np.sort(h))
+    finally:
+        c.close()
