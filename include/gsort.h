@@ -94,6 +94,12 @@ gsort_status gsort_destroy(gsort_ctx *ctx);
 gsort_status gsort_reserve(gsort_ctx *ctx, size_t n_local);
 /* Select the local sort algorithm (GSORT_LOCAL_MSD / GSORT_LOCAL_LSD) for later calls. */
 gsort_status gsort_set_local_algo(gsort_ctx *ctx, int algo);
+/* Sample sort bucket rule: 0 (default) = the reference's, bucket j = first j with key <= s[j]
+ * (mpi_sample_sort.c:148-155; every copy of a splitter value goes to the lower bucket, so a
+ * duplicate-heavy input such as Zipf overloads one rank); 1 = duplicate-aware
+ * balanced buckets (gsort_plan_split_balanced).  The concatenated output is the same sorted
+ * array either way; only the per-rank bucket sizes (gsort_sample_info) differ. */
+gsort_status gsort_set_sample_balanced(gsort_ctx *ctx, int on);
 const char *gsort_strerror(gsort_status st);
 const char *gsort_last_error(const gsort_ctx *ctx);
 int gsort_rank(const gsort_ctx *ctx);
@@ -178,6 +184,14 @@ gsort_status gsort_plan_splitters(int P, const int32_t *samples, int32_t *splitt
  * keys rank `me` sends to / receives from every rank (contiguous, in rank order). */
 gsort_status gsort_plan_split(int P, const uint64_t *n_all, const uint64_t *lt,
                               const uint64_t *le, int me, uint64_t *send, uint64_t *recv);
+/* gsort_plan_split_balanced: the same cut for the balanced sample sort, where v_q is the q-th
+ * splitter (mpi_sample_sort.c:109-128) rather than the g_q-th key: the boundary moves to
+ * clamp(min(qB, N), sum_p lt + 1, sum_p le), i.e. the copies of a splitter value are shared
+ * out in rank order instead of all going to the lower bucket (mpi_sample_sort.c:148-155); a
+ * value held once goes to the lower bucket, as there. */
+gsort_status gsort_plan_split_balanced(int P, const uint64_t *n_all, const uint64_t *lt,
+                                       const uint64_t *le, int me, uint64_t *send,
+                                       uint64_t *recv);
 
 #ifdef __cplusplus
 }

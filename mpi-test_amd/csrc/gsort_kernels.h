@@ -54,7 +54,8 @@ hipError_t launch_select_splitters(const int32_t *samples, int m, int k, int nsp
                                    int32_t *splitters, hipStream_t s);
 // K6 bucket bounds on a sorted block: bounds[j] = #keys <= splitters[j] (j < nsplit).
 hipError_t launch_bucket_bounds(const int32_t *sorted, uint64_t n, const int32_t *splitters,
-                                int nsplit, uint64_t *bounds, hipStream_t s);
+                                int nsplit, uint64_t *bounds, hipStream_t s,
+                                bool strict = false);
 // ---- MSD partition sort (gsort_kernels.hip, "MSD partition sort") -----------------------
 // K11 geometry: one workgroup sorts a bucket entirely in LDS.  A stable pass costs a wave
 // ~16 rounds of 64 keys best (measured, tools/kexp3.hip), so the workgroup size follows the

@@ -464,10 +464,15 @@ __global__ __launch_bounds__(1024) void k_select_splitters(const int32_t *sample
 // range 64x per dependent load, then one sweep of <= 64 keys.  bounds[j] = #keys <= s[j].
 __global__ __launch_bounds__(64) void k_bucket_bounds(const int32_t *__restrict__ a, uint64_t n,
                                                       const int32_t *__restrict__ spl,
-                                                      unsigned long long *bounds) {
+                                                      unsigned long long *bounds, int strict) {
+    // strict: count keys < s (lower bound) as keys <= s - 1; s = INT_MIN has none
     const int j = blockIdx.x;
     const int lane = threadIdx.x;
-    const int32_t s = spl[j];
+    if (strict && spl[j] == (int32_t)0x80000000) {
+        if (lane == 0) bounds[j] = 0;
+        return;
+    }
+    const int32_t s = strict ? spl[j] - 1 : spl[j];
     uint64_t lo = 0, hi = n;  // answer (first index with a[i] > s) lies in [lo, hi]
     while (hi - lo > 64) {
         const uint64_t step = (hi - lo) / 64;
@@ -1890,10 +1895,11 @@ hipError_t launch_select_splitters(const int32_t *samples, int m, int k, int nsp
 }
 
 hipError_t launch_bucket_bounds(const int32_t *sorted, uint64_t n, const int32_t *splitters,
-                                int nsplit, uint64_t *bounds, hipStream_t s) {
+                                int nsplit, uint64_t *bounds, hipStream_t s, bool strict) {
     if (nsplit <= 0) return hipSuccess;
     k_bucket_bounds<<<nsplit, 64, 0, s>>>(sorted, n, splitters,
-                                          reinterpret_cast<unsigned long long *>(bounds));
+                                          reinterpret_cast<unsigned long long *>(bounds),
+                                          strict ? 1 : 0);
     return hipGetLastError();
 }
 

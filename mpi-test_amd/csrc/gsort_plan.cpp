@@ -80,9 +80,14 @@ extern "C" gsort_status gsort_plan_splitters(int P, const int32_t *samples, int3
 // [s_me(q), s_me(q+1)) to q and receives s_p(me+1) - s_p(me) keys from each p.
 // (Replaces the per-pass digit routing through rank 0, mpi_radix_sort.c:139,150-192: one
 // exchange instead of one per base-P digit.)
-extern "C" gsort_status gsort_plan_split(int P, const uint64_t *n_all, const uint64_t *lt,
-                                         const uint64_t *le, int me, uint64_t *send,
-                                         uint64_t *recv) {
+// balanced (gsort_plan_split_balanced): v_q is the q-th sample splitter instead, so g_q need
+// not fall among its copies; the boundary moves to clamp(min(qB, N), LT_q + 1, LE_q) -- as
+// close to qB as v_q's copies allow, keeping at least one copy left as the reference's rule
+// does (keys <= s go left), so a splitter value held once gives exactly the reference's
+// bucket -- and the copies are again taken in rank order.
+static gsort_status plan_split(int P, const uint64_t *n_all, const uint64_t *lt,
+                               const uint64_t *le, int me, uint64_t *send, uint64_t *recv,
+                               bool balanced) {
     if (P < 1 || !n_all || (P > 1 && (!lt || !le)) || !send || !recv || me < 0 || me >= P)
         return GSORT_EINVAL;
     uint64_t N = 0;
@@ -92,9 +97,16 @@ extern "C" gsort_status gsort_plan_split(int P, const uint64_t *n_all, const uin
     std::vector<uint64_t> cut((size_t)P * (P + 1), 0);
     for (int p = 0; p < P; ++p) cut[(size_t)p * (P + 1) + P] = n_all[p];
     for (int q = 1; q < P; ++q) {
-        const uint64_t g = std::min<uint64_t>((uint64_t)q * B, N);
-        uint64_t lt_all = 0, eq_before = 0;
-        for (int p = 0; p < P; ++p) lt_all += lt[(size_t)p * (P - 1) + (q - 1)];
+        uint64_t g = std::min<uint64_t>((uint64_t)q * B, N);
+        uint64_t lt_all = 0, le_all = 0, eq_before = 0;
+        for (int p = 0; p < P; ++p) {
+            lt_all += lt[(size_t)p * (P - 1) + (q - 1)];
+            le_all += le[(size_t)p * (P - 1) + (q - 1)];
+        }
+        if (balanced) {
+            if (le_all < lt_all || le_all > N) return GSORT_EINVAL;
+            g = std::min(std::max(g, lt_all + (le_all > lt_all ? 1 : 0)), le_all);
+        }
         if (g >= N) {
             for (int p = 0; p < P; ++p) cut[(size_t)p * (P + 1) + q] = n_all[p];
             continue;
@@ -120,4 +132,16 @@ extern "C" gsort_status gsort_plan_split(int P, const uint64_t *n_all, const uin
         recv[q] = rb - ra;
     }
     return GSORT_OK;
+}
+
+extern "C" gsort_status gsort_plan_split(int P, const uint64_t *n_all, const uint64_t *lt,
+                                         const uint64_t *le, int me, uint64_t *send,
+                                         uint64_t *recv) {
+    return plan_split(P, n_all, lt, le, me, send, recv, false);
+}
+
+extern "C" gsort_status gsort_plan_split_balanced(int P, const uint64_t *n_all,
+                                                  const uint64_t *lt, const uint64_t *le, int me,
+                                                  uint64_t *send, uint64_t *recv) {
+    return plan_split(P, n_all, lt, le, me, send, recv, true);
 }

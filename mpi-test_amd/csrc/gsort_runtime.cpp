@@ -50,6 +50,7 @@ struct gsort_ctx {
     DevBuf tcounts;  // K1/K2: per-tile digit counts -> in-group offsets (u32 [tiles][256])
     DevBuf gsum;     // K2: per-group digit prefixes (u64 [groups][256])
     int local_algo = GSORT_LOCAL_MSD;
+    bool sample_balanced = false;  // gsort_set_sample_balanced
     bool atomic_rank = false;  // LDS lane-order property verified on this device (create)
     // MSD scratch: segment plan/maps, child starts, work lists (u64 {start, len} pairs)
     DevBuf m_tpfx, m_gpfx, m_segmap, m_groupmap, m_cstart, m_next[2], m_local[kLocalClasses];
@@ -1069,12 +1070,44 @@ gsort_status sample_dist(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in, int
     uint64_t *d_cnt = reinterpret_cast<uint64_t *>(c->d_small + OFF_PLAN + 16384);
     uint64_t *d_mat = d_cnt + 64;
     uint64_t *h_cnt = reinterpret_cast<uint64_t *>(c->h_small + OFF_PLAN + 16384);
-    memcpy(h_cnt, c->bucket_counts.data(), (size_t)P * 8);
-    HIP_TRY(c, hipMemcpyAsync(d_cnt, h_cnt, (size_t)P * 8, hipMemcpyHostToDevice, c->stream));
-    ST_TRY(comm_try(c, c->comm->allgather(d_cnt, d_mat, (size_t)P * 8, c->stream)));
     std::vector<uint64_t> M((size_t)P * P);
-    HIP_TRY(c, hipMemcpyAsync(M.data(), d_mat, M.size() * 8, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (!c->sample_balanced) {
+        memcpy(h_cnt, c->bucket_counts.data(), (size_t)P * 8);
+        HIP_TRY(c, hipMemcpyAsync(d_cnt, h_cnt, (size_t)P * 8, hipMemcpyHostToDevice, c->stream));
+        ST_TRY(comm_try(c, c->comm->allgather(d_cnt, d_mat, (size_t)P * 8, c->stream)));
+        HIP_TRY(c, hipMemcpyAsync(M.data(), d_mat, M.size() * 8, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+    } else {
+        // duplicate-aware buckets: keys < s_j (strict K6) and <= s_j of every rank, then the
+        // same cut rule as the distributed radix with the boundary clamped into s_j's copies
+        const int S = P - 1;
+        uint64_t *d_lt = d_bounds + 64;
+        HIP_TRY(c, launch_bucket_bounds(sorted, n_in, d_spl, S, d_lt, c->stream, true));
+        uint64_t *d_ll = d_cnt;  // this rank: [lt x S | le x S]
+        HIP_TRY(c, hipMemcpyAsync(d_ll, d_lt, (size_t)S * 8, hipMemcpyDeviceToDevice, c->stream));
+        HIP_TRY(c, hipMemcpyAsync(d_ll + S, d_bounds, (size_t)S * 8, hipMemcpyDeviceToDevice,
+                                  c->stream));
+        uint64_t *d_all2 = d_cnt + 64;
+        ST_TRY(comm_try(c, c->comm->allgather(d_ll, d_all2, (size_t)2 * S * 8, c->stream)));
+        std::vector<uint64_t> A((size_t)P * 2 * S), lt((size_t)P * S), le((size_t)P * S);
+        HIP_TRY(c, hipMemcpyAsync(A.data(), d_all2, A.size() * 8, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        for (int p = 0; p < P; ++p)
+            for (int j = 0; j < S; ++j) {
+                lt[(size_t)p * S + j] = A[(size_t)p * 2 * S + j];
+                le[(size_t)p * S + j] = A[(size_t)p * 2 * S + S + j];
+            }
+        // every rank plans every rank's row (host, identical inputs) -> the full matrix
+        std::vector<uint64_t> snd(P), rcv(P);
+        for (int p = 0; p < P; ++p) {
+            const gsort_status st =
+                gsort_plan_split_balanced(P, n_all.data(), lt.data(), le.data(), p, snd.data(),
+                                          rcv.data());
+            if (st != GSORT_OK) return set_err(c, st, "inconsistent sample bucket bounds");
+            for (int q = 0; q < P; ++q) M[(size_t)p * P + q] = snd[q];
+        }
+        for (int q = 0; q < P; ++q) c->bucket_counts[q] = M[(size_t)me * P + q];
+    }
     uint64_t total = 0;
     size_t so = 0, ro = 0;
     for (int q = 0; q < P; ++q) {
@@ -1299,6 +1332,12 @@ gsort_status gsort_set_local_algo(gsort_ctx *c, int algo) {
     if (algo != GSORT_LOCAL_MSD && algo != GSORT_LOCAL_LSD)
         return set_err(c, GSORT_EINVAL, "unknown local sort algorithm");
     c->local_algo = algo;
+    return GSORT_OK;
+}
+
+gsort_status gsort_set_sample_balanced(gsort_ctx *c, int on) {
+    ST_TRY(check_ctx(c));
+    c->sample_balanced = on != 0;
     return GSORT_OK;
 }
 

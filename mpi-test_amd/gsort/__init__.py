@@ -68,12 +68,13 @@ class Uid(ctypes.Structure):
 EXPORTS = [
     "gsort_get_uid", "gsort_create", "gsort_group_create", "gsort_group_destroy",
     "gsort_create_in_group", "gsort_destroy", "gsort_reserve", "gsort_set_local_algo",
+    "gsort_set_sample_balanced",
     "gsort_strerror",
     "gsort_last_error", "gsort_rank", "gsort_nranks", "gsort_radix", "gsort_sample",
     "gsort_sample_info", "gsort_scatter_from_root", "gsort_gather_to_root", "gsort_generate",
     "gsort_fingerprint", "gsort_device_alloc", "gsort_device_free", "gsort_copy_to_host",
     "gsort_copy_to_device", "gsort_onesweep_tile", "gsort_plan_radix_route",
-    "gsort_plan_splitters", "gsort_plan_split", "gsort_parse_text",
+    "gsort_plan_splitters", "gsort_plan_split", "gsort_plan_split_balanced", "gsort_parse_text",
 ]
 
 _lib = None
@@ -121,6 +122,8 @@ def lib():
     L.gsort_plan_radix_route.argtypes = [I, VP, U64, I, VP, VP, VP, P(SZ)]
     L.gsort_plan_splitters.argtypes = [I, VP, VP]
     L.gsort_plan_split.argtypes = [I, VP, VP, VP, I, VP, VP]
+    L.gsort_plan_split_balanced.argtypes = [I, VP, VP, VP, I, VP, VP]
+    L.gsort_set_sample_balanced.argtypes = [VP, I]
     L.gsort_parse_text.argtypes = [ctypes.c_char_p, SZ, VP, SZ, I]
     L.gsort_parse_text.restype = ctypes.c_longlong
     _lib = L
@@ -192,6 +195,10 @@ class Context:
     def set_local_algo(self, algo):
         """LOCAL_MSD (default) or LOCAL_LSD for every later local sort of this context."""
         self._c(lib().gsort_set_local_algo(self.h, algo))
+
+    def set_sample_balanced(self, on=True):
+        """Duplicate-aware balanced sample-sort buckets (gsort_set_sample_balanced)."""
+        self._c(lib().gsort_set_sample_balanced(self.h, 1 if on else 0))
 
     def _sort(self, fn, d_keys, n):
         out, nout, st = ctypes.c_void_p(), ctypes.c_size_t(), Stats()
@@ -286,8 +293,9 @@ def plan_radix_route(hist, B, me):
     return send, recv, seg[: 4 * n.value].reshape(-1, 4)
 
 
-def plan_split(n_all, lt, le, me):
-    """Host-only exact split of the distributed radix (gsort_plan_split): (send, recv)."""
+def plan_split(n_all, lt, le, me, balanced=False):
+    """Host-only exact split of the distributed radix (gsort_plan_split): (send, recv);
+    balanced: the sample sort's duplicate-aware cut (gsort_plan_split_balanced)."""
     import numpy as np
     n_all = np.ascontiguousarray(n_all, dtype=np.uint64)
     P = n_all.size
@@ -295,8 +303,9 @@ def plan_split(n_all, lt, le, me):
     le = np.ascontiguousarray(le, dtype=np.uint64).reshape(P, max(P - 1, 0))
     send = np.zeros(P, dtype=np.uint64)
     recv = np.zeros(P, dtype=np.uint64)
-    _check(lib().gsort_plan_split(P, n_all.ctypes.data, lt.ctypes.data, le.ctypes.data, me,
-                                  send.ctypes.data, recv.ctypes.data), None)
+    fn = lib().gsort_plan_split_balanced if balanced else lib().gsort_plan_split
+    _check(fn(P, n_all.ctypes.data, lt.ctypes.data, le.ctypes.data, me,
+              send.ctypes.data, recv.ctypes.data), None)
     return send, recv
 
 

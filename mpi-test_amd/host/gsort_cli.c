@@ -110,6 +110,10 @@ int gsort_cli_main(int argc, char **argv, int algo)
     gsort_ctx *ctx = NULL;
     check(gsort_create(&ctx, rank, size, -1 - local_rank(rank), size > 1 ? &uid : NULL), NULL,
           "gsort_create");
+    /* GSORT_SAMPLE_BALANCED=1: duplicate-aware sample buckets (not the reference's rule) */
+    const char *bal = getenv("GSORT_SAMPLE_BALANCED");
+    if (algo == CLI_SAMPLE && bal && atoi(bal))
+        check(gsort_set_sample_balanced(ctx, 1), ctx, "gsort_set_sample_balanced");
 
     MPI_Barrier(MPI_COMM_WORLD);
     const double start = MPI_Wtime();

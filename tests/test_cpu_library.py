@@ -174,3 +174,61 @@ def test_uid_bytes_survive_marshalling(gsort):
     u = gsort.Uid.from_bytes(raw)
     assert u.to_bytes() == raw
     assert bytes(u.internal) == raw
+
+
+def _balanced_cut_model(n_all, blocks, spl):
+    """Python model of gsort_plan_split_balanced: boundary q sits at
+    clamp(min(qB, N), LT + 1, LE) of splitter spl[q-1] (LT + 1 only when the value occurs);
+    copies of the splitter value are taken in rank order."""
+    P = len(blocks)
+    N = sum(n_all)
+    B = -(-N // P) if N else 0
+    cut = [[0] * (P + 1) for _ in range(P)]
+    for p in range(P):
+        cut[p][P] = n_all[p]
+    for q in range(1, P):
+        v = spl[q - 1]
+        lt = [int(np.searchsorted(b, v, "left")) for b in blocks]
+        le = [int(np.searchsorted(b, v, "right")) for b in blocks]
+        g = min(max(min(q * B, N), sum(lt) + (sum(le) > sum(lt))), sum(le))
+        left = g - sum(lt)
+        for p in range(P):
+            take = min(max(left, 0), le[p] - lt[p])
+            cut[p][q] = n_all[p] if g >= N else lt[p] + take
+            left -= le[p] - lt[p]
+    return cut
+
+
+@pytest.mark.parametrize("kind", ["uniform", "dups", "one_value", "empty_ranks", "tiny"])
+def test_plan_split_balanced_sample_buckets(gsort, kind):
+    """gsort_plan_split_balanced (duplicate-aware sample-sort buckets): matches the model, the
+    buckets concatenate to the sorted multiset (duplicate-heavy and empty ranks too), and a
+    splitter value held once cuts exactly where the reference's rule does (keys <= s_j go to
+    bucket j, mpi_sample_sort.c:148-155)."""
+    rng = np.random.default_rng(7 + sum(map(ord, kind)))
+    for P in (2, 3, 4, 8):
+        for trial in range(6):
+            n_all, blocks = _split_case(rng, P, kind)
+            allk = np.sort(np.concatenate(blocks)) if sum(n_all) else np.zeros(0, np.int32)
+            if allk.size == 0:
+                continue
+            spl = np.sort(rng.choice(allk, P - 1))
+            lt = np.array([[np.searchsorted(b, v, "left") for v in spl] for b in blocks],
+                          np.uint64).reshape(P, P - 1)
+            le = np.array([[np.searchsorted(b, v, "right") for v in spl] for b in blocks],
+                          np.uint64).reshape(P, P - 1)
+            sends = [gsort.plan_split(n_all, lt, le, me, balanced=True) for me in range(P)]
+            cut = _balanced_cut_model(n_all, blocks, spl)
+            buckets = []
+            for q in range(P):
+                parts = []
+                for p in range(P):
+                    assert int(sends[p][0][q]) == cut[p][q + 1] - cut[p][q], (P, trial, p, q)
+                    assert sends[q][1][p] == sends[p][0][q]
+                    parts.append(blocks[p][cut[p][q]:cut[p][q + 1]])
+                buckets.append(np.sort(np.concatenate(parts)))
+            assert np.array_equal(np.concatenate(buckets), allk)
+            for q in range(1, P):
+                if int(le[:, q - 1].sum()) - int(lt[:, q - 1].sum()) == 1:
+                    for p in range(P):
+                        assert cut[p][q] == int(le[p, q - 1]) or cut[p][q] == n_all[p]
