@@ -114,8 +114,18 @@ gsort_status comm_try(gsort_ctx *c, gsort_status st) {
     return st;
 }
 
+// GSORT_ALLOC_LIMIT=bytes (diagnostics): refuse any larger scratch allocation, naming the buffer
+std::string buf_name(gsort_ctx *c, const DevBuf &b);
+
 gsort_status ensure(gsort_ctx *c, DevBuf &b, size_t bytes) {
     if (bytes <= b.cap) return GSORT_OK;
+    static const unsigned long long limit =
+        getenv("GSORT_ALLOC_LIMIT") ? strtoull(getenv("GSORT_ALLOC_LIMIT"), nullptr, 0) : 0ull;
+    if (limit && bytes > limit)
+        return set_err(c, GSORT_ENOMEM, "allocation of " + std::to_string(bytes) +
+                                            " bytes for " + buf_name(c, b) +
+                                            " over GSORT_ALLOC_LIMIT (rank " +
+                                            std::to_string(c->rank) + ")");
     if (b.p) HIP_TRY(c, hipFree(b.p));
     b.p = nullptr;
     b.cap = 0;
@@ -266,6 +276,26 @@ static_assert(OFF_CTR + kCtrBytes <= OFF_ONE, "counter area");
 
 gsort_status ensure_list(gsort_ctx *c, DevBuf &b, uint64_t entries) {
     return ensure(c, b, (size_t)std::max<uint64_t>(entries, 1) * 16);
+}
+
+std::string buf_name(gsort_ctx *c, const DevBuf &b) {
+    const std::pair<const char *, const DevBuf *> named[] = {
+        {"tcounts", &c->tcounts}, {"gsum", &c->gsum}, {"m_tpfx", &c->m_tpfx},
+        {"m_gpfx", &c->m_gpfx}, {"m_segmap", &c->m_segmap}, {"m_groupmap", &c->m_groupmap},
+        {"m_cstart", &c->m_cstart}, {"m_next0", &c->m_next[0]}, {"m_next1", &c->m_next[1]},
+        {"m_part", &c->m_part}, {"m_fix", &c->m_fix}, {"m_cur", &c->m_cur},
+        {"m_split", &c->m_split}, {"m_rpos", &c->m_rpos}, {"m_bsize", &c->m_bsize},
+        {"m_bseg", &c->m_bseg}, {"m_blist", &c->m_blist}, {"m_gb", &c->m_gb},
+        {"m_pack", &c->m_pack}, {"m_meta", &c->m_meta}, {"m_g16", &c->m_g16}};
+    for (const auto &nb : named)
+        if (nb.second == &b) return nb.first;
+    for (int i = 0; i < S_NSLOTS; ++i)
+        if (&c->slot[i] == &b) return "slot" + std::to_string(i);
+    for (int k = 0; k < kLocalClasses; ++k) {
+        if (&c->m_local[k] == &b) return "m_local" + std::to_string(k);
+        if (&c->m_local3[k] == &b) return "m_local3_" + std::to_string(k);
+    }
+    return "?";
 }
 
 gsort_status read_counters(gsort_ctx *c, uint64_t *h) {

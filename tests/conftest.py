@@ -65,3 +65,17 @@ def gsort():
     import torch  # noqa: F401
     import gsort as _g
     return _g
+
+
+@pytest.fixture(autouse=True)
+def _gsort_memlog(request):
+    """GSORT_MEMLOG=path: append each GPU test's device free/total bytes after it ran
+    (diagnostics for device-memory growth across a test session)."""
+    yield
+    path = os.environ.get("GSORT_MEMLOG")
+    if not path or request.node.get_closest_marker("gpu") is None:
+        return
+    import torch
+    free, total = torch.cuda.mem_get_info()
+    with open(path, "a") as f:
+        f.write(f"{request.node.nodeid} {free} {total}\n")

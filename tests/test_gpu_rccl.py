@@ -6,11 +6,27 @@ gsort_radix / gsort_sample take the distributed algorithms anyway: radix select,
 the packed 16-bit exchange (to self) and the receive-side sort -- over the in-process group
 and over RCCL itself (ncclCommInitRank from a gsort_get_uid, ncclAllGather, grouped
 ncclSend/ncclRecv, ncclBroadcast).  Output must equal the oracle's sort, bit for bit.
+
+The cases run in ONE child process (this file with --child), as a real rank does: one process
+per GPU and one communicator in it.  In the pytest process itself, an 8-rank in-process group
+started after an RCCL communicator had lived and been destroyed there failed on the MI355X
+box (first a failed 512 KiB hipMalloc, then an illegal-address fault surfacing at the next
+launch; the same tests pass when the group runs first), so the RCCL communicator never shares
+a process with the in-process groups.
 """
+import json
+import os
+import subprocess
+import sys
+
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
+
+DIST_CASES = [(t, a, d) for d in ("uniform", "zipf") for a in ("radix", "sample")
+              for t in ("group", "rccl")]
+SMALL_CASES = [0, 1, 5, 16384, 16385]
 
 
 def _ctx(gsort, transport):
@@ -20,11 +36,7 @@ def _ctx(gsort, transport):
     return gsort.Context(rank=0, nranks=1, device=0, uid=gsort.get_uid()), None
 
 
-@pytest.mark.parametrize("transport", ["group", "rccl"])
-@pytest.mark.parametrize("algo", ["radix", "sample"])
-@pytest.mark.parametrize("dist_name", ["uniform", "zipf"])
-def test_one_rank_distributed_path(gsort, orc, monkeypatch, transport, algo, dist_name):
-    monkeypatch.setenv("GSORT_FORCE_DIST", "1")
+def _case_distributed_path(gsort, orc, transport, algo, dist_name):
     n = (1 << 20) + 4321
     dist = orc.UNIFORM if dist_name == "uniform" else orc.ZIPF
     keys = orc.gen(dist, 11, n)
@@ -46,9 +58,7 @@ def test_one_rank_distributed_path(gsort, orc, monkeypatch, transport, algo, dis
             grp.close()
 
 
-@pytest.mark.parametrize("n", [0, 1, 5, 16384, 16385])
-def test_one_rank_rccl_small(gsort, orc, monkeypatch, n):
-    monkeypatch.setenv("GSORT_FORCE_DIST", "1")
+def _case_rccl_small(gsort, orc, n):
     keys = orc.gen(orc.UNIFORM, 5, n)
     ctx, _ = _ctx(gsort, "rccl")
     try:
@@ -62,3 +72,55 @@ def test_one_rank_rccl_small(gsort, orc, monkeypatch, n):
         ctx.free(p)
     finally:
         ctx.close()
+
+
+def _child():
+    """Every case in this process; one JSON line of {case id: "ok" | error text}."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "mpi-test_amd")):
+        sys.path.insert(0, p)
+    import torch  # noqa: F401  (one HIP runtime per process, as conftest.gsort)
+    import gsort
+    from oracle import orc
+    orc.lib()
+    res = {}
+    for c in DIST_CASES:
+        try:
+            _case_distributed_path(gsort, orc, *c)
+            res["-".join(c)] = "ok"
+        except Exception as e:  # reported per case by the parent
+            res["-".join(c)] = repr(e)
+        print("case", c, res["-".join(c)], file=sys.stderr, flush=True)
+    for n in SMALL_CASES:
+        try:
+            _case_rccl_small(gsort, orc, n)
+            res[f"small-{n}"] = "ok"
+        except Exception as e:
+            res[f"small-{n}"] = repr(e)
+        print("case", n, res[f"small-{n}"], file=sys.stderr, flush=True)
+    print("RCCL_RESULTS " + json.dumps(res), flush=True)
+
+
+@pytest.fixture(scope="module")
+def child_results():
+    env = dict(os.environ, GSORT_FORCE_DIST="1")
+    r = subprocess.run([sys.executable, os.path.abspath(__file__), "--child"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    for line in r.stdout.splitlines():
+        if line.startswith("RCCL_RESULTS "):
+            return json.loads(line[len("RCCL_RESULTS "):])
+    pytest.fail(f"RCCL child exited {r.returncode} without results:\n{r.stderr[-4000:]}")
+
+
+@pytest.mark.parametrize("case", DIST_CASES, ids=["-".join(c) for c in DIST_CASES])
+def test_one_rank_distributed_path(child_results, case):
+    assert child_results["-".join(case)] == "ok"
+
+
+@pytest.mark.parametrize("n", SMALL_CASES)
+def test_one_rank_rccl_small(child_results, n):
+    assert child_results[f"small-{n}"] == "ok"
+
+
+if __name__ == "__main__" and "--child" in sys.argv:
+    _child()
