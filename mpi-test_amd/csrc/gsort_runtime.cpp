@@ -298,6 +298,32 @@ std::string buf_name(gsort_ctx *c, const DevBuf &b) {
     return "?";
 }
 
+// GSORT_CHECK=1 (diagnostics): host-side invariant checks between the distributed phases, so
+// a broken count fails the call with a message instead of sizing buffers or launches from it
+bool check_mode() {
+    static const bool on = getenv("GSORT_CHECK") && atoi(getenv("GSORT_CHECK"));
+    return on;
+}
+
+gsort_status check_bounds(gsort_ctx *c, const uint64_t *d, size_t m, uint64_t last,
+                          const char *what) {
+    std::vector<uint64_t> v(m);
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, hipMemcpy(v.data(), d, m * 8, hipMemcpyDeviceToHost));
+    for (size_t i = 1; i < m; ++i)
+        if (v[i] < v[i - 1])
+            return set_err(c, GSORT_EINVAL, std::string("GSORT_CHECK ") + what + ": decreases at " +
+                                                std::to_string(i) + " (rank " +
+                                                std::to_string(c->rank) + ")");
+    if (v[0] != 0 || v[m - 1] != last)
+        return set_err(c, GSORT_EINVAL, std::string("GSORT_CHECK ") + what + ": ends " +
+                                            std::to_string(v[0]) + ".." +
+                                            std::to_string(v[m - 1]) + ", want 0.." +
+                                            std::to_string(last) + " (rank " +
+                                            std::to_string(c->rank) + ")");
+    return GSORT_OK;
+}
+
 gsort_status read_counters(gsort_ctx *c, uint64_t *h) {
     HIP_TRY(c, hipMemcpyAsync(c->h_small + OFF_CTR, c->d_small + OFF_CTR, kCtrBytes,
                               hipMemcpyDeviceToHost, c->stream));
@@ -598,6 +624,16 @@ gsort_status recv_sort(gsort_ctx *c, const void *recv, bool packed16,
     toc(c, PH_COUNT, t);
     uint64_t h[3 * (kLocalClasses + 1)];
     ST_TRY(read_counters(c, h));
+    if (check_mode()) {
+        uint64_t keys = h[1];
+        for (int k = 0; k < kLocalClasses; ++k) keys += h[3 * (k + 1) + 1];
+        if (keys != n)
+            return set_err(c, GSORT_EINVAL, "GSORT_CHECK receive lists hold " +
+                                                std::to_string(keys) + " keys, want " +
+                                                std::to_string(n) + " (rank " +
+                                                std::to_string(c->rank) + ")");
+        ST_TRY(check_bounds(c, bstart, kBuckets16 + 1, n, "receive bucket starts"));
+    }
     for (int k = 0; k < kLocalClasses; ++k) {
         const uint64_t *hk = h + 3 * (k + 1);
         if (!hk[0]) continue;
@@ -774,6 +810,7 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
         toc(c, PH_PLACE, t);
     }
     int pr = stats ? stats->passes_run : 0;
+    if (check_mode()) ST_TRY(check_bounds(c, gb, kBuckets16 + 1, n_in, "sender bucket bounds"));
 
     // (2) radix select of v_q, the g_q-th smallest key, for the P-1 inner boundaries
     const int nb = P - 1, M = 257;
@@ -917,6 +954,11 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
                                     reinterpret_cast<uint64_t *>(c->m_rpos.p),
                                     reinterpret_cast<uint64_t *>(c->m_bsize.p) + 2 * kBuckets16 + 1,
                                     c->stream));
+    if (check_mode())
+        for (int p = 0; p < P; ++p)
+            ST_TRY(check_bounds(c, reinterpret_cast<uint64_t *>(c->m_rpos.p) +
+                                       (size_t)p * (kBuckets16 + 1),
+                                kBuckets16 + 1, recv[p], "received run bounds"));
     ST_TRY(recv_sort(c, rbuf, true, recv, mine, slot_ptr<uint32_t>(c, S_OUT),
                      slot_ptr<uint32_t>(c, S_TMP), stats));
     toc(c, PH_MERGE, t);
