@@ -155,7 +155,7 @@ def pmc_traffic(algo, n_local, n_gpus, prefixes=("k_scatter",)):
     """HBM bytes per launch of the dominant kernel (FETCH_SIZE x 2 + WRITE_SIZE,
     MI355X_MICROARCH.md §HBM) from the
     newest committed rocprofv3 PMC summary of this exact configuration
-    (mpi-test_amd/tools/profile_pmc.sh -> profiles/*_pmc_summary.json), else None."""
+    (tools/profile_pmc.sh -> profiles/*_pmc_summary.json), else None."""
     import glob
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json")),
                        reverse=True):

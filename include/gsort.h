@@ -164,6 +164,12 @@ size_t gsort_onesweep_tile(void);
  * reference spins on such a token until realloc fails and then reports the file invalid).  A
  * trailing delimiter adds no phantom element.  threads > 1 parses in chunks. */
 long long gsort_parse_text(const char *buf, size_t len, int32_t *out, size_t cap, int threads);
+/* gsort_format_dump: the reference's sorted dump, printf("%u|%u\n", i, int_buf[i]) per key on
+ * rank 0 (mpi_radix_sort.c:198-200, mpi_sample_sort.c:202-204), rendered as "%llu|%u\n"
+ * (index first_index + i, key as unsigned) for keys[0 .. n) into out on `threads` threads.
+ * Returns the byte count (out == NULL: only count), or -1 if cap is too small. */
+long long gsort_format_dump(const int32_t *keys, size_t n, uint64_t first_index, char *out,
+                            size_t cap, int threads);
 
 /* ---- host-only planning (no GPU; exported so CPU tests can check it) ----------------------
  * gsort_plan_radix_route: the K8 routing of one distributed LSD pass.  hist = P x 256 per-rank

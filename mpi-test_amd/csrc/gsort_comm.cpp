@@ -1,7 +1,10 @@
 // gsort_comm.cpp -- RCCL and in-process transports (see gsort_comm.h).
 #include "gsort_comm.h"
 
+#include "gsort_debug.h"
+
 #include <rccl/rccl.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -12,6 +15,58 @@
 #include <vector>
 
 namespace gsort {
+
+bool serial_mode() {
+    static const bool on = getenv("GSORT_SERIAL") && atoi(getenv("GSORT_SERIAL"));
+    return on;
+}
+bool canary_mode() {
+    static const bool on = getenv("GSORT_CANARY") && atoi(getenv("GSORT_CANARY"));
+    return on;
+}
+std::mutex &serial_mutex() {
+    static std::mutex m;
+    return m;
+}
+bool trace_mode() {
+    static const bool on = getenv("GSORT_TRACE") && atoi(getenv("GSORT_TRACE"));
+    return on;
+}
+
+namespace {
+struct TraceRec {
+    double t_us;
+    int rank;
+    const char *what;
+};
+constexpr size_t kTraceRing = 1 << 16, kTraceDump = 400;
+std::mutex g_trace_mu;
+std::vector<TraceRec> g_trace(kTraceRing);
+size_t g_trace_n = 0;
+bool g_trace_dumped = false;
+const auto g_t0 = std::chrono::steady_clock::now();
+}  // namespace
+
+void trace_op(int rank, const char *what) {
+    const double t = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() -
+                                                               g_t0).count();
+    std::lock_guard<std::mutex> lk(g_trace_mu);
+    g_trace[g_trace_n++ % kTraceRing] = {t, rank, what};
+}
+
+void trace_dump(const char *why) {
+    std::lock_guard<std::mutex> lk(g_trace_mu);
+    if (g_trace_dumped) return;
+    g_trace_dumped = true;
+    const size_t n = std::min(g_trace_n, kTraceDump);
+    fprintf(stderr, "GSORT_TRACE: %s; last %zu of %zu HIP ops (time us, rank, op):\n", why, n,
+            g_trace_n);
+    for (size_t i = g_trace_n - n; i < g_trace_n; ++i) {
+        const TraceRec &r = g_trace[i % kTraceRing];
+        fprintf(stderr, "  %12.1f r%-2d %.160s\n", r.t_us, r.rank, r.what);
+    }
+    fflush(stderr);
+}
 
 // ---------------------------------------------------------------------------------------
 // RCCL over xGMI
@@ -142,29 +197,36 @@ class GroupComm : public Comm {
         err = std::string("in-process group: ") + what;
         return GSORT_ECOMM;
     }
-    gsort_status hip(hipError_t e, const char *what) {
+    // every HIP call goes through hip_op (GSORT_SERIAL: serialized with all other contexts)
+    template <class F>
+    gsort_status hip(F &&f, const char *what) {
+        if (trace_mode()) trace_op(rank_, what);
+        const hipError_t e = hip_op(f);
         if (e == hipSuccess) return GSORT_OK;
+        if (trace_mode()) trace_dump(what);
         err = std::string(what) + ": " + hipGetErrorString(e);
         return GSORT_EHIP;
     }
 
     gsort_status allgather(const void *send, void *recv, size_t bytes, hipStream_t s) override {
-        gsort_status st = hip(hipStreamSynchronize(s), "hipStreamSynchronize");
+        gsort_status st = hip([&] { return hipStreamSynchronize(s); }, "hipStreamSynchronize");
         if (st != GSORT_OK) return st;
         g_->ptr[rank_] = send;
         if (!barrier()) return fail("barrier timeout");
         for (int r = 0; r < size_ && st == GSORT_OK; ++r)
             if (bytes)
-                st = hip(hipMemcpyAsync((char *)recv + (size_t)r * bytes, g_->ptr[r], bytes,
-                                        hipMemcpyDeviceToDevice, s), "hipMemcpyAsync");
-        if (st == GSORT_OK) st = hip(hipStreamSynchronize(s), "hipStreamSynchronize");
+                st = hip([&] {
+                    return hipMemcpyAsync((char *)recv + (size_t)r * bytes, g_->ptr[r], bytes,
+                                          hipMemcpyDeviceToDevice, s);
+                }, "hipMemcpyAsync");
+        if (st == GSORT_OK) st = hip([&] { return hipStreamSynchronize(s); }, "hipStreamSynchronize");
         if (!barrier()) return fail("barrier timeout");
         return st;
     }
     gsort_status alltoallv(const void *send, const size_t *scount, const size_t *sdispl,
                            void *recv, const size_t *rcount, const size_t *rdispl,
                            hipStream_t s) override {
-        gsort_status st = hip(hipStreamSynchronize(s), "hipStreamSynchronize");
+        gsort_status st = hip([&] { return hipStreamSynchronize(s); }, "hipStreamSynchronize");
         if (st != GSORT_OK) return st;
         g_->ptr[rank_] = send;
         g_->count[rank_] = scount;
@@ -174,23 +236,26 @@ class GroupComm : public Comm {
             const size_t c = g_->count[r][rank_];
             if (c != rcount[r]) { st = fail("send/recv count mismatch"); break; }
             if (c)
-                st = hip(hipMemcpyAsync((char *)recv + rdispl[r],
-                                        (const char *)g_->ptr[r] + g_->displ[r][rank_], c,
-                                        hipMemcpyDeviceToDevice, s), "hipMemcpyAsync");
+                st = hip([&] {
+                    return hipMemcpyAsync((char *)recv + rdispl[r],
+                                          (const char *)g_->ptr[r] + g_->displ[r][rank_], c,
+                                          hipMemcpyDeviceToDevice, s);
+                }, "hipMemcpyAsync");
         }
-        gsort_status st2 = hip(hipStreamSynchronize(s), "hipStreamSynchronize");
+        gsort_status st2 = hip([&] { return hipStreamSynchronize(s); }, "hipStreamSynchronize");
         if (!barrier()) return fail("barrier timeout");
         return st != GSORT_OK ? st : st2;
     }
     gsort_status bcast(void *buf, size_t bytes, int root, hipStream_t s) override {
-        gsort_status st = hip(hipStreamSynchronize(s), "hipStreamSynchronize");
+        gsort_status st = hip([&] { return hipStreamSynchronize(s); }, "hipStreamSynchronize");
         if (st != GSORT_OK) return st;
         g_->ptr[rank_] = buf;
         if (!barrier()) return fail("barrier timeout");
         if (rank_ != root && bytes)
-            st = hip(hipMemcpyAsync(buf, g_->ptr[root], bytes, hipMemcpyDeviceToDevice, s),
-                     "hipMemcpyAsync");
-        gsort_status st2 = hip(hipStreamSynchronize(s), "hipStreamSynchronize");
+            st = hip([&] {
+                return hipMemcpyAsync(buf, g_->ptr[root], bytes, hipMemcpyDeviceToDevice, s);
+            }, "hipMemcpyAsync");
+        gsort_status st2 = hip([&] { return hipStreamSynchronize(s); }, "hipStreamSynchronize");
         if (!barrier()) return fail("barrier timeout");
         return st != GSORT_OK ? st : st2;
     }

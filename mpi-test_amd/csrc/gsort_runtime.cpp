@@ -12,12 +12,16 @@
 
 #include <algorithm>
 #include <atomic>
+#include <map>
+#include <mutex>
+#include <set>
 #include <string>
 #include <thread>
 #include <vector>
 
 #include "gsort.h"
 #include "gsort_comm.h"
+#include "gsort_debug.h"
 #include "gsort_kernels.h"
 
 using namespace gsort;
@@ -35,8 +39,9 @@ enum Phase { PH_COUNT, PH_PASS0, PH_PASS1, PH_PASS2, PH_PASS3, PH_EXCH, PH_PLACE
 constexpr size_t kSmallBytes = 256 * 1024;  // device + pinned scratch for counts, plans
 
 struct DevBuf {
-    void *p = nullptr;
-    size_t cap = 0;
+    void *p = nullptr;     // what the kernels use
+    size_t cap = 0;        // usable bytes at p
+    void *base = nullptr;  // the allocation (p - kGuardBytes with GSORT_CANARY)
 };
 
 }  // namespace
@@ -66,8 +71,10 @@ struct gsort_ctx {
     DevBuf m_gb, m_pack, m_meta, m_g16;  // packed exchange: bucket bounds, low 16 bits, counts
     // device small area: [0, 8K) hist4 (4x256 u64) | [8K, 10K) pass digit totals (256 u64) |
     // [10K, 12K) pass digit bases (256 u64) | [20K, 256K) plans / samples / routing tables
+    DevBuf small;               // kSmallBytes; d_small aliases small.p
     char *d_small = nullptr;
     char *h_small = nullptr;  // pinned mirror
+    std::map<void *, DevBuf> user_bufs;  // gsort_device_alloc (guarded with GSORT_CANARY)
     std::vector<int32_t> splitters;
     std::vector<uint64_t> bucket_counts;
     // timing
@@ -95,12 +102,28 @@ gsort_status set_err(gsort_ctx *c, gsort_status st, const std::string &msg) {
     return st;
 }
 
+// Diagnostic modes (gsort_debug.h).  GSORT_CANARY checks every live context's guards, so the
+// contexts register themselves here.
+std::mutex g_ctx_mu;
+std::set<gsort_ctx *> g_ctxs;
+gsort_status check_all_guards(gsort_ctx *c, const char *where);
+
+// Every HIP call of the runtime goes through hip_op (GSORT_SERIAL: serialized + device-synced,
+// then with GSORT_CANARY the guards of all contexts are checked after the call).
 #define HIP_TRY(ctx, expr)                                                                   \
     do {                                                                                     \
-        hipError_t e_ = (expr);                                                              \
+        if (trace_mode()) trace_op((ctx)->rank, #expr);                                      \
+        hipError_t e_ = hip_op([&]() -> hipError_t { return (expr); });                      \
+        if (e_ != hipSuccess && trace_mode()) trace_dump(#expr);                             \
+        if (e_ != hipSuccess) fault_info(ctx, #expr);                                        \
         if (e_ != hipSuccess)                                                                \
-            return set_err(ctx, GSORT_EHIP,                                                  \
-                           std::string(#expr) + ": " + hipGetErrorString(e_));              \
+            return set_err(ctx, GSORT_EHIP, std::string(#expr) + ": " +                      \
+                                                hipGetErrorString(e_) + " (rank " +          \
+                                                std::to_string((ctx)->rank) + ")");         \
+        if (serial_mode() && canary_mode()) {                                                \
+            gsort_status g_ = check_all_guards(ctx, #expr);                                  \
+            if (g_ != GSORT_OK) return g_;                                                   \
+        }                                                                                    \
     } while (0)
 
 #define ST_TRY(expr)                         \
@@ -110,12 +133,109 @@ gsort_status set_err(gsort_ctx *c, gsort_status st, const std::string &msg) {
     } while (0)
 
 gsort_status comm_try(gsort_ctx *c, gsort_status st) {
-    if (st != GSORT_OK) c->err = c->comm->err;
+    if (st != GSORT_OK) c->err = c->comm->err + " (rank " + std::to_string(c->rank) + ")";
     return st;
 }
 
 // GSORT_ALLOC_LIMIT=bytes (diagnostics): refuse any larger scratch allocation, naming the buffer
 std::string buf_name(gsort_ctx *c, const DevBuf &b);
+
+// Device allocation of `want` usable bytes (+ guards with GSORT_CANARY).  Returns the HIP error.
+// With GSORT_CANARY every change of a buffer happens under serial_mutex, so the guard checks
+// of other threads never see a half-updated DevBuf.
+hipError_t dev_malloc(DevBuf &b, size_t want) {
+    if (!canary_mode()) {
+        b.p = b.base = nullptr;
+        b.cap = 0;
+        hipError_t e = hip_op([&] { return hipMalloc(&b.base, want); });
+        if (e != hipSuccess) { b.base = nullptr; return e; }
+        b.p = b.base;
+        b.cap = want;
+        return hipSuccess;
+    }
+    std::lock_guard<std::mutex> lk(serial_mutex());
+    void *base = nullptr;
+    hipError_t e = hipMalloc(&base, want + 2 * kGuardBytes);
+    if (e != hipSuccess) return e;
+    char *g = static_cast<char *>(base);
+    e = hipMemset(g, kGuardByte, kGuardBytes);
+    if (e == hipSuccess) e = hipMemset(g + kGuardBytes + want, kGuardByte, kGuardBytes);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e != hipSuccess) { (void)hipFree(base); return e; }
+    b.base = base;
+    b.p = g + kGuardBytes;
+    b.cap = want;
+    return hipSuccess;
+}
+
+// GSORT_FAULTINFO=1: the last kFreedRing freed device ranges, printed with every live buffer
+// when the first HIP error is seen (where a faulting address lands: past a live buffer, in a
+// freed one, or elsewhere)
+constexpr size_t kFreedRing = 512;
+std::mutex g_freed_mu;
+std::vector<std::pair<uintptr_t, size_t>> g_freed(kFreedRing);
+size_t g_freed_n = 0;
+bool faultinfo_mode() {
+    static const bool on = getenv("GSORT_FAULTINFO") && atoi(getenv("GSORT_FAULTINFO"));
+    return on;
+}
+
+hipError_t dev_free(DevBuf &b) {
+    if (faultinfo_mode() && b.base) {
+        std::lock_guard<std::mutex> lk(g_freed_mu);
+        g_freed[g_freed_n++ % kFreedRing] = {(uintptr_t)b.p, b.cap};
+    }
+    hipError_t e = hipSuccess;
+    if (canary_mode()) {
+        std::lock_guard<std::mutex> lk(serial_mutex());
+        if (b.base) e = hipFree(b.base);
+        b.p = b.base = nullptr;
+        b.cap = 0;
+        return e;
+    }
+    if (b.base) e = hip_op([&] { return hipFree(b.base); });
+    b.p = b.base = nullptr;
+    b.cap = 0;
+    return e;
+}
+
+void for_each_buf_fwd(gsort_ctx *c, void (*f)(void *, const std::string &, DevBuf &), void *u);
+
+// GSORT_FAULTINFO: print every live buffer of every context and the recently freed ranges
+void fault_info(gsort_ctx *c, const std::string &what) {
+    if (!faultinfo_mode()) return;
+    static std::atomic<bool> done{false};
+    if (done.exchange(true)) return;
+    fprintf(stderr, "GSORT_FAULTINFO: first HIP error (rank %d): %s\n", c->rank, what.c_str());
+    std::lock_guard<std::mutex> lk(g_ctx_mu);
+    for (gsort_ctx *o : g_ctxs)
+        for_each_buf_fwd(o, [](void *u, const std::string &nm, DevBuf &b) {
+            if (b.p)
+                fprintf(stderr, "  live r%d %-10s [%#zx, %#zx) %zu B\n",
+                        static_cast<gsort_ctx *>(u)->rank, nm.c_str(), (size_t)(uintptr_t)b.p,
+                        (size_t)((uintptr_t)b.p + b.cap), b.cap);
+        }, o);
+    std::lock_guard<std::mutex> lk2(g_freed_mu);
+    const size_t m = std::min(g_freed_n, kFreedRing);
+    for (size_t i = g_freed_n - m; i < g_freed_n; ++i) {
+        const auto &f = g_freed[i % kFreedRing];
+        fprintf(stderr, "  freed #%zu [%#zx, %#zx) %zu B\n", i, (size_t)f.first,
+                (size_t)(f.first + f.second), f.second);
+    }
+    fflush(stderr);
+}
+
+// An allocation failure is GSORT_ENOMEM only when HIP says out-of-memory: after an earlier
+// asynchronous kernel fault every hipMalloc fails with that sticky error, which must surface
+// as what it is (GSORT_EHIP + the HIP message), not as a bogus out-of-memory.
+gsort_status alloc_err(gsort_ctx *c, hipError_t e, size_t want, const std::string &what) {
+    (void)hipGetLastError();
+    if (trace_mode()) trace_dump("hipMalloc failed");
+    const std::string msg = "hipMalloc of " + std::to_string(want) + " bytes for " + what +
+                            " (rank " + std::to_string(c->rank) + "): " + hipGetErrorString(e);
+    if (e != hipErrorOutOfMemory) fault_info(c, msg);
+    return set_err(c, e == hipErrorOutOfMemory ? GSORT_ENOMEM : GSORT_EHIP, msg);
+}
 
 gsort_status ensure(gsort_ctx *c, DevBuf &b, size_t bytes) {
     if (bytes <= b.cap) return GSORT_OK;
@@ -126,16 +246,13 @@ gsort_status ensure(gsort_ctx *c, DevBuf &b, size_t bytes) {
                                             " bytes for " + buf_name(c, b) +
                                             " over GSORT_ALLOC_LIMIT (rank " +
                                             std::to_string(c->rank) + ")");
-    if (b.p) HIP_TRY(c, hipFree(b.p));
-    b.p = nullptr;
-    b.cap = 0;
+    hipError_t e = dev_free(b);
+    if (e != hipSuccess)
+        return set_err(c, GSORT_EHIP, "hipFree of " + buf_name(c, b) + " (rank " +
+                                          std::to_string(c->rank) + "): " + hipGetErrorString(e));
     const size_t want = (bytes + 4095) & ~size_t(4095);
-    if (hipMalloc(&b.p, want) != hipSuccess) {
-        (void)hipGetLastError();
-        b.p = nullptr;
-        return set_err(c, GSORT_ENOMEM, "hipMalloc of " + std::to_string(want) + " bytes failed");
-    }
-    b.cap = want;
+    e = dev_malloc(b, want);
+    if (e != hipSuccess) return alloc_err(c, e, want, buf_name(c, b));
     return GSORT_OK;
 }
 
@@ -278,24 +395,77 @@ gsort_status ensure_list(gsort_ctx *c, DevBuf &b, uint64_t entries) {
     return ensure(c, b, (size_t)std::max<uint64_t>(entries, 1) * 16);
 }
 
-std::string buf_name(gsort_ctx *c, const DevBuf &b) {
-    const std::pair<const char *, const DevBuf *> named[] = {
+// Every device buffer a context owns, with its name (teardown, diagnostics).
+template <class F>
+void for_each_buf(gsort_ctx *c, F &&f) {
+    const std::pair<const char *, DevBuf *> named[] = {
         {"tcounts", &c->tcounts}, {"gsum", &c->gsum}, {"m_tpfx", &c->m_tpfx},
         {"m_gpfx", &c->m_gpfx}, {"m_segmap", &c->m_segmap}, {"m_groupmap", &c->m_groupmap},
         {"m_cstart", &c->m_cstart}, {"m_next0", &c->m_next[0]}, {"m_next1", &c->m_next[1]},
         {"m_part", &c->m_part}, {"m_fix", &c->m_fix}, {"m_cur", &c->m_cur},
         {"m_split", &c->m_split}, {"m_rpos", &c->m_rpos}, {"m_bsize", &c->m_bsize},
         {"m_bseg", &c->m_bseg}, {"m_blist", &c->m_blist}, {"m_gb", &c->m_gb},
-        {"m_pack", &c->m_pack}, {"m_meta", &c->m_meta}, {"m_g16", &c->m_g16}};
-    for (const auto &nb : named)
-        if (nb.second == &b) return nb.first;
-    for (int i = 0; i < S_NSLOTS; ++i)
-        if (&c->slot[i] == &b) return "slot" + std::to_string(i);
+        {"m_pack", &c->m_pack}, {"m_meta", &c->m_meta}, {"m_g16", &c->m_g16},
+        {"small", &c->small}};
+    for (const auto &nb : named) f(std::string(nb.first), *nb.second);
+    static const char *slot_names[S_NSLOTS] = {"S_TMP",  "S_OUT", "S_CUR",  "S_SORTED",
+                                               "S_RECV", "S_IN",  "S_STAGE"};
+    for (int i = 0; i < S_NSLOTS; ++i) f(std::string(slot_names[i]), c->slot[i]);
     for (int k = 0; k < kLocalClasses; ++k) {
-        if (&c->m_local[k] == &b) return "m_local" + std::to_string(k);
-        if (&c->m_local3[k] == &b) return "m_local3_" + std::to_string(k);
+        f("m_local" + std::to_string(k), c->m_local[k]);
+        f("m_local3_" + std::to_string(k), c->m_local3[k]);
     }
-    return "?";
+    for (auto &ub : c->user_bufs) f(std::string("user"), ub.second);
+}
+
+void for_each_buf_fwd(gsort_ctx *c, void (*f)(void *, const std::string &, DevBuf &), void *u) {
+    for_each_buf(c, [&](const std::string &nm, DevBuf &b) { f(u, nm, b); });
+}
+
+std::string buf_name(gsort_ctx *c, const DevBuf &b) {
+    std::string name = "?";
+    for_each_buf(c, [&](const std::string &nm, DevBuf &x) { if (&x == &b) name = nm; });
+    return name;
+}
+
+// GSORT_CANARY: read back both guards of every buffer of every live context; the first
+// overwritten byte fails the call with the buffer, the offset and the operation just run.
+gsort_status check_ctx_guards(gsort_ctx *owner, gsort_ctx *c, const char *where) {
+    std::vector<unsigned char> h(kGuardBytes);
+    gsort_status st = GSORT_OK;
+    for_each_buf(c, [&](const std::string &nm, DevBuf &b) {
+        if (st != GSORT_OK || !b.base) return;
+        for (int side = 0; side < 2 && st == GSORT_OK; ++side) {
+            const char *g = static_cast<const char *>(b.base) +
+                            (side ? kGuardBytes + b.cap : 0);
+            if (hipMemcpy(h.data(), g, kGuardBytes, hipMemcpyDeviceToHost) != hipSuccess) {
+                st = set_err(owner, GSORT_EHIP, "GSORT_CANARY: guard read failed");
+                return;
+            }
+            for (size_t i = 0; i < kGuardBytes; ++i)
+                if (h[i] != kGuardByte) {
+                    const long long off = side ? (long long)(b.cap + i)
+                                               : -(long long)(kGuardBytes - i);
+                    st = set_err(owner, GSORT_EINVAL,
+                                 "GSORT_CANARY: rank " + std::to_string(c->rank) + " buffer " + nm +
+                                     " (" + std::to_string(b.cap) + " bytes) overwritten at byte " +
+                                     std::to_string(off) + " after " + where + " (called by rank " +
+                                     std::to_string(owner->rank) + ")");
+                    return;
+                }
+        }
+    });
+    return st;
+}
+
+gsort_status check_all_guards(gsort_ctx *c, const char *where) {
+    if (!canary_mode()) return GSORT_OK;
+    std::lock_guard<std::mutex> lk(serial_mutex());
+    if (hipDeviceSynchronize() != hipSuccess)
+        return set_err(c, GSORT_EHIP, std::string("GSORT_CANARY: device fault before ") + where);
+    std::lock_guard<std::mutex> lk2(g_ctx_mu);
+    for (gsort_ctx *o : g_ctxs) ST_TRY(check_ctx_guards(c, o, where));
+    return GSORT_OK;
 }
 
 // GSORT_CHECK=1 (diagnostics): host-side invariant checks between the distributed phases, so
@@ -1260,11 +1430,17 @@ gsort_status create_common(gsort_ctx *c, int hip_device) {
     c->device = hip_device;
     HIP_TRY(c, hipSetDevice(hip_device));
     HIP_TRY(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    HIP_TRY(c, hipMalloc(&c->d_small, kSmallBytes));
+    ST_TRY(ensure(c, c->small, kSmallBytes));
+    c->d_small = static_cast<char *>(c->small.p);
     HIP_TRY(c, hipHostMalloc(&c->h_small, kSmallBytes, hipHostMallocDefault));
-    HIP_TRY(c, hipMemset(c->d_small, 0, kSmallBytes));
+    HIP_TRY(c, hipMemsetAsync(c->d_small, 0, kSmallBytes, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
     HIP_TRY(c, hipEventCreateWithFlags(&c->ev_ctr, hipEventDisableTiming));
     if (const char *e = getenv("GSORT_PLAN16")) c->plan16 = atoi(e) != 0;
+    {
+        std::lock_guard<std::mutex> lk(g_ctx_mu);
+        g_ctxs.insert(c);
+    }
     return check_lds_order(c);
 }
 
@@ -1359,27 +1535,20 @@ gsort_status gsort_create_in_group(gsort_ctx **ctx, gsort_group *grp, int rank, 
 gsort_status gsort_destroy(gsort_ctx *c) {
     if (!c) return GSORT_EINVAL;
     // teardown: errors are not actionable here, so every status is deliberately dropped
+    {
+        std::lock_guard<std::mutex> lk(g_ctx_mu);
+        g_ctxs.erase(c);
+    }
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     delete c->comm;
-    for (auto &b : c->slot) if (b.p) (void)hipFree(b.p);
-    if (c->tcounts.p) (void)hipFree(c->tcounts.p);
-    if (c->gsum.p) (void)hipFree(c->gsum.p);
-    for (DevBuf *b : {&c->m_tpfx, &c->m_gpfx, &c->m_segmap, &c->m_groupmap, &c->m_cstart,
-                      &c->m_next[0], &c->m_next[1], &c->m_split, &c->m_rpos, &c->m_bsize,
-                      &c->m_bseg, &c->m_blist, &c->m_gb, &c->m_pack, &c->m_meta,
-                      &c->m_g16, &c->m_part, &c->m_fix, &c->m_cur})
-        if (b->p) (void)hipFree(b->p);
-    for (auto &b : c->m_local)
-        if (b.p) (void)hipFree(b.p);
-    for (auto &b : c->m_local3)
-        if (b.p) (void)hipFree(b.p);
+    for_each_buf(c, [](const std::string &, DevBuf &b) { (void)dev_free(b); });
+    c->d_small = nullptr;
     if (c->ev_ctr) (void)hipEventDestroy(c->ev_ctr);
     for (int b = 0; b < 4; ++b) {
         if (c->h_stage[b]) (void)hipHostFree(c->h_stage[b]);
         if (c->ev_stage[b]) (void)hipEventDestroy(c->ev_stage[b]);
     }
-    if (c->d_small) (void)hipFree(c->d_small);
     if (c->h_small) (void)hipHostFree(c->h_small);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1444,6 +1613,7 @@ gsort_status gsort_radix(gsort_ctx *c, const int32_t *d_keys, size_t n_local, in
     *n_out = nout;
     if (stats) { stats->keys_local_in = n_local; stats->keys_local_out = nout; }
     timing_finish(c, stats);
+    if (canary_mode()) ST_TRY(check_all_guards(c, __func__));
     return GSORT_OK;
 }
 
@@ -1477,6 +1647,7 @@ gsort_status gsort_sample(gsort_ctx *c, const int32_t *d_keys, size_t n_local, i
     *n_out = nout;
     if (stats) { stats->keys_local_in = n_local; stats->keys_local_out = nout; }
     timing_finish(c, stats);
+    if (canary_mode()) ST_TRY(check_all_guards(c, __func__));
     return GSORT_OK;
 }
 
@@ -1685,17 +1856,35 @@ gsort_status gsort_device_alloc(gsort_ctx *c, size_t bytes, void **d_ptr) {
     ST_TRY(check_ctx(c));
     if (!d_ptr) return GSORT_EINVAL;
     HIP_TRY(c, hipSetDevice(c->device));
-    if (hipMalloc(d_ptr, std::max<size_t>(bytes, 4)) != hipSuccess) {
-        (void)hipGetLastError();
-        return set_err(c, GSORT_ENOMEM, "hipMalloc failed");
+    DevBuf b;
+    const size_t want = (std::max<size_t>(bytes, 4) + 255) & ~size_t(255);
+    hipError_t e = dev_malloc(b, want);
+    if (e != hipSuccess) return alloc_err(c, e, want, "gsort_device_alloc");
+    {
+        std::unique_lock<std::mutex> lk(serial_mutex(), std::defer_lock);
+        if (canary_mode()) lk.lock();
+        c->user_bufs[b.p] = b;
     }
+    *d_ptr = b.p;
     return GSORT_OK;
 }
 
 gsort_status gsort_device_free(gsort_ctx *c, void *d_ptr) {
     ST_TRY(check_ctx(c));
     HIP_TRY(c, hipSetDevice(c->device));
-    if (d_ptr) HIP_TRY(c, hipFree(d_ptr));
+    if (!d_ptr) return GSORT_OK;
+    auto it = c->user_bufs.find(d_ptr);
+    if (it == c->user_bufs.end())
+        return set_err(c, GSORT_EINVAL, "gsort_device_free: not a gsort_device_alloc pointer");
+    DevBuf b = it->second;
+    {
+        std::unique_lock<std::mutex> lk(serial_mutex(), std::defer_lock);
+        if (canary_mode()) lk.lock();
+        c->user_bufs.erase(it);
+    }
+    hipError_t e = dev_free(b);
+    if (e != hipSuccess)
+        return set_err(c, GSORT_EHIP, std::string("hipFree: ") + hipGetErrorString(e));
     return GSORT_OK;
 }
 

@@ -84,3 +84,66 @@ extern "C" long long gsort_parse_text(const char *buf, size_t len, int32_t *out,
     for (auto &x : th) x.join();
     return (long long)off[threads];
 }
+
+// ---- debug dump printer -------------------------------------------------
+// The reference's full sorted dump is a serial printf("%u|%u\n", i, int_buf[i]) loop on rank 0
+// (mpi_radix_sort.c:198-200, mpi_sample_sort.c:202-204).  gsort_format_dump renders the same
+// bytes ("%llu|%u\n": the index, then the key as unsigned) for keys[0 .. n) with indices from
+// first_index, on several threads: each chunk's length is known from the digit counts, so the
+// chunks are sized, prefix-summed and written in place.
+namespace {
+
+inline unsigned ndigits(unsigned long long v) {
+    unsigned d = 1;
+    while (v >= 10) { v /= 10; ++d; }
+    return d;
+}
+
+inline char *put_u(char *p, unsigned long long v, unsigned nd) {
+    char *e = p + nd;
+    do { *--e = (char)('0' + v % 10); v /= 10; } while (v);
+    return p + nd;
+}
+
+size_t dump_len(const int32_t *keys, size_t a, size_t b, uint64_t first) {
+    size_t len = 0;
+    for (size_t i = a; i < b; ++i)
+        len += ndigits(first + i) + ndigits((uint32_t)keys[i]) + 2;
+    return len;
+}
+
+void dump_write(const int32_t *keys, size_t a, size_t b, uint64_t first, char *p) {
+    for (size_t i = a; i < b; ++i) {
+        const unsigned long long idx = first + i;
+        const uint32_t v = (uint32_t)keys[i];
+        p = put_u(p, idx, ndigits(idx));
+        *p++ = '|';
+        p = put_u(p, v, ndigits(v));
+        *p++ = '\n';
+    }
+}
+
+}  // namespace
+
+extern "C" long long gsort_format_dump(const int32_t *keys, size_t n, uint64_t first_index,
+                                       char *out, size_t cap, int threads) {
+    if (n && !keys) return -1;
+    if (threads < 1) threads = 1;
+    if (n < 65536) threads = 1;
+    std::vector<size_t> cut(threads + 1), len(threads), off(threads + 1, 0);
+    for (int t = 0; t <= threads; ++t) cut[t] = n / threads * t + std::min<size_t>(t, n % threads);
+    std::vector<std::thread> th;
+    for (int t = 1; t < threads; ++t)
+        th.emplace_back([&, t] { len[t] = dump_len(keys, cut[t], cut[t + 1], first_index); });
+    len[0] = dump_len(keys, cut[0], cut[1], first_index);
+    for (auto &x : th) x.join();
+    th.clear();
+    for (int t = 0; t < threads; ++t) off[t + 1] = off[t] + len[t];
+    if (!out) return (long long)off[threads];
+    if (cap < off[threads]) return -1;
+    for (int t = 1; t < threads; ++t)
+        th.emplace_back([&, t] { dump_write(keys, cut[t], cut[t + 1], first_index, out + off[t]); });
+    dump_write(keys, cut[0], cut[1], first_index, out);
+    for (auto &x : th) x.join();
+    return (long long)off[threads];
+}

@@ -75,6 +75,7 @@ EXPORTS = [
     "gsort_fingerprint", "gsort_device_alloc", "gsort_device_free", "gsort_copy_to_host",
     "gsort_copy_to_device", "gsort_onesweep_tile", "gsort_plan_radix_route",
     "gsort_plan_splitters", "gsort_plan_split", "gsort_plan_split_balanced", "gsort_parse_text",
+    "gsort_format_dump",
 ]
 
 _lib = None
@@ -126,6 +127,8 @@ def lib():
     L.gsort_set_sample_balanced.argtypes = [VP, I]
     L.gsort_parse_text.argtypes = [ctypes.c_char_p, SZ, VP, SZ, I]
     L.gsort_parse_text.restype = ctypes.c_longlong
+    L.gsort_format_dump.argtypes = [VP, SZ, U64, VP, SZ, I]
+    L.gsort_format_dump.restype = ctypes.c_longlong
     _lib = L
     return L
 
@@ -330,3 +333,14 @@ def parse_text(data, threads=1):
     n2 = lib().gsort_parse_text(data, len(data), out.ctypes.data, n, threads)
     assert n2 == n
     return out[:n]
+
+
+def format_dump(keys, first_index=0, threads=1):
+    """gsort_format_dump: the reference's "%u|%u" sorted dump lines for keys (bytes)."""
+    import numpy as np
+    keys = np.ascontiguousarray(keys, dtype=np.int32)
+    n = lib().gsort_format_dump(keys.ctypes.data, keys.size, first_index, None, 0, threads)
+    buf = ctypes.create_string_buffer(max(n, 1))
+    m = lib().gsort_format_dump(keys.ctypes.data, keys.size, first_index, buf, n, threads)
+    assert m == n
+    return buf.raw[:n]

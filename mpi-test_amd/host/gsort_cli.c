@@ -68,6 +68,24 @@ static int32_t *read_keys(const char *file, size_t *n_out)
     return keys;
 }
 
+/* the full sorted dump (radix:198-200, sample:202-204) in blocks of kDumpBlock keys, each
+ * rendered on 16 threads by gsort_format_dump and written with one fwrite */
+static void print_dump(const int32_t *keys, unsigned long long n)
+{
+    enum { kDumpBlock = 1 << 21, kMaxLine = 32 };
+    char *buf = malloc((size_t)kDumpBlock * kMaxLine);
+    if (!buf) die("print_dump: out of host memory");
+    fflush(stdout);
+    for (unsigned long long a = 0; a < n; a += kDumpBlock) {
+        const size_t m = n - a < kDumpBlock ? (size_t)(n - a) : (size_t)kDumpBlock;
+        const long long len =
+            gsort_format_dump(keys + a, m, a, buf, (size_t)kDumpBlock * kMaxLine, 16);
+        if (len < 0 || fwrite(buf, 1, (size_t)len, stdout) != (size_t)len)
+            die("print_dump: write failed");
+    }
+    free(buf);
+}
+
 static int local_rank(int rank)
 {
     const char *vars[] = {"MPI_LOCALRANKID", "OMPI_COMM_WORLD_LOCAL_RANK", "LOCAL_RANK"};
@@ -155,12 +173,8 @@ int gsort_cli_main(int argc, char **argv, int algo)
     check(gsort_gather_to_root(ctx, d_out, n_out, int_buf), ctx, "gsort_gather_to_root");
     if (rank == 0) {
         const double end = MPI_Wtime();
-        if ((algo == CLI_RADIX && debug > 2) || (algo == CLI_SAMPLE && debug)) {
-            static char obuf[1 << 20];
-            setvbuf(stdout, obuf, _IOFBF, sizeof obuf);
-            for (unsigned long long i = 0; i < n_total; i++)
-                printf("%llu|%u\n", i, (unsigned)int_buf[i]);
-        }
+        if ((algo == CLI_RADIX && debug > 2) || (algo == CLI_SAMPLE && debug))
+            print_dump(int_buf, n_total);
         /* index N/2-1 (radix:201); N = 1 would read int_buf[-1] in the reference (Q14) */
         const long long med = n_total >= 2 ? (long long)(n_total / 2) - 1 : 0;
         printf("The n/2-th sorted element: %d\n", int_buf[med]);

@@ -148,6 +148,19 @@ def test_text_parser_parallel_large(gsort, orc):
     assert np.array_equal(gsort.parse_text(text, threads=8), keys)
 
 
+def test_dump_formatter_matches_printf(gsort, orc):
+    """gsort_format_dump (the CLIs' sorted dump) == the reference's
+    printf("%u|%u\n", i, int_buf[i]) lines (mpi_radix_sort.c:198-200), negatives as 2^32+v
+    (Q15), on one and many threads and from a nonzero first index (the CLI's blocks)."""
+    keys = np.concatenate([orc.gen(orc.UNIFORM, 4, 100000) - (1 << 30),
+                           np.array([0, -1, 2**31 - 1, -2**31, 9, 10, 99, 100], np.int32)])
+    for first in (0, 999_999_999_995):
+        want = "".join(f"{first + i}|{int(v) & 0xFFFFFFFF}\n" for i, v in enumerate(keys.tolist()))
+        for th in (1, 7, 16):
+            assert gsort.format_dump(keys, first, th) == want.encode(), (first, th)
+    assert gsort.format_dump(np.zeros(0, np.int32)) == b""
+
+
 def test_cli_contract_without_gpu(tmp_path):
     """argv / invalid-file handling happens before any GPU call."""
     import subprocess

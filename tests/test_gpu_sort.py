@@ -239,14 +239,23 @@ def run_group(gsort, blocks, algo, local="msd", balanced=False):
         except Exception as e:  # surface in the main thread
             errs.append((r, e))
 
-    th = [threading.Thread(target=worker, args=(r,)) for r in range(P)]
+    th = [threading.Thread(target=worker, args=(r,), daemon=True) for r in range(P)]
     for t in th:
         t.start()
     for t in th:
         t.join(timeout=600)
+    hung = [r for r, t in enumerate(th) if t.is_alive()]
+    if hung:
+        # a worker may still be inside a group collective: leak the group rather than free
+        # the state it is waiting on
+        pytest.fail(f"in-process group ranks {hung} did not finish within 600 s")
     grp.close()
     if errs:
+        if len(errs) > 1:  # every rank's failure, in the order they happened
+            print("\n".join(f"rank {r}: {e}" for r, e in errs))
         raise errs[0][1]
+    missing = [r for r in range(P) if res[r] is None]
+    assert not missing, f"ranks {missing} returned no result"
     return res
 
 

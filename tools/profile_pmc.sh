@@ -20,5 +20,5 @@ run fetch --pmc FETCH_SIZE
 run write --pmc WRITE_SIZE
 run sq --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS
 run clk --pmc GRBM_GUI_ACTIVE GRBM_COUNT
-python3 mpi-test_amd/tools/pmc_summary.py "$OUT" > "$OUT/summary.json"
+python3 tools/pmc_summary.py "$OUT" > "$OUT/summary.json"
 echo "profile $TAG done"
