@@ -489,6 +489,23 @@ __global__ __launch_bounds__(64) void k_bucket_bounds(const int32_t *__restrict_
     if (lane == 0) bounds[j] = lo + (uint64_t)__popcll(m);
 }
 
+// Streaming copy ceiling (bench reference, not on the sort path): 16 B per lane, four loads in
+// flight per thread, grid-strided.  What a read + write pass over HBM can reach on this GPU
+// (MI355X_MICROARCH.md: 6.29 TB/s for a float4 copy).
+__global__ __launch_bounds__(256) void k_stream_copy(const uint4 *__restrict__ in,
+                                                     uint4 *__restrict__ out, uint64_t n16) {
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    for (; i + 3 * stride < n16; i += 4 * stride) {
+        const uint4 a = in[i], b = in[i + stride], c = in[i + 2 * stride], d = in[i + 3 * stride];
+        out[i] = a;
+        out[i + stride] = b;
+        out[i + 2 * stride] = c;
+        out[i + 3 * stride] = d;
+    }
+    for (; i < n16; i += stride) out[i] = in[i];
+}
+
 __global__ void k_copy(const uint32_t *__restrict__ in, uint32_t *__restrict__ out, uint64_t n) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
@@ -921,22 +938,32 @@ __global__ __launch_bounds__(BLOCK) void k_counts_h16(const uint32_t *__restrict
     const uint32_t tid = threadIdx.x;
     for (uint32_t i = tid; i < kWords; i += BLOCK) s_h[i] = 0;
     if (tid < kRadix) s_t[tid] = 0;
-    const uint64_t ntiles = (n + kSweepTile - 1) / kSweepTile;
+    // Tile lengths in 32-bit scalar arithmetic: every tile but the last is full.  (The form
+    // min(n - t0, kSweepTile) on u64 was miscompiled for gfx950 by ROCm 7.2's backend: the
+    // uniform 64-bit compare lives in VCC, the SCC copy that the length's s_cselect needs was
+    // dropped in front of the s_cbranch_vccz, and the select read the carry of an address add
+    // -- so the first, partial tile loaded a full 8192 keys, up to 32 KiB past the input.
+    // tests/test_cpu_library.py::test_kernels_isa_scc_hazard checks every kernel for it.)
+    const uint32_t ntiles = (uint32_t)((n + kSweepTile - 1) / kSweepTile);
+    const uint32_t last_len = (uint32_t)(n - (uint64_t)(ntiles - 1) * kSweepTile);
+    auto tile_len = [&](uint32_t t) -> uint32_t {
+        return t == ntiles - 1 ? last_len : (uint32_t)kSweepTile;
+    };
     uint32_t k[ITEMS];
     if (blockIdx.x < ntiles) {
-        const uint64_t t0 = (uint64_t)blockIdx.x * kSweepTile;
-        const uint32_t len = (uint32_t)min(n - t0, (uint64_t)kSweepTile);
-        load_tile<BLOCK, ITEMS, FIN>(in + t0 + tid, len == (uint32_t)kSweepTile, len, k);
+        const uint32_t len = tile_len(blockIdx.x);
+        load_tile<BLOCK, ITEMS, FIN>(in + (uint64_t)blockIdx.x * kSweepTile + tid,
+                                     len == (uint32_t)kSweepTile, len, k);
     }
-    for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         __syncthreads();  // zeroing / the previous tile's count store done
-        const uint32_t len = (uint32_t)min(n - t * kSweepTile, (uint64_t)kSweepTile);
-        const uint64_t tn = t + gridDim.x;
+        const uint32_t len = tile_len(t);
+        const uint32_t tn = t + gridDim.x;
         uint32_t kn[ITEMS];
         if (tn < ntiles) {
-            const uint64_t t0 = tn * kSweepTile;
-            const uint32_t lenn = (uint32_t)min(n - t0, (uint64_t)kSweepTile);
-            load_tile<BLOCK, ITEMS, FIN>(in + t0 + tid, lenn == (uint32_t)kSweepTile, lenn, kn);
+            const uint32_t lenn = tile_len(tn);
+            load_tile<BLOCK, ITEMS, FIN>(in + (uint64_t)tn * kSweepTile + tid,
+                                         lenn == (uint32_t)kSweepTile, lenn, kn);
         }
         // all 8 returning atomics in flight before the first wrap test (measured: a test per
         // atomic waits out each LDS round trip, 0.31 vs 0.30 ms at 2^28)
@@ -966,7 +993,7 @@ __global__ __launch_bounds__(BLOCK) void k_counts_h16(const uint32_t *__restrict
         }
         __syncthreads();
         if (tid < kRadix) {
-            tcounts[t * kRadix + tid] = s_t[tid];
+            tcounts[(uint64_t)t * kRadix + tid] = s_t[tid];
             s_t[tid] = 0;
         }
 #pragma unroll
@@ -2208,6 +2235,16 @@ hipError_t launch_lds_order_check(const uint32_t *digits, uint32_t nblocks, uint
                                   uint64_t *bad, hipStream_t s) {
     k_lds_order_check<<<nblocks, 512, 0, s>>>(digits, nbins,
                                               reinterpret_cast<unsigned long long *>(bad));
+    return hipGetLastError();
+}
+
+hipError_t launch_stream_copy(const void *in, void *out, uint64_t bytes, unsigned grid,
+                              hipStream_t s) {
+    if (bytes == 0) return hipSuccess;
+    if (bytes % 16 || (reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) % 16)
+        return hipErrorInvalidValue;
+    k_stream_copy<<<grid, 256, 0, s>>>(static_cast<const uint4 *>(in), static_cast<uint4 *>(out),
+                                       bytes / 16);
     return hipGetLastError();
 }
 

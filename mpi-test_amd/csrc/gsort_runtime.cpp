@@ -42,6 +42,9 @@ struct DevBuf {
     void *p = nullptr;     // what the kernels use
     size_t cap = 0;        // usable bytes at p
     void *base = nullptr;  // the allocation (p - kGuardBytes with GSORT_CANARY)
+    // GSORT_EFENCE: the reserved VA range [base, base + va_bytes) and its physical handle
+    size_t va_bytes = 0, map_bytes = 0;
+    hipMemGenericAllocationHandle_t handle{};
 };
 
 }  // namespace
@@ -141,9 +144,106 @@ gsort_status comm_try(gsort_ctx *c, gsort_status st) {
 std::string buf_name(gsort_ctx *c, const DevBuf &b);
 
 // Device allocation of `want` usable bytes (+ guards with GSORT_CANARY).  Returns the HIP error.
+// Allocation granularity (GSORT_ALLOC_ALIGN bytes, a power of two >= 4096).
+bool efence_mode();
+size_t alloc_align() {
+    if (efence_mode()) return 256;  // buffers end exactly (to 256 B) at the unmapped page
+    static const size_t a = [] {
+        const char *e = getenv("GSORT_ALLOC_ALIGN");
+        size_t v = e ? (size_t)strtoull(e, nullptr, 0) : 4096;
+        if (v < 4096 || (v & (v - 1))) v = 4096;
+        return v;
+    }();
+    return a;
+}
+
+// GSORT_EFENCE=1 (diagnostics): every buffer ends flush against an unmapped VA page (HIP VMM:
+// reserve a range with a free granule on each side, map physical memory only in the middle,
+// place the buffer at the end of the mapping), so any read or write past a buffer's end faults
+// at once; with GSORT_SERIAL the failing operation is then named.
+bool efence_mode() {
+    static const bool on = getenv("GSORT_EFENCE") && atoi(getenv("GSORT_EFENCE"));
+    return on;
+}
+
+hipError_t efence_malloc(DevBuf &b, size_t want) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    hipMemAllocationProp prop{};
+    prop.type = hipMemAllocationTypePinned;
+    prop.location.type = hipMemLocationTypeDevice;
+    prop.location.id = dev;
+    size_t gran = 0;
+    static const bool rec = getenv("GSORT_EFENCE_REC") && atoi(getenv("GSORT_EFENCE_REC"));
+    e = hipMemGetAllocationGranularity(&gran, &prop,
+                                       rec ? hipMemAllocationGranularityRecommended
+                                           : hipMemAllocationGranularityMinimum);
+    if (e != hipSuccess) return e;
+    static bool said = false;
+    if (!said) { said = true; fprintf(stderr, "GSORT_EFENCE: granularity %zu\n", gran); }
+    static const size_t slack = getenv("GSORT_EFENCE_SLACK")
+                                    ? (size_t)strtoull(getenv("GSORT_EFENCE_SLACK"), nullptr, 0)
+                                    : 0;
+    const size_t msize = (want + slack + gran - 1) / gran * gran, va_bytes = msize + 2 * gran;
+    void *va = nullptr;
+    e = hipMemAddressReserve(&va, va_bytes, gran, nullptr, 0);
+    if (e != hipSuccess) return e;
+    hipMemGenericAllocationHandle_t h{};
+    e = hipMemCreate(&h, msize, &prop, 0);
+    if (e != hipSuccess) { (void)hipMemAddressFree(va, va_bytes); return e; }
+    char *m = static_cast<char *>(va) + gran;
+    e = hipMemMap(m, msize, 0, h, 0);
+    if (e == hipSuccess) {
+        hipMemAccessDesc acc{};
+        acc.location.type = hipMemLocationTypeDevice;
+        acc.location.id = dev;
+        acc.flags = hipMemAccessFlagsProtReadWrite;
+        e = hipMemSetAccess(m, msize, &acc, 1);
+        if (e != hipSuccess) (void)hipMemUnmap(m, msize);
+    }
+    if (e != hipSuccess) {
+        (void)hipMemRelease(h);
+        (void)hipMemAddressFree(va, va_bytes);
+        return e;
+    }
+    b.base = va;
+    b.va_bytes = va_bytes;
+    b.map_bytes = msize;
+    b.handle = h;
+    b.p = m + msize - want - slack;  // the buffer ends at the unmapped granule (- slack)
+    b.cap = want;
+    return hipSuccess;
+}
+
+// The freed VA range stays reserved (never handed out again): re-mapping a just-unmapped range
+// to new physical pages gave wrong results on MI355X (a buffer grown mid-sort read stale
+// contents), an artifact of this diagnostic mode, not of the sort.  VA space is plentiful.
+hipError_t efence_free(DevBuf &b) {
+    char *m = static_cast<char *>(b.base) + (b.va_bytes - b.map_bytes) / 2;
+    hipError_t e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemUnmap(m, b.map_bytes);
+    if (e == hipSuccess) e = hipMemRelease(b.handle);
+    return e;
+}
+
 // With GSORT_CANARY every change of a buffer happens under serial_mutex, so the guard checks
 // of other threads never see a half-updated DevBuf.
-hipError_t dev_malloc(DevBuf &b, size_t want) {
+// GSORT_EFENCE_ONLY=name,name,...: fence only the named buffers (bisecting a fault)
+bool efence_for(const std::string &name) {
+    const char *only = getenv("GSORT_EFENCE_ONLY");
+    if (!only || !*only) return true;
+    const std::string list = std::string(",") + only + ",";
+    return list.find("," + name + ",") != std::string::npos;
+}
+
+hipError_t dev_malloc(DevBuf &b, size_t want, const std::string &name = "") {
+    if (efence_mode() && efence_for(name)) {
+        std::lock_guard<std::mutex> lk(serial_mutex());
+        b.p = b.base = nullptr;
+        b.cap = 0;
+        return efence_malloc(b, want);
+    }
     if (!canary_mode()) {
         b.p = b.base = nullptr;
         b.cap = 0;
@@ -186,6 +286,13 @@ hipError_t dev_free(DevBuf &b) {
         g_freed[g_freed_n++ % kFreedRing] = {(uintptr_t)b.p, b.cap};
     }
     hipError_t e = hipSuccess;
+    if (efence_mode() && b.va_bytes) {
+        std::lock_guard<std::mutex> lk(serial_mutex());
+        if (b.base) e = efence_free(b);
+        b.p = b.base = nullptr;
+        b.cap = b.va_bytes = b.map_bytes = 0;
+        return e;
+    }
     if (canary_mode()) {
         std::lock_guard<std::mutex> lk(serial_mutex());
         if (b.base) e = hipFree(b.base);
@@ -250,8 +357,8 @@ gsort_status ensure(gsort_ctx *c, DevBuf &b, size_t bytes) {
     if (e != hipSuccess)
         return set_err(c, GSORT_EHIP, "hipFree of " + buf_name(c, b) + " (rank " +
                                           std::to_string(c->rank) + "): " + hipGetErrorString(e));
-    const size_t want = (bytes + 4095) & ~size_t(4095);
-    e = dev_malloc(b, want);
+    const size_t want = (bytes + alloc_align() - 1) & ~(alloc_align() - 1);
+    e = dev_malloc(b, want, buf_name(c, b));
     if (e != hipSuccess) return alloc_err(c, e, want, buf_name(c, b));
     return GSORT_OK;
 }
@@ -1857,8 +1964,8 @@ gsort_status gsort_device_alloc(gsort_ctx *c, size_t bytes, void **d_ptr) {
     if (!d_ptr) return GSORT_EINVAL;
     HIP_TRY(c, hipSetDevice(c->device));
     DevBuf b;
-    const size_t want = (std::max<size_t>(bytes, 4) + 255) & ~size_t(255);
-    hipError_t e = dev_malloc(b, want);
+    const size_t want = (std::max<size_t>(bytes, 4) + alloc_align() - 1) & ~(alloc_align() - 1);
+    hipError_t e = dev_malloc(b, want, "user");
     if (e != hipSuccess) return alloc_err(c, e, want, "gsort_device_alloc");
     {
         std::unique_lock<std::mutex> lk(serial_mutex(), std::defer_lock);
@@ -1885,6 +1992,50 @@ gsort_status gsort_device_free(gsort_ctx *c, void *d_ptr) {
     hipError_t e = dev_free(b);
     if (e != hipSuccess)
         return set_err(c, GSORT_EHIP, std::string("hipFree: ") + hipGetErrorString(e));
+    return GSORT_OK;
+}
+
+gsort_status gsort_copy_ceiling(gsort_ctx *c, size_t bytes, int reps, double *ms,
+                                double *gbps) {
+    ST_TRY(check_ctx(c));
+    if (!ms || !gbps || reps < 1 || bytes < 16) return GSORT_EINVAL;
+    HIP_TRY(c, hipSetDevice(c->device));
+    bytes &= ~size_t(15);
+    DevBuf a, b;
+    hipError_t e = dev_malloc(a, bytes, "ceiling_src");
+    if (e != hipSuccess) return alloc_err(c, e, bytes, "gsort_copy_ceiling");
+    e = dev_malloc(b, bytes, "ceiling_dst");
+    if (e != hipSuccess) { (void)dev_free(a); return alloc_err(c, e, bytes, "gsort_copy_ceiling"); }
+    hipEvent_t e0 = next_event(c), e1 = nullptr;
+    if (e0) e1 = next_event(c);
+    gsort_status st = (e0 && e1) ? GSORT_OK : set_err(c, GSORT_EHIP, "hipEventCreate failed");
+    double best = 0.0;
+    auto run = [&]() -> gsort_status {
+        HIP_TRY(c, hipMemsetAsync(a.p, 0x5a, bytes, c->stream));
+        for (unsigned grid : {1024u, 2048u, 4096u, 8192u}) {  // best median over grid sizes
+            std::vector<float> t;
+            for (int r = 0; r <= reps; ++r) {  // r == 0: warm-up
+                HIP_TRY(c, hipEventRecord(e0, c->stream));
+                HIP_TRY(c, launch_stream_copy(a.p, b.p, bytes, grid, c->stream));
+                HIP_TRY(c, hipEventRecord(e1, c->stream));
+                HIP_TRY(c, hipEventSynchronize(e1));
+                float x = 0.f;
+                HIP_TRY(c, hipEventElapsedTime(&x, e0, e1));
+                if (r) t.push_back(x);
+            }
+            std::sort(t.begin(), t.end());
+            const double med = t[t.size() / 2];
+            if (best == 0.0 || med < best) best = med;
+        }
+        return GSORT_OK;
+    };
+    if (st == GSORT_OK) st = run();
+    c->ev_used = 0;
+    (void)dev_free(a);
+    (void)dev_free(b);
+    if (st != GSORT_OK) return st;
+    *ms = best;
+    *gbps = 2.0 * (double)bytes / (best * 1e-3) / 1e9;
     return GSORT_OK;
 }
 

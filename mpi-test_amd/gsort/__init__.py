@@ -75,7 +75,7 @@ EXPORTS = [
     "gsort_fingerprint", "gsort_device_alloc", "gsort_device_free", "gsort_copy_to_host",
     "gsort_copy_to_device", "gsort_onesweep_tile", "gsort_plan_radix_route",
     "gsort_plan_splitters", "gsort_plan_split", "gsort_plan_split_balanced", "gsort_parse_text",
-    "gsort_format_dump",
+    "gsort_format_dump", "gsort_copy_ceiling",
 ]
 
 _lib = None
@@ -120,6 +120,7 @@ def lib():
     L.gsort_device_free.argtypes = [VP, VP]
     L.gsort_copy_to_host.argtypes = [VP, VP, VP, SZ]
     L.gsort_copy_to_device.argtypes = [VP, VP, VP, SZ]
+    L.gsort_copy_ceiling.argtypes = [VP, SZ, I, P(ctypes.c_double), P(ctypes.c_double)]
     L.gsort_plan_radix_route.argtypes = [I, VP, U64, I, VP, VP, VP, P(SZ)]
     L.gsort_plan_splitters.argtypes = [I, VP, VP]
     L.gsort_plan_split.argtypes = [I, VP, VP, VP, I, VP, VP]
@@ -242,6 +243,13 @@ class Context:
 
     def free(self, p):
         self._c(lib().gsort_device_free(self.h, ctypes.c_void_p(p)))
+
+    def copy_ceiling(self, nbytes, reps=10):
+        """gsort_copy_ceiling: (ms, GB/s) of the in-library streaming copy of nbytes."""
+        ms, gbps = ctypes.c_double(), ctypes.c_double()
+        self._c(lib().gsort_copy_ceiling(self.h, nbytes, reps, ctypes.byref(ms),
+                                         ctypes.byref(gbps)))
+        return ms.value, gbps.value
 
     def to_host(self, d_ptr, n):
         import numpy as np

@@ -245,3 +245,14 @@ def test_plan_split_balanced_sample_buckets(gsort, kind):
                 if int(le[:, q - 1].sum()) - int(lt[:, q - 1].sum()) == 1:
                     for p in range(P):
                         assert cut[p][q] == int(le[p, q - 1]) or cut[p][q] == n_all[p]
+
+
+def test_kernels_isa_scc_hazard():
+    """The gfx950 code object has no SCC consumer fed by an arithmetic SCC writer: the ROCm 7.2
+    miscompile that made K1h read up to 32 KiB past its input (tools/isa_scc_check.py; K1h
+    now computes tile lengths in 32-bit scalar arithmetic).  Disassembles the built library."""
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "isa_scc_check.py")],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]

@@ -208,19 +208,9 @@ def test_fingerprint_matches_oracle(ctx, orc):
 # ---------------------------------------------------------------------------------------
 # multi-rank on one GPU (in-process rank group)
 # ---------------------------------------------------------------------------------------
-# Known issue: late in a long GPU session, the 8-rank in-process group
-# (8 contexts on one GPU in one process) intermittently hit an oversized scratch allocation or an
-# illegal address in test_radix_multirank_balanced_blocks[8-msd]; the same test passed in a
-# fresh process and under GSORT_ALLOC_LIMIT.  Not isolated yet, so the 8-rank group cases run
-# only with GSORT_TEST_GROUP8=1 and cannot take the GPU down in the default suite.
-def group8_gate(P):
-    if P >= 8 and os.environ.get("GSORT_TEST_GROUP8") != "1":
-        pytest.skip("8-rank in-process group: set GSORT_TEST_GROUP8=1 (known intermittent issue)")
-
-
 def run_group(gsort, blocks, algo, local="msd", balanced=False):
+    """P ranks as P threads of this process, one context each, on one GPU."""
     P = len(blocks)
-    group8_gate(P)
     grp = gsort.Group(P)
     res, errs = [None] * P, []
 
