@@ -1038,6 +1038,12 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
     for (uint64_t v : n_all) N += v;
     uint64_t B, mine;
     block_of(N, P, me, &B, &mine);
+    // the packed exchange sends one u32 count per (destination, 16-bit bucket): every rank's
+    // block, and so every count, must stay below 2^32 keys (decided identically on all ranks)
+    for (int r = 0; r < P; ++r)
+        if (n_all[r] >= (1ull << 32))
+            return set_err(c, GSORT_EINVAL, "radix: a rank holds >= 2^32 keys (rank " +
+                                                std::to_string(r) + "); split the input further");
     const uint64_t cap = std::max<uint64_t>(std::max(n_in, mine), 1);
     ST_TRY(ensure(c, c->slot[S_TMP], cap * 4));
     ST_TRY(ensure(c, c->slot[S_RECV], std::max<uint64_t>(mine, 1) * 4));
