@@ -58,37 +58,106 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--local", choices=["msd", "lsd"], default="msd",
                     help="local sort algorithm (DESIGN.md 5)")
+    ap.add_argument("--spawn", action="store_true",
+                    help="launch the rank processes from this one even at --gpus 1 "
+                         "(without WORLD_SIZE in the environment, --gpus N > 1 always does)")
     return ap.parse_args()
+
+
+# ---------------------------------------------------------------------------------------
+# Self-launch: `python bench.py --gpus N` without a launcher starts N rank processes itself
+# (one per GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their environment), before this
+# process touches the GPU, and forwards rank 0's JSON line.  Under torch.distributed.run the
+# environment is already set and this is skipped.
+# ---------------------------------------------------------------------------------------
+def spawn_ranks(a):
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(a.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus),
+                   LOCAL_WORLD_SIZE=str(a.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env, stdout=subprocess.PIPE if r == 0 else sys.stderr))
+    line = procs[0].stdout.read().decode()
+    rc = 0
+    for p in procs:
+        rc = max(rc, p.wait())
+    sys.stdout.write(line)
+    sys.stdout.flush()
+    return rc
 
 
 # ---------------------------------------------------------------------------------------
 # CPU baseline: the reference itself, on the host cores, before any GPU work
 # ---------------------------------------------------------------------------------------
+def host_cpu():
+    """The box's CPU: model name and the logical CPUs this process may use."""
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count()
+    return {"cpu_model": model, "host_logical_cpus": os.cpu_count(), "usable_cpus": usable}
+
+
+def run_reference(prog, np_, path, mpirun):
+    """One reference program under mpirun; (program-timer seconds, wall seconds, stdout)."""
+    ref = os.path.join(ROOT, "oracle", "_ref", prog)
+    t0 = time.time()
+    r = subprocess.run([mpirun, "-np", str(np_), ref, path], capture_output=True, text=True,
+                       timeout=300)
+    wall = time.time() - t0
+    m = re.search(r"Endtime\(\)-Starttime\(\) = ([0-9.]+) sec", r.stderr)
+    if r.returncode != 0 or not m:
+        raise RuntimeError(f"{prog} rc={r.returncode}: {r.stderr[-300:]}")
+    return float(m.group(1)), wall, r.stdout.strip().splitlines()[-1]
+
+
 def cpu_baseline(dist, seed):
+    """The reference itself (oracle/_ref: radix_sort and sample_sort built unchanged from their
+    sources with their own flags, -O0) under mpirun -np 4 on BASELINE configs[0]'s 2^24 keys,
+    timed by their own stderr timers (mpi_radix_sort.c:98,197,203; mpi_sample_sort.c:61,201,
+    207), which exclude the text read.  The 2^28 point is not run by default: the survey
+    measured ref-radix at 2^28 (P=8) at 25.8 s plus a ~25 s text read, past the bench budget."""
     keys_log2, np_ = 24, 4  # BASELINE configs[0]: reference radix, mpirun -np 4, 2^24 keys
     n = 1 << keys_log2
-    ref = os.path.join(ROOT, "oracle", "_ref", "radix_sort")
     gen = os.path.join(PKG, "bin", "gen_keys")
     mpirun = shutil.which("mpirun") or "/opt/conda/bin/mpirun"
     tmp = tempfile.mkdtemp(prefix="gsort_cpu_")
+    host = host_cpu()
     try:
         path = os.path.join(tmp, "keys.txt")
         subprocess.run([gen, dist, str(n), str(seed), path], check=True)
-        if os.path.exists(ref) and os.path.exists(mpirun):
-            t0 = time.time()
-            r = subprocess.run([mpirun, "-np", str(np_), ref, path], capture_output=True,
-                               text=True, timeout=300)
-            wall = time.time() - t0
-            m = re.search(r"Endtime\(\)-Starttime\(\) = ([0-9.]+) sec", r.stderr)
-            if r.returncode == 0 and m:
-                t = float(m.group(1))
-                return {"value": n / t / 1e9, "unit": "GKeys/s", "cores": np_,
-                        "kind": "reference",
-                        "sample": f"reference radix_sort (oracle/_ref, -O0 as shipped) under "
-                                  f"mpirun -np {np_}, 2^{keys_log2} {dist} keys seed {seed}; "
-                                  f"program timer {t:.3f} s (excludes its text read), "
-                                  f"wall {wall:.1f} s",
-                        "median_line": r.stdout.strip().splitlines()[-1]}
+        if os.path.exists(os.path.join(ROOT, "oracle", "_ref", "radix_sort")) and \
+                os.path.exists(mpirun):
+            t, wall, med = run_reference("radix_sort", np_, path, mpirun)
+            out = {"value": n / t / 1e9, "unit": "GKeys/s", "cores": np_, "kind": "reference",
+                   "sample": f"reference radix_sort (oracle/_ref, -O0 as shipped) under "
+                             f"mpirun -np {np_} (one core per rank), 2^{keys_log2} {dist} keys "
+                             f"seed {seed}; program timer {t:.3f} s (excludes its text read), "
+                             f"wall {wall:.1f} s",
+                   "median_line": med, **host,
+                   "large_point": "2^28 not run by default (ref-radix 2^28 P=8: 25.8 s + "
+                                  "~25 s read, SURVEY.md 6); N >= 2^31: n/a, the reference's "
+                                  "int N overflows (mpi_radix_sort.c:65)"}
+            try:
+                ts, walls, meds = run_reference("sample_sort", np_, path, mpirun)
+                out["sample_sort"] = {"value": n / ts / 1e9, "unit": "GKeys/s", "cores": np_,
+                                      "program_s": ts, "wall_s": round(walls, 1),
+                                      "median_line": meds}
+            except Exception as e:  # reported, never fatal
+                out["sample_sort"] = {"value": None, "error": repr(e)}
+            return out
         # fallback: the oracle's scalar port of the build's algorithm, one core
         from oracle import orc
         keys = orc.read_ints(path, cap=n)
@@ -96,7 +165,8 @@ def cpu_baseline(dist, seed):
         orc.lsd8(keys)
         t = time.perf_counter() - t0
         return {"value": n / t / 1e9, "unit": "GKeys/s", "cores": 1, "kind": "port",
-                "sample": f"oracle lsd8 (scalar C port), 2^{keys_log2} {dist} keys, {t:.3f} s"}
+                "sample": f"oracle lsd8 (scalar C port), 2^{keys_log2} {dist} keys, {t:.3f} s",
+                **host}
     except Exception as e:  # the baseline is reported, never fatal
         return {"value": None, "unit": "GKeys/s", "cores": None, "kind": None,
                 "sample": f"cpu baseline failed: {e!r}"}
@@ -174,27 +244,15 @@ def pmc_traffic(algo, n_local, n_gpus, prefixes=("k_scatter",)):
     return None
 
 
-def copy_ceiling(n_local, reps=10):
-    """Device-to-device copy of n_local int32 keys (torch copy_ = hipMemcpyAsync D2D), timed
-    with events on torch's stream: the practical HBM ceiling of one read + write pass."""
-    import torch
-    x = torch.empty(n_local, dtype=torch.int32, device="cuda")
-    y = torch.empty_like(x)
-    y.copy_(x)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ts = []
-    for _ in range(reps):
-        e0.record()
-        y.copy_(x)
-        e1.record()
-        e1.synchronize()
-        ts.append(e0.elapsed_time(e1))
-    ts.sort()
-    ms = ts[len(ts) // 2]
-    del x, y
-    torch.cuda.empty_cache()
-    return {"ms": round(ms, 4), "GBps": round(n_local * 8 / (ms * 1e-3) / 1e9, 1),
-            "how": "torch copy_ (hipMemcpyAsync D2D) of the same keys, median of 10"}
+def copy_ceiling(ctx, n_local, reps=10):
+    """The practical HBM ceiling of one read + write pass: libgsort's 16-B-per-lane streaming
+    copy kernel (gsort_copy_ceiling) over the same 4 * n_local bytes, HIP events on its stream,
+    median of `reps` (MI355X_MICROARCH.md: 6.29 TB/s float4 copy; the variants measured are
+    in tools/experiments/copy_ceiling.hip)."""
+    ms, gbps = ctx.copy_ceiling(n_local * 4, reps)
+    return {"ms": round(ms, 4), "GBps": round(gbps, 1),
+            "how": "gsort_copy_ceiling: k_stream_copy (16-KiB chunk per block, 16 B per lane, "
+                   f"nontemporal stores) of the same {n_local * 4} bytes, median of {reps}"}
 
 
 def drop_in_e2e(ctx, fn, d_in, n, reps=3):
@@ -224,12 +282,14 @@ def main():
     sys.stdout.flush()
     os.dup2(2, 1)
     a = parse()
+    if "WORLD_SIZE" not in os.environ and (a.gpus > 1 or a.spawn):
+        os.dup2(json_fd, 1)
+        sys.exit(spawn_ranks(a))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus:
-        if a.gpus > 1 and world == 1:
-            sys.exit("--gpus N>1 must be launched with torch.distributed.run (one rank/GPU)")
+        sys.exit(f"bench: --gpus {a.gpus} but WORLD_SIZE={world}")
     dist_name = a.dist
 
     cpu = None
@@ -301,7 +361,7 @@ def main():
     ms_step = elapsed * 1e3 / a.steps
     value = n_total / (ms_step / 1e3) / 1e9
 
-    ceiling = copy_ceiling(n_local) if rank == 0 else None
+    ceiling = copy_ceiling(ctx, n_local) if rank == 0 else None
     drop_in = drop_in_e2e(ctx, fn, d_in, n_local) if world == 1 else None
 
     rooflines = kernel_rooflines(stats, n_local)

@@ -153,9 +153,9 @@ gsort_status gsort_device_alloc(gsort_ctx *ctx, size_t bytes, void **d_ptr);
 gsort_status gsort_device_free(gsort_ctx *ctx, void *d_ptr);
 gsort_status gsort_copy_to_host(gsort_ctx *ctx, void *h_dst, const void *d_src, size_t bytes);
 gsort_status gsort_copy_to_device(gsort_ctx *ctx, void *d_dst, const void *h_src, size_t bytes);
-/* The bench's HBM ceiling for a read + write pass: a 16-B-per-lane streaming copy kernel of
- * `bytes` between two scratch buffers, timed with hipEvents (median of reps, best over a few
- * grid sizes).  *ms = one copy, *gbps = 2 * bytes / time (read + write). */
+/* The bench's HBM ceiling for a read + write pass: a streaming copy kernel (16 B per lane,
+ * one block per 16 KiB chunk, nontemporal stores) of `bytes` between two scratch buffers,
+ * timed with hipEvents, median of reps.  *ms = one copy, *gbps = 2 * bytes / time. */
 gsort_status gsort_copy_ceiling(gsort_ctx *ctx, size_t bytes, int reps, double *ms, double *gbps);
 /* Which kernel configuration the local sort uses (tile = keys per workgroup). */
 size_t gsort_onesweep_tile(void);

@@ -199,10 +199,9 @@ hipError_t launch_meta_counts(const uint64_t *gb, const uint64_t *rng, int nrng,
 // bad[0] += violations (zeroed by the caller).
 hipError_t launch_lds_order_check(const uint32_t *digits, uint32_t nblocks, uint32_t nbins,
                                   uint64_t *bad, hipStream_t s);
-// Streaming 16-B-per-lane copy of `bytes` (multiple of 16, 16-B aligned) with `grid` blocks of
-// 256 threads: the bench's read + write ceiling.
-hipError_t launch_stream_copy(const void *in, void *out, uint64_t bytes, unsigned grid,
-                              hipStream_t s);
+// Streaming copy of `bytes` (multiple of 16, 16-B aligned): one block per 16 KiB chunk, 16 B
+// per lane, nontemporal stores -- the bench's read + write ceiling.
+hipError_t launch_stream_copy(const void *in, void *out, uint64_t bytes, hipStream_t s);
 // Plain device copy kernel (used when a sort has no non-trivial pass).
 hipError_t launch_copy(const uint32_t *in, uint32_t *out, uint64_t n, hipStream_t s);
 

@@ -489,21 +489,27 @@ __global__ __launch_bounds__(64) void k_bucket_bounds(const int32_t *__restrict_
     if (lane == 0) bounds[j] = lo + (uint64_t)__popcll(m);
 }
 
-// Streaming copy ceiling (bench reference, not on the sort path): 16 B per lane, four loads in
-// flight per thread, grid-strided.  What a read + write pass over HBM can reach on this GPU
-// (MI355X_MICROARCH.md: 6.29 TB/s for a float4 copy).
-__global__ __launch_bounds__(256) void k_stream_copy(const uint4 *__restrict__ in,
-                                                     uint4 *__restrict__ out, uint64_t n16) {
-    const uint64_t stride = (uint64_t)gridDim.x * 256;
-    uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    for (; i + 3 * stride < n16; i += 4 * stride) {
-        const uint4 a = in[i], b = in[i + stride], c = in[i + 2 * stride], d = in[i + 3 * stride];
-        out[i] = a;
-        out[i + stride] = b;
-        out[i + 2 * stride] = c;
-        out[i + 3 * stride] = d;
+// Streaming copy ceiling (bench reference, not on the sort path): one 256-thread block per
+// contiguous 16 KiB chunk, four 16-B loads in flight per lane, nontemporal stores.  The best of
+// the variants measured in tools/experiments/copy_ceiling.hip (grid-strided loops, wider
+// unrolls, 1024-thread blocks, nontemporal loads, hipMemcpyAsync): 5.76 TB/s over 1 GiB,
+// 6.0 TB/s over 4 GiB (MI355X_MICROARCH.md quotes 6.29 TB/s for a float4 copy).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void k_stream_copy(const u32x4 *__restrict__ in,
+                                                     u32x4 *__restrict__ out, uint64_t n16) {
+    constexpr int U = 4;
+    const uint64_t base = (uint64_t)blockIdx.x * (U * 256);
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint64_t j = base + u * 256 + threadIdx.x;
+        if (j < n16) v[u] = in[j];
     }
-    for (; i < n16; i += stride) out[i] = in[i];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint64_t j = base + u * 256 + threadIdx.x;
+        if (j < n16) __builtin_nontemporal_store(v[u], out + j);
+    }
 }
 
 __global__ void k_copy(const uint32_t *__restrict__ in, uint32_t *__restrict__ out, uint64_t n) {
@@ -2238,13 +2244,14 @@ hipError_t launch_lds_order_check(const uint32_t *digits, uint32_t nblocks, uint
     return hipGetLastError();
 }
 
-hipError_t launch_stream_copy(const void *in, void *out, uint64_t bytes, unsigned grid,
-                              hipStream_t s) {
+hipError_t launch_stream_copy(const void *in, void *out, uint64_t bytes, hipStream_t s) {
     if (bytes == 0) return hipSuccess;
     if (bytes % 16 || (reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) % 16)
         return hipErrorInvalidValue;
-    k_stream_copy<<<grid, 256, 0, s>>>(static_cast<const uint4 *>(in), static_cast<uint4 *>(out),
-                                       bytes / 16);
+    const uint64_t n16 = bytes / 16, grid = (n16 + 1023) / 1024;
+    if (grid > 0x7fffffffull) return hipErrorInvalidValue;
+    k_stream_copy<<<(unsigned)grid, 256, 0, s>>>(static_cast<const u32x4 *>(in),
+                                                 static_cast<u32x4 *>(out), n16);
     return hipGetLastError();
 }
 

@@ -2018,21 +2018,18 @@ gsort_status gsort_copy_ceiling(gsort_ctx *c, size_t bytes, int reps, double *ms
     double best = 0.0;
     auto run = [&]() -> gsort_status {
         HIP_TRY(c, hipMemsetAsync(a.p, 0x5a, bytes, c->stream));
-        for (unsigned grid : {1024u, 2048u, 4096u, 8192u}) {  // best median over grid sizes
-            std::vector<float> t;
-            for (int r = 0; r <= reps; ++r) {  // r == 0: warm-up
-                HIP_TRY(c, hipEventRecord(e0, c->stream));
-                HIP_TRY(c, launch_stream_copy(a.p, b.p, bytes, grid, c->stream));
-                HIP_TRY(c, hipEventRecord(e1, c->stream));
-                HIP_TRY(c, hipEventSynchronize(e1));
-                float x = 0.f;
-                HIP_TRY(c, hipEventElapsedTime(&x, e0, e1));
-                if (r) t.push_back(x);
-            }
-            std::sort(t.begin(), t.end());
-            const double med = t[t.size() / 2];
-            if (best == 0.0 || med < best) best = med;
+        std::vector<float> t;
+        for (int r = 0; r <= reps; ++r) {  // r == 0: warm-up
+            HIP_TRY(c, hipEventRecord(e0, c->stream));
+            HIP_TRY(c, launch_stream_copy(a.p, b.p, bytes, c->stream));
+            HIP_TRY(c, hipEventRecord(e1, c->stream));
+            HIP_TRY(c, hipEventSynchronize(e1));
+            float x = 0.f;
+            HIP_TRY(c, hipEventElapsedTime(&x, e0, e1));
+            if (r) t.push_back(x);
         }
+        std::sort(t.begin(), t.end());
+        best = t[t.size() / 2];
         return GSORT_OK;
     };
     if (st == GSORT_OK) st = run();

@@ -42,7 +42,7 @@ def main(root):
     summary = {"kernels": {}}
     st = stats(os.path.join(root, "stats"))
     pmc = {}
-    for sub in ("fetch", "write", "sq", "clk"):
+    for sub in ("fetch", "write", "sq", "clk", "xgmi"):
         for k, cs in counters(os.path.join(root, sub)).items():
             for c, vals in cs.items():
                 pmc.setdefault(k, {})[c] = sum(vals) / len(vals)
@@ -69,6 +69,12 @@ def main(root):
             v["hbm_bytes"] = v["hbm_read_bytes"] + v["hbm_write_bytes"]
             if v.get("avg_us"):
                 v["hbm_GBps"] = v["hbm_bytes"] / (v["avg_us"] * 1e3)
+        if "TCC_EA0_RDREQ_sum" in v and "TCC_EA0_RDREQ_DRAM_sum" in v:
+            # requests the L2s sent to the fabric but not to this GPU's DRAM: peer GPUs (xGMI)
+            # or host memory; ~0 for a kernel that only touches local HBM
+            v["ea_rdreq_non_dram"] = v["TCC_EA0_RDREQ_sum"] - v["TCC_EA0_RDREQ_DRAM_sum"]
+            v["ea_wrreq_non_dram"] = v.get("TCC_EA0_WRREQ_sum", 0.0) - \
+                v.get("TCC_EA0_WRREQ_DRAM_sum", 0.0)
         if "GRBM_GUI_ACTIVE" in v and v.get("avg_us"):
             v["eff_clock_GHz"] = v["GRBM_GUI_ACTIVE"] / 8 / (v["avg_us"] * 1e3)
     json.dump(summary, sys.stdout, indent=1, sort_keys=True)

@@ -20,5 +20,8 @@ run fetch --pmc FETCH_SIZE
 run write --pmc WRITE_SIZE
 run sq --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS
 run clk --pmc GRBM_GUI_ACTIVE GRBM_COUNT
+# peer (xGMI) evidence for the exchange: EA requests that did not go to local DRAM
+# (TCC_EA0_RDREQ - TCC_EA0_RDREQ_DRAM, TCC_EA0_WRREQ - TCC_EA0_WRREQ_DRAM)
+run xgmi --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_DRAM_sum
 python3 tools/pmc_summary.py "$OUT" > "$OUT/summary.json"
 echo "profile $TAG done"
