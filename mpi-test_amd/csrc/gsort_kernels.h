@@ -112,28 +112,37 @@ hipError_t launch_seg_count(const SegPass &sp, hipStream_t s);
 // K3u over the planned segment tiles (after launch_seg_count).
 hipError_t launch_seg_partition(const SegPass &sp, hipStream_t s);
 // ---- two-level plan front end (gsort_kernels.hip, "Two-level plan") ----------------------
-// K1h workgroups (one per CU) and the size of their partial 16-bit histograms (u32 words).
+// K1h workgroups (at most; one per CU) and the size of their partial 16-bit histograms (u32).
 constexpr uint32_t kH16Blocks = 256;
 constexpr size_t kH16PartWords = 32768;
-// K1h: level-3 tile counts (as launch_tile_counts1 with shift 24) + per-workgroup packed
-// histograms of the top 16 bits into part (nblk x kH16PartWords u32), wrap repairs into fix
-// (65536 u64, zeroed by the caller).  Returns the workgroup count in *nblk.
-hipError_t launch_counts_h16(const uint32_t *in, uint64_t n, bool flip, uint32_t *tcounts,
-                             uint32_t *part, uint64_t *fix, uint32_t *nblk, hipStream_t s);
-// K12h: child counts / starts of the 65536 level-2 children from the K1h partials and the
-// level-3 scan (bases / totals, 256 u64 each): cstart (65537 u64, cstart[65536] = n), the K3a
-// cursors cur (65536 u32, relative to their level-3 bucket), tpfx (257 u32) and the work lists (wl2: children of level-2
-// buckets; wl3: level-3 buckets finished by K11).  force: every non-empty level-3 bucket is a
-// level-2 bucket.  A WorkLists with ctr == nullptr is not filled.
-hipError_t launch_plan_h16(const uint32_t *part, uint32_t nblk, const uint64_t *fix,
-                           const uint64_t *bases, const uint64_t *totals, uint64_t n, bool force,
-                           uint64_t *cstart, uint32_t *cur, uint32_t *tpfx, const WorkLists &wl2,
-                           const WorkLists &wl3, hipStream_t s);
-// K3a: level 2 of every level-2 bucket (in = level 3's output, ordered u32) by digit 2 into
-// out (ordered u32), or with out16 != nullptr only the low 16 bits into out16.
-hipError_t launch_partition_h16(const uint32_t *in, uint32_t *out, uint16_t *out16, uint64_t n,
-                                const uint32_t *tpfx, const uint64_t *bases,
-                                const uint64_t *totals, uint32_t *cur, hipStream_t s);
+constexpr uint32_t kH16Shards = 8;  // level-3 cursors / wrap repairs per XCD shard
+// K1h: per-workgroup packed histograms of the top 16 bits (ordered u32) into part (nblk x
+// kH16PartWords u32), wrap repairs into fix (kH16Shards x 65536 u64, zeroed by the caller).
+// Returns the workgroup count (a multiple of kH16Shards) in *nblk.
+hipError_t launch_hist16(const uint32_t *in, uint64_t n, bool flip, uint32_t *part, uint64_t *fix,
+                         uint32_t *nblk, hipStream_t s);
+// K12a + K12b: from the K1h partials, ccount (65536 child counts), t3 (kH16Shards x 256 level-3
+// counts per shard), tot (256), then bases / totals (256 u64 each: the level-3 buckets),
+// cstart (65537 u64: the 16-bit bucket bounds, cstart[65536] = n), the level-2 child cursors
+// cur (65536 u32, from their bucket's start), the level-3 cursors cur3 (kH16Shards x 256 u32,
+// from their bucket's start), the K3a tile plan tpfx (257 u32) and the work lists (wl2:
+// children of level-2 buckets; wl3: level-3 buckets finished by K11; ctr == nullptr: not
+// filled).  force: every non-empty level-3 bucket is a level-2 bucket.
+hipError_t launch_plan16(const uint32_t *part, uint32_t nblk, const uint64_t *fix, uint64_t n,
+                         bool force, uint64_t *ccount, uint64_t *t3, uint64_t *tot,
+                         uint64_t *bases, uint64_t *totals, uint64_t *cstart, uint32_t *cur,
+                         uint32_t *cur3, uint32_t *tpfx, const WorkLists &wl2,
+                         const WorkLists &wl3, hipStream_t s);
+// K3r: level 3 of the int32 input by the top digit into out (ordered u32), runs reserved on cur3.
+hipError_t launch_partition3r(const uint32_t *in, uint32_t *out, uint64_t n, uint32_t *cur3,
+                              const uint64_t *bases, hipStream_t s);
+// K12c + K3a: level 2 of every level-2 bucket (in = level 3's output, ordered u32) by digit 2
+// into out (ordered u32), or with out16 != nullptr only the low 16 bits into out16.  tdesc:
+// scratch for kTileDescBytes per level-2 tile (sweep_tiles(n) + 256 tiles).
+constexpr size_t kTileDescBytes = 16;
+hipError_t launch_partition2r(const uint32_t *in, uint32_t *out, uint16_t *out16, uint64_t n,
+                              const uint32_t *tpfx, void *tdesc, const uint64_t *bases,
+                              const uint64_t *totals, uint32_t *cur, hipStream_t s);
 // K11: sort each listed bucket (all of class cls: <= kLocalCap[cls] keys) on digits
 // 0..ndigits-1 in LDS, store as int32 into out (same positions; in == out allowed).
 // flip_in: the input is int32 (else ordered u32).  atomic_rank: stable ranks from LDS atomics

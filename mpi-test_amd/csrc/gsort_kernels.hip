@@ -903,27 +903,30 @@ __global__ __launch_bounds__(BLOCK) void k_seg_partition(
 }
 
 // =======================================================================================
-// Two-level plan (default MSD front end): level 2 without its own counting pass.
-//   K1h  level-3 tile counts (as K1) + a histogram of the top 16 bits, in the same read
-//   K2   scan of the level-3 tile counts (unchanged)
-//   K12h from the 16-bit histogram: every level-2 child's count and start, the level-2
-//        cursors, the work lists and the level-2 tile plan -- all before level 3 runs
-//   K3u  level 3 (unchanged)
-//   K3a  level 2: K3u whose tiles reserve their digit runs with one atomicAdd per digit on the
-//        child's cursor (an MSD level needs every key in its child, not a stable order)
-// Level 2 then costs 8 B/key instead of 12 (no K1s re-read, no K2s scans), and the host reads
-// the work-list counters while levels 3 and 2 run instead of between them.
+// Two-level plan (default MSD front end): levels 3 and 2 without per-tile counting passes.
+//   K1h  histogram of the top 16 bits of every key (one returning LDS atomic per key)
+//   K12a the 65536 level-2 child counts, and each level-3 bucket's count per shard
+//   K12b bucket bases, child starts, the level-3 (per shard) and level-2 cursors, the K11
+//        work lists and the K3a tile plan -- all before level 3 runs
+//   K3r  level 3: every pair of input tiles reserves its 256 digit runs with one atomicAdd per
+//        digit on its shard's bucket cursors (an MSD level only needs every key in its
+//        bucket, not a stable order), then scatters through LDS
+//   K3a  level 2: the same over the tiles of every level-3 bucket, on its child cursors
+// A shard is one XCD's share of the tiles: tile pair p is processed by workgroup p of K1h's
+// and K3r's grids, which runs on XCD p % 8 (workgroups are dealt round-robin over the 8
+// XCDs), and counts / reserves under shard p % 8.  So every cursor takes 1/8 of a bucket's
+// reservations (a single device-scope counter saturates near 88 M atomics/s,
+// MI355X_MICROARCH.md 'dequeue'), and consecutive runs of a bucket share one XCD's L2.
+// Replaced (v0-v8): K1 + K2 tile counts and scans for level 3, and a second LDS atomic per key
+// in K1h for them.  Level 3 + 2 + K11 = 4 + 8 + 8 + 8 = 28 B/key.
 // =======================================================================================
+constexpr uint32_t kShards = kH16Shards;
 
-// K1h: tcounts[tile][256] = top-digit counts of every kSweepTile tile (exactly as K1), and per
-// workgroup a histogram of the top 16 bits (ordered u32) kept in LDS as packed u16 pairs
-// (32768 words, 128 KiB: one workgroup per CU, striding over the tiles; the next tile's loads
-// are in flight while the current one is counted).  At the end each workgroup stores its words
-// to part[blockIdx.x][.].  A u16 half that wraps is repaired through fix[] (u64, zeroed by the
-// caller): every wrap is seen by exactly one thread, whose atomic returned 0xffff in that half.
-// A wrapped low half lost 65536 and carried one into the high half; a carry out of the whole
-// word (a high half wrapping, or a low add on 0xffffffff) lost 65536 of the high bin.  Hence
-// count[h] = sum_b half_h(part[b]) + fix[h] (mod 2^64).
+// A u16 half of K1h's packed LDS counters that wraps is seen by exactly one thread, whose
+// returning atomic read 0xffff in that half, and repaired through fix[] (u64, zeroed by the
+// caller): a wrapped low half lost 65536 and carried one into the high half; a carry out of
+// the whole word (a high half wrapping, or a low add on 0xffffffff) lost 65536 of the high bin.
+// Hence count[h] = sum_b half_h(part[b]) + fix[h] (mod 2^64), per shard.
 __device__ __forceinline__ void h16_wrap(unsigned long long *fix, uint32_t b, uint32_t old) {
     atomicAdd(&fix[b], 65536ull);
     if (!(b & 1u)) {
@@ -932,78 +935,75 @@ __device__ __forceinline__ void h16_wrap(unsigned long long *fix, uint32_t b, ui
     }
 }
 
+// K1h: per workgroup, a histogram of the top 16 bits (ordered u32) of its tiles, as 32768
+// packed u16 pairs in LDS (128 KiB: one 1024-thread workgroup per CU), stored to
+// part[blockIdx.x][.] at the end.  Workgroup b takes the tile pairs p = b, b + G, b + 2G, ..
+// (G = gridDim.x, a multiple of kShards, so shard p % 8 == b % 8) and prefetches its next tile
+// while it counts the current one.  Wraps go to fix[b % 8][.].
 template <int BLOCK, bool FIN>
-__global__ __launch_bounds__(BLOCK) void k_counts_h16(const uint32_t *__restrict__ in, uint64_t n,
-                                                      uint32_t *__restrict__ tcounts,
-                                                      uint32_t *__restrict__ part,
-                                                      unsigned long long *__restrict__ fix) {
+__global__ __launch_bounds__(BLOCK) void k_hist16(const uint32_t *__restrict__ in, uint64_t n,
+                                                  uint32_t *__restrict__ part,
+                                                  unsigned long long *__restrict__ fix) {
     constexpr int ITEMS = kSweepTile / BLOCK;
     constexpr uint32_t kWords = kBuckets16 / 2;
     __shared__ uint32_t s_h[kWords];
-    __shared__ uint32_t s_t[kRadix];
     const uint32_t tid = threadIdx.x;
     for (uint32_t i = tid; i < kWords; i += BLOCK) s_h[i] = 0;
-    if (tid < kRadix) s_t[tid] = 0;
-    // Tile lengths in 32-bit scalar arithmetic: every tile but the last is full.  (The form
-    // min(n - t0, kSweepTile) on u64 was miscompiled for gfx950 by ROCm 7.2's backend: the
-    // uniform 64-bit compare lives in VCC, the SCC copy that the length's s_cselect needs was
-    // dropped in front of the s_cbranch_vccz, and the select read the carry of an address add
-    // -- so the first, partial tile loaded a full 8192 keys, up to 32 KiB past the input.
-    // tests/test_cpu_library.py::test_kernels_isa_scc_hazard checks every kernel for it.)
+    // tile lengths in 32-bit scalar arithmetic (tools/isa_scc_check.py: the u64 min() form was
+    // miscompiled by ROCm 7.2 and loaded a full tile past the input's end)
     const uint32_t ntiles = (uint32_t)((n + kSweepTile - 1) / kSweepTile);
     const uint32_t last_len = (uint32_t)(n - (uint64_t)(ntiles - 1) * kSweepTile);
     auto tile_len = [&](uint32_t t) -> uint32_t {
         return t == ntiles - 1 ? last_len : (uint32_t)kSweepTile;
     };
+    auto tile_of = [&](uint32_t i) -> uint32_t {  // this workgroup's i-th tile
+        return 2 * (blockIdx.x + (i >> 1) * gridDim.x) + (i & 1);
+    };
+    unsigned long long *fx = fix + (uint64_t)(blockIdx.x % kShards) * kBuckets16;
+    uint32_t t = tile_of(0);
     uint32_t k[ITEMS];
-    if (blockIdx.x < ntiles) {
-        const uint32_t len = tile_len(blockIdx.x);
-        load_tile<BLOCK, ITEMS, FIN>(in + (uint64_t)blockIdx.x * kSweepTile + tid,
+    if (t < ntiles) {
+        const uint32_t len = tile_len(t);
+        load_tile<BLOCK, ITEMS, FIN>(in + (uint64_t)t * kSweepTile + tid,
                                      len == (uint32_t)kSweepTile, len, k);
     }
-    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        __syncthreads();  // zeroing / the previous tile's count store done
+    __syncthreads();  // zeroing done
+    for (uint32_t i = 1; t < ntiles; ++i) {
         const uint32_t len = tile_len(t);
-        const uint32_t tn = t + gridDim.x;
+        const uint32_t tn = tile_of(i);
         uint32_t kn[ITEMS];
         if (tn < ntiles) {
             const uint32_t lenn = tile_len(tn);
             load_tile<BLOCK, ITEMS, FIN>(in + (uint64_t)tn * kSweepTile + tid,
                                          lenn == (uint32_t)kSweepTile, lenn, kn);
         }
-        // all 8 returning atomics in flight before the first wrap test (measured: a test per
-        // atomic waits out each LDS round trip, 0.31 vs 0.30 ms at 2^28)
+        // all returning atomics in flight before the first wrap test
         uint32_t old[ITEMS];
         bool wrap = false;
 #pragma unroll
-        for (int i = 0; i < ITEMS; ++i) {
-            old[i] = 0;
-            if ((uint32_t)(i * BLOCK) + tid < len) {
-                atomicAdd(&s_t[k[i] >> 24], 1u);
-                const uint32_t b = k[i] >> 16;
-                old[i] = atomicAdd(&s_h[b >> 1], 1u << ((b & 1u) << 4));
+        for (int j = 0; j < ITEMS; ++j) {
+            old[j] = 0;
+            if ((uint32_t)(j * BLOCK) + tid < len) {
+                const uint32_t b = k[j] >> 16;
+                old[j] = atomicAdd(&s_h[b >> 1], 1u << ((b & 1u) << 4));
             }
         }
 #pragma unroll
-        for (int i = 0; i < ITEMS; ++i)
-            wrap |= (uint32_t)(i * BLOCK) + tid < len &&
-                    ((old[i] >> (((k[i] >> 16) & 1u) << 4)) & 0xffffu) == 0xffffu;
+        for (int j = 0; j < ITEMS; ++j)
+            wrap |= (uint32_t)(j * BLOCK) + tid < len &&
+                    ((old[j] >> (((k[j] >> 16) & 1u) << 4)) & 0xffffu) == 0xffffu;
         if (wrap) {
 #pragma unroll
-            for (int i = 0; i < ITEMS; ++i) {
-                const uint32_t b = k[i] >> 16;
-                if ((uint32_t)(i * BLOCK) + tid < len &&
-                    ((old[i] >> ((b & 1u) << 4)) & 0xffffu) == 0xffffu)
-                    h16_wrap(fix, b, old[i]);
+            for (int j = 0; j < ITEMS; ++j) {
+                const uint32_t b = k[j] >> 16;
+                if ((uint32_t)(j * BLOCK) + tid < len &&
+                    ((old[j] >> ((b & 1u) << 4)) & 0xffffu) == 0xffffu)
+                    h16_wrap(fx, b, old[j]);
             }
         }
-        __syncthreads();
-        if (tid < kRadix) {
-            tcounts[(uint64_t)t * kRadix + tid] = s_t[tid];
-            s_t[tid] = 0;
-        }
 #pragma unroll
-        for (int i = 0; i < ITEMS; ++i) k[i] = kn[i];
+        for (int j = 0; j < ITEMS; ++j) k[j] = kn[j];
+        t = tn;
     }
     __syncthreads();
     uint32_t *dst = part + (uint64_t)blockIdx.x * kWords;
@@ -1039,121 +1039,183 @@ __device__ __forceinline__ unsigned long long block_excl_scan(unsigned long long
     return excl;
 }
 
-// K12h: block s = level-3 digit, thread e = level-2 digit.  c = the child's key count (the
-// K1h partials of nblk workgroups + fix), cstart[s*256+e] = its first position (bases[s] + the
-// exclusive scan over e: the 65536 bucket bounds of the top 16 bits, cstart[65536] = n), and
-// for a level-2 bucket the K3a cursor cur[.] (u32, from the bucket start) and the child classified into wl2 (K11
-// classes / next level); any other non-empty bucket s goes whole to wl3 (K11 on three digits).
-// Block 0 also writes tpfx[0..256], the K3a tiles before each level-2 bucket.
-__global__ __launch_bounds__(kRadix) void k_plan_h16(
-    const uint32_t *__restrict__ part, uint32_t nblk, const unsigned long long *__restrict__ fix,
-    const unsigned long long *__restrict__ bases, const unsigned long long *__restrict__ totals,
-    uint64_t n, int force, unsigned long long *__restrict__ cstart,
-    uint32_t *__restrict__ cur, uint32_t *__restrict__ tpfx, WorkLists wl2,
-    WorkLists wl3) {
+// K12a: block s = level-3 digit, thread e = level-2 digit.  The count of child (s, e) in shard
+// x = the e-half of word s*128 + e/2 summed over the partials b = x (mod 8), + fix[x][s*256+e].
+// Writes ccount[s*256+e] (all shards), t3[x*256+s] (bucket s in shard x) and tot[s].
+// nblk is a multiple of kShards.
+__global__ __launch_bounds__(kRadix) void k_plan16_count(const uint32_t *__restrict__ part,
+                                                         uint32_t nblk,
+                                                         const unsigned long long *__restrict__ fix,
+                                                         unsigned long long *__restrict__ ccount,
+                                                         unsigned long long *__restrict__ t3,
+                                                         unsigned long long *__restrict__ tot) {
     constexpr uint32_t kWords = kBuckets16 / 2;
-    __shared__ uint32_t s_lo[kRadix], s_hi[kRadix];
-    __shared__ unsigned long long s_w[kRadix / 64];
-    const uint32_t s = blockIdx.x, e = threadIdx.x;
-    // thread e sums word s*128 + (e & 127) (children 2j, 2j+1) over every other partial
-    const uint32_t word = s * (kRadix / 2) + (e & 127u);
-    uint32_t lo = 0, hi = 0;
-    uint32_t b = e >> 7;
-    for (; b + 14 < nblk; b += 16) {
-        uint32_t v[8];
+    __shared__ uint32_t s_lo[kShards][kRadix / 2], s_hi[kShards][kRadix / 2];
+    __shared__ unsigned long long s_red[kShards][kRadix / 64];
+    const uint32_t s = blockIdx.x, e = threadIdx.x, lane = e & 63, wv = e >> 6;
+    // this thread: word s*128 + (e & 127) over the partials b = par (mod 2), i.e. the shards
+    // par, par + 2, par + 4, par + 6 (b, b + 2, b + 4, b + 6 of every group of eight)
+    const uint32_t par = e >> 7, word = s * (kRadix / 2) + (e & 127u);
+    uint32_t lo[4] = {0, 0, 0, 0}, hi[4] = {0, 0, 0, 0};
+    for (uint32_t b = par; b < nblk; b += kShards) {
+        uint32_t v[4];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = part[(uint64_t)(b + 2 * j) * kWords + word];
+        for (int j = 0; j < 4; ++j) v[j] = part[(uint64_t)(b + 2 * j) * kWords + word];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) { lo += v[j] & 0xffffu; hi += v[j] >> 16; }
+        for (int j = 0; j < 4; ++j) { lo[j] += v[j] & 0xffffu; hi[j] += v[j] >> 16; }
     }
-    for (; b < nblk; b += 2) {
-        const uint32_t v = part[(uint64_t)b * kWords + word];
-        lo += v & 0xffffu;
-        hi += v >> 16;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        s_lo[par + 2 * j][e & 127u] = lo[j];
+        s_hi[par + 2 * j][e & 127u] = hi[j];
     }
-    s_lo[e] = lo;
-    s_hi[e] = hi;
     __syncthreads();
-    const uint32_t j = e >> 1;
-    const unsigned long long c =
-        (unsigned long long)((e & 1u) ? s_hi[j] + s_hi[j + 128] : s_lo[j] + s_lo[j + 128]) +
-        fix[s * kRadix + e];
-    unsigned long long sum;
-    const unsigned long long excl = block_excl_scan(c, s_w, &sum);
-    const unsigned long long tot = totals[s], st = bases[s] + excl;
-    cstart[s * kRadix + e] = st;
-    if (s == 0 && e == 0) cstart[kBuckets16] = n;
-    if (level2_bucket(tot, force)) {
-        cur[s * kRadix + e] = (uint32_t)excl;  // relative to the bucket start
-        if (wl2.ctr) classify_block(st, c, wl2);
-    } else if (wl3.ctr) {
-        classify_block(e == 0 ? bases[s] : 0ull, e == 0 ? tot : 0ull, wl3);
+    const uint32_t w2 = e >> 1;
+    unsigned long long c = 0, cx[kShards];
+#pragma unroll
+    for (uint32_t x = 0; x < kShards; ++x) {
+        cx[x] = (unsigned long long)((e & 1u) ? s_hi[x][w2] : s_lo[x][w2]) +
+                fix[(uint64_t)x * kBuckets16 + s * kRadix + e];
+        c += cx[x];
     }
-    if (s == 0) {
-        const unsigned long long te = totals[e];
-        const unsigned long long nt =
-            level2_bucket(te, force) ? (te + kSweepTile - 1) / kSweepTile : 0ull;
-        unsigned long long all;
-        const unsigned long long tx = block_excl_scan(nt, s_w, &all);
-        tpfx[e] = (uint32_t)tx;
-        if (e == 0) tpfx[kRadix] = (uint32_t)all;
+    ccount[s * kRadix + e] = c;
+#pragma unroll
+    for (uint32_t x = 0; x < kShards; ++x) {
+        unsigned long long r = cx[x];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) r += __shfl_xor(r, o);
+        if (lane == 0) s_red[x][wv] = r;
+    }
+    __syncthreads();
+    if (e < kShards) {
+        unsigned long long r = 0;
+        for (uint32_t ww = 0; ww < kRadix / 64; ++ww) r += s_red[e][ww];
+        t3[e * kRadix + s] = r;
+    }
+    if (e == kShards) {
+        unsigned long long r = 0;
+        for (uint32_t x = 0; x < kShards; ++x)
+            for (uint32_t ww = 0; ww < kRadix / 64; ++ww) r += s_red[x][ww];
+        tot[s] = r;
     }
 }
 
-// K3a: level 2 over the level-2 buckets' tiles (grid >= tpfx[256]; surplus blocks exit).
-// Tile t belongs to bucket s with tpfx[s] <= t < tpfx[s+1] (binary search in LDS); its runs are
-// reserved on cur[s][.] (K12h).  Input: level 3's output (ordered u32).
-template <int BLOCK, int ITEMS, typename OT = uint32_t>
-__global__ __launch_bounds__(BLOCK) void k_partition_h16(
-    const uint32_t *__restrict__ in, OT *__restrict__ out, const uint32_t *__restrict__ tpfx,
-    const unsigned long long *__restrict__ bases, const unsigned long long *__restrict__ totals,
-    uint32_t *__restrict__ cur) {
-    constexpr int TILE = BLOCK * ITEMS;
-    static_assert(TILE == kSweepTile, "level-2 tiles are kSweepTile keys");
-    __shared__ uint32_t s_keys[TILE];
-    __shared__ uint32_t s_cur[kRadix];
-    __shared__ OT *s_dst[kRadix];
-    __shared__ uint32_t s_wsum[kRadix / 64];
-    __shared__ uint32_t s_tp[kRadix + 1];
-    const uint32_t tid = threadIdx.x;
-    if (tid <= kRadix) s_tp[tid] = tpfx[tid];
+// K12b: block s, thread e.  bases[s] = the keys of level-3 buckets < s; child (s, e) starts at
+// cstart[s*256+e] = bases[s] + its exclusive scan over e (the 65536 bucket bounds of the top 16
+// bits; cstart[65536] = n); a level-2 bucket's child cursors cur[s*256+e] (u32, from bases[s])
+// and the child in wl2 (K11 classes / next level); any other non-empty bucket s whole in wl3
+// (K11 on three digits); the level-3 cursors cur3[x*256+s] = the keys of bucket s in shards
+// < x (u32, from bases[s]).  Block 0 also writes bases / totals (256 u64 each) and tpfx[0..256],
+// the K3a tiles before each level-2 bucket.
+__global__ __launch_bounds__(kRadix) void k_plan16_place(
+    const unsigned long long *__restrict__ ccount, const unsigned long long *__restrict__ t3,
+    const unsigned long long *__restrict__ tot, uint64_t n, int force,
+    unsigned long long *__restrict__ bases, unsigned long long *__restrict__ totals,
+    unsigned long long *__restrict__ cstart, uint32_t *__restrict__ cur,
+    uint32_t *__restrict__ cur3, uint32_t *__restrict__ tpfx, WorkLists wl2, WorkLists wl3) {
+    __shared__ unsigned long long s_w[kRadix / 64];
+    __shared__ unsigned long long s_base;
+    const uint32_t s = blockIdx.x, e = threadIdx.x;
+    const unsigned long long te = tot[e];
+    unsigned long long all;
+    const unsigned long long be = block_excl_scan(te, s_w, &all);
+    if (e == s) s_base = be;
+    if (s == 0) { bases[e] = be; totals[e] = te; }
     __syncthreads();
-    const uint32_t t = xcd_tile(blockIdx.x, gridDim.x);
-    if (t >= s_tp[kRadix]) return;
+    const unsigned long long b0 = s_base, ts = tot[s];
+    const unsigned long long c = ccount[s * kRadix + e];
+    unsigned long long sum;
+    const unsigned long long excl = block_excl_scan(c, s_w, &sum);
+    const unsigned long long st = b0 + excl;
+    cstart[s * kRadix + e] = st;
+    if (s == 0 && e == 0) cstart[kBuckets16] = n;
+    if (e == 0) {
+        unsigned long long r = 0;
+        for (uint32_t x = 0; x < kShards; ++x) {
+            cur3[x * kRadix + s] = (uint32_t)r;
+            r += t3[x * kRadix + s];
+        }
+    }
+    if (level2_bucket(ts, force)) {
+        cur[s * kRadix + e] = (uint32_t)excl;
+        if (wl2.ctr) classify_block(st, c, wl2);
+    } else if (wl3.ctr) {
+        classify_block(e == 0 ? b0 : 0ull, e == 0 ? ts : 0ull, wl3);
+    }
+    if (s == 0) {
+        const unsigned long long nt =
+            level2_bucket(te, force) ? (te + kSweepTile - 1) / kSweepTile : 0ull;
+        unsigned long long ntall;
+        const unsigned long long tx = block_excl_scan(nt, s_w, &ntall);
+        tpfx[e] = (uint32_t)tx;
+        if (e == 0) tpfx[kRadix] = (uint32_t)ntall;
+    }
+}
+
+// K12c: the K3a tile descriptors, one thread per level-2 tile t < tpfx[256]: its bucket s
+// (tpfx[s] <= t < tpfx[s+1]), first key and length.  K3a then reaches its keys after one
+// (scalar) load instead of a tpfx load, an LDS binary search and two dependent loads of the
+// bucket bounds -- a chain every one of its ~16K single-pair workgroups exposed.
+struct TileDesc {
+    unsigned long long t0;
+    uint32_t len, seg;
+};
+__global__ __launch_bounds__(256) void k_tile_desc(const uint32_t *__restrict__ tpfx,
+                                                   const unsigned long long *__restrict__ bases,
+                                                   const unsigned long long *__restrict__ totals,
+                                                   uint32_t max_tiles,
+                                                   TileDesc *__restrict__ desc) {
+    __shared__ uint32_t s_tp[kRadix + 1];
+    for (uint32_t i = threadIdx.x; i <= kRadix; i += 256) s_tp[i] = tpfx[i];
+    __syncthreads();
+    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= max_tiles || t >= s_tp[kRadix]) return;
     uint32_t lo = 0, hi = kRadix;  // s_tp[lo] <= t < s_tp[hi]
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
         if (s_tp[mid] <= t) lo = mid;
         else hi = mid;
     }
-    const uint64_t b0 = bases[lo], end = b0 + totals[lo];
-    const uint64_t t0 = b0 + (uint64_t)(t - s_tp[lo]) * TILE;
-    const uint32_t len = (uint32_t)(end - t0 < (uint64_t)TILE ? end - t0 : (uint64_t)TILE);
-    partition_tile<BLOCK, ITEMS, false, false, OT>(in, t0, len, 16, nullptr, s_keys, s_cur, s_dst,
-                                                   s_wsum, cur + (uint64_t)lo * kRadix, out + b0);
+    const unsigned long long b0 = bases[lo], end = b0 + totals[lo];
+    const unsigned long long t0 = b0 + (unsigned long long)(t - s_tp[lo]) * kSweepTile;
+    const unsigned long long rem = end - t0;
+    desc[t] = {t0, (rem >> 13) ? (uint32_t)kSweepTile : (uint32_t)rem, lo};
 }
 
-// K3a2: K3a over PAIRS of level-2 tiles (2p, 2p+1 of the tile plan; grid >= ceil(tiles/2)).
-// Both tiles are ranked before either reservation is needed, so the two atomics are in flight
-// together and their round trip hides behind twice the scan + LDS scatter work; LDS holds both
-// tiles (2 x 32 KiB: still two 1024-thread workgroups per CU).
-template <int BLOCK, int ITEMS, typename OT = uint32_t>
-__global__ __launch_bounds__(BLOCK) void k_partition2_h16(
-    const uint32_t *__restrict__ in, OT *__restrict__ out, const uint32_t *__restrict__ tpfx,
-    const unsigned long long *__restrict__ bases, const unsigned long long *__restrict__ totals,
-    uint32_t *__restrict__ cur) {
-    constexpr int TILE = BLOCK * ITEMS, shift = 16;
-    static_assert(TILE == kSweepTile, "level-2 tiles are kSweepTile keys");
+// K3r / K3a: one workgroup per PAIR of tiles.  Both tiles are ranked (one LDS atomic per key)
+// before either reservation is needed, so the two reservations (one returning device-scope
+// atomicAdd per non-empty digit) are in flight together and their round trip hides behind
+// twice the LDS scan + scatter; LDS holds both tiles (2 x 32 KiB: two 1024-thread workgroups
+// per CU).
+//   L3 (K3r): level 3 of the input (int32, FIN flips to ordered u32): tile pair p = blockIdx.x,
+//     tiles 2p and 2p+1; digit runs reserved on cur[(p % 8) * 256 + d] (K12b's cur3), placed
+//     at bases[d] + the reservation.
+//   !L3 (K3a): level 2 of every level-2 bucket (in = level 3's output, ordered u32): the
+//     K12b tile plan tpfx maps tile t to bucket s (tpfx[s] <= t < tpfx[s+1]); pairs are dealt
+//     XCD-contiguously (xcd_tile); runs reserved on cur[s * 256 + d], placed at bases[s] + the
+//     reservation; out may be uint16_t (only the low 16 bits: the distributed sender's packed
+//     send buffer).
+template <int BLOCK, int ITEMS, bool L3, bool FIN, typename OT = uint32_t>
+__global__ __launch_bounds__(BLOCK) void k_partition_res(
+    const uint32_t *__restrict__ in, OT *__restrict__ out, uint64_t n,
+    const uint32_t *__restrict__ tpfx, const TileDesc *__restrict__ desc,
+    const unsigned long long *__restrict__ bases, uint32_t *__restrict__ cur) {
+    constexpr int TILE = BLOCK * ITEMS, shift = L3 ? 24 : 16;
+    static_assert(TILE == kSweepTile, "reservation tiles are kSweepTile keys");
     __shared__ uint32_t s_keys[2][TILE];
     __shared__ uint32_t s_cur[2][kRadix];
     __shared__ OT *s_dst[2][kRadix];
     __shared__ uint32_t s_wsum[2][kRadix / 64];
-    __shared__ uint32_t s_tp[kRadix + 1];
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    if (tid <= kRadix) s_tp[tid] = tpfx[tid];
-    if (tid < kRadix) { s_cur[0][tid] = 0; s_cur[1][tid] = 0; }
-    __syncthreads();
-    const uint32_t pr = xcd_tile(blockIdx.x, gridDim.x), ntile = s_tp[kRadix];
+    uint32_t pr, ntile, last_len = 0;
+    if (L3) {
+        pr = blockIdx.x;
+        ntile = (uint32_t)((n + TILE - 1) / TILE);
+        last_len = (uint32_t)(n - (uint64_t)(ntile - 1) * TILE);
+    } else {
+        pr = xcd_tile(blockIdx.x, gridDim.x);
+        ntile = tpfx[kRadix];
+    }
     if (2 * pr >= ntile) return;
     uint32_t seg[2], len[2];
     uint64_t t0[2];
@@ -1162,22 +1224,26 @@ __global__ __launch_bounds__(BLOCK) void k_partition2_h16(
         const uint32_t t = 2 * pr + h;
         seg[h] = 0; len[h] = 0; t0[h] = 0;
         if (t < ntile) {
-            uint32_t lo = 0, hi = kRadix;  // s_tp[lo] <= t < s_tp[hi]
-            while (hi - lo > 1) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (s_tp[mid] <= t) lo = mid;
-                else hi = mid;
+            if (L3) {
+                t0[h] = (uint64_t)t * TILE;
+                len[h] = t == ntile - 1 ? last_len : (uint32_t)TILE;
+            } else {
+                const TileDesc d = desc[t];
+                t0[h] = d.t0;
+                len[h] = d.len;
+                seg[h] = d.seg;
             }
-            const uint64_t b0 = bases[lo], end = b0 + totals[lo];
-            seg[h] = lo;
-            t0[h] = b0 + (uint64_t)(t - s_tp[lo]) * TILE;
-            len[h] = (uint32_t)(end - t0[h] < (uint64_t)TILE ? end - t0[h] : (uint64_t)TILE);
         }
     }
+    if (tid < kRadix) { s_cur[0][tid] = 0; s_cur[1][tid] = 0; }
+    uint32_t *cursor[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) cursor[h] = cur + (L3 ? (pr % kShards) : seg[h]) * kRadix;
     uint32_t k[2][ITEMS], r[2][ITEMS];
 #pragma unroll
     for (int h = 0; h < 2; ++h)
-        load_tile<BLOCK, ITEMS, false>(in + t0[h] + tid, len[h] == (uint32_t)TILE, len[h], k[h]);
+        load_tile<BLOCK, ITEMS, FIN>(in + t0[h] + tid, len[h] == (uint32_t)TILE, len[h], k[h]);
+    __syncthreads();  // s_cur zeroed
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -1190,7 +1256,7 @@ __global__ __launch_bounds__(BLOCK) void k_partition2_h16(
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const uint32_t c = s_cur[h][tid];
-            if (c) pos[h] = atomicAdd(&cur[seg[h] * kRadix + tid], c);
+            if (c) pos[h] = atomicAdd(&cursor[h][tid], c);
             uint32_t v = c;
 #pragma unroll
             for (int o = 1; o < 64; o <<= 1) {
@@ -1219,7 +1285,7 @@ __global__ __launch_bounds__(BLOCK) void k_partition2_h16(
     if (tid < kRadix) {
 #pragma unroll
         for (int h = 0; h < 2; ++h)
-            s_dst[h][tid] = out + (bases[seg[h]] + pos[h]) - excl[h];
+            s_dst[h][tid] = out + ((L3 ? bases[tid] : bases[seg[h]]) + pos[h]) - excl[h];
     }
     __syncthreads();
 #pragma unroll
@@ -2007,52 +2073,68 @@ hipError_t launch_seg_partition(const SegPass &sp, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_counts_h16(const uint32_t *in, uint64_t n, bool flip, uint32_t *tcounts,
-                             uint32_t *part, uint64_t *fix, uint32_t *nblk, hipStream_t s) {
-    const uint64_t tiles = sweep_tiles(n);
-    const uint32_t g = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(tiles, 1), kH16Blocks);
-    *nblk = g;
+hipError_t launch_hist16(const uint32_t *in, uint64_t n, bool flip, uint32_t *part, uint64_t *fix,
+                         uint32_t *nblk, hipStream_t s) {
+    if (n == 0) return hipErrorInvalidValue;
+    const uint64_t pairs = (sweep_tiles(n) + 1) / 2;
+    // a multiple of kShards (shard of tile pair p == p % 8 == the counting workgroup % 8)
+    const uint64_t g = std::min<uint64_t>((pairs + kShards - 1) / kShards * kShards, kH16Blocks);
+    static_assert(kH16Blocks % kShards == 0, "K1h grid");
+    *nblk = (uint32_t)g;
     auto *fx = reinterpret_cast<unsigned long long *>(fix);
-    if (flip) k_counts_h16<1024, true><<<g, 1024, 0, s>>>(in, n, tcounts, part, fx);
-    else k_counts_h16<1024, false><<<g, 1024, 0, s>>>(in, n, tcounts, part, fx);
+    if (flip) k_hist16<1024, true><<<(unsigned)g, 1024, 0, s>>>(in, n, part, fx);
+    else k_hist16<1024, false><<<(unsigned)g, 1024, 0, s>>>(in, n, part, fx);
     return hipGetLastError();
 }
 
-hipError_t launch_plan_h16(const uint32_t *part, uint32_t nblk, const uint64_t *fix,
-                           const uint64_t *bases, const uint64_t *totals, uint64_t n, bool force,
-                           uint64_t *cstart, uint32_t *cur, uint32_t *tpfx, const WorkLists &wl2,
-                           const WorkLists &wl3, hipStream_t s) {
+hipError_t launch_plan16(const uint32_t *part, uint32_t nblk, const uint64_t *fix, uint64_t n,
+                         bool force, uint64_t *ccount, uint64_t *t3, uint64_t *tot,
+                         uint64_t *bases, uint64_t *totals, uint64_t *cstart, uint32_t *cur,
+                         uint32_t *cur3, uint32_t *tpfx, const WorkLists &wl2,
+                         const WorkLists &wl3, hipStream_t s) {
     using ull = unsigned long long;
-    k_plan_h16<<<kRadix, kRadix, 0, s>>>(
-        part, nblk, reinterpret_cast<const ull *>(fix), reinterpret_cast<const ull *>(bases),
-        reinterpret_cast<const ull *>(totals), n, force ? 1 : 0, reinterpret_cast<ull *>(cstart),
-        cur, tpfx, wl2, wl3);
+    if (nblk % kShards) return hipErrorInvalidValue;
+    k_plan16_count<<<kRadix, kRadix, 0, s>>>(part, nblk, reinterpret_cast<const ull *>(fix),
+                                              reinterpret_cast<ull *>(ccount),
+                                              reinterpret_cast<ull *>(t3),
+                                              reinterpret_cast<ull *>(tot));
+    k_plan16_place<<<kRadix, kRadix, 0, s>>>(
+        reinterpret_cast<const ull *>(ccount), reinterpret_cast<const ull *>(t3),
+        reinterpret_cast<const ull *>(tot), n, force ? 1 : 0, reinterpret_cast<ull *>(bases),
+        reinterpret_cast<ull *>(totals), reinterpret_cast<ull *>(cstart), cur, cur3, tpfx, wl2,
+        wl3);
     return hipGetLastError();
 }
 
-hipError_t launch_partition_h16(const uint32_t *in, uint32_t *out, uint16_t *out16, uint64_t n,
-                                const uint32_t *tpfx, const uint64_t *bases,
-                                const uint64_t *totals, uint32_t *cur, hipStream_t s) {
+hipError_t launch_partition3r(const uint32_t *in, uint32_t *out, uint64_t n, uint32_t *cur3,
+                              const uint64_t *bases, hipStream_t s) {
     using ull = unsigned long long;
     if (n == 0) return hipSuccess;
-    const unsigned g = (unsigned)(sweep_tiles(n) + kRadix);  // >= the level-2 tiles
+    constexpr int B = kPartBlock, I = kSweepTile / kPartBlock;
+    const uint64_t pairs = (sweep_tiles(n) + 1) / 2;
+    k_partition_res<B, I, true, true><<<(unsigned)pairs, B, 0, s>>>(
+        in, out, n, nullptr, nullptr, reinterpret_cast<const ull *>(bases), cur3);
+    return hipGetLastError();
+}
+
+hipError_t launch_partition2r(const uint32_t *in, uint32_t *out, uint16_t *out16, uint64_t n,
+                              const uint32_t *tpfx, void *tdesc, const uint64_t *bases,
+                              const uint64_t *totals, uint32_t *cur, hipStream_t s) {
+    using ull = unsigned long long;
+    if (n == 0) return hipSuccess;
     constexpr int B = kPartBlock, I = kSweepTile / kPartBlock;
     const ull *bs = reinterpret_cast<const ull *>(bases);
     const ull *tt = reinterpret_cast<const ull *>(totals);
-    uint32_t *cu = cur;
-    static const int pairs = [] {
-        const char *e = getenv("GSORT_K3A_PAIRS");
-        return e ? atoi(e) : 1;
-    }();
-    if (pairs) {
-        const unsigned g2 = (g + 1) / 2;
-        if (out16) k_partition2_h16<B, I, uint16_t><<<g2, B, 0, s>>>(in, out16, tpfx, bs, tt, cu);
-        else k_partition2_h16<B, I><<<g2, B, 0, s>>>(in, out, tpfx, bs, tt, cu);
-    } else if (out16) {
-        k_partition_h16<B, I, uint16_t><<<g, B, 0, s>>>(in, out16, tpfx, bs, tt, cu);
-    } else {
-        k_partition_h16<B, I><<<g, B, 0, s>>>(in, out, tpfx, bs, tt, cu);
-    }
+    // the level-2 tiles number at most sweep_tiles(n) + 256 (one partial tile per bucket)
+    const uint32_t max_tiles = (uint32_t)(sweep_tiles(n) + kRadix);
+    TileDesc *desc = static_cast<TileDesc *>(tdesc);
+    k_tile_desc<<<(max_tiles + 255) / 256, 256, 0, s>>>(tpfx, bs, tt, max_tiles, desc);
+    const unsigned g2 = (max_tiles + 1) / 2;
+    if (out16)
+        k_partition_res<B, I, false, false, uint16_t><<<g2, B, 0, s>>>(in, out16, n, tpfx, desc,
+                                                                        bs, cur);
+    else
+        k_partition_res<B, I, false, false><<<g2, B, 0, s>>>(in, out, n, tpfx, desc, bs, cur);
     return hipGetLastError();
 }
 

@@ -67,6 +67,8 @@ struct gsort_ctx {
     // level-2 cursors, K11 lists of the level-3 buckets; counters read while levels 3/2 run
     bool plan16 = true;
     DevBuf m_part, m_fix, m_cur, m_local3[kLocalClasses];
+    DevBuf m_ccount, m_t3, m_cur3;  // K12a child counts, per-shard level-3 counts + totals, K3r cursors
+    DevBuf m_tdesc;                 // K12c: K3a tile descriptors
     hipEvent_t ev_ctr = nullptr;
     DevBuf m_split;  // radix select thresholds + counts of the distributed radix
     DevBuf m_rpos, m_bsize;  // receive side: run bucket bounds (P x 65537), bucket size/start
@@ -510,6 +512,8 @@ void for_each_buf(gsort_ctx *c, F &&f) {
         {"m_gpfx", &c->m_gpfx}, {"m_segmap", &c->m_segmap}, {"m_groupmap", &c->m_groupmap},
         {"m_cstart", &c->m_cstart}, {"m_next0", &c->m_next[0]}, {"m_next1", &c->m_next[1]},
         {"m_part", &c->m_part}, {"m_fix", &c->m_fix}, {"m_cur", &c->m_cur},
+        {"m_ccount", &c->m_ccount}, {"m_t3", &c->m_t3}, {"m_cur3", &c->m_cur3},
+        {"m_tdesc", &c->m_tdesc},
         {"m_split", &c->m_split}, {"m_rpos", &c->m_rpos}, {"m_bsize", &c->m_bsize},
         {"m_bseg", &c->m_bseg}, {"m_blist", &c->m_blist}, {"m_gb", &c->m_gb},
         {"m_pack", &c->m_pack}, {"m_meta", &c->m_meta}, {"m_g16", &c->m_g16},
@@ -696,13 +700,14 @@ gsort_status msd_levels(gsort_ctx *c, int L, uint32_t *cur, uint32_t *out, uint3
 }
 
 
-// Levels 3 and 2 through the two-level plan (gsort_kernels.hip, "Two-level plan"): K1h + K2
-// + K12h, then K3u (level 3, in -> tmp) and K3a (level 2, tmp -> out, or the low 16 bits ->
-// out16 with group16).  The work-list counters are copied to the host right after K12h and read
-// once levels 3 and 2 are queued, so the GPU never waits on the host in the common case.  Then
-// K11 for the small level-3 buckets (three digits, tmp -> out) and for the level-2 children
-// (two digits, in place in out); children still larger than kLocalMax go on through
-// msd_levels from level 1.  cstart (65537 u64) receives the 16-bit bucket bounds.
+// Levels 3 and 2 through the two-level plan (gsort_kernels.hip, "Two-level plan"): K1h (the
+// 16-bit histogram) + K12a/K12b (counts, bases, bucket bounds, cursors, work lists), then K3r
+// (level 3, in -> tmp, runs reserved on per-shard bucket cursors) and K3a (level 2, tmp -> out,
+// or the low 16 bits -> out16 with group16).  The work-list counters are copied to the host
+// right after K12b and read once levels 3 and 2 are queued, so the GPU never waits on the host
+// in the common case.  Then K11 for the small level-3 buckets (three digits, tmp -> out) and
+// for the level-2 children (two digits, in place in out); children still larger than kLocalMax
+// go on through msd_levels from level 1.  cstart (65537 u64) receives the 16-bit bucket bounds.
 gsort_status msd_sort_h16(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *out,
                           uint32_t *tmp, gsort_stats *stats, bool group16, uint16_t *out16,
                           uint64_t *cstart) {
@@ -710,10 +715,15 @@ gsort_status msd_sort_h16(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
     uint64_t *bases = reinterpret_cast<uint64_t *>(c->d_small + OFF_BASES);
     uint64_t *ctr = reinterpret_cast<uint64_t *>(c->d_small + OFF_CTR);
     uint64_t *ctr3 = reinterpret_cast<uint64_t *>(c->d_small + OFF_CTR3);
+    constexpr size_t kFixBytes = (size_t)kH16Shards * kBuckets16 * 8;
     ST_TRY(ensure(c, c->m_part, (size_t)kH16Blocks * kH16PartWords * 4));
-    ST_TRY(ensure(c, c->m_fix, (size_t)kBuckets16 * 8));
+    ST_TRY(ensure(c, c->m_fix, kFixBytes));
     ST_TRY(ensure(c, c->m_cur, (size_t)kBuckets16 * 4));
     ST_TRY(ensure(c, c->m_tpfx, (kRadix + 1) * 4));
+    ST_TRY(ensure(c, c->m_ccount, (size_t)kBuckets16 * 8));
+    ST_TRY(ensure(c, c->m_t3, (size_t)(kH16Shards + 1) * kRadix * 8));
+    ST_TRY(ensure(c, c->m_cur3, (size_t)kH16Shards * kRadix * 4));
+    ST_TRY(ensure(c, c->m_tdesc, (size_t)(sweep_tiles(n) + kRadix) * kTileDescBytes));
     if (!cstart) {
         ST_TRY(ensure(c, c->m_cstart, (size_t)(kBuckets16 + 1) * 8));
         cstart = reinterpret_cast<uint64_t *>(c->m_cstart.p);
@@ -739,16 +749,19 @@ gsort_status msd_sort_h16(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
     }
     uint32_t *tpfx = reinterpret_cast<uint32_t *>(c->m_tpfx.p);
     uint32_t *cur = reinterpret_cast<uint32_t *>(c->m_cur.p);
+    uint32_t *cur3 = reinterpret_cast<uint32_t *>(c->m_cur3.p);
+    uint64_t *t3 = reinterpret_cast<uint64_t *>(c->m_t3.p);
     uint32_t nblk = 0;
     hipEvent_t t = tic(c);
-    HIP_TRY(c, hipMemsetAsync(c->m_fix.p, 0, (size_t)kBuckets16 * 8, c->stream));
+    HIP_TRY(c, hipMemsetAsync(c->m_fix.p, 0, kFixBytes, c->stream));
     if (!group16) HIP_TRY(c, hipMemsetAsync(ctr, 0, OFF_CTR3 + kCtrBytes - OFF_CTR, c->stream));
-    HIP_TRY(c, launch_counts_h16(in, n, true, d_tcounts(c), reinterpret_cast<uint32_t *>(c->m_part.p),
-                                 reinterpret_cast<uint64_t *>(c->m_fix.p), &nblk, c->stream));
-    HIP_TRY(c, launch_scan_tiles(d_tcounts(c), n, d_gsum(c), totals, bases, c->stream));
-    HIP_TRY(c, launch_plan_h16(reinterpret_cast<uint32_t *>(c->m_part.p), nblk,
-                               reinterpret_cast<uint64_t *>(c->m_fix.p), bases, totals, n, group16,
-                               cstart, cur, tpfx, wl2, wl3, c->stream));
+    HIP_TRY(c, launch_hist16(in, n, true, reinterpret_cast<uint32_t *>(c->m_part.p),
+                             reinterpret_cast<uint64_t *>(c->m_fix.p), &nblk, c->stream));
+    HIP_TRY(c, launch_plan16(reinterpret_cast<uint32_t *>(c->m_part.p), nblk,
+                             reinterpret_cast<uint64_t *>(c->m_fix.p), n, group16,
+                             reinterpret_cast<uint64_t *>(c->m_ccount.p), t3,
+                             t3 + (size_t)kH16Shards * kRadix, bases, totals, cstart, cur, cur3,
+                             tpfx, wl2, wl3, c->stream));
     toc(c, PH_COUNT, t);
     if (!group16) {
         HIP_TRY(c, hipMemcpyAsync(c->h_small + OFF_CTR, c->d_small + OFF_CTR,
@@ -756,11 +769,11 @@ gsort_status msd_sort_h16(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
         HIP_TRY(c, hipEventRecord(c->ev_ctr, c->stream));
     }
     t = tic(c);
-    HIP_TRY(c, launch_partition(in, tmp, n, 24, d_tcounts(c), d_gsum(c), bases, true, c->stream));
+    HIP_TRY(c, launch_partition3r(in, tmp, n, cur3, bases, c->stream));
     toc(c, PH_LEVEL3, t);
     t = tic(c);
-    HIP_TRY(c, launch_partition_h16(tmp, out, group16 ? out16 : nullptr, n, tpfx, bases, totals,
-                                    cur, c->stream));
+    HIP_TRY(c, launch_partition2r(tmp, out, group16 ? out16 : nullptr, n, tpfx, c->m_tdesc.p,
+                                  bases, totals, cur, c->stream));
     toc(c, PH_LEVEL2, t);
     if (stats) { stats->keys_level[0] += n; stats->keys_level[1] += n; }
     int levels = 2;
@@ -810,9 +823,9 @@ gsort_status msd_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *ou
         if (stats) { stats->buckets_local += 1; stats->keys_bucket_sort += n; }
         return GSORT_OK;
     }
-    ST_TRY(ensure_pass_scratch(c, n));
     if (c->plan16 && (!group16 || out16) && n < (1ull << 32))
         return msd_sort_h16(c, in, n, out, tmp, stats, group16, out16, group16 ? gb : nullptr);
+    ST_TRY(ensure_pass_scratch(c, n));
     uint64_t *totals = reinterpret_cast<uint64_t *>(c->d_small + OFF_TOT);
     uint64_t *bases = reinterpret_cast<uint64_t *>(c->d_small + OFF_BASES);
     ST_TRY(ensure_list(c, c->m_next[0], kRadix));
