@@ -100,6 +100,17 @@ gsort_status gsort_set_local_algo(gsort_ctx *ctx, int algo);
  * balanced buckets (gsort_plan_split_balanced).  The concatenated output is the same sorted
  * array either way; only the per-rank bucket sizes (gsort_sample_info) differ. */
 gsort_status gsort_set_sample_balanced(gsort_ctx *ctx, int on);
+/* Reference-compat radix: outside the parity domain (negative keys, P = 1,
+ * P = 3's digit under-count) the reference's radix sort is not a numeric sort but a stable sort
+ * of the values by the base-P digits of |v| it extracts (number_digit_at, mpi_radix_sort.c:54-58),
+ * number_digits(max element) of them (:48-52, :100), one stable pass each (:133-195).
+ * radix_p > 0: later gsort_radix calls reproduce that order for a reference run with radix_p
+ * processes (any rank count of this context; the order does not depend on the block layout);
+ * radix_p = -1: with P = this context's rank count; 0: off (numeric order, the default).
+ * Inputs on which the reference indexes outside its buckets (an INT_MIN key, Q5) or allocates a
+ * negative last block (N < (P-1) * ceil(N/P) + 1, Q8) return GSORT_EINVAL.  Inside the parity
+ * domain both orders are the same sorted array. */
+gsort_status gsort_set_ref_compat(gsort_ctx *ctx, int radix_p);
 const char *gsort_strerror(gsort_status st);
 const char *gsort_last_error(const gsort_ctx *ctx);
 int gsort_rank(const gsort_ctx *ctx);
@@ -202,6 +213,14 @@ gsort_status gsort_plan_split(int P, const uint64_t *n_all, const uint64_t *lt,
 gsort_status gsort_plan_split_balanced(int P, const uint64_t *n_all, const uint64_t *lt,
                                        const uint64_t *le, int me, uint64_t *send,
                                        uint64_t *recv);
+
+/* gsort_plan_ref_digits: the reference radix sort's digit plan with its own double math --
+ * loop = number_digits(max_element, P) (mpi_radix_sort.c:48-52, :100; <= 0 means no pass, as at
+ * P = 1), mod[d] = (int)pow(P, d+1) as x86 converts it (out of range -> INT_MIN) and
+ * scale[d] = pow(P, d) for d < loop (mpi_radix_sort.c:57).  mod / scale may be NULL; they must
+ * hold cap entries, and loop > cap with either given returns GSORT_EINVAL. */
+gsort_status gsort_plan_ref_digits(int P, int32_t max_element, int *loop, int32_t *mod,
+                                   double *scale, int cap);
 
 #ifdef __cplusplus
 }

@@ -30,10 +30,12 @@ hipError_t launch_tile_counts(const uint32_t *in, uint64_t n, int shift, bool fl
 hipError_t launch_scan_tiles(uint32_t *tcounts, uint64_t n, uint64_t *gsum, uint64_t *totals,
                              uint64_t *bases, hipStream_t s);
 // K3: one stable LSD pass over digit shift/8 using the K2 offsets; flip_in / flip_out apply
-// the int32 <-> ordered-u32 map on load / store.
+// the int32 <-> ordered-u32 map on load / store.  vin != nullptr: a key-value pass (value
+// vin[i] travels with key i into vout; no flips).
 hipError_t launch_scatter(const uint32_t *in, uint32_t *out, uint64_t n, int shift,
                           const uint32_t *toff, const uint64_t *gpfx, const uint64_t *bases,
-                          bool flip_in, bool flip_out, hipStream_t s);
+                          bool flip_in, bool flip_out, hipStream_t s,
+                          const uint32_t *vin = nullptr, uint32_t *vout = nullptr);
 // K8 receive-side placement: segs[k] = {src_off (in recv buffer), dst_off, len}; copies the
 // segments into out and (if hist != nullptr) accumulates the 256-bin histogram of digit
 // `next_shift/8` of the placed keys (ordered-u32 form); flip_out maps back to int32 on store.
@@ -211,6 +213,13 @@ hipError_t launch_lds_order_check(const uint32_t *digits, uint32_t nblocks, uint
 // Streaming copy of `bytes` (multiple of 16, 16-B aligned): one block per 16 KiB chunk, 16 B
 // per lane, nontemporal stores -- the bench's read + write ceiling.
 hipError_t launch_stream_copy(const void *in, void *out, uint64_t bytes, hipStream_t s);
+// Reference-compat key map: K20 mm[0] = min(mm[0], keys), mm[1] = max(..)
+// (mm preset by the caller); K19 key[i] = the mixed-radix number of the reference's base-P
+// digits 1..loop of |a[i]| (mod[d] = the reference's (int)pow(P, d+1) as x86 converts it,
+// scale[d] = pow(P, d)); bad[0] += keys the reference would put outside its buckets.
+hipError_t launch_minmax(const int32_t *a, uint64_t n, int *mm, hipStream_t s);
+hipError_t launch_compat_keys(const int32_t *a, uint64_t n, int P, int loop, const int *mod,
+                              const double *scale, uint32_t *key, uint64_t *bad, hipStream_t s);
 // Plain device copy kernel (used when a sort has no non-trivial pass).
 hipError_t launch_copy(const uint32_t *in, uint32_t *out, uint64_t n, hipStream_t s);
 

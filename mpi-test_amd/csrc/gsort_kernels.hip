@@ -214,19 +214,24 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t ntiles) {
 //      at kernel start.  Tiles are assigned to workgroups XCD-contiguously (xcd_tile).
 //   4. stream LDS out in order: consecutive lanes hit consecutive addresses within a digit.
 // ---------------------------------------------------------------------------------------
-template <int BLOCK, int ITEMS, bool FIN, bool FOUT>
+//   KV (the reference-compat sort, gsort_set_ref_compat): every key carries a 32-bit value
+//   (vin -> vout), scattered through LDS beside it, so the pass is a stable key-value pass.
+template <int BLOCK, int ITEMS, bool FIN, bool FOUT, bool KV = false>
 __global__ __launch_bounds__(BLOCK) void k_scatter(const uint32_t *__restrict__ in,
                                                    uint32_t *__restrict__ out, uint64_t n,
                                                    int shift,
                                                    const uint32_t *__restrict__ toff,
                                                    const unsigned long long *__restrict__ gpfx,
-                                                   const unsigned long long *__restrict__ bases) {
+                                                   const unsigned long long *__restrict__ bases,
+                                                   const uint32_t *__restrict__ vin = nullptr,
+                                                   uint32_t *__restrict__ vout = nullptr) {
     constexpr int WAVES = BLOCK / 64;
     constexpr int TILE = BLOCK * ITEMS;
     static_assert(TILE == kSweepTile, "K1/K2 count tiles of kSweepTile keys");
     static_assert(BLOCK >= kRadix, "one thread per digit in the scan");
     static_assert(TILE <= 65536, "ranks are packed as 16 bits");
     __shared__ uint32_t s_keys[TILE];
+    __shared__ uint32_t s_vals[KV ? TILE : 1];
     __shared__ uint32_t s_wofs[WAVES * kRadix];  // per-wave counts, then per-wave tile offsets
     __shared__ uint32_t *s_dst[kRadix];          // out + global offset - tile start, by digit
     __shared__ uint32_t s_wsum[kRadix / 64];
@@ -245,19 +250,29 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(const uint32_t *__restrict__ 
                    toff[(uint64_t)tile * kRadix + tid];
 
     uint32_t k[ITEMS];
+    uint32_t v[KV ? ITEMS : 1];
     {
-        const uint32_t *src = in + tbase + (uint64_t)w * 64 * ITEMS + lane;
+        const uint64_t o = (uint64_t)w * 64 * ITEMS + lane;
+        const uint32_t *src = in + tbase + o;
         if (full) {
 #pragma unroll
             for (int i = 0; i < ITEMS; ++i) k[i] = FIN ? (src[i * 64] ^ kFlip) : src[i * 64];
+            if constexpr (KV) {
+#pragma unroll
+                for (int i = 0; i < ITEMS; ++i) v[i] = vin[tbase + o + i * 64];
+            }
         } else {
             const uint64_t lim = n - tbase;  // valid keys in this tile
-            const uint64_t o = (uint64_t)w * 64 * ITEMS + lane;
 #pragma unroll
             for (int i = 0; i < ITEMS; ++i) {
                 // sentinels sort after every valid key of digit 255 (they are last in order)
                 k[i] = (o + i * 64 < lim) ? (FIN ? (src[i * 64] ^ kFlip) : src[i * 64])
                                           : 0xFFFFFFFFu;
+            }
+            if constexpr (KV) {
+#pragma unroll
+                for (int i = 0; i < ITEMS; ++i)
+                    v[i] = (o + i * 64 < lim) ? vin[tbase + o + i * 64] : 0u;
             }
         }
     }
@@ -324,6 +339,7 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(const uint32_t *__restrict__ 
         const uint32_t d = (k[i] >> shift) & 255u;
         const uint32_t r = (i & 1) ? (rk[i >> 1] >> 16) : (rk[i >> 1] & 0xFFFFu);
         s_keys[wc[d] + r] = k[i];
+        if constexpr (KV) s_vals[wc[d] + r] = v[i];
     }
     __syncthreads();
 
@@ -334,9 +350,80 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(const uint32_t *__restrict__ 
         const uint32_t j = (uint32_t)(i * BLOCK + tid);
         if (full || j < lim) {
             const uint32_t key = s_keys[j];
-            s_dst[(key >> shift) & 255u][j] = FOUT ? (key ^ kFlip) : key;
+            uint32_t *dst = s_dst[(key >> shift) & 255u] + j;
+            *dst = FOUT ? (key ^ kFlip) : key;
+            if constexpr (KV) vout[dst - out] = s_vals[j];
         }
     }
+}
+
+// ---------------------------------------------------------------------------------------
+// Reference-compat key map (gsort_set_ref_compat).  The reference
+// radix sort orders keys by base-P digits of |v| (mpi_radix_sort.c:54-58), number_digits(max)
+// of them (:48-52, :100), one stable pass per digit (:133-195): a stable sort of the values by
+// the mixed-radix number of those digits, which is |v| mod P^loop for in-range moduli.
+// K20 finds the min / max key (loop needs the max; INT_MIN has no |v|), K19 writes that
+// composite key for every value; the stable key-value LSD passes (k_scatter<.., KV>) then sort
+// the values by it.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_minmax(const int32_t *__restrict__ a, uint64_t n,
+                                                int *__restrict__ mm) {
+    int lo = 2147483647, hi = -2147483647 - 1;
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+        const int v = a[i];
+        lo = min(lo, v);
+        hi = max(hi, v);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        lo = min(lo, __shfl_xor(lo, o));
+        hi = max(hi, __shfl_xor(hi, o));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMin(&mm[0], lo);
+        atomicMax(&mm[1], hi);
+    }
+}
+
+// K19: key[i] = sum over d = 1..loop of digit_d(|v|) * P^(d-1), digit_d = x86_dtoi(rem / scale[d])
+// with rem = |v| % mod[d] (mod[d] = x86_dtoi(P^d), the reference's (int)pow; 0 or -1: 0).
+// bad[0] counts keys whose digit falls outside [0, P) or whose key does not fit 32 bits (the
+// reference indexes outside its buckets there).  The caller rejects INT_MIN beforehand.
+constexpr int kCompatMaxDigits = 64;
+struct CompatDigits {
+    int P, loop;
+    int mod[kCompatMaxDigits];
+    double scale[kCompatMaxDigits];
+    unsigned long long weight[kCompatMaxDigits];  // P^(d-1), saturated
+};
+
+__device__ __forceinline__ int x86_dtoi(double x) {
+    return (x > -2147483649.0 && x < 2147483648.0) ? (int)x : (-2147483647 - 1);
+}
+
+__global__ __launch_bounds__(256) void k_compat_keys(const int32_t *__restrict__ a, uint64_t n,
+                                                     CompatDigits cd, uint32_t *__restrict__ key,
+                                                     unsigned long long *__restrict__ bad) {
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    uint32_t nbad = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+        const int v = a[i];
+        const int mag = v < 0 ? -v : v;
+        unsigned long long k = 0;
+        bool ok = mag >= 0;
+        for (int d = 0; d < cd.loop; ++d) {
+            const int m = cd.mod[d];
+            const int rem = (m == 0 || m == -1) ? 0 : mag % m;
+            const int dig = x86_dtoi(__ddiv_rn((double)rem, cd.scale[d]));
+            ok &= dig >= 0 && dig < cd.P;
+            if (dig > 0) k += (unsigned long long)dig * cd.weight[d];
+        }
+        ok &= k < (1ull << 32);
+        key[i] = (uint32_t)k;
+        nbad += !ok;
+    }
+    if (nbad) atomicAdd(bad, (unsigned long long)nbad);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1935,13 +2022,18 @@ hipError_t launch_scan_tiles(uint32_t *tcounts, uint64_t n, uint64_t *gsum, uint
 
 hipError_t launch_scatter(const uint32_t *in, uint32_t *out, uint64_t n, int shift,
                           const uint32_t *toff, const uint64_t *gpfx, const uint64_t *bases,
-                          bool flip_in, bool flip_out, hipStream_t s) {
+                          bool flip_in, bool flip_out, hipStream_t s, const uint32_t *vin,
+                          uint32_t *vout) {
     if (n == 0) return hipSuccess;
     const unsigned g = (unsigned)sweep_tiles(n);
     auto *gp = reinterpret_cast<const unsigned long long *>(gpfx);
     auto *bs = reinterpret_cast<const unsigned long long *>(bases);
     constexpr int B = kSweepBlock, I = kSweepItems;
-    if (flip_in && flip_out)
+    if (vin) {  // the reference-compat key-value pass (keys are never flipped there)
+        if (flip_in || flip_out || !vout) return hipErrorInvalidValue;
+        k_scatter<B, I, false, false, true><<<g, B, 0, s>>>(in, out, n, shift, toff, gp, bs,
+                                                            vin, vout);
+    } else if (flip_in && flip_out)
         k_scatter<B, I, true, true><<<g, B, 0, s>>>(in, out, n, shift, toff, gp, bs);
     else if (flip_in)
         k_scatter<B, I, true, false><<<g, B, 0, s>>>(in, out, n, shift, toff, gp, bs);
@@ -2334,6 +2426,31 @@ hipError_t launch_stream_copy(const void *in, void *out, uint64_t bytes, hipStre
     if (grid > 0x7fffffffull) return hipErrorInvalidValue;
     k_stream_copy<<<(unsigned)grid, 256, 0, s>>>(static_cast<const u32x4 *>(in),
                                                  static_cast<u32x4 *>(out), n16);
+    return hipGetLastError();
+}
+
+hipError_t launch_minmax(const int32_t *a, uint64_t n, int *mm, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    k_minmax<<<grid_for(n, 256, 2048), 256, 0, s>>>(a, n, mm);
+    return hipGetLastError();
+}
+
+hipError_t launch_compat_keys(const int32_t *a, uint64_t n, int P, int loop, const int *mod,
+                              const double *scale, uint32_t *key, uint64_t *bad, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    if (P < 2 || loop < 1 || loop > kCompatMaxDigits) return hipErrorInvalidValue;
+    CompatDigits cd{};
+    cd.P = P;
+    cd.loop = loop;
+    unsigned long long w = 1;
+    for (int d = 0; d < loop; ++d) {
+        cd.mod[d] = mod[d];
+        cd.scale[d] = scale[d];
+        cd.weight[d] = w;
+        w = w > (1ull << 40) ? (1ull << 40) : w * (unsigned long long)P;  // digits there are 0
+    }
+    k_compat_keys<<<grid_for(n, 256, 2048), 256, 0, s>>>(
+        a, n, cd, key, reinterpret_cast<unsigned long long *>(bad));
     return hipGetLastError();
 }
 

@@ -6,6 +6,7 @@
 // the round trip: from the all-gathered per-rank digit counts every rank computes the global
 // position of each (source rank, digit) run and therefore which contiguous slice of its
 // locally digit-sorted block goes to which destination, and where received runs land.
+#include <math.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -144,4 +145,33 @@ extern "C" gsort_status gsort_plan_split_balanced(int P, const uint64_t *n_all,
                                                   const uint64_t *lt, const uint64_t *le, int me,
                                                   uint64_t *send, uint64_t *recv) {
     return plan_split(P, n_all, lt, le, me, send, recv, true);
+}
+
+// The reference radix sort's digit plan for the compat key map (gsort_set_ref_compat):
+//   loop     = number_digits(max_element, P) = (int)(log(|max| or 1) / log(P)) + 1
+//              (mpi_radix_sort.c:48-52, :91, :100; max_element starts at -1, :77)
+//   mod[d]   = (int)pow(P, d + 1)     the modulus of number_digit_at at position d + 1 (:57)
+//   scale[d] = pow(P, d)              its divisor
+// with glibc's log / pow and x86's double -> int conversion (cvttsd2si: every out-of-range
+// value, inf and nan become INT_MIN), so P = 1 gives loop = INT_MIN + 1 (no pass, quirk Q1) and
+// P = 3 reproduces the reference's floating-point digit under-count (Q3).
+static int x86_dtoi(double x) {
+    if (!(x > -2147483649.0 && x < 2147483648.0)) return INT32_MIN;
+    return (int)x;
+}
+
+extern "C" gsort_status gsort_plan_ref_digits(int P, int32_t max_element, int *loop,
+                                              int32_t *mod, double *scale, int cap) {
+    if (P < 1 || !loop) return GSORT_EINVAL;
+    const int64_t mag = max_element < 0 ? -(int64_t)max_element : max_element;
+    if (max_element == INT32_MIN) return GSORT_EINVAL;  // abs(INT_MIN) is undefined there
+    const double l = log(mag > 0 ? (double)mag : 1.0) / log((double)P);
+    const int lp = x86_dtoi(l);
+    *loop = lp == INT32_MIN ? INT32_MIN + 1 : lp + 1;
+    if (*loop > cap) return (mod || scale) ? GSORT_EINVAL : GSORT_OK;
+    for (int d = 0; d < *loop; ++d) {
+        if (mod) mod[d] = x86_dtoi(pow((double)P, (double)(d + 1)));
+        if (scale) scale[d] = pow((double)P, (double)d);
+    }
+    return GSORT_OK;
 }

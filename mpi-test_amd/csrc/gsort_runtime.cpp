@@ -59,6 +59,9 @@ struct gsort_ctx {
     DevBuf gsum;     // K2: per-group digit prefixes (u64 [groups][256])
     int local_algo = GSORT_LOCAL_MSD;
     bool sample_balanced = false;  // gsort_set_sample_balanced
+    int ref_compat = 0;            // gsort_set_ref_compat: 0 off, -1 P = nranks, else P
+    // reference-compat radix: composite keys (two), values in flight, min/max + bad counter
+    DevBuf m_ckey[2], m_vtmp[3], m_cmm;
     bool atomic_rank = false;  // LDS lane-order property verified on this device (create)
     // MSD scratch: segment plan/maps, child starts, work lists (u64 {start, len} pairs)
     DevBuf m_tpfx, m_gpfx, m_segmap, m_groupmap, m_cstart, m_next[2], m_local[kLocalClasses];
@@ -437,7 +440,8 @@ gsort_status count_tiles(gsort_ctx *c, const uint32_t *src, uint64_t n, int digi
 // K2 + K3: one stable LSD pass src -> dst over `digit`, tile counts already in tcounts.
 // The pass's 256 digit counts are left in the small area at OFF_TOT (used for routing).
 gsort_status scan_and_scatter(gsort_ctx *c, const uint32_t *src, uint32_t *dst, uint64_t n,
-                              int digit, bool flip_in, bool flip_out) {
+                              int digit, bool flip_in, bool flip_out,
+                              const uint32_t *vin = nullptr, uint32_t *vout = nullptr) {
     uint64_t *totals = reinterpret_cast<uint64_t *>(c->d_small + OFF_TOT);
     uint64_t *bases = reinterpret_cast<uint64_t *>(c->d_small + OFF_BASES);
     hipEvent_t t = tic(c);
@@ -445,7 +449,7 @@ gsort_status scan_and_scatter(gsort_ctx *c, const uint32_t *src, uint32_t *dst, 
     toc(c, PH_COUNT, t);
     t = tic(c);
     HIP_TRY(c, launch_scatter(src, dst, n, 8 * digit, d_tcounts(c), d_gsum(c), bases, flip_in,
-                              flip_out, c->stream));
+                              flip_out, c->stream, vin, vout));
     toc(c, PH_PASS0 + digit, t);
     return GSORT_OK;
 }
@@ -517,6 +521,8 @@ void for_each_buf(gsort_ctx *c, F &&f) {
         {"m_split", &c->m_split}, {"m_rpos", &c->m_rpos}, {"m_bsize", &c->m_bsize},
         {"m_bseg", &c->m_bseg}, {"m_blist", &c->m_blist}, {"m_gb", &c->m_gb},
         {"m_pack", &c->m_pack}, {"m_meta", &c->m_meta}, {"m_g16", &c->m_g16},
+        {"m_ckey0", &c->m_ckey[0]}, {"m_ckey1", &c->m_ckey[1]}, {"m_vtmp0", &c->m_vtmp[0]},
+        {"m_vtmp1", &c->m_vtmp[1]}, {"m_vtmp2", &c->m_vtmp[2]}, {"m_cmm", &c->m_cmm},
         {"small", &c->small}};
     for (const auto &nb : named) f(std::string(nb.first), *nb.second);
     static const char *slot_names[S_NSLOTS] = {"S_TMP",  "S_OUT", "S_CUR",  "S_SORTED",
@@ -1270,9 +1276,14 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
 // the ranks owning their global positions (one grouped send/recv round), then place the
 // received runs (K8).  Keeps the reference's invariant that rank q holds positions
 // [qB, (q+1)B) after each pass (mpi_radix_sort.c:139,:192) without moving keys through rank 0.
+// sort_keys != nullptr (the reference-compat sort): the passes sort the u32 keys sort_keys[i]
+// (never flipped) stably and d_keys[i] travels with them as the value; the output is the
+// values.  Keys and values go through the same exchange and placement, so the order is
+// (key, source rank, source order), the reference's per-pass order (mpi_radix_sort.c:164-192).
 gsort_status radix_dist(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in, int32_t **d_out,
-                        uint64_t *n_out, gsort_stats *stats) {
+                        uint64_t *n_out, gsort_stats *stats, const uint32_t *sort_keys = nullptr) {
     const int P = c->nranks, me = c->rank;
+    const bool kv = sort_keys != nullptr, fl = !kv;
     std::vector<uint64_t> n_all;
     ST_TRY(allgather_u64(c, n_in, n_all));
     uint64_t N = 0;
@@ -1281,6 +1292,9 @@ gsort_status radix_dist(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in, int3
     block_of(N, P, me, &B, &mine);
     const uint64_t cap = std::max<uint64_t>(std::max(n_in, B), 1);
     for (Slot s : {S_CUR, S_SORTED, S_RECV, S_OUT}) ST_TRY(ensure(c, c->slot[s], cap * 4));
+    if (kv)
+        for (DevBuf *b : {&c->slot[S_TMP], &c->m_vtmp[0], &c->m_vtmp[1], &c->m_vtmp[2]})
+            ST_TRY(ensure(c, *b, cap * 4));
     ST_TRY(ensure_pass_scratch(c, cap));
     if (N == 0) { *d_out = slot_ptr<int32_t>(c, S_OUT); *n_out = 0; return GSORT_OK; }
 
@@ -1289,10 +1303,10 @@ gsort_status radix_dist(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in, int3
     // same trivial digits.
     uint64_t *d_hist = reinterpret_cast<uint64_t *>(c->d_small + OFF_HIST);
     uint64_t *d_tot = reinterpret_cast<uint64_t *>(c->d_small + OFF_TOT);
+    const uint32_t *src = kv ? sort_keys : reinterpret_cast<const uint32_t *>(d_keys);
     HIP_TRY(c, hipMemsetAsync(d_hist, 0, 4 * kRadix * 8, c->stream));
     hipEvent_t t = tic(c);
-    HIP_TRY(c, launch_tile_counts(reinterpret_cast<const uint32_t *>(d_keys), n_in, 0, true,
-                                  d_tcounts(c), d_hist, c->stream));
+    HIP_TRY(c, launch_tile_counts(src, n_in, 0, fl, d_tcounts(c), d_hist, c->stream));
     toc(c, PH_COUNT, t);
     DevBuf &allh = c->slot[S_STAGE];
     ST_TRY(ensure(c, allh, (size_t)P * 4 * kRadix * 8));
@@ -1314,17 +1328,22 @@ gsort_status radix_dist(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in, int3
 
     std::vector<uint64_t> hp((size_t)P * kRadix), send(P), recv(P), seg((size_t)4 * P * kRadix);
     std::vector<size_t> sc(P), sd(P), rc(P), rd(P);
-    const uint32_t *src = reinterpret_cast<const uint32_t *>(d_keys);
     uint64_t n_src = n_in;
-    uint32_t *placed[2] = {slot_ptr<uint32_t>(c, S_CUR), slot_ptr<uint32_t>(c, S_OUT)};
+    uint32_t *placed[2] = {slot_ptr<uint32_t>(c, S_CUR), slot_ptr<uint32_t>(c, kv ? S_TMP : S_OUT)};
+    // kv: the values' source, sorted / received copies and placed blocks (the last into S_OUT)
+    const uint32_t *vsrc = reinterpret_cast<const uint32_t *>(d_keys);
+    uint32_t *vsorted = reinterpret_cast<uint32_t *>(c->m_vtmp[0].p);
+    uint32_t *vrecv = reinterpret_cast<uint32_t *>(c->m_vtmp[1].p);
+    uint32_t *vplaced = reinterpret_cast<uint32_t *>(c->m_vtmp[2].p);
     const int k = (int)active.size();
     for (int i = 0; i < k; ++i) {
         const int p = active[i];
         const bool first = i == 0, last = i == k - 1;
         // this rank's tile counts and totals of digit p, then everyone's totals
-        if (!(first && p == 0)) ST_TRY(count_tiles(c, src, n_src, p, first));
+        if (!(first && p == 0)) ST_TRY(count_tiles(c, src, n_src, p, first && fl));
         uint32_t *sorted = slot_ptr<uint32_t>(c, S_SORTED);
-        ST_TRY(scan_and_scatter(c, src, sorted, n_src, p, first, false));
+        ST_TRY(scan_and_scatter(c, src, sorted, n_src, p, first && fl, false, kv ? vsrc : nullptr,
+                                kv ? vsorted : nullptr));
         if (n_src == 0) HIP_TRY(c, hipMemsetAsync(d_tot, 0, kRadix * 8, c->stream));
         uint64_t *d_allt = reinterpret_cast<uint64_t *>(allh.p);
         ST_TRY(comm_try(c, c->comm->allgather(d_tot, d_allt, kRadix * 8, c->stream)));
@@ -1340,7 +1359,7 @@ gsort_status radix_dist(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in, int3
             sc[q] = send[q] * 4; sd[q] = so; so += sc[q];
             rc[q] = recv[q] * 4; rd[q] = ro; ro += rc[q];
             if (stats && q != me) {
-                stats->bytes_sent += sc[q];
+                stats->bytes_sent += sc[q] * (kv ? 2 : 1);
                 stats->max_pair_bytes = std::max<uint64_t>(stats->max_pair_bytes, sc[q]);
             }
         }
@@ -1348,6 +1367,9 @@ gsort_status radix_dist(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in, int3
         t = tic(c);
         ST_TRY(comm_try(c, c->comm->alltoallv(sorted, sc.data(), sd.data(), rbuf, rc.data(),
                                               rd.data(), c->stream)));
+        if (kv)
+            ST_TRY(comm_try(c, c->comm->alltoallv(vsorted, sc.data(), sd.data(), vrecv,
+                                                  rc.data(), rd.data(), c->stream)));
         toc(c, PH_EXCH, t);
         if (stats) stats->exchanges++;
         // placement table: {offset in recv buffer, dest offset, length}
@@ -1362,9 +1384,17 @@ gsort_status radix_dist(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in, int3
             h_seg[3 * s + 2] = seg[4 * s + 3];
         }
         HIP_TRY(c, hipMemcpyAsync(d_seg, h_seg, nseg * 24, hipMemcpyHostToDevice, c->stream));
-        uint32_t *dst = last ? slot_ptr<uint32_t>(c, S_OUT) : placed[i & 1];
+        uint32_t *dst = last && !kv ? slot_ptr<uint32_t>(c, S_OUT) : placed[i & 1];
         t = tic(c);
-        HIP_TRY(c, launch_place(rbuf, dst, d_seg, (int)nseg, mine, nullptr, 0, last, c->stream));
+        if (!(kv && last))  // kv: the keys of the last pass are not needed
+            HIP_TRY(c, launch_place(rbuf, dst, d_seg, (int)nseg, mine, nullptr, 0, last && fl,
+                                    c->stream));
+        if (kv) {
+            uint32_t *vdst = last ? slot_ptr<uint32_t>(c, S_OUT) : vplaced;
+            HIP_TRY(c, launch_place(vrecv, vdst, d_seg, (int)nseg, mine, nullptr, 0, false,
+                                    c->stream));
+            vsrc = vdst;
+        }
         toc(c, PH_PLACE, t);
         src = dst;
         n_src = mine;
@@ -1372,6 +1402,113 @@ gsort_status radix_dist(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in, int3
     if (stats) stats->passes_run = k;
     *d_out = slot_ptr<int32_t>(c, S_OUT);
     *n_out = mine;
+    return GSORT_OK;
+}
+
+// ---- reference-compat radix (gsort_set_ref_compat) -----------------------
+// The reference's radix sort is a stable sort of the values by the base-P digits of |v| that
+// number_digit_at extracts (mpi_radix_sort.c:54-58), loop = number_digits(max) of them (:100).
+// K20 + an all-gather give the global min / max, gsort_plan_ref_digits the reference's digit
+// plan, K19 the composite key of every value; then stable key-value LSD passes: locally, or
+// through radix_dist's exchange (kv), so rank q ends with positions [qB, (q+1)B).
+gsort_status radix_compat(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in, int32_t **d_out,
+                          uint64_t *n_out, gsort_stats *stats) {
+    const int Pref = c->ref_compat > 0 ? c->ref_compat : c->nranks;
+    std::vector<uint64_t> n_all;
+    ST_TRY(allgather_u64(c, n_in, n_all));
+    uint64_t N = 0;
+    for (uint64_t v : n_all) N += v;
+    const uint64_t Bref = (N + Pref - 1) / Pref;
+    if (N > 0 && (int64_t)N - (int64_t)(Bref * (uint64_t)(Pref - 1)) <= 0)
+        return set_err(c, GSORT_EINVAL, "ref compat: the reference's last block would be empty "
+                                        "(N < (P-1)*ceil(N/P) + 1, quirk Q8)");
+    const size_t cap = std::max<uint64_t>(n_in, 1) * 4;
+    ST_TRY(ensure(c, c->m_cmm, 16));
+    ST_TRY(ensure(c, c->m_ckey[0], cap));
+    // global min / max (K20)
+    int32_t *h_mm = reinterpret_cast<int32_t *>(c->h_small + OFF_PLAN);
+    HIP_TRY(c, hipStreamSynchronize(c->stream));  // h_small may feed an earlier copy
+    h_mm[0] = INT32_MAX;
+    h_mm[1] = INT32_MIN;
+    memset(h_mm + 2, 0, 8);  // K19's bad-key counter
+    HIP_TRY(c, hipMemcpyAsync(c->m_cmm.p, h_mm, 16, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, launch_minmax(d_keys, n_in, reinterpret_cast<int *>(c->m_cmm.p), c->stream));
+    HIP_TRY(c, hipMemcpyAsync(h_mm, c->m_cmm.p, 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    std::vector<uint64_t> mm;
+    ST_TRY(allgather_u64(c, (uint64_t)(uint32_t)h_mm[0] | ((uint64_t)(uint32_t)h_mm[1] << 32), mm));
+    int32_t gmin = INT32_MAX, gmax = -1;  // the reference's max_element starts at -1 (:77)
+    for (int r = 0; r < c->nranks; ++r) {
+        if (!n_all[r]) continue;
+        gmin = std::min(gmin, (int32_t)(uint32_t)mm[r]);
+        gmax = std::max(gmax, (int32_t)(uint32_t)(mm[r] >> 32));
+    }
+    if (N > 0 && gmin == INT32_MIN)
+        return set_err(c, GSORT_EINVAL, "ref compat: an INT_MIN key has no |v|; the reference "
+                                        "indexes a negative bucket there (quirk Q5)");
+    int loop = 0;
+    int32_t mod[64];
+    double scale[64];
+    if (gsort_plan_ref_digits(Pref, gmax, &loop, mod, scale, 64) != GSORT_OK)
+        return set_err(c, GSORT_EINVAL, "ref compat: digit plan");
+    uint32_t *key = reinterpret_cast<uint32_t *>(c->m_ckey[0].p);
+    if (loop < 1) {  // no pass (P = 1, Q1): the input order, only redistributed
+        HIP_TRY(c, hipMemsetAsync(key, 0, cap, c->stream));
+    } else {
+        HIP_TRY(c, launch_compat_keys(d_keys, n_in, Pref, loop, mod, scale, key,
+                                      reinterpret_cast<uint64_t *>(c->m_cmm.p) + 1, c->stream));
+        uint64_t *h_bad = reinterpret_cast<uint64_t *>(c->h_small + OFF_PLAN);
+        HIP_TRY(c, hipMemcpyAsync(h_bad, reinterpret_cast<uint64_t *>(c->m_cmm.p) + 1, 8,
+                                  hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        std::vector<uint64_t> bad;
+        ST_TRY(allgather_u64(c, *h_bad, bad));
+        for (uint64_t b : bad)
+            if (b) return set_err(c, GSORT_EINVAL, "ref compat: a digit outside [0, P) (the "
+                                                   "reference indexes outside its buckets)");
+    }
+    if (c->comm) return radix_dist(c, d_keys, n_in, d_out, n_out, stats, key);
+    // one rank: the stable key-value LSD passes locally (K1 + four histograms, K2, K3 kv)
+    ST_TRY(ensure(c, c->slot[S_OUT], cap));
+    ST_TRY(ensure(c, c->m_ckey[1], cap));
+    ST_TRY(ensure(c, c->m_vtmp[0], cap));
+    ST_TRY(ensure(c, c->m_vtmp[1], cap));
+    ST_TRY(ensure_pass_scratch(c, n_in));
+    *d_out = slot_ptr<int32_t>(c, S_OUT);
+    *n_out = n_in;
+    if (n_in == 0) return GSORT_OK;
+    uint64_t *d_hist = reinterpret_cast<uint64_t *>(c->d_small + OFF_HIST);
+    uint64_t *h_hist = reinterpret_cast<uint64_t *>(c->h_small + OFF_HIST);
+    HIP_TRY(c, hipMemsetAsync(d_hist, 0, 4 * kRadix * 8, c->stream));
+    hipEvent_t t = tic(c);
+    HIP_TRY(c, launch_tile_counts(key, n_in, 0, false, d_tcounts(c), d_hist, c->stream));
+    toc(c, PH_COUNT, t);
+    HIP_TRY(c, hipMemcpyAsync(h_hist, d_hist, 4 * kRadix * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    std::vector<int> active;
+    for (int p = 0; p < 4; ++p) {
+        const uint64_t *h = h_hist + p * kRadix;
+        if (*std::max_element(h, h + kRadix) < n_in) active.push_back(p);
+    }
+    if (active.empty()) {
+        HIP_TRY(c, launch_copy(reinterpret_cast<const uint32_t *>(d_keys),
+                               slot_ptr<uint32_t>(c, S_OUT), n_in, c->stream));
+        return GSORT_OK;
+    }
+    uint32_t *kb[2] = {key, reinterpret_cast<uint32_t *>(c->m_ckey[1].p)};
+    uint32_t *vb[2] = {reinterpret_cast<uint32_t *>(c->m_vtmp[0].p),
+                       reinterpret_cast<uint32_t *>(c->m_vtmp[1].p)};
+    const uint32_t *vsrc = reinterpret_cast<const uint32_t *>(d_keys);
+    const int k = (int)active.size();
+    for (int i = 0; i < k; ++i) {
+        const bool last = i == k - 1;
+        uint32_t *vdst = last ? slot_ptr<uint32_t>(c, S_OUT) : vb[i & 1];
+        if (!(i == 0 && active[0] == 0)) ST_TRY(count_tiles(c, kb[i & 1], n_in, active[i], false));
+        ST_TRY(scan_and_scatter(c, kb[i & 1], kb[(i & 1) ^ 1], n_in, active[i], false, false, vsrc,
+                                vdst));
+        vsrc = vdst;
+    }
+    if (stats) stats->passes_run = k;
     return GSORT_OK;
 }
 
@@ -1708,6 +1845,13 @@ gsort_status gsort_set_sample_balanced(gsort_ctx *c, int on) {
     return GSORT_OK;
 }
 
+gsort_status gsort_set_ref_compat(gsort_ctx *c, int radix_p) {
+    ST_TRY(check_ctx(c));
+    if (radix_p < -1) return set_err(c, GSORT_EINVAL, "ref compat: radix_p must be >= -1");
+    c->ref_compat = radix_p;
+    return GSORT_OK;
+}
+
 gsort_status gsort_radix(gsort_ctx *c, const int32_t *d_keys, size_t n_local, int32_t **d_out,
                          size_t *n_out, gsort_stats *stats) {
     ST_TRY(check_ctx(c));
@@ -1718,7 +1862,9 @@ gsort_status gsort_radix(gsort_ctx *c, const int32_t *d_keys, size_t n_local, in
     hipEvent_t t0 = tic(c);
     gsort_status st;
     uint64_t nout = 0;
-    if (!c->comm) {
+    if (c->ref_compat) {
+        st = radix_compat(c, d_keys, n_local, d_out, &nout, stats);
+    } else if (!c->comm) {
         const size_t cap = std::max<size_t>(n_local, 1) * 4;
         ST_TRY(ensure(c, c->slot[S_TMP], cap));
         ST_TRY(ensure(c, c->slot[S_OUT], cap));

@@ -75,7 +75,7 @@ EXPORTS = [
     "gsort_fingerprint", "gsort_device_alloc", "gsort_device_free", "gsort_copy_to_host",
     "gsort_copy_to_device", "gsort_onesweep_tile", "gsort_plan_radix_route",
     "gsort_plan_splitters", "gsort_plan_split", "gsort_plan_split_balanced", "gsort_parse_text",
-    "gsort_format_dump", "gsort_copy_ceiling",
+    "gsort_format_dump", "gsort_copy_ceiling", "gsort_set_ref_compat", "gsort_plan_ref_digits",
 ]
 
 _lib = None
@@ -126,6 +126,8 @@ def lib():
     L.gsort_plan_split.argtypes = [I, VP, VP, VP, I, VP, VP]
     L.gsort_plan_split_balanced.argtypes = [I, VP, VP, VP, I, VP, VP]
     L.gsort_set_sample_balanced.argtypes = [VP, I]
+    L.gsort_set_ref_compat.argtypes = [VP, I]
+    L.gsort_plan_ref_digits.argtypes = [I, ctypes.c_int32, P(I), VP, VP, I]
     L.gsort_parse_text.argtypes = [ctypes.c_char_p, SZ, VP, SZ, I]
     L.gsort_parse_text.restype = ctypes.c_longlong
     L.gsort_format_dump.argtypes = [VP, SZ, U64, VP, SZ, I]
@@ -203,6 +205,12 @@ class Context:
     def set_sample_balanced(self, on=True):
         """Duplicate-aware balanced sample-sort buckets (gsort_set_sample_balanced)."""
         self._c(lib().gsort_set_sample_balanced(self.h, 1 if on else 0))
+
+    def set_ref_compat(self, radix_p=-1):
+        """Reference-compat radix order (gsort_set_ref_compat): radix_p > 0 reproduces the
+        reference's output order for an `mpirun -np radix_p` run, -1 uses this context's rank
+        count, 0 restores the numeric sort."""
+        self._c(lib().gsort_set_ref_compat(self.h, radix_p))
 
     def _sort(self, fn, d_keys, n):
         out, nout, st = ctypes.c_void_p(), ctypes.c_size_t(), Stats()
@@ -326,6 +334,18 @@ def plan_splitters(samples, P):
     out = np.zeros(max(P - 1, 1), dtype=np.int32)
     _check(lib().gsort_plan_splitters(P, samples.ctypes.data, out.ctypes.data), None)
     return out[: P - 1]
+
+
+def plan_ref_digits(P, max_element, cap=64):
+    """Host-only reference digit plan (gsort_plan_ref_digits): (loop, mod, scale)."""
+    import numpy as np
+    loop = ctypes.c_int()
+    mod = np.zeros(cap, dtype=np.int32)
+    scale = np.zeros(cap, dtype=np.float64)
+    _check(lib().gsort_plan_ref_digits(P, max_element, ctypes.byref(loop), mod.ctypes.data,
+                                       scale.ctypes.data, cap), None)
+    k = max(loop.value, 0)
+    return loop.value, mod[:k], scale[:k]
 
 
 def parse_text(data, threads=1):

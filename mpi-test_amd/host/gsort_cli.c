@@ -45,8 +45,10 @@ static void check(gsort_status st, gsort_ctx *ctx, const char *what)
     die(msg);
 }
 
-/* rank-0 reader (mpi_radix_sort.c:73-97): whole file, then a %d-compatible parse */
-static int32_t *read_keys(const char *file, size_t *n_out)
+/* rank-0 reader (mpi_radix_sort.c:73-97): whole file, then a %d-compatible parse.
+ * phantom (reference-compat mode): the reference's !feof loop stores one more element -- a copy
+ * of the last value -- when anything follows the last number (quirk Q6, mpi_radix_sort.c:85-91) */
+static int32_t *read_keys(const char *file, size_t *n_out, int phantom)
 {
     char msg[4096 + 64];
     snprintf(msg, sizeof msg, "sort(): '%s' is not a valid file for read.", file);
@@ -62,8 +64,10 @@ static int32_t *read_keys(const char *file, size_t *n_out)
     int32_t *keys = malloc(cap * sizeof(int32_t));
     if (!keys) die(msg);
     long long n = gsort_parse_text(buf, len, keys, cap, 16);
+    const int trailing = len > 0 && strchr(" \t\n\v\f\r", buf[len - 1]) != NULL;
     free(buf);
     if (n <= 0) die(msg); /* empty or non-numeric: the reference never completes a valid run */
+    if (phantom && trailing && (size_t)n < cap) keys[n] = keys[n - 1], n++;
     *n_out = (size_t)n;
     return keys;
 }
@@ -110,11 +114,16 @@ int gsort_cli_main(int argc, char **argv, int algo)
     const char *file = argv[1];
     const int debug = argc == 3 ? atoi(argv[2]) : 0;
 
+    /* GSORT_REF_COMPAT=1 (radix_sort): the reference's own output order outside the parity
+     * domain -- negative keys, P = 1, P = 3 (gsort_set_ref_compat) -- and its reader's phantom
+     * element after trailing whitespace */
+    const char *cmp = getenv("GSORT_REF_COMPAT");
+    const int compat = algo == CLI_RADIX && cmp && atoi(cmp);
     int32_t *int_buf = NULL;
     unsigned long long n_total = 0;
     if (rank == 0) {
         size_t n;
-        int_buf = read_keys(file, &n);
+        int_buf = read_keys(file, &n, compat);
         n_total = n;
     }
 
@@ -132,6 +141,7 @@ int gsort_cli_main(int argc, char **argv, int algo)
     const char *bal = getenv("GSORT_SAMPLE_BALANCED");
     if (algo == CLI_SAMPLE && bal && atoi(bal))
         check(gsort_set_sample_balanced(ctx, 1), ctx, "gsort_set_sample_balanced");
+    if (compat) check(gsort_set_ref_compat(ctx, -1), ctx, "gsort_set_ref_compat");
 
     MPI_Barrier(MPI_COMM_WORLD);
     const double start = MPI_Wtime();

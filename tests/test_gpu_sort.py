@@ -208,8 +208,9 @@ def test_fingerprint_matches_oracle(ctx, orc):
 # ---------------------------------------------------------------------------------------
 # multi-rank on one GPU (in-process rank group)
 # ---------------------------------------------------------------------------------------
-def run_group(gsort, blocks, algo, local="msd", balanced=False):
-    """P ranks as P threads of this process, one context each, on one GPU."""
+def run_group(gsort, blocks, algo, local="msd", balanced=False, setup=None):
+    """P ranks as P threads of this process, one context each, on one GPU.  setup(ctx) runs
+    on every rank's context before the sort."""
     P = len(blocks)
     grp = gsort.Group(P)
     res, errs = [None] * P, []
@@ -219,6 +220,8 @@ def run_group(gsort, blocks, algo, local="msd", balanced=False):
             with gsort.Context(rank=r, group=grp) as c:
                 c.set_local_algo(gsort.LOCAL_MSD if local == "msd" else gsort.LOCAL_LSD)
                 c.set_sample_balanced(balanced)
+                if setup is not None:
+                    setup(c)
                 p = c.alloc(max(blocks[r].size, 1) * 4)
                 c.to_device(blocks[r], p)
                 fn = c.radix if algo == "radix" else c.sample
