@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--dist", choices=["uniform", "zipf"], default="uniform")
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-stats", action="store_true",
+                    help="experiment: time the steps without per-phase events")
     ap.add_argument("--local", choices=["msd", "lsd"], default="msd",
                     help="local sort algorithm (DESIGN.md 5)")
     ap.add_argument("--spawn", action="store_true",
@@ -334,11 +336,13 @@ def main():
     stats = []
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        _, n_out, st = fn(d_in, n_local)
+        _, n_out, st = fn(d_in, n_local, not a.no_stats)
         stats.append(st)
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
+    if a.no_stats:  # experiment: the un-instrumented step time; stats from extra steps
+        stats = [fn(d_in, n_local)[2] for _ in range(a.steps)]
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

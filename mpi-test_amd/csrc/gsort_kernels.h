@@ -13,6 +13,15 @@ constexpr int kScanGroup = 32;                           // tiles per K2a scan g
 constexpr int kPartBlock = 1024;                         // K3u: 1024 threads x 8 keys per tile
 constexpr int kRadix = 256;
 
+// Kernel-attached timing (gsort_kernels.hip, launch_k): while a timer is set on a thread, every
+// kernel that thread launches records its end into a fresh event from make(u) (last_stop).
+struct LaunchTimer {
+    hipEvent_t last_stop = nullptr;
+    hipEvent_t (*make)(void *) = nullptr;
+    void *u = nullptr;
+};
+void set_launch_timer(LaunchTimer *t);  // nullptr: untimed launches
+
 inline uint64_t sweep_tiles(uint64_t n) { return (n + kSweepTile - 1) / kSweepTile; }
 inline uint64_t scan_groups(uint64_t n) { return (sweep_tiles(n) + kScanGroup - 1) / kScanGroup; }
 
@@ -130,11 +139,16 @@ hipError_t launch_hist16(const uint32_t *in, uint64_t n, bool flip, uint32_t *pa
 // from their bucket's start), the K3a tile plan tpfx (257 u32) and the work lists (wl2:
 // children of level-2 buckets; wl3: level-3 buckets finished by K11; ctr == nullptr: not
 // filled).  force: every non-empty level-3 bucket is a level-2 bucket.
-hipError_t launch_plan16(const uint32_t *part, uint32_t nblk, const uint64_t *fix, uint64_t n,
+// K12a leaves fix zeroed for the next K1h and zeroes zero[0 .. nzero) (<= 256 u64: the
+// work-list counters) before K12b counts into them.
+hipError_t launch_plan16(const uint32_t *part, uint32_t nblk, uint64_t *fix, uint64_t n,
                          bool force, uint64_t *ccount, uint64_t *t3, uint64_t *tot,
                          uint64_t *bases, uint64_t *totals, uint64_t *cstart, uint32_t *cur,
                          uint32_t *cur3, uint32_t *tpfx, const WorkLists &wl2,
-                         const WorkLists &wl3, hipStream_t s);
+                         const WorkLists &wl3, uint64_t *zero, uint32_t nzero, hipStream_t s);
+// K12p: dst[0 .. n) = src[0 .. n) in pinned host memory, then *flag = seq (system release).
+hipError_t launch_publish(const uint64_t *src, uint32_t n, uint64_t *dst, uint64_t *flag,
+                          uint64_t seq, hipStream_t s);
 // K3r: level 3 of the int32 input by the top digit into out (ordered u32), runs reserved on cur3.
 hipError_t launch_partition3r(const uint32_t *in, uint32_t *out, uint64_t n, uint32_t *cur3,
                               const uint64_t *bases, hipStream_t s);

@@ -14,6 +14,8 @@
 //   K5     mpi_sample_sort.c:109-125 sort samples at the root, pick splitters
 //   K6     mpi_sample_sort.c:148-155 bucket partition (here: bounds on the sorted block)
 //   K8     mpi_radix_sort.c:164-192 per-pass placement (receive side of the exchange)
+#include <hip/hip_ext.h>
+
 #include "gsort_kernels.h"
 
 namespace gsort {
@@ -424,6 +426,22 @@ __global__ __launch_bounds__(256) void k_compat_keys(const int32_t *__restrict__
         nbad += !ok;
     }
     if (nbad) atomicAdd(bad, (unsigned long long)nbad);
+}
+
+// ---------------------------------------------------------------------------------------
+// K12p: publish n u64 counters to pinned host memory, then seq to *flag with a system-scope
+// release, so the host reads the MSD work-list counters by polling (no copy, no event on the
+// stream).  One workgroup of 64 threads.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_publish(const unsigned long long *__restrict__ src,
+                                                uint32_t n, unsigned long long *dst,
+                                                unsigned long long *flag,
+                                                unsigned long long seq) {
+    for (uint32_t i = threadIdx.x; i < n; i += 64) dst[i] = src[i];
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0)
+        __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1064,22 +1082,35 @@ __global__ __launch_bounds__(BLOCK) void k_hist16(const uint32_t *__restrict__ i
             load_tile<BLOCK, ITEMS, FIN>(in + (uint64_t)tn * kSweepTile + tid,
                                          lenn == (uint32_t)kSweepTile, lenn, kn);
         }
-        // all returning atomics in flight before the first wrap test
+        // all returning atomics in flight before the first wrap test; every tile but the
+        // input's last is full, and its atomics and wrap tests go without per-key bounds
+        // (tools/experiments/kexp13.hip: the bounded form cost 12 %)
         uint32_t old[ITEMS];
         bool wrap = false;
+        if (len == (uint32_t)kSweepTile) {
 #pragma unroll
-        for (int j = 0; j < ITEMS; ++j) {
-            old[j] = 0;
-            if ((uint32_t)(j * BLOCK) + tid < len) {
+            for (int j = 0; j < ITEMS; ++j) {
                 const uint32_t b = k[j] >> 16;
                 old[j] = atomicAdd(&s_h[b >> 1], 1u << ((b & 1u) << 4));
             }
-        }
 #pragma unroll
-        for (int j = 0; j < ITEMS; ++j)
-            wrap |= (uint32_t)(j * BLOCK) + tid < len &&
-                    ((old[j] >> (((k[j] >> 16) & 1u) << 4)) & 0xffffu) == 0xffffu;
-        if (wrap) {
+            for (int j = 0; j < ITEMS; ++j)
+                wrap |= ((old[j] >> (((k[j] >> 16) & 1u) << 4)) & 0xffffu) == 0xffffu;
+        } else {
+#pragma unroll
+            for (int j = 0; j < ITEMS; ++j) {
+                old[j] = 0;
+                if ((uint32_t)(j * BLOCK) + tid < len) {
+                    const uint32_t b = k[j] >> 16;
+                    old[j] = atomicAdd(&s_h[b >> 1], 1u << ((b & 1u) << 4));
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < ITEMS; ++j)
+                wrap |= (uint32_t)(j * BLOCK) + tid < len &&
+                        ((old[j] >> (((k[j] >> 16) & 1u) << 4)) & 0xffffu) == 0xffffu;
+        }
+        if (__builtin_expect(wrap, 0)) {
 #pragma unroll
             for (int j = 0; j < ITEMS; ++j) {
                 const uint32_t b = k[j] >> 16;
@@ -1130,12 +1161,17 @@ __device__ __forceinline__ unsigned long long block_excl_scan(unsigned long long
 // x = the e-half of word s*128 + e/2 summed over the partials b = x (mod 8), + fix[x][s*256+e].
 // Writes ccount[s*256+e] (all shards), t3[x*256+s] (bucket s in shard x) and tot[s].
 // nblk is a multiple of kShards.
+// K12a also leaves fix[] zeroed for the next K1h (each entry is read by one thread, then
+// cleared) and block 0 zeroes the nzero work-list counters at zero (K12b's atomics follow), so
+// a sort needs no memset before K1h.
 __global__ __launch_bounds__(kRadix) void k_plan16_count(const uint32_t *__restrict__ part,
                                                          uint32_t nblk,
-                                                         const unsigned long long *__restrict__ fix,
+                                                         unsigned long long *__restrict__ fix,
                                                          unsigned long long *__restrict__ ccount,
                                                          unsigned long long *__restrict__ t3,
-                                                         unsigned long long *__restrict__ tot) {
+                                                         unsigned long long *__restrict__ tot,
+                                                         unsigned long long *__restrict__ zero,
+                                                         uint32_t nzero) {
     constexpr uint32_t kWords = kBuckets16 / 2;
     __shared__ uint32_t s_lo[kShards][kRadix / 2], s_hi[kShards][kRadix / 2];
     __shared__ unsigned long long s_red[kShards][kRadix / 64];
@@ -1161,11 +1197,13 @@ __global__ __launch_bounds__(kRadix) void k_plan16_count(const uint32_t *__restr
     unsigned long long c = 0, cx[kShards];
 #pragma unroll
     for (uint32_t x = 0; x < kShards; ++x) {
-        cx[x] = (unsigned long long)((e & 1u) ? s_hi[x][w2] : s_lo[x][w2]) +
-                fix[(uint64_t)x * kBuckets16 + s * kRadix + e];
+        unsigned long long *f = &fix[(uint64_t)x * kBuckets16 + s * kRadix + e];
+        cx[x] = (unsigned long long)((e & 1u) ? s_hi[x][w2] : s_lo[x][w2]) + *f;
+        *f = 0;
         c += cx[x];
     }
     ccount[s * kRadix + e] = c;
+    if (s == 0 && e < nzero) zero[e] = 0;
 #pragma unroll
     for (uint32_t x = 0; x < kShards; ++x) {
         unsigned long long r = cx[x];
@@ -1980,10 +2018,31 @@ unsigned grid_for(uint64_t n, unsigned block, unsigned cap) {
 
 }  // namespace
 
+// Every kernel of the library launches through launch_k.  With a launch timer set on the
+// calling thread (the runtime's gsort_stats timing), the dispatch itself carries a fresh stop
+// event (hipExtLaunchKernel), so timing a sort adds no marker packets between its kernels: a
+// hipEventRecord between two kernels left ~5-8 us of idle, 4 % of a 2^28-key sort, and an
+// attached start event ~5 us (tools/experiments/launch_gap.hip).
+namespace {
+thread_local LaunchTimer *tl_timer = nullptr;
+}  // namespace
+
+void set_launch_timer(LaunchTimer *t) { tl_timer = t; }
+
+template <typename... KA, typename... A>
+inline void launch_k(void (*k)(KA...), dim3 g, dim3 b, uint32_t shm, hipStream_t s, A... a) {
+    hipEvent_t e1 = nullptr;
+    if (LaunchTimer *t = tl_timer) {
+        e1 = t->make(t->u);
+        if (e1) t->last_stop = e1;
+    }
+    hipExtLaunchKernelGGL(k, g, b, shm, s, nullptr, e1, 0u, static_cast<KA>(a)...);
+}
+
 hipError_t launch_generate(int dist, uint64_t seed, uint64_t start, uint64_t n, int32_t *out,
                            hipStream_t s) {
     if (n == 0) return hipSuccess;
-    k_generate<<<grid_for(n, 256, 4096), 256, 0, s>>>(dist, seed, start, n, out);
+    launch_k(k_generate, grid_for(n, 256, 4096), 256, 0, s, dist, seed, start, n, out);
     return hipGetLastError();
 }
 
@@ -1998,11 +2057,11 @@ hipError_t launch_tile_counts(const uint32_t *in, uint64_t n, int shift, bool fl
     const bool vec = (reinterpret_cast<uintptr_t>(in) & 15) == 0;
     if (hist4) {
         if (shift != 0) return hipErrorInvalidValue;  // ALL4 counts tiles by digit 0
-        if (vec) k_tile_counts<B, true, true><<<g, B, 0, s>>>(in, n, 0, fl, tcounts, h, ntiles);
-        else k_tile_counts<B, true, false><<<g, B, 0, s>>>(in, n, 0, fl, tcounts, h, ntiles);
+        if (vec) launch_k(k_tile_counts<B, true, true>, g, B, 0, s, in, n, 0, fl, tcounts, h, ntiles);
+        else launch_k(k_tile_counts<B, true, false>, g, B, 0, s, in, n, 0, fl, tcounts, h, ntiles);
     } else {
-        if (vec) k_tile_counts<B, false, true><<<g, B, 0, s>>>(in, n, shift, fl, tcounts, h, ntiles);
-        else k_tile_counts<B, false, false><<<g, B, 0, s>>>(in, n, shift, fl, tcounts, h, ntiles);
+        if (vec) launch_k(k_tile_counts<B, false, true>, g, B, 0, s, in, n, shift, fl, tcounts, h, ntiles);
+        else launch_k(k_tile_counts<B, false, false>, g, B, 0, s, in, n, shift, fl, tcounts, h, ntiles);
     }
     return hipGetLastError();
 }
@@ -2014,9 +2073,9 @@ hipError_t launch_scan_tiles(uint32_t *tcounts, uint64_t n, uint64_t *gsum, uint
     const uint32_t ng = (uint32_t)scan_groups(n);
     auto *gs = reinterpret_cast<unsigned long long *>(gsum);
     auto *tot = reinterpret_cast<unsigned long long *>(totals);
-    k_scan_tiles<<<ng, kRadix, 0, s>>>(tcounts, ntiles, gs);
-    k_scan_groups<<<kRadix, 1024, 0, s>>>(gs, ng, tot);
-    k_scan_digits<<<1, kRadix, 0, s>>>(tot, reinterpret_cast<unsigned long long *>(bases));
+    launch_k(k_scan_tiles, ng, kRadix, 0, s, tcounts, ntiles, gs);
+    launch_k(k_scan_groups, kRadix, 1024, 0, s, gs, ng, tot);
+    launch_k(k_scan_digits, 1, kRadix, 0, s, tot, reinterpret_cast<unsigned long long *>(bases));
     return hipGetLastError();
 }
 
@@ -2031,16 +2090,20 @@ hipError_t launch_scatter(const uint32_t *in, uint32_t *out, uint64_t n, int shi
     constexpr int B = kSweepBlock, I = kSweepItems;
     if (vin) {  // the reference-compat key-value pass (keys are never flipped there)
         if (flip_in || flip_out || !vout) return hipErrorInvalidValue;
-        k_scatter<B, I, false, false, true><<<g, B, 0, s>>>(in, out, n, shift, toff, gp, bs,
+        launch_k(k_scatter<B, I, false, false, true>, g, B, 0, s, in, out, n, shift, toff, gp, bs,
                                                             vin, vout);
     } else if (flip_in && flip_out)
-        k_scatter<B, I, true, true><<<g, B, 0, s>>>(in, out, n, shift, toff, gp, bs);
+        launch_k(k_scatter<B, I, true, true>, g, B, 0, s, in, out, n, shift, toff, gp, bs, nullptr,
+                 nullptr);
     else if (flip_in)
-        k_scatter<B, I, true, false><<<g, B, 0, s>>>(in, out, n, shift, toff, gp, bs);
+        launch_k(k_scatter<B, I, true, false>, g, B, 0, s, in, out, n, shift, toff, gp, bs, nullptr,
+                 nullptr);
     else if (flip_out)
-        k_scatter<B, I, false, true><<<g, B, 0, s>>>(in, out, n, shift, toff, gp, bs);
+        launch_k(k_scatter<B, I, false, true>, g, B, 0, s, in, out, n, shift, toff, gp, bs, nullptr,
+                 nullptr);
     else
-        k_scatter<B, I, false, false><<<g, B, 0, s>>>(in, out, n, shift, toff, gp, bs);
+        launch_k(k_scatter<B, I, false, false>, g, B, 0, s, in, out, n, shift, toff, gp, bs, nullptr,
+                 nullptr);
     return hipGetLastError();
 }
 
@@ -2050,7 +2113,7 @@ hipError_t launch_place(const uint32_t *recv, uint32_t *out, const uint64_t *seg
     if (n_out == 0 || nseg == 0) return hipSuccess;
     constexpr int B = 256, I = 16;
     const unsigned g = (unsigned)((n_out + B * I - 1) / (B * I));
-    k_place<B, I><<<g, B, 0, s>>>(recv, out, reinterpret_cast<const unsigned long long *>(segs),
+    launch_k(k_place<B, I>, g, B, 0, s, recv, out, reinterpret_cast<const unsigned long long *>(segs),
                                   nseg, n_out, reinterpret_cast<unsigned long long *>(hist),
                                   next_shift, flip_out ? kFlip : 0u);
     return hipGetLastError();
@@ -2059,14 +2122,14 @@ hipError_t launch_place(const uint32_t *recv, uint32_t *out, const uint64_t *seg
 hipError_t launch_fingerprint(const int32_t *keys, uint64_t n, unsigned long long *acc,
                               hipStream_t s) {
     if (n == 0) return hipSuccess;
-    k_fingerprint<<<grid_for(n, 256, 2048), 256, 0, s>>>(keys, n, acc);
+    launch_k(k_fingerprint, grid_for(n, 256, 2048), 256, 0, s, keys, n, acc);
     return hipGetLastError();
 }
 
 hipError_t launch_count_below(const int32_t *sorted, uint64_t n, const uint64_t *xs, int m,
                               uint64_t *out, hipStream_t s) {
     if (m <= 0) return hipSuccess;
-    k_count_below<<<(m + 255) / 256, 256, 0, s>>>(sorted, n,
+    launch_k(k_count_below, (m + 255) / 256, 256, 0, s, sorted, n,
                                                   reinterpret_cast<const unsigned long long *>(xs),
                                                   m, reinterpret_cast<unsigned long long *>(out));
     return hipGetLastError();
@@ -2074,21 +2137,21 @@ hipError_t launch_count_below(const int32_t *sorted, uint64_t n, const uint64_t 
 
 hipError_t launch_regular_sample(const int32_t *sorted, uint64_t interval, int k, int32_t *out,
                                  hipStream_t s) {
-    k_regular_sample<<<1, 64 * ((k + 63) / 64), 0, s>>>(sorted, interval, k, out);
+    launch_k(k_regular_sample, 1, 64 * ((k + 63) / 64), 0, s, sorted, interval, k, out);
     return hipGetLastError();
 }
 
 hipError_t launch_select_splitters(const int32_t *samples, int m, int k, int nsplit,
                                    int32_t *splitters, hipStream_t s) {
     if (m > 1024 || nsplit <= 0) return nsplit <= 0 ? hipSuccess : hipErrorInvalidValue;
-    k_select_splitters<<<1, 1024, 0, s>>>(samples, m, k, nsplit, splitters);
+    launch_k(k_select_splitters, 1, 1024, 0, s, samples, m, k, nsplit, splitters);
     return hipGetLastError();
 }
 
 hipError_t launch_bucket_bounds(const int32_t *sorted, uint64_t n, const int32_t *splitters,
                                 int nsplit, uint64_t *bounds, hipStream_t s, bool strict) {
     if (nsplit <= 0) return hipSuccess;
-    k_bucket_bounds<<<nsplit, 64, 0, s>>>(sorted, n, splitters,
+    launch_k(k_bucket_bounds, nsplit, 64, 0, s, sorted, n, splitters,
                                           reinterpret_cast<unsigned long long *>(bounds),
                                           strict ? 1 : 0);
     return hipGetLastError();
@@ -2099,10 +2162,10 @@ hipError_t launch_tile_counts1(const uint32_t *in, uint64_t n, int shift, bool f
     if (n == 0) return hipSuccess;
     const unsigned g = (unsigned)sweep_tiles(n);
     if (flip)
-        k_seg_counts<512, false, true><<<g, 512, 0, s>>>(in, n, nullptr, nullptr, nullptr, nullptr,
+        launch_k(k_seg_counts<512, false, true>, g, 512, 0, s, in, n, nullptr, nullptr, nullptr, nullptr,
                                                          0, shift, tcounts);
     else
-        k_seg_counts<512, false, false><<<g, 512, 0, s>>>(in, n, nullptr, nullptr, nullptr,
+        launch_k(k_seg_counts<512, false, false>, g, 512, 0, s, in, n, nullptr, nullptr, nullptr,
                                                           nullptr, 0, shift, tcounts);
     return hipGetLastError();
 }
@@ -2115,15 +2178,15 @@ hipError_t launch_partition(const uint32_t *in, uint32_t *out, uint64_t n, int s
     auto *gp = reinterpret_cast<const unsigned long long *>(gpfx);
     auto *bs = reinterpret_cast<const unsigned long long *>(bases);
     constexpr int B = kPartBlock, I = kSweepTile / kPartBlock;
-    if (flip_in) k_partition<B, I, true><<<g, B, 0, s>>>(in, out, n, shift, toff, gp, bs);
-    else k_partition<B, I, false><<<g, B, 0, s>>>(in, out, n, shift, toff, gp, bs);
+    if (flip_in) launch_k(k_partition<B, I, true>, g, B, 0, s, in, out, n, shift, toff, gp, bs);
+    else launch_k(k_partition<B, I, false>, g, B, 0, s, in, out, n, shift, toff, gp, bs);
     return hipGetLastError();
 }
 
 hipError_t launch_classify_buckets(const uint64_t *bases, const uint64_t *totals,
                                    const WorkLists &wl, hipStream_t s) {
     using ull = unsigned long long;
-    k_classify_buckets<<<1, kRadix, 0, s>>>(reinterpret_cast<const ull *>(bases),
+    launch_k(k_classify_buckets, 1, kRadix, 0, s, reinterpret_cast<const ull *>(bases),
                                             reinterpret_cast<const ull *>(totals), wl);
     return hipGetLastError();
 }
@@ -2133,13 +2196,13 @@ hipError_t launch_seg_count(const SegPass &sp, hipStream_t s) {
     if (sp.nseg == 0) return hipSuccess;
     const ull *segs = reinterpret_cast<const ull *>(sp.segs);
     ull *gsum = reinterpret_cast<ull *>(sp.gsum);
-    k_seg_plan<<<1, 1024, 0, s>>>(segs, sp.nseg, sp.tpfx, sp.gpfx);
-    k_seg_map<<<sp.nseg, 256, 0, s>>>(sp.tpfx, sp.gpfx, sp.segmap, sp.groupmap);
-    k_seg_counts<512, true, false><<<sp.max_tiles, 512, 0, s>>>(
+    launch_k(k_seg_plan, 1, 1024, 0, s, segs, sp.nseg, sp.tpfx, sp.gpfx);
+    launch_k(k_seg_map, sp.nseg, 256, 0, s, sp.tpfx, sp.gpfx, sp.segmap, sp.groupmap);
+    launch_k(k_seg_counts<512, true, false>, sp.max_tiles, 512, 0, s,
         sp.in, 0, segs, sp.tpfx, sp.gpfx, sp.segmap, sp.nseg, sp.shift, sp.tcounts);
-    k_seg_scan_tiles<<<sp.max_groups, kRadix, 0, s>>>(sp.tcounts, sp.tpfx, sp.gpfx, sp.groupmap,
+    launch_k(k_seg_scan_tiles, sp.max_groups, kRadix, 0, s, sp.tcounts, sp.tpfx, sp.gpfx, sp.groupmap,
                                                       sp.nseg, gsum);
-    k_seg_scan_groups<<<sp.nseg, kRadix, 0, s>>>(gsum, segs, sp.gpfx,
+    launch_k(k_seg_scan_groups, sp.nseg, kRadix, 0, s, gsum, segs, sp.gpfx,
                                                  reinterpret_cast<ull *>(sp.cstart), sp.lists);
     return hipGetLastError();
 }
@@ -2151,15 +2214,15 @@ hipError_t launch_seg_partition(const SegPass &sp, hipStream_t s) {
     ull *gsum = reinterpret_cast<ull *>(sp.gsum);
     constexpr int B = kPartBlock, I = kSweepTile / kPartBlock;
     if (sp.out16)
-        k_seg_partition<B, I, false, uint16_t><<<sp.max_tiles, B, 0, s>>>(
+        launch_k(k_seg_partition<B, I, false, uint16_t>, sp.max_tiles, B, 0, s,
             sp.in, sp.out16, sp.shift, sp.tcounts, gsum, reinterpret_cast<const ull *>(sp.cstart),
             segs, sp.tpfx, sp.gpfx, sp.segmap, sp.nseg);
     else if (sp.flip_out)
-        k_seg_partition<B, I, true><<<sp.max_tiles, B, 0, s>>>(
+        launch_k(k_seg_partition<B, I, true>, sp.max_tiles, B, 0, s,
             sp.in, sp.out, sp.shift, sp.tcounts, gsum, reinterpret_cast<const ull *>(sp.cstart),
             segs, sp.tpfx, sp.gpfx, sp.segmap, sp.nseg);
     else
-        k_seg_partition<B, I, false><<<sp.max_tiles, B, 0, s>>>(
+        launch_k(k_seg_partition<B, I, false>, sp.max_tiles, B, 0, s,
             sp.in, sp.out, sp.shift, sp.tcounts, gsum, reinterpret_cast<const ull *>(sp.cstart),
             segs, sp.tpfx, sp.gpfx, sp.segmap, sp.nseg);
     return hipGetLastError();
@@ -2174,23 +2237,22 @@ hipError_t launch_hist16(const uint32_t *in, uint64_t n, bool flip, uint32_t *pa
     static_assert(kH16Blocks % kShards == 0, "K1h grid");
     *nblk = (uint32_t)g;
     auto *fx = reinterpret_cast<unsigned long long *>(fix);
-    if (flip) k_hist16<1024, true><<<(unsigned)g, 1024, 0, s>>>(in, n, part, fx);
-    else k_hist16<1024, false><<<(unsigned)g, 1024, 0, s>>>(in, n, part, fx);
+    if (flip) launch_k(k_hist16<1024, true>, (unsigned)g, 1024, 0, s, in, n, part, fx);
+    else launch_k(k_hist16<1024, false>, (unsigned)g, 1024, 0, s, in, n, part, fx);
     return hipGetLastError();
 }
 
-hipError_t launch_plan16(const uint32_t *part, uint32_t nblk, const uint64_t *fix, uint64_t n,
+hipError_t launch_plan16(const uint32_t *part, uint32_t nblk, uint64_t *fix, uint64_t n,
                          bool force, uint64_t *ccount, uint64_t *t3, uint64_t *tot,
                          uint64_t *bases, uint64_t *totals, uint64_t *cstart, uint32_t *cur,
                          uint32_t *cur3, uint32_t *tpfx, const WorkLists &wl2,
-                         const WorkLists &wl3, hipStream_t s) {
+                         const WorkLists &wl3, uint64_t *zero, uint32_t nzero, hipStream_t s) {
     using ull = unsigned long long;
-    if (nblk % kShards) return hipErrorInvalidValue;
-    k_plan16_count<<<kRadix, kRadix, 0, s>>>(part, nblk, reinterpret_cast<const ull *>(fix),
-                                              reinterpret_cast<ull *>(ccount),
-                                              reinterpret_cast<ull *>(t3),
-                                              reinterpret_cast<ull *>(tot));
-    k_plan16_place<<<kRadix, kRadix, 0, s>>>(
+    if (nblk % kShards || nzero > kRadix) return hipErrorInvalidValue;
+    launch_k(k_plan16_count, kRadix, kRadix, 0, s, part, nblk, reinterpret_cast<ull *>(fix),
+             reinterpret_cast<ull *>(ccount), reinterpret_cast<ull *>(t3),
+             reinterpret_cast<ull *>(tot), reinterpret_cast<ull *>(zero), zero ? nzero : 0u);
+    launch_k(k_plan16_place, kRadix, kRadix, 0, s,
         reinterpret_cast<const ull *>(ccount), reinterpret_cast<const ull *>(t3),
         reinterpret_cast<const ull *>(tot), n, force ? 1 : 0, reinterpret_cast<ull *>(bases),
         reinterpret_cast<ull *>(totals), reinterpret_cast<ull *>(cstart), cur, cur3, tpfx, wl2,
@@ -2204,7 +2266,7 @@ hipError_t launch_partition3r(const uint32_t *in, uint32_t *out, uint64_t n, uin
     if (n == 0) return hipSuccess;
     constexpr int B = kPartBlock, I = kSweepTile / kPartBlock;
     const uint64_t pairs = (sweep_tiles(n) + 1) / 2;
-    k_partition_res<B, I, true, true><<<(unsigned)pairs, B, 0, s>>>(
+    launch_k(k_partition_res<B, I, true, true>, (unsigned)pairs, B, 0, s,
         in, out, n, nullptr, nullptr, reinterpret_cast<const ull *>(bases), cur3);
     return hipGetLastError();
 }
@@ -2220,20 +2282,20 @@ hipError_t launch_partition2r(const uint32_t *in, uint32_t *out, uint16_t *out16
     // the level-2 tiles number at most sweep_tiles(n) + 256 (one partial tile per bucket)
     const uint32_t max_tiles = (uint32_t)(sweep_tiles(n) + kRadix);
     TileDesc *desc = static_cast<TileDesc *>(tdesc);
-    k_tile_desc<<<(max_tiles + 255) / 256, 256, 0, s>>>(tpfx, bs, tt, max_tiles, desc);
+    launch_k(k_tile_desc, (max_tiles + 255) / 256, 256, 0, s, tpfx, bs, tt, max_tiles, desc);
     const unsigned g2 = (max_tiles + 1) / 2;
     if (out16)
-        k_partition_res<B, I, false, false, uint16_t><<<g2, B, 0, s>>>(in, out16, n, tpfx, desc,
+        launch_k(k_partition_res<B, I, false, false, uint16_t>, g2, B, 0, s, in, out16, n, tpfx, desc,
                                                                         bs, cur);
     else
-        k_partition_res<B, I, false, false><<<g2, B, 0, s>>>(in, out, n, tpfx, desc, bs, cur);
+        launch_k(k_partition_res<B, I, false, false>, g2, B, 0, s, in, out, n, tpfx, desc, bs, cur);
     return hipGetLastError();
 }
 
 hipError_t launch_unpack16(const uint16_t *in, uint64_t n, uint32_t h, int32_t *out,
                            hipStream_t s) {
     if (n == 0) return hipSuccess;
-    k_unpack16<<<grid_for(n, 256, 4096), 256, 0, s>>>(in, n, h, out);
+    launch_k(k_unpack16, grid_for(n, 256, 4096), 256, 0, s, in, n, h, out);
     return hipGetLastError();
 }
 
@@ -2241,7 +2303,7 @@ hipError_t launch_gb_from_plan(const uint64_t *bases, const uint64_t *totals,
                                const uint64_t *segs, uint32_t nseg, const uint64_t *cstart,
                                uint64_t n, uint64_t *gb, hipStream_t s) {
     using ull = unsigned long long;
-    k_gb_from_plan<<<kRadix, kRadix, 0, s>>>(
+    launch_k(k_gb_from_plan, kRadix, kRadix, 0, s,
         reinterpret_cast<const ull *>(bases), reinterpret_cast<const ull *>(totals),
         reinterpret_cast<const ull *>(segs), nseg, reinterpret_cast<const ull *>(cstart), n,
         reinterpret_cast<ull *>(gb));
@@ -2252,7 +2314,7 @@ hipError_t launch_count_below16(const uint16_t *a, const uint64_t *gb, const uin
                                 int m, uint64_t *out, hipStream_t s) {
     using ull = unsigned long long;
     if (m <= 0) return hipSuccess;
-    k_count_below16<<<(m + 255) / 256, 256, 0, s>>>(a, reinterpret_cast<const ull *>(gb),
+    launch_k(k_count_below16, (m + 255) / 256, 256, 0, s, a, reinterpret_cast<const ull *>(gb),
                                                     reinterpret_cast<const ull *>(xs), m,
                                                     reinterpret_cast<ull *>(out));
     return hipGetLastError();
@@ -2268,11 +2330,11 @@ hipError_t launch_local_sort(const uint32_t *in, uint32_t *out, const uint64_t *
     do {                                                                                       \
         static_assert((uint64_t)B * I == kLocalCap[cls_of(B, I)], "class geometry");          \
         if (atomic_rank) {                                                                     \
-            if (flip_in) k_local_sort<B, I, true, true><<<nlist, B, 0, s>>>(in, out, l, ndigits); \
-            else k_local_sort<B, I, false, true><<<nlist, B, 0, s>>>(in, out, l, ndigits);        \
+            if (flip_in) launch_k(k_local_sort<B, I, true, true>, nlist, B, 0, s, in, out, l, ndigits); \
+            else launch_k(k_local_sort<B, I, false, true>, nlist, B, 0, s, in, out, l, ndigits);        \
         } else {                                                                               \
-            if (flip_in) k_local_sort<B, I, true, false><<<nlist, B, 0, s>>>(in, out, l, ndigits); \
-            else k_local_sort<B, I, false, false><<<nlist, B, 0, s>>>(in, out, l, ndigits);       \
+            if (flip_in) launch_k(k_local_sort<B, I, true, false>, nlist, B, 0, s, in, out, l, ndigits); \
+            else launch_k(k_local_sort<B, I, false, false>, nlist, B, 0, s, in, out, l, ndigits);       \
         }                                                                                      \
     } while (0)
     switch (cls) {
@@ -2289,7 +2351,7 @@ hipError_t launch_run_bounds(const int32_t *recv, const uint64_t *roff, const ui
     using ull = unsigned long long;
     if (P < 1 || P > 64) return hipErrorInvalidValue;
     const uint64_t m = (uint64_t)P * (kBuckets16 + 1);
-    k_run_bounds<<<(unsigned)((m + 255) / 256), 256, 0, s>>>(
+    launch_k(k_run_bounds, (unsigned)((m + 255) / 256), 256, 0, s,
         recv, reinterpret_cast<const ull *>(roff), reinterpret_cast<const ull *>(rlen), P,
         reinterpret_cast<ull *>(pos));
     return hipGetLastError();
@@ -2302,8 +2364,8 @@ hipError_t launch_pos_from_meta(const uint32_t *meta, const uint64_t *moff, uint
     if (P < 1 || P > 64) return hipErrorInvalidValue;
     const MetaCounts gen{meta, reinterpret_cast<const ull *>(moff), h_lo, nh};
     ull *part = reinterpret_cast<ull *>(scratch);
-    k_rowscan_reduce<<<dim3(kScanBlocks, P), 1024, 0, s>>>(gen, part);
-    k_rowscan_apply<<<dim3(kScanBlocks, P), 1024, 0, s>>>(gen, part, reinterpret_cast<ull *>(pos),
+    launch_k(k_rowscan_reduce<decltype(gen)>, dim3(kScanBlocks, P), 1024, 0, s, gen, part);
+    launch_k(k_rowscan_apply<decltype(gen)>, dim3(kScanBlocks, P), 1024, 0, s, gen, part, reinterpret_cast<ull *>(pos),
                                                           kBuckets16 + 1);
     return hipGetLastError();
 }
@@ -2311,14 +2373,14 @@ hipError_t launch_pos_from_meta(const uint32_t *meta, const uint64_t *moff, uint
 hipError_t launch_recv_classify(const uint64_t *pos, int P, uint64_t *bsize, uint64_t *bstart,
                                 const WorkLists &wl, uint64_t *scratch, hipStream_t s) {
     using ull = unsigned long long;
-    k_bucket_sizes<<<kBuckets16 / 256, 256, 0, s>>>(reinterpret_cast<const ull *>(pos), P,
+    launch_k(k_bucket_sizes, kBuckets16 / 256, 256, 0, s, reinterpret_cast<const ull *>(pos), P,
                                                      reinterpret_cast<ull *>(bsize));
     const RowValues gen{reinterpret_cast<const ull *>(bsize)};
     ull *part = reinterpret_cast<ull *>(scratch);
-    k_rowscan_reduce<<<dim3(kScanBlocks, 1), 1024, 0, s>>>(gen, part);
-    k_rowscan_apply<<<dim3(kScanBlocks, 1), 1024, 0, s>>>(gen, part, reinterpret_cast<ull *>(bstart),
+    launch_k(k_rowscan_reduce<decltype(gen)>, dim3(kScanBlocks, 1), 1024, 0, s, gen, part);
+    launch_k(k_rowscan_apply<decltype(gen)>, dim3(kScanBlocks, 1), 1024, 0, s, gen, part, reinterpret_cast<ull *>(bstart),
                                                           kBuckets16 + 1);
-    k_classify_gather<<<kBuckets16 / kRadix, kRadix, 0, s>>>(
+    launch_k(k_classify_gather, kBuckets16 / kRadix, kRadix, 0, s,
         reinterpret_cast<const ull *>(bsize), reinterpret_cast<const ull *>(bstart), wl);
     return hipGetLastError();
 }
@@ -2338,8 +2400,8 @@ hipError_t launch_gather_sort(const void *recv, bool packed16, const uint64_t *p
     auto *r16 = reinterpret_cast<const uint16_t *>(recv);
 #define GSORT_K11G(B, I, AT)                                                                   \
     do {                                                                                       \
-        if (packed16) k_gather_sort<B, I, AT><<<nlist, B, 0, s>>>(r16, ps, ro, P, bs, l, out); \
-        else k_gather_sort<B, I, AT><<<nlist, B, 0, s>>>(r32, ps, ro, P, bs, l, out);          \
+        if (packed16) launch_k(k_gather_sort<B, I, AT, uint16_t>, nlist, B, 0, s, r16, ps, ro, P, bs, l, out); \
+        else launch_k(k_gather_sort<B, I, AT, int32_t>, nlist, B, 0, s, r32, ps, ro, P, bs, l, out);          \
     } while (0)
     switch (cls) {
         case 1: if (atomic_rank) GSORT_K11G(256, 18, true); else GSORT_K11G(256, 18, false); break;
@@ -2359,10 +2421,10 @@ hipError_t launch_gather_copy(const void *recv, bool packed16, const uint64_t *p
     auto *bz = reinterpret_cast<const ull *>(bsize);
     auto *bs = reinterpret_cast<const ull *>(bstart);
     if (packed16)
-        k_gather_copy<<<kBuckets16, 256, 0, s>>>(reinterpret_cast<const uint16_t *>(recv), ps, ro,
+        launch_k(k_gather_copy<uint16_t>, kBuckets16, 256, 0, s, reinterpret_cast<const uint16_t *>(recv), ps, ro,
                                                  P, bz, bs, out);
     else
-        k_gather_copy<<<kBuckets16, 256, 0, s>>>(reinterpret_cast<const int32_t *>(recv), ps, ro,
+        launch_k(k_gather_copy<int32_t>, kBuckets16, 256, 0, s, reinterpret_cast<const int32_t *>(recv), ps, ro,
                                                  P, bz, bs, out);
     return hipGetLastError();
 }
@@ -2379,10 +2441,10 @@ hipError_t launch_hist_expand(const void *recv, bool packed16, const uint64_t *p
     auto *bs = reinterpret_cast<const ull *>(bstart);
     auto *l = reinterpret_cast<const ull *>(list);
     if (packed16)
-        k_hist_expand<<<nlist, 1024, 0, s>>>(reinterpret_cast<const uint16_t *>(recv), ps, ro, P,
+        launch_k(k_hist_expand<uint16_t>, nlist, 1024, 0, s, reinterpret_cast<const uint16_t *>(recv), ps, ro, P,
                                              bs, l, out);
     else
-        k_hist_expand<<<nlist, 1024, 0, s>>>(reinterpret_cast<const int32_t *>(recv), ps, ro, P,
+        launch_k(k_hist_expand<int32_t>, nlist, 1024, 0, s, reinterpret_cast<const int32_t *>(recv), ps, ro, P,
                                              bs, l, out);
     return hipGetLastError();
 }
@@ -2390,7 +2452,7 @@ hipError_t launch_hist_expand(const void *recv, bool packed16, const uint64_t *p
 hipError_t launch_list_to_segments(uint64_t *list, uint32_t n, const uint64_t *bstart,
                                    hipStream_t s) {
     if (n == 0) return hipSuccess;
-    k_list_to_segments<<<(n + 255) / 256, 256, 0, s>>>(
+    launch_k(k_list_to_segments, (n + 255) / 256, 256, 0, s,
         reinterpret_cast<unsigned long long *>(list), n,
         reinterpret_cast<const unsigned long long *>(bstart));
     return hipGetLastError();
@@ -2398,14 +2460,14 @@ hipError_t launch_list_to_segments(uint64_t *list, uint32_t n, const uint64_t *b
 
 hipError_t launch_pack16(const int32_t *a, uint64_t n, uint16_t *out, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    k_pack16<<<grid_for(n, 256, 8192), 256, 0, s>>>(a, n, out);
+    launch_k(k_pack16, grid_for(n, 256, 8192), 256, 0, s, a, n, out);
     return hipGetLastError();
 }
 
 hipError_t launch_meta_counts(const uint64_t *gb, const uint64_t *rng, int nrng, uint32_t *meta,
                               hipStream_t s) {
     if (nrng <= 0) return hipSuccess;
-    k_meta_counts<<<dim3(kBuckets16 / 256, nrng), 256, 0, s>>>(
+    launch_k(k_meta_counts, dim3(kBuckets16 / 256, nrng), 256, 0, s,
         reinterpret_cast<const unsigned long long *>(gb),
         reinterpret_cast<const unsigned long long *>(rng), meta);
     return hipGetLastError();
@@ -2413,7 +2475,7 @@ hipError_t launch_meta_counts(const uint64_t *gb, const uint64_t *rng, int nrng,
 
 hipError_t launch_lds_order_check(const uint32_t *digits, uint32_t nblocks, uint32_t nbins,
                                   uint64_t *bad, hipStream_t s) {
-    k_lds_order_check<<<nblocks, 512, 0, s>>>(digits, nbins,
+    launch_k(k_lds_order_check, nblocks, 512, 0, s, digits, nbins,
                                               reinterpret_cast<unsigned long long *>(bad));
     return hipGetLastError();
 }
@@ -2424,14 +2486,14 @@ hipError_t launch_stream_copy(const void *in, void *out, uint64_t bytes, hipStre
         return hipErrorInvalidValue;
     const uint64_t n16 = bytes / 16, grid = (n16 + 1023) / 1024;
     if (grid > 0x7fffffffull) return hipErrorInvalidValue;
-    k_stream_copy<<<(unsigned)grid, 256, 0, s>>>(static_cast<const u32x4 *>(in),
+    launch_k(k_stream_copy, (unsigned)grid, 256, 0, s, static_cast<const u32x4 *>(in),
                                                  static_cast<u32x4 *>(out), n16);
     return hipGetLastError();
 }
 
 hipError_t launch_minmax(const int32_t *a, uint64_t n, int *mm, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    k_minmax<<<grid_for(n, 256, 2048), 256, 0, s>>>(a, n, mm);
+    launch_k(k_minmax, grid_for(n, 256, 2048), 256, 0, s, a, n, mm);
     return hipGetLastError();
 }
 
@@ -2449,14 +2511,22 @@ hipError_t launch_compat_keys(const int32_t *a, uint64_t n, int P, int loop, con
         cd.weight[d] = w;
         w = w > (1ull << 40) ? (1ull << 40) : w * (unsigned long long)P;  // digits there are 0
     }
-    k_compat_keys<<<grid_for(n, 256, 2048), 256, 0, s>>>(
+    launch_k(k_compat_keys, grid_for(n, 256, 2048), 256, 0, s,
         a, n, cd, key, reinterpret_cast<unsigned long long *>(bad));
+    return hipGetLastError();
+}
+
+hipError_t launch_publish(const uint64_t *src, uint32_t n, uint64_t *dst, uint64_t *flag,
+                          uint64_t seq, hipStream_t s) {
+    using ull = unsigned long long;
+    launch_k(k_publish, 1, 64, 0, s, reinterpret_cast<const ull *>(src), n,
+             reinterpret_cast<ull *>(dst), reinterpret_cast<ull *>(flag), (ull)seq);
     return hipGetLastError();
 }
 
 hipError_t launch_copy(const uint32_t *in, uint32_t *out, uint64_t n, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    k_copy<<<grid_for(n, 256, 8192), 256, 0, s>>>(in, out, n);
+    launch_k(k_copy, grid_for(n, 256, 8192), 256, 0, s, in, out, n);
     return hipGetLastError();
 }
 

@@ -37,6 +37,7 @@ enum Phase { PH_COUNT, PH_PASS0, PH_PASS1, PH_PASS2, PH_PASS3, PH_EXCH, PH_PLACE
              PH_MERGE, PH_TOTAL, PH_LEVEL3, PH_LEVEL2, PH_LEVEL1, PH_LEVEL0, PH_BUCKET, PH_N };
 
 constexpr size_t kSmallBytes = 256 * 1024;  // device + pinned scratch for counts, plans
+constexpr size_t kMailBytes = 4096;          // K12p mailbox: flag, then the counters (u64)
 
 struct DevBuf {
     void *p = nullptr;     // what the kernels use
@@ -72,7 +73,11 @@ struct gsort_ctx {
     DevBuf m_part, m_fix, m_cur, m_local3[kLocalClasses];
     DevBuf m_ccount, m_t3, m_cur3;  // K12a child counts, per-shard level-3 counts + totals, K3r cursors
     DevBuf m_tdesc;                 // K12c: K3a tile descriptors
-    hipEvent_t ev_ctr = nullptr;
+    // K12p mailbox: pinned host memory the GPU writes the work-list counters into, then a
+    // sequence number (polled by the host: no copy or event on the stream)
+    uint64_t *h_mail = nullptr, *d_mail = nullptr;
+    uint64_t mail_seq = 0;
+    void *fix_clean = nullptr;  // m_fix.p when it is known to be zero (K12a clears it after use)
     DevBuf m_split;  // radix select thresholds + counts of the distributed radix
     DevBuf m_rpos, m_bsize;  // receive side: run bucket bounds (P x 65537), bucket size/start
     DevBuf m_bseg, m_blist;  // boundary groups of the distributed radix: scratch, K11 list
@@ -91,6 +96,7 @@ struct gsort_ctx {
     size_t ev_used = 0;
     struct Span { int phase; hipEvent_t a, b; };
     std::vector<Span> spans;
+    LaunchTimer timer;  // kernel-attached timing events (tic / toc)
     // host staging of the drop-in path (gsort_scatter_from_root / gsort_gather_to_root):
     // kStageBufs pinned chunks, allocated on first use
     char *h_stage[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -375,29 +381,64 @@ T *slot_ptr(gsort_ctx *c, Slot s) { return reinterpret_cast<T *>(c->slot[s].p); 
 hipEvent_t next_event(gsort_ctx *c) {
     if (c->ev_used == c->ev_pool.size()) {
         hipEvent_t e;
-        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        // GSORT_EVENT_FLAGS (experiment): hipEventCreateWithFlags flags of the timing events
+        static const unsigned fl = getenv("GSORT_EVENT_FLAGS")
+                                       ? (unsigned)strtoul(getenv("GSORT_EVENT_FLAGS"), nullptr, 0)
+                                       : 0u;
+        if (hipEventCreateWithFlags(&e, fl) != hipSuccess) return nullptr;
         c->ev_pool.push_back(e);
     }
     return c->ev_pool[c->ev_used++];
 }
+// Phase spans of gsort_stats.  tic/toc time the kernels launched between them with the stop
+// events the kernels' own dispatches carry (LaunchTimer, gsort_kernels.h): a span runs from
+// the stop of the kernel before it (or, first in a call, an event recorded while the stream
+// is idle) to the stop of its last kernel, so it includes one launch gap (~1 us) and the
+// stream carries no marker packets between kernels; a span without a kernel is dropped.
+// (A hipEventRecord between two kernels left ~5-8 us of idle, an attached start event ~5 us:
+// tools/experiments/launch_gap.hip.)  Spans whose work is not a library kernel (RCCL
+// collectives, copies) use tic_rec / toc_rec, which record both events on the stream.
+hipEvent_t timer_make(void *u) { return next_event(static_cast<gsort_ctx *>(u)); }
 hipEvent_t tic(gsort_ctx *c) {
+    if (!c->timing) return nullptr;
+    if (!c->timer.last_stop) {
+        hipEvent_t e = next_event(c);
+        if (!e || hipEventRecord(e, c->stream) != hipSuccess) return nullptr;
+        c->timer.last_stop = e;
+    }
+    return c->timer.last_stop;
+}
+void toc(gsort_ctx *c, int phase, hipEvent_t a) {
+    if (!c->timing || !a || c->timer.last_stop == a) return;
+    c->spans.push_back({phase, a, c->timer.last_stop});
+}
+hipEvent_t tic_rec(gsort_ctx *c) {
     if (!c->timing) return nullptr;
     hipEvent_t e = next_event(c);
     if (e && hipEventRecord(e, c->stream) != hipSuccess) e = nullptr;
     return e;
 }
-void toc(gsort_ctx *c, int phase, hipEvent_t a) {
+void toc_rec(gsort_ctx *c, int phase, hipEvent_t a) {
     if (!c->timing || !a) return;
     hipEvent_t b = next_event(c);
     if (!b || hipEventRecord(b, c->stream) != hipSuccess) return;
     c->spans.push_back({phase, a, b});
+    c->timer.last_stop = b;  // the next kernel span starts here
 }
 void timing_begin(gsort_ctx *c, gsort_stats *st) {
     c->timing = st != nullptr;
     c->ev_used = 0;
     c->spans.clear();
+    c->timer.last_stop = nullptr;
+    c->timer.make = timer_make;
+    c->timer.u = c;
+    set_launch_timer(st ? &c->timer : nullptr);
     if (st) memset(st, 0, sizeof(*st));
 }
+// Clears this thread's launch timer when a timed call returns (on every path).
+struct TimerScope {
+    ~TimerScope() { set_launch_timer(nullptr); }
+};
 void timing_finish(gsort_ctx *c, gsort_stats *st) {
     if (!st) return;
     for (auto &sp : c->spans) {
@@ -706,6 +747,28 @@ gsort_status msd_levels(gsort_ctx *c, int L, uint32_t *cur, uint32_t *out, uint3
 }
 
 
+// Wait for K12p's sequence number seq in the mailbox (the counters behind it are then
+// visible).  A stream error, or the stream going idle without the flag, returns GSORT_EHIP
+// instead of spinning forever.
+gsort_status wait_mail(gsort_ctx *c, uint64_t seq) {
+    volatile uint64_t *flag = c->h_mail;
+    for (uint64_t spin = 0; *flag != seq; ++spin) {
+        if ((spin & 1023) == 1023) {
+            const hipError_t q = hipStreamQuery(c->stream);
+            if (q != hipErrorNotReady && *flag != seq) {
+                if (q != hipSuccess)
+                    return set_err(c, GSORT_EHIP, std::string("K12p counters: ") +
+                                                      hipGetErrorString(q) + " (rank " +
+                                                      std::to_string(c->rank) + ")");
+                return set_err(c, GSORT_EHIP, "K12p counters: stream idle without the flag");
+            }
+            std::this_thread::yield();
+        }
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    return GSORT_OK;
+}
+
 // Levels 3 and 2 through the two-level plan (gsort_kernels.hip, "Two-level plan"): K1h (the
 // 16-bit histogram) + K12a/K12b (counts, bases, bucket bounds, cursors, work lists), then K3r
 // (level 3, in -> tmp, runs reserved on per-shard bucket cursors) and K3a (level 2, tmp -> out,
@@ -758,22 +821,24 @@ gsort_status msd_sort_h16(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
     uint32_t *cur3 = reinterpret_cast<uint32_t *>(c->m_cur3.p);
     uint64_t *t3 = reinterpret_cast<uint64_t *>(c->m_t3.p);
     uint32_t nblk = 0;
+    constexpr uint32_t kCtrWords = (uint32_t)((OFF_CTR3 + kCtrBytes - OFF_CTR) / 8);
+    static_assert(kCtrWords <= kRadix && kCtrWords * 8 <= kMailBytes - 64, "counter words");
+    if (c->fix_clean != c->m_fix.p)  // new allocation: K12a keeps it zero from here on
+        HIP_TRY(c, hipMemsetAsync(c->m_fix.p, 0, kFixBytes, c->stream));
+    c->fix_clean = nullptr;
     hipEvent_t t = tic(c);
-    HIP_TRY(c, hipMemsetAsync(c->m_fix.p, 0, kFixBytes, c->stream));
-    if (!group16) HIP_TRY(c, hipMemsetAsync(ctr, 0, OFF_CTR3 + kCtrBytes - OFF_CTR, c->stream));
     HIP_TRY(c, launch_hist16(in, n, true, reinterpret_cast<uint32_t *>(c->m_part.p),
                              reinterpret_cast<uint64_t *>(c->m_fix.p), &nblk, c->stream));
     HIP_TRY(c, launch_plan16(reinterpret_cast<uint32_t *>(c->m_part.p), nblk,
                              reinterpret_cast<uint64_t *>(c->m_fix.p), n, group16,
                              reinterpret_cast<uint64_t *>(c->m_ccount.p), t3,
                              t3 + (size_t)kH16Shards * kRadix, bases, totals, cstart, cur, cur3,
-                             tpfx, wl2, wl3, c->stream));
+                             tpfx, wl2, wl3, group16 ? nullptr : ctr, kCtrWords, c->stream));
+    c->fix_clean = c->m_fix.p;
+    const uint64_t seq = ++c->mail_seq;
+    if (!group16)
+        HIP_TRY(c, launch_publish(ctr, kCtrWords, c->d_mail + 8, c->d_mail, seq, c->stream));
     toc(c, PH_COUNT, t);
-    if (!group16) {
-        HIP_TRY(c, hipMemcpyAsync(c->h_small + OFF_CTR, c->d_small + OFF_CTR,
-                                  OFF_CTR3 + kCtrBytes - OFF_CTR, hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(c, hipEventRecord(c->ev_ctr, c->stream));
-    }
     t = tic(c);
     HIP_TRY(c, launch_partition3r(in, tmp, n, cur3, bases, c->stream));
     toc(c, PH_LEVEL3, t);
@@ -784,10 +849,11 @@ gsort_status msd_sort_h16(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
     if (stats) { stats->keys_level[0] += n; stats->keys_level[1] += n; }
     int levels = 2;
     if (!group16) {
-        HIP_TRY(c, hipEventSynchronize(c->ev_ctr));
+        ST_TRY(wait_mail(c, seq));
         uint64_t h[3 * (kLocalClasses + 1)], h3[3 * (kLocalClasses + 1)];
-        memcpy(h, c->h_small + OFF_CTR, kCtrBytes);
-        memcpy(h3, c->h_small + OFF_CTR3, kCtrBytes);
+        const char *mail = reinterpret_cast<const char *>(c->h_mail + 8);
+        memcpy(h, mail, kCtrBytes);
+        memcpy(h3, mail + (OFF_CTR3 - OFF_CTR), kCtrBytes);
         if (stats) stats->keys_level[1] -= h3[1] + h3[4] + h3[7];  // K11'd at level 3
         for (int k = 0; k < kLocalClasses; ++k) {
             const uint64_t *hk = h3 + 3 * (k + 1);
@@ -1123,7 +1189,7 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
     ST_TRY(ensure(c, c->slot[S_STAGE], (size_t)P * std::max(nb, 1) * M * 8));
     uint64_t *d_xs = reinterpret_cast<uint64_t *>(c->m_split.p);
     uint64_t *d_cnt = d_xs + (size_t)nb * M;
-    t = tic(c);
+    t = tic_rec(c);
     for (int k = 0; k < 4; ++k) {
         const int shift = 24 - 8 * k;
         for (int q = 0; q < nb; ++q)
@@ -1169,7 +1235,7 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
             }
         }
     }
-    toc(c, PH_SAMPLE, t);
+    toc_rec(c, PH_SAMPLE, t);
     // (3) cut points from the last round: lt = count(< v_q), le = count(< v_q + 1)
     std::vector<uint64_t> lt((size_t)P * nb), le((size_t)P * nb), send(P), recv(P);
     for (int p = 0; p < P; ++p)
@@ -1230,7 +1296,7 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
             if (recv[q]) { rc[q] = nh[me] * 4; rd[q] = ro * 4; ro += nh[me]; }
         }
     }
-    t = tic(c);
+    t = tic_rec(c);
     ST_TRY(comm_try(c, c->comm->alltoallv(meta_s, sc.data(), sd.data(), meta_r, rc.data(),
                                           rd.data(), c->stream)));
     size_t so = 0, ro = 0;
@@ -1246,7 +1312,7 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
     uint16_t *rbuf = slot_ptr<uint16_t>(c, S_RECV);
     ST_TRY(comm_try(c, c->comm->alltoallv(pack, sc.data(), sd.data(), rbuf, rc.data(),
                                           rd.data(), c->stream)));
-    toc(c, PH_EXCH, t);
+    toc_rec(c, PH_EXCH, t);
     if (stats) stats->exchanges = 1;
     // (5) the P received runs -> one sorted block (recv_sort), their bucket bounds from the counts
     t = tic(c);
@@ -1364,13 +1430,13 @@ gsort_status radix_dist(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in, int3
             }
         }
         uint32_t *rbuf = slot_ptr<uint32_t>(c, S_RECV);
-        t = tic(c);
+        t = tic_rec(c);
         ST_TRY(comm_try(c, c->comm->alltoallv(sorted, sc.data(), sd.data(), rbuf, rc.data(),
                                               rd.data(), c->stream)));
         if (kv)
             ST_TRY(comm_try(c, c->comm->alltoallv(vsorted, sc.data(), sd.data(), vrecv,
                                                   rc.data(), rd.data(), c->stream)));
-        toc(c, PH_EXCH, t);
+        toc_rec(c, PH_EXCH, t);
         if (stats) stats->exchanges++;
         // placement table: {offset in recv buffer, dest offset, length}
         uint64_t *h_seg = reinterpret_cast<uint64_t *>(c->h_small + OFF_PLAN);
@@ -1540,7 +1606,7 @@ gsort_status sample_dist(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in, int
                       reinterpret_cast<uint32_t *>(sorted), slot_ptr<uint32_t>(c, S_TMP), &pr));
 
     // K4 samples -> root (grouped send/recv), K5 on root, broadcast splitters
-    hipEvent_t t = tic(c);
+    hipEvent_t t = tic_rec(c);
     int32_t *d_samp = reinterpret_cast<int32_t *>(c->d_small + OFF_PLAN);
     int32_t *d_all = d_samp + 64;
     int32_t *d_spl = d_all + 1024 + 64;
@@ -1555,7 +1621,7 @@ gsort_status sample_dist(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in, int
     if (me == 0) HIP_TRY(c, launch_select_splitters(d_all, P * k, k, P - 1, d_spl, c->stream));
     ST_TRY(comm_try(c, c->comm->bcast(d_spl, (size_t)(P - 1) * 4, 0, c->stream)));
     HIP_TRY(c, launch_bucket_bounds(sorted, n_in, d_spl, P - 1, d_bounds, c->stream));
-    toc(c, PH_SAMPLE, t);
+    toc_rec(c, PH_SAMPLE, t);
     int32_t *h_spl = reinterpret_cast<int32_t *>(c->h_small + OFF_PLAN);
     uint64_t *h_bounds = reinterpret_cast<uint64_t *>(c->h_small + OFF_PLAN + 1024);
     HIP_TRY(c, hipMemcpyAsync(h_spl, d_spl, (size_t)(P - 1) * 4, hipMemcpyDeviceToHost, c->stream));
@@ -1629,10 +1695,10 @@ gsort_status sample_dist(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in, int
     ST_TRY(ensure(c, c->slot[S_OUT], cap2 * 4));
     ST_TRY(ensure(c, c->slot[S_TMP], cap2 * 4));
     int32_t *rbuf = slot_ptr<int32_t>(c, S_RECV);
-    t = tic(c);
+    t = tic_rec(c);
     ST_TRY(comm_try(c, c->comm->alltoallv(sorted, sc.data(), sd.data(), rbuf, rc.data(),
                                           rd.data(), c->stream)));
-    toc(c, PH_EXCH, t);
+    toc_rec(c, PH_EXCH, t);
     if (stats) stats->exchanges = 1;
     // final local order of the received bucket (mpi_sample_sort.c:174): the P received runs
     // are sorted slices of the senders' sorted blocks -> recv_sort
@@ -1696,9 +1762,12 @@ gsort_status create_common(gsort_ctx *c, int hip_device) {
     ST_TRY(ensure(c, c->small, kSmallBytes));
     c->d_small = static_cast<char *>(c->small.p);
     HIP_TRY(c, hipHostMalloc(&c->h_small, kSmallBytes, hipHostMallocDefault));
+    HIP_TRY(c, hipHostMalloc(reinterpret_cast<void **>(&c->h_mail), kMailBytes,
+                             hipHostMallocDefault));
+    memset(c->h_mail, 0, kMailBytes);
+    HIP_TRY(c, hipHostGetDevicePointer(reinterpret_cast<void **>(&c->d_mail), c->h_mail, 0));
     HIP_TRY(c, hipMemsetAsync(c->d_small, 0, kSmallBytes, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
-    HIP_TRY(c, hipEventCreateWithFlags(&c->ev_ctr, hipEventDisableTiming));
     if (const char *e = getenv("GSORT_PLAN16")) c->plan16 = atoi(e) != 0;
     {
         std::lock_guard<std::mutex> lk(g_ctx_mu);
@@ -1807,12 +1876,12 @@ gsort_status gsort_destroy(gsort_ctx *c) {
     delete c->comm;
     for_each_buf(c, [](const std::string &, DevBuf &b) { (void)dev_free(b); });
     c->d_small = nullptr;
-    if (c->ev_ctr) (void)hipEventDestroy(c->ev_ctr);
     for (int b = 0; b < 4; ++b) {
         if (c->h_stage[b]) (void)hipHostFree(c->h_stage[b]);
         if (c->ev_stage[b]) (void)hipEventDestroy(c->ev_stage[b]);
     }
     if (c->h_small) (void)hipHostFree(c->h_small);
+    if (c->h_mail) (void)hipHostFree(c->h_mail);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -1859,7 +1928,8 @@ gsort_status gsort_radix(gsort_ctx *c, const int32_t *d_keys, size_t n_local, in
     ST_TRY(check_input(c, d_keys));
     ST_TRY(reset_call(c));
     timing_begin(c, stats);
-    hipEvent_t t0 = tic(c);
+    TimerScope timer_scope;
+    hipEvent_t t0 = c->comm ? tic_rec(c) : tic(c);
     gsort_status st;
     uint64_t nout = 0;
     if (c->ref_compat) {
@@ -1880,7 +1950,8 @@ gsort_status gsort_radix(gsort_ctx *c, const int32_t *d_keys, size_t n_local, in
         st = radix_dist_exact(c, d_keys, n_local, d_out, &nout, stats);
     }
     if (st != GSORT_OK) return st;
-    toc(c, PH_TOTAL, t0);
+    if (c->comm) toc_rec(c, PH_TOTAL, t0);
+    else toc(c, PH_TOTAL, t0);
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     *n_out = nout;
     if (stats) { stats->keys_local_in = n_local; stats->keys_local_out = nout; }
@@ -1896,7 +1967,8 @@ gsort_status gsort_sample(gsort_ctx *c, const int32_t *d_keys, size_t n_local, i
     ST_TRY(check_input(c, d_keys));
     ST_TRY(reset_call(c));
     timing_begin(c, stats);
-    hipEvent_t t0 = tic(c);
+    TimerScope timer_scope;
+    hipEvent_t t0 = c->comm ? tic_rec(c) : tic(c);
     uint64_t nout = 0;
     if (!c->comm) {
         // one rank: no splitters, one bucket (the reference reads splitters[-1] here, Q10)
@@ -1914,7 +1986,8 @@ gsort_status gsort_sample(gsort_ctx *c, const int32_t *d_keys, size_t n_local, i
     } else {
         ST_TRY(sample_dist(c, d_keys, n_local, d_out, &nout, stats));
     }
-    toc(c, PH_TOTAL, t0);
+    if (c->comm) toc_rec(c, PH_TOTAL, t0);
+    else toc(c, PH_TOTAL, t0);
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     *n_out = nout;
     if (stats) { stats->keys_local_in = n_local; stats->keys_local_out = nout; }

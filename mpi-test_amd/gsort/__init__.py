@@ -212,18 +212,19 @@ class Context:
         count, 0 restores the numeric sort."""
         self._c(lib().gsort_set_ref_compat(self.h, radix_p))
 
-    def _sort(self, fn, d_keys, n):
+    def _sort(self, fn, d_keys, n, stats=True):
         out, nout, st = ctypes.c_void_p(), ctypes.c_size_t(), Stats()
         self._c(fn(self.h, ctypes.c_void_p(d_keys), n, ctypes.byref(out), ctypes.byref(nout),
-                   ctypes.byref(st)))
-        return out.value or 0, nout.value, st.as_dict()
+                   ctypes.byref(st) if stats else None))
+        return out.value or 0, nout.value, st.as_dict() if stats else None
 
-    def radix(self, d_keys, n):
-        """Device-resident radix sort: returns (d_out, n_out, stats); d_out is ctx-owned."""
-        return self._sort(lib().gsort_radix, d_keys, n)
+    def radix(self, d_keys, n, stats=True):
+        """Device-resident radix sort: returns (d_out, n_out, stats); d_out is ctx-owned.
+        stats=False passes no gsort_stats (no per-phase events on the stream)."""
+        return self._sort(lib().gsort_radix, d_keys, n, stats)
 
-    def sample(self, d_keys, n):
-        return self._sort(lib().gsort_sample, d_keys, n)
+    def sample(self, d_keys, n, stats=True):
+        return self._sort(lib().gsort_sample, d_keys, n, stats)
 
     def sample_info(self):
         import numpy as np
