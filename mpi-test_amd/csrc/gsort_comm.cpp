@@ -92,16 +92,19 @@ class RcclComm : public Comm {
                            hipStream_t s) override {
         gsort_status st = check(ncclGroupStart(), "ncclGroupStart");
         if (st != GSORT_OK) return st;
-        // messages go in pieces of at most kMaxMsg bytes (matched in order on both sides):
-        // measured, a 2 GiB self-message came back wrong, 512 MiB ones are exact
+        // messages go in pieces of at most max_msg_ = 2^30 bytes (matched in order on both
+        // sides): measured on MI355X with RCCL of ROCm 7.2, a self ncclSend/ncclRecv of
+        // 2^30 + 256 bytes or more comes back wrong (keys missing) while 2^30-byte pieces are
+        // exact (tests/test_gpu_rccl.py pins both sides of the boundary;
+        // GSORT_RCCL_MAX_MSG overrides the piece size for that test)
         for (int q = 0; q < size_ && st == GSORT_OK; ++q) {
-            for (size_t o = 0; o < scount[q] && st == GSORT_OK; o += kMaxMsg)
+            for (size_t o = 0; o < scount[q] && st == GSORT_OK; o += max_msg_)
                 st = check(ncclSend((const char *)send + sdispl[q] + o,
-                                    std::min(kMaxMsg, scount[q] - o), ncclChar, q, comm_, s),
+                                    std::min(max_msg_, scount[q] - o), ncclChar, q, comm_, s),
                            "ncclSend");
-            for (size_t o = 0; o < rcount[q] && st == GSORT_OK; o += kMaxMsg)
+            for (size_t o = 0; o < rcount[q] && st == GSORT_OK; o += max_msg_)
                 st = check(ncclRecv((char *)recv + rdispl[q] + o,
-                                    std::min(kMaxMsg, rcount[q] - o), ncclChar, q, comm_, s),
+                                    std::min(max_msg_, rcount[q] - o), ncclChar, q, comm_, s),
                            "ncclRecv");
         }
         gsort_status st2 = check(ncclGroupEnd(), "ncclGroupEnd");
@@ -112,7 +115,12 @@ class RcclComm : public Comm {
     }
 
   private:
-    static constexpr size_t kMaxMsg = size_t(1) << 30;
+    static size_t max_msg() {
+        const char *e = getenv("GSORT_RCCL_MAX_MSG");
+        const size_t v = e ? (size_t)strtoull(e, nullptr, 0) : 0;
+        return v ? v : size_t(1) << 30;
+    }
+    const size_t max_msg_ = max_msg();
     ncclComm_t comm_;
 };
 

@@ -74,6 +74,77 @@ def _case_rccl_small(gsort, orc, n):
         ctx.close()
 
 
+BIG_N = 5 << 28  # 1.25 * 2^30 keys: the packed self-message is 2.5 GiB (> 2^31 bytes)
+
+
+def _case_rccl_big(gsort):
+    """One RCCL rank sorting BIG_N keys through the distributed radix: its packed 16-bit
+    exchange sends 2 * BIG_N bytes to itself, in pieces of GSORT_RCCL_MAX_MSG bytes."""
+    ctx, _ = _ctx(gsort, "rccl")
+    try:
+        p = ctx.alloc(BIG_N * 4)
+        ctx.generate(gsort.UNIFORM, 3, 0, BIG_N, p)
+        fin = ctx.fingerprint(p, BIG_N)
+        out, m, st = ctx.radix(p, BIG_N)
+        fout = ctx.fingerprint(out, m)
+        ctx.free(p)
+        ok = m == BIG_N and fout["sorted"] and (fout["sum"], fout["xor"]) == (fin["sum"],
+                                                                             fin["xor"])
+        return "ok" if ok else f"wrong output (n={m}, sorted={fout['sorted']})"
+    finally:
+        ctx.close()
+
+
+def _child_big():
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "mpi-test_amd")):
+        sys.path.insert(0, p)
+    import torch  # noqa: F401
+    import gsort
+    try:
+        r = _case_rccl_big(gsort)
+    except Exception as e:
+        r = repr(e)
+    print("RCCL_BIG " + json.dumps(r), flush=True)
+
+
+def _run_big(max_msg):
+    env = dict(os.environ, GSORT_FORCE_DIST="1")
+    if max_msg:
+        env["GSORT_RCCL_MAX_MSG"] = str(max_msg)
+    r = subprocess.run([sys.executable, os.path.abspath(__file__), "--child-big"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    for line in r.stdout.splitlines():
+        if line.startswith("RCCL_BIG "):
+            return json.loads(line[len("RCCL_BIG "):])
+    pytest.fail(f"RCCL big child exited {r.returncode}:\n{r.stderr[-4000:]}")
+
+
+def test_rccl_self_message_over_2gib_in_pieces():
+    """The product's exchange (<= 1 GiB pieces) moves a 2.5 GiB self-message exactly."""
+    assert _run_big(None) == "ok"
+
+
+@pytest.mark.parametrize("piece", [(1 << 30) + 256, 1 << 40], ids=["2^30+256", "single"])
+def test_rccl_self_message_pieces_past_the_limit(piece):
+    """The same 2.5 GiB self-message in pieces just over 2^30 bytes, and as ONE ncclSend /
+    ncclRecv pair (GSORT_RCCL_MAX_MSG).  Measured on MI355X: both wrong (the sorted output
+    misses keys), as are 1.25, 1.5, 1.75 and 2 GiB - 4 KiB pieces (tools/rccl_piece_sweep.sh,
+    profiles/r02_rccl_piece_sweep.txt), while 2^30-byte pieces are exact: the limit is the
+    2^30-byte boundary, hence the product's 1 GiB pieces (gsort_comm.cpp)."""
+    r = _run_big(piece)
+    print(f"pieces of {piece} bytes:", r)
+    # pins the RCCL limit the product works around; if this starts passing, RCCL moves such
+    # messages now and the 2^30-byte piece size in gsort_comm.cpp can be raised
+    assert r != "ok", "RCCL now moves > 2^30-byte self-messages exactly: revisit kMaxMsg"
+    assert r.startswith("wrong output"), r
+
+
+def test_rccl_self_message_exactly_2p30_pieces():
+    """Pieces of exactly 2^30 bytes (the product's size, set explicitly): exact."""
+    assert _run_big(1 << 30) == "ok"
+
+
 def _child():
     """Every case in this process; one JSON line of {case id: "ok" | error text}."""
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -124,3 +195,5 @@ def test_one_rank_rccl_small(child_results, n):
 
 if __name__ == "__main__" and "--child" in sys.argv:
     _child()
+if __name__ == "__main__" and "--child-big" in sys.argv:
+    _child_big()

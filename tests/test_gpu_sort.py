@@ -436,3 +436,31 @@ def test_drop_in_staged_round_trip(gsort, n):
         np.testing.assert_array_equal(back, np.sort(h))
     finally:
         c.close()
+
+
+def test_ballot_rank_fallback(gsort, orc):
+    """K11 / K11g with the 8-ballot stable ranks (wave_rank<false>): the path a context takes
+    when its creation-time check of the LDS lane-order property fails, forced here with
+    GSORT_BALLOT_RANK=1 (read at context creation)."""
+    old = os.environ.get("GSORT_BALLOT_RANK")
+    os.environ["GSORT_BALLOT_RANK"] = "1"
+    try:
+        ctx = gsort.Context()
+        blocks = None
+        cases = [orc.gen(orc.UNIFORM, 21, n) for n in (1, 777, 16384, 16385, (1 << 22) + 3)]
+        cases += [orc.gen(orc.ZIPF, 22, 1 << 21), _h16_wrap_pair(orc)[: 1 << 22]]
+        for keys in cases:
+            for algo in ("radix", "sample"):
+                got, _ = sort_on_gpu(ctx, keys, algo)
+                assert np.array_equal(got, np.sort(keys)), (keys.size, algo)
+        ctx.close()
+        keys = orc.gen(orc.UNIFORM, 23, 300001)
+        B = -(-keys.size // 4)
+        blocks = [keys[r * B:(r + 1) * B] for r in range(4)]
+        res = run_group(gsort, blocks, "radix")  # contexts created with the variable set
+        assert np.array_equal(np.concatenate([r[0] for r in res]), np.sort(keys))
+    finally:
+        if old is None:
+            os.environ.pop("GSORT_BALLOT_RANK")
+        else:
+            os.environ["GSORT_BALLOT_RANK"] = old
