@@ -229,8 +229,15 @@ def pmc_traffic(algo, n_local, n_gpus, prefixes=("k_scatter",)):
     newest committed rocprofv3 PMC summary of this exact configuration
     (tools/profile_pmc.sh -> profiles/*_pmc_summary.json), else None."""
     import glob
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json")),
-                       reverse=True):
+    import re
+
+    def version(path):  # newest round, then newest version (r02_v11 after r02_v8a)
+        m = re.match(r"r(\d+)_v(\d+)", os.path.basename(path))
+        return (int(m.group(1)), int(m.group(2))) if m else (0, 0)
+
+    paths = [p for p in glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json"))
+             if "fd_" not in os.path.basename(p)]  # forced-distributed runs price other kernels
+    for path in sorted(paths, key=version, reverse=True):
         try:
             d = json.load(open(path))
             cfg = d["bench"]["config"]
