@@ -29,6 +29,13 @@ typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 namespace {
 constexpr int BLOCK = 1024, ITEMS = kSweepTile / BLOCK;  // 8 keys per thread per tile
 
+// 1 GiB copy with plain (write-back, cache-allocating) stores, as K11 stores its output
+__global__ __launch_bounds__(256) void k_plain_copy(const v4u *__restrict__ in, v4u *__restrict__ out,
+                                                    uint64_t n16) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n16) out[i] = in[i];
+}
+
 __device__ __forceinline__ uint32_t hash_key(uint32_t i) {
     uint32_t z = i * 0x9E3779B9u;
     z ^= z >> 15; z *= 0x85EBCA6Bu; z ^= z >> 13;
@@ -157,6 +164,57 @@ int main(int argc, char **argv) {
         CK(launch_hist16(in, n, true, part_ref, fix, &nblk, 0));
     }, false);
     CK(hipMemcpy(h_ref.data(), part_ref, pbytes, hipMemcpyDeviceToHost));
+    // the product kernel right after a 1 GiB write-heavy pass (as in a sort loop, where K1h
+    // follows the previous sort's K11): is K1h slowed by the dirty lines draining?
+    {
+        uint32_t *junk;
+        CK(hipMalloc(&junk, n * 4));
+        std::vector<float> t;
+        for (int r = 0; r < reps + 2; ++r) {
+            CK(launch_stream_copy(in, junk, n * 4, 0));
+            CK(hipMemset(fix, 0, (size_t)kH16Shards * kBuckets16 * 8));
+            CK(hipEventRecord(e0, 0));
+            CK(launch_hist16(in, n, true, part_ref, fix, &nblk, 0));
+            CK(hipEventRecord(e1, 0));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            if (r >= 2) t.push_back(ms);
+        }
+        std::sort(t.begin(), t.end());
+        printf("%-34s median %.4f ms  min %.4f\n", "product after 1 GiB copy", t[t.size() / 2], t[0]);
+        t.clear();
+        for (int r = 0; r < reps + 2; ++r) {
+            CK(launch_stream_copy(in, junk, n * 4, 0));
+            CK(hipDeviceSynchronize());
+            CK(hipMemset(fix, 0, (size_t)kH16Shards * kBuckets16 * 8));
+            CK(hipEventRecord(e0, 0));
+            CK(launch_hist16(in, n, true, part_ref, fix, &nblk, 0));
+            CK(hipEventRecord(e1, 0));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            if (r >= 2) t.push_back(ms);
+        }
+        std::sort(t.begin(), t.end());
+        printf("%-34s median %.4f ms  min %.4f\n", "product after copy + host sync", t[t.size() / 2], t[0]);
+        t.clear();
+        for (int r = 0; r < reps + 2; ++r) {
+            k_plain_copy<<<(unsigned)(n / 4 / 256), 256>>>((const v4u *)in, (v4u *)junk, n / 4);
+            CK(hipDeviceSynchronize());
+            CK(hipMemset(fix, 0, (size_t)kH16Shards * kBuckets16 * 8));
+            CK(hipEventRecord(e0, 0));
+            CK(launch_hist16(in, n, true, part_ref, fix, &nblk, 0));
+            CK(hipEventRecord(e1, 0));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            if (r >= 2) t.push_back(ms);
+        }
+        std::sort(t.begin(), t.end());
+        printf("%-34s median %.4f ms  min %.4f\n", "product after PLAIN-store copy", t[t.size() / 2], t[0]);
+        CK(hipFree(junk));
+    }
     const unsigned G = nblk;
 #define V(L, A, D, S, chk)                                                                  \
     time("L" #L " A" #A " D" #D " S" #S, [&] { k1h<L, A, D, S><<<G, BLOCK>>>(in, ntiles, part, sink); }, chk)
