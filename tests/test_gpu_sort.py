@@ -121,7 +121,15 @@ def _msd_cases(orc):
     rng = lambda s: np.random.default_rng(s)  # noqa: E731
     return {
         # one bucket / first level only
-        # K11 class caps (kLocalCap: 4608, 9216, 16384) and one past each
+        # K11 class caps (kLocalCap: 2304, 4608, 6144, 8192, 8704, 9216, 16384), one past each
+        "n_cap2304": lambda: orc.gen(orc.UNIFORM, 15, 2304),
+        "n_cap2304_plus1": lambda: orc.gen(orc.UNIFORM, 16, 2305),
+        "n_cap6144": lambda: orc.gen(orc.UNIFORM, 17, 6144),
+        "n_cap6144_plus1": lambda: orc.gen(orc.UNIFORM, 18, 6145),
+        "n_cap8192": lambda: orc.gen(orc.UNIFORM, 19, 8192),
+        "n_cap8192_plus1": lambda: orc.gen(orc.UNIFORM, 20, 8193),
+        "n_cap8704": lambda: orc.gen(orc.UNIFORM, 21, 8704),
+        "n_cap8704_plus1": lambda: orc.gen(orc.UNIFORM, 22, 8705),
         "n_cap1": lambda: orc.gen(orc.UNIFORM, 11, 4608),
         "n_cap1_plus1": lambda: orc.gen(orc.UNIFORM, 12, 4609),
         "n_cap2": lambda: orc.gen(orc.UNIFORM, 13, 9216),
