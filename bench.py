@@ -199,21 +199,24 @@ def kernel_rooflines(stats, n_local):
         [x for s in stats for x in s["ms_pass"]],
         [n_local for s in stats for x in s["ms_pass"]], PASS_BYTES_PER_KEY)
     # MSD levels: ms_level[0] = level 3 (K3u k_partition); with the two-level plan (default,
-    # GSORT_PLAN16 != 0) ms_level[1] = level 2 (K3a k_partition_h16, runs reserved by atomics);
+    # GSORT_PLAN16 != 0) ms_level[0] = level 3 (K3r) and ms_level[1] = level 2 (K3a), runs reserved by atomics;
     # every other level is a segmented K3u (k_seg_partition)
     plan16 = os.environ.get("GSORT_PLAN16", "1") != "0"
     seg_from = 2 if plan16 else 1
-    if plan16:  # K1h reads every key once (4 B/key); the phase also holds K2 + K12h (~25 us)
-        add("k_counts_h16 (K1h: level-3 tile counts + 16-bit histogram; with K2 + K12h)",
-            ("k_counts_h16",), [s["ms_hist"] if s["ms_level"][1] > 0 else 0.0 for s in stats],
+    if plan16:  # K1h reads every key once (4 B/key); the phase also holds K12a/b/p (~27 us)
+        add("k_hist16 (K1h: 16-bit histogram; with K12a + K12b + K12p)",
+            ("k_hist16",), [s["ms_hist"] if s["ms_level"][1] > 0 else 0.0 for s in stats],
             [n_local for s in stats], 4)
-    add("k_partition (K3u: level 3, unstable MSD partition of the whole block)",
-        ("k_partition<",), [s["ms_level"][0] for s in stats],
-        [s["keys_level"][0] for s in stats], PASS_BYTES_PER_KEY)
-    if plan16:
-        add("k_partition_h16 (K3a: level 2, runs reserved by atomics on the K12h cursors)",
-            ("k_partition_h16", "k_partition2_h16"), [s["ms_level"][1] for s in stats],
+        add("k_partition_res L3 (K3r: level 3, runs reserved on per-XCD-shard cursors)",
+            ("k_partition_res<1024, 8, true",), [s["ms_level"][0] for s in stats],
+            [s["keys_level"][0] for s in stats], PASS_BYTES_PER_KEY)
+        add("k_partition_res L2 (K3a: level 2, runs reserved on the K12b child cursors)",
+            ("k_partition_res<1024, 8, false",), [s["ms_level"][1] for s in stats],
             [s["keys_level"][1] for s in stats], PASS_BYTES_PER_KEY)
+    else:
+        add("k_partition (K3u: level 3, unstable MSD partition of the whole block)",
+            ("k_partition<",), [s["ms_level"][0] for s in stats],
+            [s["keys_level"][0] for s in stats], PASS_BYTES_PER_KEY)
     add("k_seg_partition (K3u: segmented MSD level)", ("k_seg_partition",),
         [x for s in stats for x in s["ms_level"][seg_from:]],
         [k for s in stats for k in s["keys_level"][seg_from:]], PASS_BYTES_PER_KEY)
@@ -340,16 +343,18 @@ def main():
         fn(d_in, n_local)
     barrier()
     torch.cuda.synchronize()
-    stats = []
+    # one gsort_stats per step, filled in place and converted after the timed region
+    raw = [gsort.Stats() if not a.no_stats else False for _ in range(a.steps)]
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        _, n_out, st = fn(d_in, n_local, not a.no_stats)
-        stats.append(st)
+    for i in range(a.steps):
+        fn(d_in, n_local, raw[i])
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
     if a.no_stats:  # experiment: the un-instrumented step time; stats from extra steps
         stats = [fn(d_in, n_local)[2] for _ in range(a.steps)]
+    else:
+        stats = [r.as_dict() for r in raw]
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -213,14 +213,18 @@ class Context:
         self._c(lib().gsort_set_ref_compat(self.h, radix_p))
 
     def _sort(self, fn, d_keys, n, stats=True):
-        out, nout, st = ctypes.c_void_p(), ctypes.c_size_t(), Stats()
+        out, nout = ctypes.c_void_p(), ctypes.c_size_t()
+        st = stats if isinstance(stats, Stats) else Stats() if stats else None
         self._c(fn(self.h, ctypes.c_void_p(d_keys), n, ctypes.byref(out), ctypes.byref(nout),
-                   ctypes.byref(st) if stats else None))
-        return out.value or 0, nout.value, st.as_dict() if stats else None
+                   ctypes.byref(st) if st is not None else None))
+        if isinstance(stats, Stats):
+            return out.value or 0, nout.value, stats  # filled in place, unconverted
+        return out.value or 0, nout.value, st.as_dict() if st is not None else None
 
     def radix(self, d_keys, n, stats=True):
         """Device-resident radix sort: returns (d_out, n_out, stats); d_out is ctx-owned.
-        stats=False passes no gsort_stats (no per-phase events on the stream)."""
+        stats=False passes no gsort_stats (no per-phase timing); a Stats instance is filled in
+        place and returned as is (a timing loop converts it afterwards)."""
         return self._sort(lib().gsort_radix, d_keys, n, stats)
 
     def sample(self, d_keys, n, stats=True):
