@@ -70,9 +70,13 @@ hipError_t launch_bucket_bounds(const int32_t *sorted, uint64_t n, const int32_t
 // ---- MSD partition sort (gsort_kernels.hip, "MSD partition sort") -----------------------
 // K11 geometry: one workgroup sorts a bucket entirely in LDS.  A stable pass costs a wave
 // ~16 rounds of 64 keys best (measured, tools/kexp3.hip), so the workgroup size follows the
-// bucket size: class 1 = 256 threads x 18 keys, class 2 = 512 x 18, class 3 = 512 x 32.
-constexpr int kLocalClasses = 3;
-constexpr uint64_t kLocalCap[kLocalClasses + 1] = {0, 256 * 18, 512 * 18, 512 * 32};
+// bucket size: class 1 = 256 threads x 18 keys, class 2 = 512 x 18, class 3 = 512 x 32,
+// class 4 = 1024 x 32 (one workgroup per CU: 144 KiB of LDS).  Class 4 keeps the children of a
+// level-2 bucket in one pass when they outgrow 16 384 keys (2^29 31-bit keys, 2^28 30-bit
+// keys): without it each went through a level-1 partition into ~64-key buckets (3.7x slower
+// sort, tools/run_length_probe.py).
+constexpr int kLocalClasses = 4;
+constexpr uint64_t kLocalCap[kLocalClasses + 1] = {0, 256 * 18, 512 * 18, 512 * 32, 1024 * 32};
 constexpr uint64_t kLocalMax = kLocalCap[kLocalClasses];
 inline int local_class(uint64_t len) {
     for (int k = 1; k <= kLocalClasses; ++k)

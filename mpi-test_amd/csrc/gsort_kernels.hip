@@ -2007,7 +2007,7 @@ __global__ __launch_bounds__(512) void k_lds_order_check(const uint32_t *__restr
 }
 
 constexpr int cls_of(int block, int items) {
-    return block == 256 ? 1 : items == 18 ? 2 : 3;
+    return block == 256 ? 1 : block == 1024 ? 4 : items == 18 ? 2 : 3;
 }
 
 unsigned grid_for(uint64_t n, unsigned block, unsigned cap) {
@@ -2340,7 +2340,8 @@ hipError_t launch_local_sort(const uint32_t *in, uint32_t *out, const uint64_t *
     switch (cls) {
         case 1: GSORT_K11(256, 18); break;
         case 2: GSORT_K11(512, 18); break;
-        default: GSORT_K11(512, 32); break;
+        case 3: GSORT_K11(512, 32); break;
+        default: GSORT_K11(1024, 32); break;
     }
 #undef GSORT_K11
     return hipGetLastError();
@@ -2406,7 +2407,8 @@ hipError_t launch_gather_sort(const void *recv, bool packed16, const uint64_t *p
     switch (cls) {
         case 1: if (atomic_rank) GSORT_K11G(256, 18, true); else GSORT_K11G(256, 18, false); break;
         case 2: if (atomic_rank) GSORT_K11G(512, 18, true); else GSORT_K11G(512, 18, false); break;
-        default: if (atomic_rank) GSORT_K11G(512, 32, true); else GSORT_K11G(512, 32, false); break;
+        case 3: if (atomic_rank) GSORT_K11G(512, 32, true); else GSORT_K11G(512, 32, false); break;
+        default: if (atomic_rank) GSORT_K11G(1024, 32, true); else GSORT_K11G(1024, 32, false); break;
     }
 #undef GSORT_K11G
     return hipGetLastError();

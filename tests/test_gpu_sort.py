@@ -134,8 +134,13 @@ def _msd_cases(orc):
         "n_cap1_plus1": lambda: orc.gen(orc.UNIFORM, 12, 4609),
         "n_cap2": lambda: orc.gen(orc.UNIFORM, 13, 9216),
         "n_cap2_plus1": lambda: orc.gen(orc.UNIFORM, 14, 9217),
-        "n_localmax": lambda: orc.gen(orc.UNIFORM, 1, 16384),
-        "n_localmax_plus1": lambda: orc.gen(orc.UNIFORM, 2, 16385),
+        "n_cap3": lambda: orc.gen(orc.UNIFORM, 1, 16384),
+        "n_cap3_plus1": lambda: orc.gen(orc.UNIFORM, 2, 16385),
+        "n_localmax": lambda: orc.gen(orc.UNIFORM, 23, 32768),
+        "n_localmax_plus1": lambda: orc.gen(orc.UNIFORM, 24, 32769),
+        # level-2 children straddling 16 384 keys (class 3 / class 4 of K11)
+        "children_16k_2p26_28bit": lambda: rng(9).integers(0, 1 << 28, 1 << 26).astype(np.int32),
+        "children_32k_2p26_27bit": lambda: rng(10).integers(0, 1 << 27, 1 << 26).astype(np.int32),
         "uniform31_2p26": lambda: orc.gen(orc.UNIFORM, 6, 1 << 26),
         # top digits trivial: buckets stay oversized down to the last level (digit 0)
         "below_2p16": lambda: rng(7).integers(0, 1 << 16, 1 << 20).astype(np.int32),
