@@ -31,6 +31,53 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
 }
 
 // ---------------------------------------------------------------------------------------
+// Duplicate-aggregated LDS counter atomics.  Skewed inputs (sorted runs, many equal keys, the
+// top digits of a Zipf stream) send most lanes of a wave to ONE counter, and same-address LDS
+// atomics serialize lane by lane (an all-equal 2^28-key sort ran 4.5x slower than a uniform
+// one, tools/dist_probe.py).  So the lanes whose counter equals the first active lane's add
+// their total with one atomic from that lane (the others of them add 0 to their own spare
+// word), and every lane gets back the value it would have seen had the adds been serialized in
+// lane order -- which is the order the hardware serializes same-address lanes in, so the
+// stable per-wave ranks of K11 stay stable.  Other lanes add as before.
+// spare: 64 words, one per lane (distinct banks).
+// ---------------------------------------------------------------------------------------
+constexpr int kAggSpare = 64;
+
+__device__ __forceinline__ uint32_t lane_rank(uint64_t m) {  // set bits of m below this lane
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// Rank on ctr[idx] (+1 per lane); returns the lane's rank among the adds to ctr[idx].
+__device__ __forceinline__ uint32_t agg_rank(uint32_t *ctr, uint32_t idx, uint32_t *spare) {
+    const uint32_t idx0 = __builtin_amdgcn_readfirstlane(idx);
+    const bool eq = idx == idx0;
+    const uint64_t m = __ballot(eq);
+    const uint32_t lr = lane_rank(m);
+    uint32_t *a = !eq ? ctr + idx : lr == 0 ? ctr + idx0 : spare + (threadIdx.x & 63);
+    const uint32_t v = !eq ? 1u : lr == 0 ? (uint32_t)__popcll(m) : 0u;
+    const uint32_t old = atomicAdd(a, v);
+    return eq ? __builtin_amdgcn_readfirstlane(old) + lr : old;
+}
+
+// K1h's packed pair counters: word w = b >> 1 gains 1 << (16 * (b & 1)) per lane.  The lanes on
+// the first active lane's WORD (either half) add their sum with one atomic; each gets the word
+// value of the lane-order serialization (so the wrap test and repair see a consistent order).
+__device__ __forceinline__ uint32_t agg_add_pair(uint32_t *words, uint32_t b, uint32_t *spare) {
+    const uint32_t w = b >> 1, w0 = __builtin_amdgcn_readfirstlane(w);
+    const bool eq = w == w0;
+    const uint64_t m = __ballot(eq), mhi = __ballot(eq && (b & 1u));
+    const uint64_t mlo = m & ~mhi;
+    const uint32_t lr = lane_rank(m);
+    const uint32_t inc = 1u << ((b & 1u) << 4);
+    uint32_t *a = !eq ? words + w : lr == 0 ? words + w0 : spare + (threadIdx.x & 63);
+    const uint32_t v = !eq ? inc
+                     : lr == 0 ? (uint32_t)__popcll(mlo) + ((uint32_t)__popcll(mhi) << 16) : 0u;
+    const uint32_t old = atomicAdd(a, v);
+    return eq ? __builtin_amdgcn_readfirstlane(old) + lane_rank(mlo) + (lane_rank(mhi) << 16)
+              : old;
+}
+
+// ---------------------------------------------------------------------------------------
 // K10: canonical splitmix64 stream; identical to oracle.c orc_gen_one.
 // ---------------------------------------------------------------------------------------
 __global__ void k_generate(int dist, uint64_t seed, uint64_t start, uint64_t n, int32_t *out) {
@@ -703,7 +750,7 @@ __device__ __forceinline__ void partition_tile(const uint32_t *__restrict__ in, 
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i)
         if (full || (uint32_t)(i * BLOCK + tid) < len)
-            r[i] = atomicAdd(&s_cur[(k[i] >> shift) & 255u], 1u);
+            r[i] = agg_rank(s_cur, (k[i] >> shift) & 255u, s_cur + kRadix);
     __syncthreads();
     uint32_t c = 0, excl = 0;
     unsigned long long pos = 0;
@@ -751,7 +798,7 @@ __global__ __launch_bounds__(BLOCK) void k_partition(const uint32_t *__restrict_
     constexpr int TILE = BLOCK * ITEMS;
     static_assert(TILE == kSweepTile, "K1/K2 count tiles of kSweepTile keys");
     __shared__ uint32_t s_keys[TILE];
-    __shared__ uint32_t s_cur[kRadix];
+    __shared__ uint32_t s_cur[kRadix + kAggSpare];  // + agg_rank spare words
     __shared__ uint32_t *s_dst[kRadix];
     __shared__ uint32_t s_wsum[kRadix / 64];
     const uint32_t tile = xcd_tile(blockIdx.x, gridDim.x);
@@ -850,7 +897,7 @@ __global__ __launch_bounds__(BLOCK) void k_seg_counts(const uint32_t *__restrict
                                                       uint32_t nseg, int shift,
                                                       uint32_t *__restrict__ tcounts) {
     constexpr int ITEMS = kSweepTile / BLOCK;
-    __shared__ uint32_t s_h[kRadix];
+    __shared__ uint32_t s_h[kRadix + kAggSpare];
     const uint32_t t = blockIdx.x, tid = threadIdx.x;
     uint64_t t0;
     uint32_t len;
@@ -869,7 +916,7 @@ __global__ __launch_bounds__(BLOCK) void k_seg_counts(const uint32_t *__restrict
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i)
-        if ((uint32_t)(i * BLOCK) + tid < len) atomicAdd(&s_h[(k[i] >> shift) & 255u], 1u);
+        if ((uint32_t)(i * BLOCK) + tid < len) agg_rank(s_h, (k[i] >> shift) & 255u, s_h + kRadix);
     __syncthreads();
     for (uint32_t b = tid; b < kRadix; b += BLOCK) tcounts[(uint64_t)t * kRadix + b] = s_h[b];
 }
@@ -903,15 +950,74 @@ __global__ __launch_bounds__(kRadix) void k_seg_scan_tiles(uint32_t *__restrict_
 // level, the rest to K11's size classes.  Called by all kRadix threads of a block (one child
 // each): the block reserves its entries with one global atomic per list, so the counters see
 // a few atomics per block, not one per child.
-__device__ __forceinline__ void classify_block(uint64_t start, uint64_t len, const WorkLists &wl) {
+// merge (the block's children are consecutive buckets of one parent, in key order): runs of
+// small children (<= kMergeWin keys each) are merged into one K11 entry of <= 2 kMergeWin keys
+// -- children whose starts fall in one kMergeWin-aligned window of the parent -- sorted with one
+// more digit (the digit that split them), flagged in the entry's high word.  Dense or sorted
+// inputs otherwise end in ~256-key buckets, one K11 workgroup each at a few % of its slots
+// (a sorted 2^28-key input spent 2.1 ms in K11, tools/dist_probe.py).
+constexpr uint64_t kMergeWin = kLocalCap[2] / 2;
+
+__device__ __forceinline__ void classify_block(uint64_t start, uint64_t len, const WorkLists &wl,
+                                               bool merge = false) {
     constexpr int NL = kLocalClasses + 1;
     __shared__ unsigned int s_n[NL];
     __shared__ unsigned long long s_keys[NL], s_max[NL], s_base[NL];
-    const uint32_t tid = threadIdx.x;
+    __shared__ unsigned long long s_gsum[kRadix], s_gkey[kRadix], s_wx[kRadix / 64];
+    __shared__ unsigned int s_gcnt[kRadix], s_wl[kRadix / 64];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     if (tid < NL) { s_n[tid] = 0; s_keys[tid] = 0; s_max[tid] = 0; }
-    __syncthreads();
+    uint32_t extra = 0;  // digits the K11 entry sorts beyond its list's
+    bool absorbed = false;
+    merge = merge && !wl.force_next;
+    if (merge) {
+        // exclusive prefix of the children's lengths (block scan)
+        unsigned long long x = len;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const unsigned long long t = __shfl_up(x, o);
+            if ((int)lane >= o) x += t;
+        }
+        if (lane == 63) s_wx[w] = x;
+        s_gsum[tid] = 0;
+        s_gcnt[tid] = 0;
+        __syncthreads();
+        unsigned long long excl = x - len;
+        for (uint32_t ww = 0; ww < w; ++ww) excl += s_wx[ww];
+        const bool small = len > 0 && len <= kMergeWin;
+        const unsigned long long g = excl / kMergeWin;
+        s_gkey[tid] = small ? g : ~0ull;
+        __syncthreads();
+        // the group's first child: the nearest child at or before this one opening group g
+        // (an inclusive max-scan of the opening children's indices)
+        const bool opens = small && (tid == 0 || s_gkey[tid - 1] != g);
+        uint32_t lead = opens ? tid : 0u;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t t = __shfl_up(lead, o);
+            if ((int)lane >= o) lead = max(lead, t);
+        }
+        if (lane == 63) s_wl[w] = lead;
+        __syncthreads();
+        for (uint32_t ww = 0; ww < w; ++ww) lead = max(lead, s_wl[ww]);
+        if (small) {
+            atomicAdd(&s_gsum[lead], len);
+            atomicAdd(&s_gcnt[lead], 1u);
+        }
+        __syncthreads();
+        if (small) {
+            if (!opens) {
+                absorbed = true;
+            } else {
+                len = s_gsum[tid];
+                extra = s_gcnt[tid] > 1 ? 1u : 0u;
+            }
+        }
+    } else {
+        __syncthreads();
+    }
     int which = -1;
-    if (len > 0) {
+    if (len > 0 && !absorbed) {
         which = 0;
         if (!wl.force_next)
             for (int k = 1; k < NL; ++k)
@@ -935,7 +1041,7 @@ __device__ __forceinline__ void classify_block(uint64_t start, uint64_t len, con
         unsigned long long *list = reinterpret_cast<unsigned long long *>(wl.list[which]);
         const unsigned long long i = s_base[which] + idx;
         list[2 * i] = start;
-        list[2 * i + 1] = len;
+        list[2 * i + 1] = len | ((unsigned long long)extra << 32);
     }
 }
 
@@ -970,7 +1076,7 @@ __global__ __launch_bounds__(kRadix) void k_seg_scan_groups(
     for (uint32_t ww = 0; ww < w; ++ww) excl += s_w[ww];
     const uint64_t start = segs[2 * s] + excl;
     cstart[(uint64_t)s * kRadix + d] = start;
-    if (wl.ctr) classify_block(start, run, wl);
+    if (wl.ctr) classify_block(start, run, wl, true);
 }
 
 // Level-3 children: the 256 buckets of the global pass.
@@ -978,7 +1084,7 @@ __global__ __launch_bounds__(kRadix) void k_classify_buckets(
     const unsigned long long *__restrict__ bases, const unsigned long long *__restrict__ totals,
     WorkLists wl) {
     const uint32_t d = threadIdx.x;
-    classify_block(bases[d], totals[d], wl);
+    classify_block(bases[d], totals[d], wl, true);
 }
 
 // K3u (segmented): one block per segment tile.
@@ -992,7 +1098,7 @@ __global__ __launch_bounds__(BLOCK) void k_seg_partition(
     constexpr int TILE = BLOCK * ITEMS;
     static_assert(TILE == kSweepTile, "segment tiles are kSweepTile keys");
     __shared__ uint32_t s_keys[TILE];
-    __shared__ uint32_t s_cur[kRadix];
+    __shared__ uint32_t s_cur[kRadix + kAggSpare];  // + agg_rank spare words
     __shared__ OT *s_dst[kRadix];
     __shared__ uint32_t s_wsum[kRadix / 64];
     const uint32_t t = xcd_tile(blockIdx.x, gridDim.x);
@@ -1051,7 +1157,8 @@ __global__ __launch_bounds__(BLOCK) void k_hist16(const uint32_t *__restrict__ i
                                                   unsigned long long *__restrict__ fix) {
     constexpr int ITEMS = kSweepTile / BLOCK;
     constexpr uint32_t kWords = kBuckets16 / 2;
-    __shared__ uint32_t s_h[kWords];
+    __shared__ uint32_t s_h[kWords + kAggSpare];
+    uint32_t *spare = s_h + kWords;
     const uint32_t tid = threadIdx.x;
     for (uint32_t i = tid; i < kWords; i += BLOCK) s_h[i] = 0;
     // tile lengths in 32-bit scalar arithmetic (tools/isa_scc_check.py: the u64 min() form was
@@ -1087,7 +1194,18 @@ __global__ __launch_bounds__(BLOCK) void k_hist16(const uint32_t *__restrict__ i
         // (tools/experiments/kexp13.hip: the bounded form cost 12 %)
         uint32_t old[ITEMS];
         bool wrap = false;
-        if (len == (uint32_t)kSweepTile) {
+        // skewed wave (its first item's keys all in one packed word: duplicates, sorted runs,
+        // Zipf): aggregated adds; otherwise plain ones (the aggregation's VALU would cost the
+        // uniform case ~25 %)
+        const uint32_t w0 = __builtin_amdgcn_readfirstlane(k[0] >> 17);
+        const bool skew = __ballot((k[0] >> 17) == w0) == __builtin_amdgcn_read_exec();
+        if (len == (uint32_t)kSweepTile && skew) {
+#pragma unroll
+            for (int j = 0; j < ITEMS; ++j) old[j] = agg_add_pair(s_h, k[j] >> 16, spare);
+#pragma unroll
+            for (int j = 0; j < ITEMS; ++j)
+                wrap |= ((old[j] >> (((k[j] >> 16) & 1u) << 4)) & 0xffffu) == 0xffffu;
+        } else if (len == (uint32_t)kSweepTile) {
 #pragma unroll
             for (int j = 0; j < ITEMS; ++j) {
                 const uint32_t b = k[j] >> 16;
@@ -1100,10 +1218,7 @@ __global__ __launch_bounds__(BLOCK) void k_hist16(const uint32_t *__restrict__ i
 #pragma unroll
             for (int j = 0; j < ITEMS; ++j) {
                 old[j] = 0;
-                if ((uint32_t)(j * BLOCK) + tid < len) {
-                    const uint32_t b = k[j] >> 16;
-                    old[j] = atomicAdd(&s_h[b >> 1], 1u << ((b & 1u) << 4));
-                }
+                if ((uint32_t)(j * BLOCK) + tid < len) old[j] = agg_add_pair(s_h, k[j] >> 16, spare);
             }
 #pragma unroll
             for (int j = 0; j < ITEMS; ++j)
@@ -1263,7 +1378,7 @@ __global__ __launch_bounds__(kRadix) void k_plan16_place(
     }
     if (level2_bucket(ts, force)) {
         cur[s * kRadix + e] = (uint32_t)excl;
-        if (wl2.ctr) classify_block(st, c, wl2);
+        if (wl2.ctr) classify_block(st, c, wl2, true);
     } else if (wl3.ctr) {
         classify_block(e == 0 ? b0 : 0ull, e == 0 ? ts : 0ull, wl3);
     }
@@ -1331,6 +1446,7 @@ __global__ __launch_bounds__(BLOCK) void k_partition_res(
     __shared__ uint32_t s_cur[2][kRadix];
     __shared__ OT *s_dst[2][kRadix];
     __shared__ uint32_t s_wsum[2][kRadix / 64];
+    __shared__ uint32_t s_spare[kAggSpare];
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     uint32_t pr, ntile, last_len = 0;
     if (L3) {
@@ -1374,7 +1490,7 @@ __global__ __launch_bounds__(BLOCK) void k_partition_res(
 #pragma unroll
         for (int i = 0; i < ITEMS; ++i)
             if ((uint32_t)(i * BLOCK) + tid < len[h])
-                r[h][i] = atomicAdd(&s_cur[h][(k[h][i] >> shift) & 255u], 1u);
+                r[h][i] = agg_rank(s_cur[h], (k[h][i] >> shift) & 255u, s_spare);
     __syncthreads();
     uint32_t excl[2] = {0, 0}, pos[2] = {0, 0};
     if (tid < kRadix) {
@@ -1577,12 +1693,14 @@ __global__ __launch_bounds__(BLOCK) void k_local_sort(const uint32_t *__restrict
     __shared__ uint32_t s_a[TILE];
     __shared__ uint32_t s_wc[WAVES * kRadix];  // per-wave digit counts, then offsets
     const uint64_t start = list[2 * blockIdx.x];
-    const uint32_t len = (uint32_t)list[2 * blockIdx.x + 1];
+    const uint64_t e = list[2 * blockIdx.x + 1];  // len | extra digits << 32 (merged children)
+    const uint32_t len = (uint32_t)e;
     if (threadIdx.x < kRadix) s_wc[threadIdx.x] = 0;
     uint32_t k[ITEMS];
     load_bucket<BLOCK, ITEMS, FIN>(in + start, len, k);
     __syncthreads();
-    sort_bucket<BLOCK, ITEMS, ATOMIC>(k, len, ndigits, out + start, s_a, s_wc);
+    sort_bucket<BLOCK, ITEMS, ATOMIC>(k, len, min(ndigits + (int)(e >> 32), 4), out + start, s_a,
+                                      s_wc);
 }
 
 // K11g (receive side of the distributed sorts): bucket h of the 2^16 top-16-bit buckets of
