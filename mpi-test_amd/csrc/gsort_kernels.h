@@ -113,6 +113,7 @@ struct SegPass {
     uint32_t nseg;
     int shift;
     bool flip_out;
+    bool flip_in = false;          // in is the int32 input (first level of a sort that starts there)
     uint32_t max_tiles, max_groups;
     uint32_t *tpfx, *gpfx;         // nseg + 1 each
     uint32_t *segmap, *groupmap;   // max_tiles / max_groups
@@ -149,20 +150,23 @@ hipError_t launch_plan16(const uint32_t *part, uint32_t nblk, uint64_t *fix, uin
                          bool force, uint64_t *ccount, uint64_t *t3, uint64_t *tot,
                          uint64_t *bases, uint64_t *totals, uint64_t *cstart, uint32_t *cur,
                          uint32_t *cur3, uint32_t *tpfx, const WorkLists &wl2,
-                         const WorkLists &wl3, uint64_t *zero, uint32_t nzero, hipStream_t s);
+                         const WorkLists &wl3, uint64_t *zero, uint32_t nzero, uint32_t *flags,
+                         hipStream_t s);
 // K12p: dst[0 .. n) = src[0 .. n) in pinned host memory, then *flag = seq (system release).
 hipError_t launch_publish(const uint64_t *src, uint32_t n, uint64_t *dst, uint64_t *flag,
                           uint64_t seq, hipStream_t s);
 // K3r: level 3 of the int32 input by the top digit into out (ordered u32), runs reserved on cur3.
+// flags (K12b's trivial-level word, or nullptr): see k_partition_res.
 hipError_t launch_partition3r(const uint32_t *in, uint32_t *out, uint64_t n, uint32_t *cur3,
-                              const uint64_t *bases, hipStream_t s);
+                              const uint64_t *bases, const uint32_t *flags, hipStream_t s);
 // K12c + K3a: level 2 of every level-2 bucket (in = level 3's output, ordered u32) by digit 2
 // into out (ordered u32), or with out16 != nullptr only the low 16 bits into out16.  tdesc:
 // scratch for kTileDescBytes per level-2 tile (sweep_tiles(n) + 256 tiles).
 constexpr size_t kTileDescBytes = 16;
 hipError_t launch_partition2r(const uint32_t *in, uint32_t *out, uint16_t *out16, uint64_t n,
                               const uint32_t *tpfx, void *tdesc, const uint64_t *bases,
-                              const uint64_t *totals, uint32_t *cur, hipStream_t s);
+                              const uint64_t *totals, uint32_t *cur, const uint32_t *flags,
+                              const uint32_t *raw, hipStream_t s);
 // K11: sort each listed bucket (all of class cls: <= kLocalCap[cls] keys) on digits
 // 0..ndigits-1 in LDS, store as int32 into out (same positions; in == out allowed).
 // flip_in: the input is int32 (else ordered u32).  atomic_rank: stable ranks from LDS atomics

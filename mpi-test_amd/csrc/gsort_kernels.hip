@@ -1088,7 +1088,7 @@ __global__ __launch_bounds__(kRadix) void k_classify_buckets(
 }
 
 // K3u (segmented): one block per segment tile.
-template <int BLOCK, int ITEMS, bool FOUT, typename OT = uint32_t>
+template <int BLOCK, int ITEMS, bool FOUT, typename OT = uint32_t, bool FIN = false>
 __global__ __launch_bounds__(BLOCK) void k_seg_partition(
     const uint32_t *__restrict__ in, OT *__restrict__ out, int shift,
     const uint32_t *__restrict__ toff, const unsigned long long *__restrict__ gpfx64,
@@ -1109,7 +1109,7 @@ __global__ __launch_bounds__(BLOCK) void k_seg_partition(
         dst_base = out + cstart[(uint64_t)st.seg * kRadix + threadIdx.x] +
                    gpfx64[(uint64_t)st.group * kRadix + threadIdx.x] +
                    toff[(uint64_t)t * kRadix + threadIdx.x];
-    partition_tile<BLOCK, ITEMS, false, FOUT, OT>(in, st.t0, st.len, shift, dst_base, s_keys, s_cur,
+    partition_tile<BLOCK, ITEMS, FIN, FOUT, OT>(in, st.t0, st.len, shift, dst_base, s_keys, s_cur,
                                               s_dst, s_wsum);
 }
 
@@ -1352,7 +1352,8 @@ __global__ __launch_bounds__(kRadix) void k_plan16_place(
     const unsigned long long *__restrict__ tot, uint64_t n, int force,
     unsigned long long *__restrict__ bases, unsigned long long *__restrict__ totals,
     unsigned long long *__restrict__ cstart, uint32_t *__restrict__ cur,
-    uint32_t *__restrict__ cur3, uint32_t *__restrict__ tpfx, WorkLists wl2, WorkLists wl3) {
+    uint32_t *__restrict__ cur3, uint32_t *__restrict__ tpfx, WorkLists wl2, WorkLists wl3,
+    uint32_t *__restrict__ flags) {
     __shared__ unsigned long long s_w[kRadix / 64];
     __shared__ unsigned long long s_base;
     const uint32_t s = blockIdx.x, e = threadIdx.x;
@@ -1364,6 +1365,11 @@ __global__ __launch_bounds__(kRadix) void k_plan16_place(
     __syncthreads();
     const unsigned long long b0 = s_base, ts = tot[s];
     const unsigned long long c = ccount[s * kRadix + e];
+    // trivial levels (zeroed by K12a): bit 0 = bucket s holds every key, bit 1 = child (s, e)
+    if (flags && n > 0) {
+        if (e == 0 && ts == n) atomicOr(flags, 1u);
+        if (c == n) atomicOr(flags, 2u);
+    }
     unsigned long long sum;
     const unsigned long long excl = block_excl_scan(c, s_w, &sum);
     const unsigned long long st = b0 + excl;
@@ -1435,13 +1441,25 @@ __global__ __launch_bounds__(256) void k_tile_desc(const uint32_t *__restrict__ 
 //     XCD-contiguously (xcd_tile); runs reserved on cur[s * 256 + d], placed at bases[s] + the
 //     reservation; out may be uint16_t (only the low 16 bits: the distributed sender's packed
 //     send buffer).
+// Trivial levels (flags != nullptr: K12b's word, bit 0 = one level-3 bucket holds every key,
+// bit 1 = one 16-bit child does): K3r does nothing when bit 0 is set, and K3a then partitions
+// the int32 input raw itself (flipping on load); K3a does nothing when bit 1 is set (the
+// caller continues from level 1 on the input).  Each level that moved keys without changing
+// their order cost a full pass (16-bit keys took four partitions).
 template <int BLOCK, int ITEMS, bool L3, bool FIN, typename OT = uint32_t>
 __global__ __launch_bounds__(BLOCK) void k_partition_res(
     const uint32_t *__restrict__ in, OT *__restrict__ out, uint64_t n,
     const uint32_t *__restrict__ tpfx, const TileDesc *__restrict__ desc,
-    const unsigned long long *__restrict__ bases, uint32_t *__restrict__ cur) {
+    const unsigned long long *__restrict__ bases, uint32_t *__restrict__ cur,
+    const uint32_t *__restrict__ flags, const uint32_t *__restrict__ raw) {
     constexpr int TILE = BLOCK * ITEMS, shift = L3 ? 24 : 16;
     static_assert(TILE == kSweepTile, "reservation tiles are kSweepTile keys");
+    uint32_t flip = 0;
+    if (flags) {
+        const uint32_t f = *flags;
+        if (f & (L3 ? 1u : 2u)) return;
+        if (!L3 && (f & 1u)) { in = raw; flip = kFlip; }
+    }
     __shared__ uint32_t s_keys[2][TILE];
     __shared__ uint32_t s_cur[2][kRadix];
     __shared__ OT *s_dst[2][kRadix];
@@ -1482,8 +1500,13 @@ __global__ __launch_bounds__(BLOCK) void k_partition_res(
     for (int h = 0; h < 2; ++h) cursor[h] = cur + (L3 ? (pr % kShards) : seg[h]) * kRadix;
     uint32_t k[2][ITEMS], r[2][ITEMS];
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+    for (int h = 0; h < 2; ++h) {
         load_tile<BLOCK, ITEMS, FIN>(in + t0[h] + tid, len[h] == (uint32_t)TILE, len[h], k[h]);
+        if (!L3) {
+#pragma unroll
+            for (int i = 0; i < ITEMS; ++i) k[h][i] ^= flip;
+        }
+    }
     __syncthreads();  // s_cur zeroed
 #pragma unroll
     for (int h = 0; h < 2; ++h)
@@ -2316,8 +2339,12 @@ hipError_t launch_seg_count(const SegPass &sp, hipStream_t s) {
     ull *gsum = reinterpret_cast<ull *>(sp.gsum);
     launch_k(k_seg_plan, 1, 1024, 0, s, segs, sp.nseg, sp.tpfx, sp.gpfx);
     launch_k(k_seg_map, sp.nseg, 256, 0, s, sp.tpfx, sp.gpfx, sp.segmap, sp.groupmap);
-    launch_k(k_seg_counts<512, true, false>, sp.max_tiles, 512, 0, s,
-        sp.in, 0, segs, sp.tpfx, sp.gpfx, sp.segmap, sp.nseg, sp.shift, sp.tcounts);
+    if (sp.flip_in)
+        launch_k(k_seg_counts<512, true, true>, sp.max_tiles, 512, 0, s,
+            sp.in, 0, segs, sp.tpfx, sp.gpfx, sp.segmap, sp.nseg, sp.shift, sp.tcounts);
+    else
+        launch_k(k_seg_counts<512, true, false>, sp.max_tiles, 512, 0, s,
+            sp.in, 0, segs, sp.tpfx, sp.gpfx, sp.segmap, sp.nseg, sp.shift, sp.tcounts);
     launch_k(k_seg_scan_tiles, sp.max_groups, kRadix, 0, s, sp.tcounts, sp.tpfx, sp.gpfx, sp.groupmap,
                                                       sp.nseg, gsum);
     launch_k(k_seg_scan_groups, sp.nseg, kRadix, 0, s, gsum, segs, sp.gpfx,
@@ -2331,7 +2358,12 @@ hipError_t launch_seg_partition(const SegPass &sp, hipStream_t s) {
     const ull *segs = reinterpret_cast<const ull *>(sp.segs);
     ull *gsum = reinterpret_cast<ull *>(sp.gsum);
     constexpr int B = kPartBlock, I = kSweepTile / kPartBlock;
-    if (sp.out16)
+    if (sp.flip_in) {  // level 1 straight from the int32 input (levels 3 and 2 trivial)
+        if (sp.out16 || sp.flip_out) return hipErrorInvalidValue;
+        launch_k(k_seg_partition<B, I, false, uint32_t, true>, sp.max_tiles, B, 0, s,
+            sp.in, sp.out, sp.shift, sp.tcounts, gsum, reinterpret_cast<const ull *>(sp.cstart),
+            segs, sp.tpfx, sp.gpfx, sp.segmap, sp.nseg);
+    } else if (sp.out16)
         launch_k(k_seg_partition<B, I, false, uint16_t>, sp.max_tiles, B, 0, s,
             sp.in, sp.out16, sp.shift, sp.tcounts, gsum, reinterpret_cast<const ull *>(sp.cstart),
             segs, sp.tpfx, sp.gpfx, sp.segmap, sp.nseg);
@@ -2364,7 +2396,8 @@ hipError_t launch_plan16(const uint32_t *part, uint32_t nblk, uint64_t *fix, uin
                          bool force, uint64_t *ccount, uint64_t *t3, uint64_t *tot,
                          uint64_t *bases, uint64_t *totals, uint64_t *cstart, uint32_t *cur,
                          uint32_t *cur3, uint32_t *tpfx, const WorkLists &wl2,
-                         const WorkLists &wl3, uint64_t *zero, uint32_t nzero, hipStream_t s) {
+                         const WorkLists &wl3, uint64_t *zero, uint32_t nzero, uint32_t *flags,
+                         hipStream_t s) {
     using ull = unsigned long long;
     if (nblk % kShards || nzero > kRadix) return hipErrorInvalidValue;
     launch_k(k_plan16_count, kRadix, kRadix, 0, s, part, nblk, reinterpret_cast<ull *>(fix),
@@ -2374,24 +2407,26 @@ hipError_t launch_plan16(const uint32_t *part, uint32_t nblk, uint64_t *fix, uin
         reinterpret_cast<const ull *>(ccount), reinterpret_cast<const ull *>(t3),
         reinterpret_cast<const ull *>(tot), n, force ? 1 : 0, reinterpret_cast<ull *>(bases),
         reinterpret_cast<ull *>(totals), reinterpret_cast<ull *>(cstart), cur, cur3, tpfx, wl2,
-        wl3);
+        wl3, flags);
     return hipGetLastError();
 }
 
 hipError_t launch_partition3r(const uint32_t *in, uint32_t *out, uint64_t n, uint32_t *cur3,
-                              const uint64_t *bases, hipStream_t s) {
+                              const uint64_t *bases, const uint32_t *flags, hipStream_t s) {
     using ull = unsigned long long;
     if (n == 0) return hipSuccess;
     constexpr int B = kPartBlock, I = kSweepTile / kPartBlock;
     const uint64_t pairs = (sweep_tiles(n) + 1) / 2;
     launch_k(k_partition_res<B, I, true, true>, (unsigned)pairs, B, 0, s,
-        in, out, n, nullptr, nullptr, reinterpret_cast<const ull *>(bases), cur3);
+        in, out, n, nullptr, nullptr, reinterpret_cast<const ull *>(bases), cur3, flags,
+        (const uint32_t *)nullptr);
     return hipGetLastError();
 }
 
 hipError_t launch_partition2r(const uint32_t *in, uint32_t *out, uint16_t *out16, uint64_t n,
                               const uint32_t *tpfx, void *tdesc, const uint64_t *bases,
-                              const uint64_t *totals, uint32_t *cur, hipStream_t s) {
+                              const uint64_t *totals, uint32_t *cur, const uint32_t *flags,
+                              const uint32_t *raw, hipStream_t s) {
     using ull = unsigned long long;
     if (n == 0) return hipSuccess;
     constexpr int B = kPartBlock, I = kSweepTile / kPartBlock;
@@ -2403,10 +2438,11 @@ hipError_t launch_partition2r(const uint32_t *in, uint32_t *out, uint16_t *out16
     launch_k(k_tile_desc, (max_tiles + 255) / 256, 256, 0, s, tpfx, bs, tt, max_tiles, desc);
     const unsigned g2 = (max_tiles + 1) / 2;
     if (out16)
-        launch_k(k_partition_res<B, I, false, false, uint16_t>, g2, B, 0, s, in, out16, n, tpfx, desc,
-                                                                        bs, cur);
+        launch_k(k_partition_res<B, I, false, false, uint16_t>, g2, B, 0, s, in, out16, n, tpfx,
+                 desc, bs, cur, flags, raw);
     else
-        launch_k(k_partition_res<B, I, false, false>, g2, B, 0, s, in, out, n, tpfx, desc, bs, cur);
+        launch_k(k_partition_res<B, I, false, false>, g2, B, 0, s, in, out, n, tpfx, desc, bs,
+                 cur, flags, raw);
     return hipGetLastError();
 }
 

@@ -110,6 +110,7 @@ namespace {
 // [12K+256, 12K+352): the counters of the level-3 K11 lists of the two-level plan
 constexpr size_t OFF_HIST = 0, OFF_TOT = 8192, OFF_BASES = 10240, OFF_CTR = 12288,
                  OFF_ONE = 12416, OFF_CTR3 = 12544, OFF_PLAN = 20480;
+constexpr size_t OFF_FLAGS = 12408;  // K12b's trivial-level word, inside the published range
 
 gsort_status set_err(gsort_ctx *c, gsort_status st, const std::string &msg) {
     if (c) c->err = msg;
@@ -543,7 +544,7 @@ gsort_status lsd_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *ou
 // K11 in LDS and stored to out as int32.  The host reads two counters per level (a few us) to
 // size the next launches.  Same reference hot loops as lsd_sort.
 constexpr size_t kCtrBytes = 3 * 8 * (kLocalClasses + 1);
-static_assert(OFF_CTR + kCtrBytes <= OFF_ONE, "counter area");
+static_assert(OFF_CTR + kCtrBytes <= OFF_FLAGS && OFF_FLAGS + 4 <= OFF_ONE, "counter area");
 
 gsort_status ensure_list(gsort_ctx *c, DevBuf &b, uint64_t entries) {
     return ensure(c, b, (size_t)std::max<uint64_t>(entries, 1) * 16);
@@ -675,9 +676,10 @@ WorkLists work_lists(gsort_ctx *c, int next) {
 // than kLocalMax, ordered u32 in `cur`) and m_local[k] (K11 buckets of `cur`, digits L..0
 // left).  Level L partitions cur -> the other buffer (tmp <-> out); level 0 stores int32 into
 // out, as does K11.
+// flip_first: cur is the int32 input itself (the first level flips on load).
 gsort_status msd_levels(gsort_ctx *c, int L, uint32_t *cur, uint32_t *out, uint32_t *tmp,
                         int cur_list, uint64_t *h, gsort_stats *stats, int *levels,
-                        int last_level = 0, uint16_t *out16 = nullptr) {
+                        int last_level = 0, uint16_t *out16 = nullptr, bool flip_first = false) {
     auto lst = [](DevBuf &b) { return reinterpret_cast<uint64_t *>(b.p); };
     uint64_t *ctr = reinterpret_cast<uint64_t *>(c->d_small + OFF_CTR);
     auto lists = [&](int next) { return work_lists(c, next); };
@@ -712,6 +714,8 @@ gsort_status msd_levels(gsort_ctx *c, int L, uint32_t *cur, uint32_t *out, uint3
         SegPass sp;
         sp.in = cur;
         sp.out = dst;
+        sp.flip_in = flip_first;
+        flip_first = false;
         sp.segs = lst(c->m_next[cur_list]);
         sp.nseg = (uint32_t)nseg;
         sp.shift = 8 * L;
@@ -822,6 +826,9 @@ gsort_status msd_sort_h16(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
     uint64_t *t3 = reinterpret_cast<uint64_t *>(c->m_t3.p);
     uint32_t nblk = 0;
     constexpr uint32_t kCtrWords = (uint32_t)((OFF_CTR3 + kCtrBytes - OFF_CTR) / 8);
+    // K12b's trivial-level word (zeroed by K12a and published with the counters); the
+    // distributed sender (group16) needs every level's output, so it never skips
+    uint32_t *flags = group16 ? nullptr : reinterpret_cast<uint32_t *>(c->d_small + OFF_FLAGS);
     static_assert(kCtrWords <= kRadix && kCtrWords * 8 <= kMailBytes - 64, "counter words");
     if (c->fix_clean != c->m_fix.p)  // new allocation: K12a keeps it zero from here on
         HIP_TRY(c, hipMemsetAsync(c->m_fix.p, 0, kFixBytes, c->stream));
@@ -833,28 +840,46 @@ gsort_status msd_sort_h16(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
                              reinterpret_cast<uint64_t *>(c->m_fix.p), n, group16,
                              reinterpret_cast<uint64_t *>(c->m_ccount.p), t3,
                              t3 + (size_t)kH16Shards * kRadix, bases, totals, cstart, cur, cur3,
-                             tpfx, wl2, wl3, group16 ? nullptr : ctr, kCtrWords, c->stream));
+                             tpfx, wl2, wl3, group16 ? nullptr : ctr, kCtrWords, flags,
+                             c->stream));
     c->fix_clean = c->m_fix.p;
     const uint64_t seq = ++c->mail_seq;
     if (!group16)
         HIP_TRY(c, launch_publish(ctr, kCtrWords, c->d_mail + 8, c->d_mail, seq, c->stream));
     toc(c, PH_COUNT, t);
     t = tic(c);
-    HIP_TRY(c, launch_partition3r(in, tmp, n, cur3, bases, c->stream));
+    HIP_TRY(c, launch_partition3r(in, tmp, n, cur3, bases, flags, c->stream));
     toc(c, PH_LEVEL3, t);
     t = tic(c);
     HIP_TRY(c, launch_partition2r(tmp, out, group16 ? out16 : nullptr, n, tpfx, c->m_tdesc.p,
-                                  bases, totals, cur, c->stream));
+                                  bases, totals, cur, flags, in, c->stream));
     toc(c, PH_LEVEL2, t);
-    if (stats) { stats->keys_level[0] += n; stats->keys_level[1] += n; }
     int levels = 2;
+    if (group16 && stats) { stats->keys_level[0] += n; stats->keys_level[1] += n; }
     if (!group16) {
         ST_TRY(wait_mail(c, seq));
         uint64_t h[3 * (kLocalClasses + 1)], h3[3 * (kLocalClasses + 1)];
         const char *mail = reinterpret_cast<const char *>(c->h_mail + 8);
         memcpy(h, mail, kCtrBytes);
         memcpy(h3, mail + (OFF_CTR3 - OFF_CTR), kCtrBytes);
-        if (stats) stats->keys_level[1] -= h3[1] + h3[4] + h3[7];  // K11'd at level 3
+        uint32_t fl = 0;
+        memcpy(&fl, mail + (OFF_FLAGS - OFF_CTR), 4);
+        const bool triv3 = fl & 1u, triv2 = fl & 2u;
+        levels = 2 - (int)triv3 - (int)triv2;
+        if (stats) {
+            if (!triv3) stats->keys_level[0] += n;
+            if (!triv2) stats->keys_level[1] += n;
+            for (int k = 0; k < kLocalClasses; ++k)  // K11'd whole at level 3
+                stats->keys_level[1] -= std::min<uint64_t>(h3[3 * (k + 1) + 1],
+                                                           stats->keys_level[1]);
+        }
+        if (triv2) {  // levels 3 and 2 moved nothing: level 1 reads the int32 input
+            if (stats) stats->passes_run = levels;
+            ST_TRY(msd_levels(c, 1, const_cast<uint32_t *>(in), out, tmp, 0, h, stats, &levels,
+                              0, nullptr, true));
+            if (stats) stats->passes_run = levels;
+            return GSORT_OK;
+        }
         for (int k = 0; k < kLocalClasses; ++k) {
             const uint64_t *hk = h3 + 3 * (k + 1);
             if (!hk[0]) continue;
