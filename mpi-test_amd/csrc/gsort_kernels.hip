@@ -1841,9 +1841,9 @@ __global__ __launch_bounds__(256) void k_bucket_sizes(const unsigned long long *
 
 __global__ __launch_bounds__(kRadix) void k_classify_gather(
     const unsigned long long *__restrict__ bsize, const unsigned long long *__restrict__ bstart,
-    WorkLists wl) {
+    WorkLists wl, uint32_t h0, uint32_t h1) {
     const uint32_t h = blockIdx.x * kRadix + threadIdx.x;
-    const uint64_t len = bsize[h];
+    const uint64_t len = h >= h0 && h < h1 ? bsize[h] : 0ull;
     // {bucket id, len}: K11g classes, and list 0 (K18 or, past kHxMax, the MSD levels)
     classify_block(h, len, wl);
 }
@@ -2525,8 +2525,8 @@ hipError_t launch_pos_from_meta(const uint32_t *meta, const uint64_t *moff, uint
     return hipGetLastError();
 }
 
-hipError_t launch_recv_classify(const uint64_t *pos, int P, uint64_t *bsize, uint64_t *bstart,
-                                const WorkLists &wl, uint64_t *scratch, hipStream_t s) {
+hipError_t launch_recv_bounds(const uint64_t *pos, int P, uint64_t *bsize, uint64_t *bstart,
+                              uint64_t *scratch, hipStream_t s) {
     using ull = unsigned long long;
     launch_k(k_bucket_sizes, kBuckets16 / 256, 256, 0, s, reinterpret_cast<const ull *>(pos), P,
                                                      reinterpret_cast<ull *>(bsize));
@@ -2535,8 +2535,37 @@ hipError_t launch_recv_classify(const uint64_t *pos, int P, uint64_t *bsize, uin
     launch_k(k_rowscan_reduce<decltype(gen)>, dim3(kScanBlocks, 1), 1024, 0, s, gen, part);
     launch_k(k_rowscan_apply<decltype(gen)>, dim3(kScanBlocks, 1), 1024, 0, s, gen, part, reinterpret_cast<ull *>(bstart),
                                                           kBuckets16 + 1);
+    return hipGetLastError();
+}
+
+hipError_t launch_classify_range(const uint64_t *bsize, const uint64_t *bstart,
+                                 const WorkLists &wl, uint32_t h0, uint32_t h1, hipStream_t s) {
+    using ull = unsigned long long;
     launch_k(k_classify_gather, kBuckets16 / kRadix, kRadix, 0, s,
-        reinterpret_cast<const ull *>(bsize), reinterpret_cast<const ull *>(bstart), wl);
+        reinterpret_cast<const ull *>(bsize), reinterpret_cast<const ull *>(bstart), wl, h0, h1);
+    return hipGetLastError();
+}
+
+hipError_t launch_recv_classify(const uint64_t *pos, int P, uint64_t *bsize, uint64_t *bstart,
+                                const WorkLists &wl, uint64_t *scratch, hipStream_t s) {
+    const hipError_t e = launch_recv_bounds(pos, P, bsize, bstart, scratch, s);
+    if (e != hipSuccess) return e;
+    return launch_classify_range(bsize, bstart, wl, 0, kBuckets16, s);
+}
+
+__global__ __launch_bounds__(256) void k_pick_u64(const unsigned long long *__restrict__ src,
+                                                  const unsigned long long *__restrict__ idx,
+                                                  uint32_t n, unsigned long long *__restrict__ dst) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) dst[i] = src[idx[i]];
+}
+
+hipError_t launch_pick_u64(const uint64_t *src, const uint64_t *idx, uint32_t n, uint64_t *dst,
+                           hipStream_t s) {
+    using ull = unsigned long long;
+    if (n == 0) return hipSuccess;
+    launch_k(k_pick_u64, (n + 255) / 256, 256, 0, s, reinterpret_cast<const ull *>(src),
+             reinterpret_cast<const ull *>(idx), n, reinterpret_cast<ull *>(dst));
     return hipGetLastError();
 }
 

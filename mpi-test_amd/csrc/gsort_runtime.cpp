@@ -38,6 +38,7 @@ enum Phase { PH_COUNT, PH_PASS0, PH_PASS1, PH_PASS2, PH_PASS3, PH_EXCH, PH_PLACE
 
 constexpr size_t kSmallBytes = 256 * 1024;  // device + pinned scratch for counts, plans
 constexpr size_t kMailBytes = 4096;          // K12p mailbox: flag, then the counters (u64)
+constexpr int kMaxXChunks = 8;               // chunks of the distributed radix exchange
 
 struct DevBuf {
     void *p = nullptr;     // what the kernels use
@@ -82,6 +83,10 @@ struct gsort_ctx {
     DevBuf m_rpos, m_bsize;  // receive side: run bucket bounds (P x 65537), bucket size/start
     DevBuf m_bseg, m_blist;  // boundary groups of the distributed radix: scratch, K11 list
     DevBuf m_gb, m_pack, m_meta, m_g16;  // packed exchange: bucket bounds, low 16 bits, counts
+    // chunked exchange of the distributed radix: the stream the chunks' RCCL transfers run on
+    // (high priority) and the event each chunk's arrival sets (created on first use)
+    hipStream_t xstream = nullptr;
+    hipEvent_t ev_x[kMaxXChunks + 1] = {};
     // device small area: [0, 8K) hist4 (4x256 u64) | [8K, 10K) pass digit totals (256 u64) |
     // [10K, 12K) pass digit bases (256 u64) | [20K, 256K) plans / samples / routing tables
     DevBuf small;               // kSmallBytes; d_small aliases small.p
@@ -629,6 +634,15 @@ gsort_status check_all_guards(gsort_ctx *c, const char *where) {
 
 // GSORT_CHECK=1 (diagnostics): host-side invariant checks between the distributed phases, so
 // a broken count fails the call with a message instead of sizing buffers or launches from it
+// GSORT_XCHUNKS: chunks of the distributed radix exchange (1 .. kMaxXChunks, the same on every
+// rank).  Default 1: on one MI355X (1-rank RCCL) 4 chunks overlapped with the receive sort took
+// 2.91 ms per 2^28 keys against 2.36 ms unchunked -- the RCCL copies starve beside K11g
+// (DESIGN.md 6); chunking stays selectable for multi-GPU nodes, where it is unmeasured.
+int x_chunks() {
+    const char *e = getenv("GSORT_XCHUNKS");  // read per sort (tests switch it in-process)
+    return std::min(std::max(e ? atoi(e) : 1, 1), kMaxXChunks);
+}
+
 bool check_mode() {
     static const bool on = getenv("GSORT_CHECK") && atoi(getenv("GSORT_CHECK"));
     return on;
@@ -1321,39 +1335,189 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
             if (recv[q]) { rc[q] = nh[me] * 4; rd[q] = ro * 4; ro += nh[me]; }
         }
     }
+    // (5a) the chunk plan.  Chunk k of destination q = its buckets [hbq(q, k), hbq(q, k + 1)):
+    // the sender and the receiver split q's bucket range identically, so chunk k of the run
+    // p -> q is pack[max(cut, gb[hbq]) ..) on the sender and pos[p][hbq] on the receiver.
+    const int C = x_chunks();
+    auto hbq = [&](int q, int k) -> uint64_t { return hlo[q] + nh[q] * (uint64_t)k / C; };
+    std::vector<uint64_t> roffs(P + 1, 0);
+    for (int p = 0; p < P; ++p) roffs[p + 1] = roffs[p] + recv[p];
+    uint64_t *h_pl = reinterpret_cast<uint64_t *>(c->h_small + OFF_PLAN);
+    uint64_t *d_pl = reinterpret_cast<uint64_t *>(c->d_small + OFF_PLAN);
+    // OFF_PLAN: [0, 2P) run offsets + lengths (u64) | +1 KiB: pick indices | +8 KiB: picked
+    // values | +16 KiB: the chunks' work-list counters
+    constexpr size_t kPickIdx = 1024 / 8, kPicked = 8192 / 8, kChunkCtr = 16384;
+    uint64_t *d_r = d_pl;
+    uint32_t npick_s = 0, npick = 0;
+    {
+        for (int p = 0; p < P; ++p) { h_pl[p] = roffs[p]; h_pl[P + p] = recv[p]; }
+        uint64_t *idx = h_pl + kPickIdx;
+        for (int q = 0; q < P; ++q)
+            if (send[q])
+                for (int k = 1; k < C; ++k) idx[npick++] = hbq(q, k);
+        npick_s = npick;
+        for (int p = 0; p < P; ++p)
+            if (recv[p])
+                for (int k = 1; k < C; ++k) idx[npick++] = (uint64_t)p * (kBuckets16 + 1) + hbq(me, k);
+        static_assert(2 * 64 * (kMaxXChunks - 1) <= kPicked - kPickIdx, "pick area");
+        HIP_TRY(c, hipMemcpyAsync(d_pl, h_pl, (kPickIdx + npick) * 8, hipMemcpyHostToDevice,
+                                  c->stream));
+    }
     t = tic_rec(c);
     ST_TRY(comm_try(c, c->comm->alltoallv(meta_s, sc.data(), sd.data(), meta_r, rc.data(),
                                           rd.data(), c->stream)));
-    size_t so = 0, ro = 0;
-    for (int q = 0; q < P; ++q) {
-        sc[q] = send[q] * 2; sd[q] = so; so += sc[q];
-        rc[q] = recv[q] * 2; rd[q] = ro; ro += rc[q];
-        if (stats && q != me) {
-            stats->bytes_sent += sc[q];
-            stats->max_pair_bytes = std::max<uint64_t>(stats->max_pair_bytes, sc[q]);
-        }
-    }
-    if (ro != mine * 2) return set_err(c, GSORT_EINVAL, "exchange plan does not fill the block");
-    uint16_t *rbuf = slot_ptr<uint16_t>(c, S_RECV);
-    ST_TRY(comm_try(c, c->comm->alltoallv(pack, sc.data(), sd.data(), rbuf, rc.data(),
-                                          rd.data(), c->stream)));
     toc_rec(c, PH_EXCH, t);
-    if (stats) stats->exchanges = 1;
-    // (5) the P received runs -> one sorted block (recv_sort), their bucket bounds from the counts
+    for (int q = 0; q < P; ++q)
+        if (stats && q != me) {
+            stats->bytes_sent += send[q] * 2;
+            stats->max_pair_bytes = std::max<uint64_t>(stats->max_pair_bytes, send[q] * 2);
+        }
+    if (roffs[P] != mine) return set_err(c, GSORT_EINVAL, "exchange plan does not fill the block");
+    uint16_t *rbuf = slot_ptr<uint16_t>(c, S_RECV);
+    if (C == 1) {  // one exchange, queued behind the counts: the plan below overlaps it
+        t = tic_rec(c);
+        for (int q = 0; q < P; ++q) {
+            sc[q] = send[q] * 2;
+            sd[q] = cut[q] * 2;
+            rc[q] = recv[q] * 2;
+            rd[q] = roffs[q] * 2;
+        }
+        ST_TRY(comm_try(c, c->comm->alltoallv(pack, sc.data(), sd.data(), rbuf, rc.data(),
+                                              rd.data(), c->stream)));
+        toc_rec(c, PH_EXCH, t);
+    }
+    // (5b) the receive plan from the counts alone: run bounds, bucket starts, and the K11g / K18
+    // work lists of every chunk (list entries of chunk k from entry hbq(me, k) - hlo[me] on)
     t = tic(c);
     ST_TRY(ensure(c, c->m_rpos, (size_t)P * (kBuckets16 + 1) * 8));
     ST_TRY(ensure(c, c->m_bsize, kBsizeBytes));
-    HIP_TRY(c, launch_pos_from_meta(meta_r, d_moff, (uint32_t)hlo[me], (uint32_t)nh[me], P,
-                                    reinterpret_cast<uint64_t *>(c->m_rpos.p),
-                                    reinterpret_cast<uint64_t *>(c->m_bsize.p) + 2 * kBuckets16 + 1,
-                                    c->stream));
-    if (check_mode())
+    ST_TRY(ensure_list(c, c->m_next[0], kBuckets16));
+    for (auto &b : c->m_local) ST_TRY(ensure_list(c, b, kBuckets16));
+    uint64_t *pos = reinterpret_cast<uint64_t *>(c->m_rpos.p);
+    uint64_t *bsize = reinterpret_cast<uint64_t *>(c->m_bsize.p), *bstart = bsize + kBuckets16;
+    uint64_t *cctr = reinterpret_cast<uint64_t *>(c->d_small + OFF_PLAN + kChunkCtr);
+    HIP_TRY(c, launch_pos_from_meta(meta_r, d_moff, (uint32_t)hlo[me], (uint32_t)nh[me], P, pos,
+                                    bstart + kBuckets16 + 1, c->stream));
+    HIP_TRY(c, hipMemsetAsync(cctr, 0, (size_t)C * kCtrBytes, c->stream));
+    HIP_TRY(c, launch_recv_bounds(pos, P, bsize, bstart, bstart + kBuckets16 + 1, c->stream));
+    auto chunk_lists = [&](int k) {
+        WorkLists wl = work_lists(c, 0);
+        const uint64_t off = 2 * (hbq(me, k) - hlo[me]);
+        for (auto &l : wl.list) l += off;
+        wl.ctr = cctr + (size_t)k * (kCtrBytes / 8);
+        return wl;
+    };
+    for (int k = 0; k < C; ++k)
+        HIP_TRY(c, launch_classify_range(bsize, bstart, chunk_lists(k), (uint32_t)hbq(me, k),
+                                         (uint32_t)hbq(me, k + 1), c->stream));
+    HIP_TRY(c, launch_pick_u64(gb, d_pl + kPickIdx, npick_s, d_pl + kPicked, c->stream));
+    HIP_TRY(c, launch_pick_u64(pos, d_pl + kPickIdx + npick_s, npick - npick_s,
+                               d_pl + kPicked + npick_s, c->stream));
+    toc(c, PH_COUNT, t);
+    HIP_TRY(c, hipMemcpyAsync(h_pl + kPicked, d_pl + kPicked, npick * 8, hipMemcpyDeviceToHost,
+                              c->stream));
+    HIP_TRY(c, hipMemcpyAsync(c->h_small + OFF_PLAN + kChunkCtr, cctr, (size_t)C * kCtrBytes,
+                              hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    std::vector<uint64_t> hc((size_t)C * (kCtrBytes / 8));
+    memcpy(hc.data(), c->h_small + OFF_PLAN + kChunkCtr, (size_t)C * kCtrBytes);
+    if (check_mode()) {
         for (int p = 0; p < P; ++p)
-            ST_TRY(check_bounds(c, reinterpret_cast<uint64_t *>(c->m_rpos.p) +
-                                       (size_t)p * (kBuckets16 + 1),
-                                kBuckets16 + 1, recv[p], "received run bounds"));
-    ST_TRY(recv_sort(c, rbuf, true, recv, mine, slot_ptr<uint32_t>(c, S_OUT),
-                     slot_ptr<uint32_t>(c, S_TMP), stats));
+            ST_TRY(check_bounds(c, pos + (size_t)p * (kBuckets16 + 1), kBuckets16 + 1, recv[p],
+                                "received run bounds"));
+        uint64_t keys = 0;
+        for (int k = 0; k < C; ++k)
+            for (int l = 0; l <= kLocalClasses; ++l) keys += hc[(size_t)k * (kCtrBytes / 8) + 3 * l + 1];
+        if (keys != mine)
+            return set_err(c, GSORT_EINVAL, "GSORT_CHECK chunk lists hold " + std::to_string(keys) +
+                                                " keys, want " + std::to_string(mine) + " (rank " +
+                                                std::to_string(me) + ")");
+    }
+    bool big = false;  // a bucket past K18's reach: the unchunked receive (MSD levels 1, 0)
+    for (int k = 0; k < C; ++k) {
+        const uint64_t *h = &hc[(size_t)k * (kCtrBytes / 8)];
+        big = big || (h[0] && h[2] > kHxMax);
+    }
+    // the cut of every destination's run per chunk (sender) and of every source's (receiver)
+    std::vector<uint64_t> s_off((size_t)P * (C + 1)), r_off((size_t)P * (C + 1));
+    {
+        const uint64_t *pk = h_pl + kPicked;
+        uint32_t i = 0;
+        for (int q = 0; q < P; ++q) {
+            uint64_t *so = &s_off[(size_t)q * (C + 1)];
+            so[0] = cut[q];
+            so[C] = cut[q + 1];
+            for (int k = 1; k < C; ++k)
+                so[k] = send[q] ? std::min(std::max(pk[i++], so[k - 1]), cut[q + 1]) : cut[q];
+        }
+        for (int p = 0; p < P; ++p) {
+            uint64_t *ro = &r_off[(size_t)p * (C + 1)];
+            ro[0] = 0;
+            ro[C] = recv[p];
+            for (int k = 1; k < C; ++k)
+                ro[k] = recv[p] ? std::min(std::max(pk[i++], ro[k - 1]), recv[p]) : 0;
+        }
+    }
+    const int CX = C == 1 ? 0 : big ? 1 : C;  // exchanges still to issue on xstream
+    if (CX && !c->xstream) {
+        int lo = 0, hi = 0;
+        HIP_TRY(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
+        HIP_TRY(c, hipStreamCreateWithPriority(&c->xstream, hipStreamNonBlocking, hi));
+        for (auto &e : c->ev_x) HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    // (4) the keys' low 16 bits, chunk by chunk on xstream once the pack and the plan are done
+    hipEvent_t xa = nullptr;
+    if (CX) {
+        HIP_TRY(c, hipEventRecord(c->ev_x[kMaxXChunks], c->stream));
+        HIP_TRY(c, hipStreamWaitEvent(c->xstream, c->ev_x[kMaxXChunks], 0));
+        if (c->timing && (xa = next_event(c))) HIP_TRY(c, hipEventRecord(xa, c->xstream));
+    }
+    for (int k = 0; k < CX; ++k) {
+        const int k1 = big ? C : k + 1;
+        for (int q = 0; q < P; ++q) {
+            const uint64_t *so = &s_off[(size_t)q * (C + 1)], *ro = &r_off[(size_t)q * (C + 1)];
+            sc[q] = (so[k1] - so[k]) * 2;
+            sd[q] = so[k] * 2;
+            rc[q] = (ro[k1] - ro[k]) * 2;
+            rd[q] = (roffs[q] + ro[k]) * 2;
+        }
+        ST_TRY(comm_try(c, c->comm->alltoallv(pack, sc.data(), sd.data(), rbuf, rc.data(),
+                                              rd.data(), c->xstream)));
+        if (xa && k == CX - 1) {  // before the last arrival event, so complete when it is
+            hipEvent_t xb = next_event(c);
+            if (xb && hipEventRecord(xb, c->xstream) == hipSuccess)
+                c->spans.push_back({PH_EXCH, xa, xb});
+        }
+        HIP_TRY(c, hipEventRecord(c->ev_x[k], c->xstream));
+    }
+    if (stats) stats->exchanges = 1;
+    // (5c) chunk k's buckets are sorted (K11g by size class, K18 past kLocalMax) as soon as
+    // chunk k has arrived, while the next chunks are in flight
+    t = tic(c);
+    uint32_t *out = slot_ptr<uint32_t>(c, S_OUT);
+    if (big) {
+        if (CX) HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_x[0], 0));
+        ST_TRY(recv_sort(c, rbuf, true, recv, mine, out, slot_ptr<uint32_t>(c, S_TMP), stats));
+    } else {
+        for (int k = 0; k < C; ++k) {
+            if (CX) HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_x[k], 0));
+            const uint64_t *h = &hc[(size_t)k * (kCtrBytes / 8)];
+            const WorkLists wl = chunk_lists(k);
+            for (int cl = 0; cl < kLocalClasses; ++cl) {
+                const uint64_t *hk = h + 3 * (cl + 1);
+                if (!hk[0]) continue;
+                HIP_TRY(c, launch_gather_sort(rbuf, true, pos, d_r, P, bstart, wl.list[cl + 1],
+                                              (uint32_t)hk[0], cl + 1, c->atomic_rank, out,
+                                              c->stream));
+                if (stats) { stats->buckets_local += hk[0]; stats->keys_bucket_sort += hk[1]; }
+            }
+            if (h[0]) {
+                HIP_TRY(c, launch_hist_expand(rbuf, true, pos, d_r, P, bstart, wl.list[0],
+                                              (uint32_t)h[0], out, c->stream));
+                if (stats) { stats->buckets_local += h[0]; stats->keys_bucket_sort += h[1]; }
+            }
+        }
+    }
     toc(c, PH_MERGE, t);
     if (stats) stats->passes_run = pr;
     *d_out = slot_ptr<int32_t>(c, S_OUT);
@@ -1898,6 +2062,7 @@ gsort_status gsort_destroy(gsort_ctx *c) {
     }
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->xstream) (void)hipStreamSynchronize(c->xstream);
     delete c->comm;
     for_each_buf(c, [](const std::string &, DevBuf &b) { (void)dev_free(b); });
     c->d_small = nullptr;
@@ -1908,6 +2073,9 @@ gsort_status gsort_destroy(gsort_ctx *c) {
     if (c->h_small) (void)hipHostFree(c->h_small);
     if (c->h_mail) (void)hipHostFree(c->h_mail);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
+    for (auto e : c->ev_x)
+        if (e) (void)hipEventDestroy(e);
+    if (c->xstream) (void)hipStreamDestroy(c->xstream);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return GSORT_OK;
