@@ -194,6 +194,11 @@ hipError_t launch_unpack16(const uint16_t *in, uint64_t n, uint32_t h, int32_t *
 hipError_t launch_gb_from_plan(const uint64_t *bases, const uint64_t *totals,
                                const uint64_t *segs, uint32_t nseg, const uint64_t *cstart,
                                uint64_t n, uint64_t *gb, hipStream_t s);
+// K13s: one radix-select round decided on the device (boundary q: prefix[q] += the largest
+// digit d whose all-gathered count of keys below prefix[q] + (d << shift) stays <= g[q]; the
+// next round's M thresholds prefix[q] + (d << (shift - 8)) written to xs).
+hipError_t launch_select_digit(const uint64_t *all, const uint64_t *g, uint64_t N, int P, int nb,
+                               int M, int shift, uint64_t *prefix, uint64_t *xs, hipStream_t s);
 // K13 on the packed buffer (bucket bounds gb): out[i] = #keys < xs[i] (ordered u32).
 hipError_t launch_count_below16(const uint16_t *a, const uint64_t *gb, const uint64_t *xs,
                                 int m, uint64_t *out, hipStream_t s);

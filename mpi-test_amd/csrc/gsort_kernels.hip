@@ -2474,6 +2474,43 @@ hipError_t launch_count_below16(const uint16_t *a, const uint64_t *gb, const uin
     return hipGetLastError();
 }
 
+// K13s (radix select, a round decided on the device): boundary q = block, digit d = thread.
+// all = the P all-gathered rows of nb x M counts, all[p][q][d] = rank p's keys below
+// prefix[q] + (d << shift); the round's digit is the largest d < 256 whose global count stays
+// <= g[q] (the counts grow with d), prefix[q] gains it, and the next round's M thresholds
+// prefix[q] + (d << (shift - 8)) go to xs.  Boundaries at the end (g[q] >= N) keep their prefix.
+__global__ __launch_bounds__(256) void k_select_digit(const unsigned long long *__restrict__ all,
+                                                      const unsigned long long *__restrict__ g,
+                                                      unsigned long long N, int P, int nb, int M,
+                                                      int shift, unsigned long long *prefix,
+                                                      unsigned long long *__restrict__ xs) {
+    __shared__ uint32_t s_ok;
+    const int q = blockIdx.x, d = threadIdx.x;
+    unsigned long long below = 0;
+    for (int p = 0; p < P; ++p) below += all[((size_t)p * nb + q) * M + d];
+    const unsigned long long gq = g[q], p0 = prefix[q];
+    if (d == 0) s_ok = 0;
+    __syncthreads();
+    const uint64_t okm = __ballot(below <= gq);
+    if ((d & 63) == 0) atomicAdd(&s_ok, (uint32_t)__popcll(okm));
+    __syncthreads();
+    const uint32_t best = s_ok ? s_ok - 1 : 0;
+    const unsigned long long pf = gq >= N ? p0 : p0 + ((unsigned long long)best << shift);
+    if (d == 0) prefix[q] = pf;
+    for (int j = d; j < M; j += 256) xs[(size_t)q * M + j] = pf + ((unsigned long long)j << (shift - 8));
+}
+
+hipError_t launch_select_digit(const uint64_t *all, const uint64_t *g, uint64_t N, int P, int nb,
+                               int M, int shift, uint64_t *prefix, uint64_t *xs, hipStream_t s) {
+    using ull = unsigned long long;
+    if (nb <= 0) return hipSuccess;
+    if (shift < 8 || M < 256) return hipErrorInvalidValue;
+    launch_k(k_select_digit, nb, 256, 0, s, reinterpret_cast<const ull *>(all),
+             reinterpret_cast<const ull *>(g), (ull)N, P, nb, M, shift,
+             reinterpret_cast<ull *>(prefix), reinterpret_cast<ull *>(xs));
+    return hipGetLastError();
+}
+
 hipError_t launch_local_sort(const uint32_t *in, uint32_t *out, const uint64_t *list,
                              uint32_t nlist, int cls, int ndigits, bool flip_in,
                              bool atomic_rank, hipStream_t s) {

@@ -1219,27 +1219,44 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
     int pr = stats ? stats->passes_run : 0;
     if (check_mode()) ST_TRY(check_bounds(c, gb, kBuckets16 + 1, n_in, "sender bucket bounds"));
 
-    // (2) radix select of v_q, the g_q-th smallest key, for the P-1 inner boundaries
+    // (2) radix select of v_q, the g_q-th smallest key, for the P-1 inner boundaries.  Rounds 0
+    // and 2 are decided on the device (K13s writes the next round's thresholds), rounds 1 and 3
+    // on the host, which needs their counts: two host synchronisations for the four rounds.
     const int nb = P - 1, M = 257;
-    std::vector<uint64_t> g(nb), prefix(nb, 0), hx((size_t)nb * M), all((size_t)P * nb * M);
+    std::vector<uint64_t> g(nb), prefix(nb, 0), hx((size_t)2 * nb + (size_t)nb * M),
+        all((size_t)P * nb * M);
     std::vector<int> dsel(nb, 0);
     for (int q = 0; q < nb; ++q) g[q] = std::min<uint64_t>((uint64_t)(q + 1) * B, N);
-    ST_TRY(ensure(c, c->m_split, (size_t)std::max(nb, 1) * M * 16));
+    ST_TRY(ensure(c, c->m_split, (size_t)std::max(nb, 1) * (M * 16 + 16)));
     ST_TRY(ensure(c, c->slot[S_STAGE], (size_t)P * std::max(nb, 1) * M * 8));
-    uint64_t *d_xs = reinterpret_cast<uint64_t *>(c->m_split.p);
+    // m_split: prefix (nb) | g (nb) | thresholds (nb x M) | counts (nb x M), u64
+    uint64_t *d_pref = reinterpret_cast<uint64_t *>(c->m_split.p), *d_g = d_pref + nb;
+    uint64_t *d_xs = d_g + nb;
     uint64_t *d_cnt = d_xs + (size_t)nb * M;
+    const uint64_t *d_all = reinterpret_cast<const uint64_t *>(c->slot[S_STAGE].p);
     t = tic_rec(c);
     for (int k = 0; k < 4; ++k) {
         const int shift = 24 - 8 * k;
-        for (int q = 0; q < nb; ++q)
-            for (int d = 0; d < M; ++d) hx[(size_t)q * M + d] = prefix[q] + ((uint64_t)d << shift);
-        HIP_TRY(c, hipMemcpyAsync(d_xs, hx.data(), hx.size() * 8, hipMemcpyHostToDevice,
-                                  c->stream));
+        if (k % 2 == 0) {  // thresholds from the host's prefix
+            for (int q = 0; q < nb; ++q) { hx[q] = prefix[q]; hx[nb + q] = g[q]; }
+            for (int q = 0; q < nb; ++q)
+                for (int d = 0; d < M; ++d)
+                    hx[2 * nb + (size_t)q * M + d] = prefix[q] + ((uint64_t)d << shift);
+            HIP_TRY(c, hipMemcpyAsync(d_pref, hx.data(), hx.size() * 8, hipMemcpyHostToDevice,
+                                      c->stream));
+        }
         HIP_TRY(c, launch_count_below16(pack, gb, d_xs, nb * M, d_cnt, c->stream));
         ST_TRY(comm_try(c, c->comm->allgather(d_cnt, c->slot[S_STAGE].p, (size_t)nb * M * 8,
                                               c->stream)));
-        HIP_TRY(c, hipMemcpyAsync(all.data(), c->slot[S_STAGE].p, all.size() * 8,
-                                  hipMemcpyDeviceToHost, c->stream));
+        if (k % 2 == 0) {
+            HIP_TRY(c, launch_select_digit(d_all, d_g, N, P, nb, M, shift, d_pref, d_xs,
+                                           c->stream));
+            continue;
+        }
+        HIP_TRY(c, hipMemcpyAsync(all.data(), d_all, all.size() * 8, hipMemcpyDeviceToHost,
+                                  c->stream));
+        HIP_TRY(c, hipMemcpyAsync(prefix.data(), d_pref, (size_t)nb * 8, hipMemcpyDeviceToHost,
+                                  c->stream));
         HIP_TRY(c, hipStreamSynchronize(c->stream));
         for (int q = 0; q < nb; ++q) {
             if (g[q] >= N) continue;  // boundary at the end: every key goes left
