@@ -176,7 +176,7 @@ def cpu_baseline(dist, seed):
         shutil.rmtree(tmp, ignore_errors=True)
 
 
-def kernel_rooflines(stats, n_local):
+def kernel_rooflines(stats, n_local, plan=0):
     """Per kernel class: total device time over the timed steps (HIP events recorded on
     libgsort's stream around every launch), launches, algorithmic bytes:
     K3 / K3u read + write every key of the launch (8 B/key), K11 reads and writes every key of
@@ -201,12 +201,18 @@ def kernel_rooflines(stats, n_local):
     # MSD levels: ms_level[0] = level 3 (K3u k_partition); with the two-level plan (default,
     # GSORT_PLAN16 != 0) ms_level[0] = level 3 (K3r) and ms_level[1] = level 2 (K3a), runs reserved by atomics;
     # every other level is a segmented K3u (k_seg_partition)
+    # The sampled plan (plan 1): K1e reads 1/64 of the keys (0.0625 B/key; the
+    # phase also holds K12e-a/b), then K3r / K3a (EST) and K11e (k_local_sort_e) as below.
     plan16 = os.environ.get("GSORT_PLAN16", "1") != "0"
     seg_from = 2 if plan16 else 1
+    if plan == 1:
+        add("k_est_sample (K1e: 1/64 sample histogram; with K12e-a + K12e-b)",
+            ("k_est_sample",), [s["ms_hist"] for s in stats], [n_local for s in stats], 0.0625)
     if plan16:  # K1h reads every key once (4 B/key); the phase also holds K12a/b/p (~27 us)
-        add("k_hist16 (K1h: 16-bit histogram; with K12a + K12b + K12p)",
-            ("k_hist16",), [s["ms_hist"] if s["ms_level"][1] > 0 else 0.0 for s in stats],
-            [n_local for s in stats], 4)
+        if plan != 1:
+            add("k_hist16 (K1h: 16-bit histogram; with K12a + K12b + K12p)",
+                ("k_hist16",), [s["ms_hist"] if s["ms_level"][1] > 0 else 0.0 for s in stats],
+                [n_local for s in stats], 4)
         add("k_partition_res L3 (K3r: level 3, runs reserved on per-XCD-shard cursors)",
             ("k_partition_res<1024, 8, true",), [s["ms_level"][0] for s in stats],
             [s["keys_level"][0] for s in stats], PASS_BYTES_PER_KEY)
@@ -220,9 +226,15 @@ def kernel_rooflines(stats, n_local):
     add("k_seg_partition (K3u: segmented MSD level)", ("k_seg_partition",),
         [x for s in stats for x in s["ms_level"][seg_from:]],
         [k for s in stats for k in s["keys_level"][seg_from:]], PASS_BYTES_PER_KEY)
-    add("k_local_sort (K11: in-LDS sort of the small buckets)", ("k_local_sort",),
-        [s["ms_bucket_sort"] for s in stats], [s["keys_bucket_sort"] for s in stats],
-        PASS_BYTES_PER_KEY)
+    if plan == 1:
+        add("k_local_sort_e (K11e: in-LDS sort of every level-2 child into its exact place; "
+            "with K12g)", ("k_local_sort_e",),
+            [s["ms_bucket_sort"] for s in stats], [s["keys_bucket_sort"] for s in stats],
+            PASS_BYTES_PER_KEY)
+    else:
+        add("k_local_sort (K11: in-LDS sort of the small buckets)", ("k_local_sort",),
+            [s["ms_bucket_sort"] for s in stats], [s["keys_bucket_sort"] for s in stats],
+            PASS_BYTES_PER_KEY)
     return out
 
 
@@ -351,6 +363,7 @@ def main():
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
+    plan = ctx.last_plan()
     if a.no_stats:  # experiment: the un-instrumented step time; stats from extra steps
         stats = [fn(d_in, n_local)[2] for _ in range(a.steps)]
     else:
@@ -380,7 +393,7 @@ def main():
     ceiling = copy_ceiling(ctx, n_local) if rank == 0 else None
     drop_in = drop_in_e2e(ctx, fn, d_in, n_local) if world == 1 else None
 
-    rooflines = kernel_rooflines(stats, n_local)
+    rooflines = kernel_rooflines(stats, n_local, plan)
     dom = max(rooflines, key=lambda r: r["total_ms"])
     pmc = pmc_traffic(a.algo, n_local, world, dom["pmc_prefixes"])
     traffic = pmc["hbm_bytes_per_launch"] if pmc else None
@@ -432,6 +445,8 @@ def main():
         "phases_ms_avg": phases,
         "passes_run": last["passes_run"],
         "local_algo": "lsd" if last["local_algo"] == gsort.LOCAL_LSD else "msd",
+        "local_plan": {0: "exact two-level", 1: "sampled", 2: "sampled, re-sorted exact"}.get(
+            plan, str(plan)),
         "verified": bool(ok),
     }
     if last["exchanges"]:

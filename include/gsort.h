@@ -138,6 +138,11 @@ gsort_status gsort_sample(gsort_ctx *ctx, const int32_t *d_keys, size_t n_local,
  * and this rank's P bucket lengths ("[COMMON] r: Bucket j=len", :156-158). */
 gsort_status gsort_sample_info(const gsort_ctx *ctx, int32_t *splitters,
                                uint64_t *bucket_counts);
+/* Which plan the last one-rank local sort of ctx took (diagnostics; no reference
+ * counterpart): 0 the exact two-level plan (or a small / distributed case), 1 the sampled
+ * plan, 2 the sampled plan found the block ineligible or a region overflowed, and the block
+ * was sorted again on the exact plan (GSORT_EST=0 turns the sampled plan off). */
+int gsort_last_plan(const gsort_ctx *ctx);
 
 /* ---- drop-in staging (replaces MPI_Scatter / MPI_Gather(v) through rank 0) ---------------
  * gsort_scatter_from_root: rank 0's host array (n_total keys; h_root ignored elsewhere) ->

@@ -256,6 +256,45 @@ hipError_t launch_stream_copy(const void *in, void *out, uint64_t bytes, hipStre
 hipError_t launch_minmax(const int32_t *a, uint64_t n, int *mm, hipStream_t s);
 hipError_t launch_compat_keys(const int32_t *a, uint64_t n, int P, int loop, const int *mod,
                               const double *scale, uint32_t *key, uint64_t *bad, hipStream_t s);
+// ---- sampled plan (gsort_kernels.hip, "Sampled plan") -----------------------
+// Levels 3 and 2 sized from a 1/64 sample instead of K1h's full histogram: in (int32) ->
+// level 3 into the gapped regions of x -> level 2 into the gapped regions of y -> K11e into
+// out (int32, exact positions).  eflag[0] bit 2: ineligible (nothing past the plan ran);
+// eflag[1]: a region overflowed (the output is wrong).  Either way the caller re-sorts on the
+// exact plan; both are known once K12g has run (the runtime reads them with the K11e list
+// counts).  Sizes (u32 unless noted): part8 kEstWGs x 16384, part3 kEstWGs x 2048, msamp
+// kEstWGs, capc / cur2 / lim2 / init2 65536, cap3 / cur3 / lim3 / init3 2048, r2 / r3 / bases3 /
+// bases2 256 u64, tp 257, tdesc est_max_tiles(n) x kTileDescBytes, dump kSweepTile keys;
+// wl.list[1..4] 65536 entries each, wl.ctr the 15 counters (zeroed by the front).
+constexpr uint32_t kEstWGs = 128;
+constexpr uint32_t kEstBlockKeysHost = 512;  // one 8-key sample segment per block
+constexpr uint64_t kEstMinKeys = 1ull << 22;   // below: too few samples per child
+constexpr uint64_t kEstMaxKeys = 1ull << 31;   // level-3 regions stay below 2^32 keys
+inline uint64_t est_max_tiles(uint64_t n) { return sweep_tiles(n) + 8 * 256; }
+struct EstPlan {
+    const uint32_t *in;
+    uint64_t n;
+    bool flip_in;
+    uint32_t *x, *y, *out;
+    uint64_t capx, capy;  // keys of x and y
+    uint32_t *part8, *part3, *msamp;
+    uint32_t *capc, *cap3;
+    uint64_t *r2, *r3, *bases3, *bases2;
+    uint32_t *cur2, *lim2, *init2, *cur3, *lim3, *init3;
+    uint32_t *tp;
+    void *tdesc;
+    uint32_t *dump;
+    uint32_t *eflag;
+    WorkLists wl;
+    double slack;
+    bool atomic_rank;
+};
+hipError_t launch_est_front(const EstPlan &p, hipStream_t s);   // K1e + K12e
+hipError_t launch_est_level3(const EstPlan &p, hipStream_t s);  // K3r
+hipError_t launch_est_level2(const EstPlan &p, hipStream_t s);  // K12f + K3a
+hipError_t launch_est_classify(const EstPlan &p, hipStream_t s);  // K12g
+// K11e over class list cls (nlist entries: the host reads the counts K12g made)
+hipError_t launch_local_sort_e(const EstPlan &p, int cls, uint32_t nlist, hipStream_t s);
 // Plain device copy kernel (used when a sort has no non-trivial pass).
 hipError_t launch_copy(const uint32_t *in, uint32_t *out, uint64_t n, hipStream_t s);
 

@@ -16,6 +16,8 @@
 //   K8     mpi_radix_sort.c:164-192 per-pass placement (receive side of the exchange)
 #include <hip/hip_ext.h>
 
+#include <algorithm>
+
 #include "gsort_kernels.h"
 
 namespace gsort {
@@ -1446,18 +1448,25 @@ __global__ __launch_bounds__(256) void k_tile_desc(const uint32_t *__restrict__ 
 // the int32 input raw itself (flipping on load); K3a does nothing when bit 1 is set (the
 // caller continues from level 1 on the input).  Each level that moved keys without changing
 // their order cost a full pass (16-bit keys took four partitions).
-template <int BLOCK, int ITEMS, bool L3, bool FIN, typename OT = uint32_t>
+// EST (the sampled plan, "Sampled plan" below): every cursor run must end below its limit
+// lim[same index as cur] (the run's region, sized from a sample); a run that would not fits
+// raises *ovf and goes to the TILE-key scratch `dump` instead (the caller then re-sorts on the
+// exact plan).  flags bit 2 (the sample found the input ineligible): do nothing.
+template <int BLOCK, int ITEMS, bool L3, bool FIN, typename OT = uint32_t, bool EST = false>
 __global__ __launch_bounds__(BLOCK) void k_partition_res(
     const uint32_t *__restrict__ in, OT *__restrict__ out, uint64_t n,
     const uint32_t *__restrict__ tpfx, const TileDesc *__restrict__ desc,
     const unsigned long long *__restrict__ bases, uint32_t *__restrict__ cur,
-    const uint32_t *__restrict__ flags, const uint32_t *__restrict__ raw) {
+    const uint32_t *__restrict__ flags, const uint32_t *__restrict__ raw,
+    const uint32_t *__restrict__ lim = nullptr, uint32_t *__restrict__ ovf = nullptr,
+    OT *__restrict__ dump = nullptr) {
     constexpr int TILE = BLOCK * ITEMS, shift = L3 ? 24 : 16;
     static_assert(TILE == kSweepTile, "reservation tiles are kSweepTile keys");
     uint32_t flip = 0;
     if (flags) {
         const uint32_t f = *flags;
-        if (f & (L3 ? 1u : 2u)) return;
+        if (f & (L3 ? 5u : 6u)) return;
+        if (EST && !L3 && *ovf) return;  // level 3 overflowed: the exact plan sorts again
         if (!L3 && (f & 1u)) { in = raw; flip = kFlip; }
     }
     __shared__ uint32_t s_keys[2][TILE];
@@ -1515,11 +1524,12 @@ __global__ __launch_bounds__(BLOCK) void k_partition_res(
             if ((uint32_t)(i * BLOCK) + tid < len[h])
                 r[h][i] = agg_rank(s_cur[h], (k[h][i] >> shift) & 255u, s_spare);
     __syncthreads();
-    uint32_t excl[2] = {0, 0}, pos[2] = {0, 0};
+    uint32_t excl[2] = {0, 0}, pos[2] = {0, 0}, cnt[2] = {0, 0};
     if (tid < kRadix) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const uint32_t c = s_cur[h][tid];
+            cnt[h] = c;
             if (c) pos[h] = atomicAdd(&cursor[h][tid], c);
             uint32_t v = c;
 #pragma unroll
@@ -1548,8 +1558,15 @@ __global__ __launch_bounds__(BLOCK) void k_partition_res(
                 s_keys[h][s_cur[h][(k[h][i] >> shift) & 255u] + r[h][i]] = k[h][i];
     if (tid < kRadix) {
 #pragma unroll
-        for (int h = 0; h < 2; ++h)
-            s_dst[h][tid] = out + ((L3 ? bases[tid] : bases[seg[h]]) + pos[h]) - excl[h];
+        for (int h = 0; h < 2; ++h) {
+            OT *d = out + ((L3 ? bases[tid] : bases[seg[h]]) + pos[h]) - excl[h];
+            if (EST && cnt[h] &&
+                (uint64_t)pos[h] + cnt[h] > lim[(L3 ? (pr % kShards) : seg[h]) * kRadix + tid]) {
+                atomicOr(ovf, 1u);
+                d = dump - excl[h];
+            }
+            s_dst[h][tid] = d;
+        }
     }
     __syncthreads();
 #pragma unroll
@@ -2147,6 +2164,354 @@ __global__ __launch_bounds__(512) void k_lds_order_check(const uint32_t *__restr
     if (nbad) atomicAdd(bad, (unsigned long long)nbad);
 }
 
+// =======================================================================================
+// Sampled plan (the default local MSD sort for large blocks).  The two-level
+// plan reads every key once only to size the level-3 buckets and level-2 children (K1h, 4 B
+// per key of the 28).  Here a 1/64 sample sizes them instead: every region gets its estimate
+// plus 6 sigma of sampling error, so the partitions write into gapped regions (level 3 into X,
+// level 2 into Y) whose true fill is only known afterwards, and K11 sorts each child from Y
+// into its exact place in the output.  24 B/key.  A run that would overflow its region is
+// diverted to a scratch tile and flagged (the runtime then re-sorts on the exact plan), so the
+// estimate decides speed, never the result.
+//   K1e k_est_sample: sample histograms (8 consecutive keys at a hashed offset of every
+//       512-key block: short segments keep the estimate of position-correlated input, e.g.
+//       concatenated sorted runs, close to that of independent samples), 65536 u8 child
+//       counters + 8 x 256 shard counters per workgroup
+//   K12e k_est_caps / k_est_place: region capacities, bases and cursors; eligibility
+//   K3r / K3a (EST): the reservation partitions with region limits
+//   K12f k_est_tiles: K3a tile descriptors over the level-3 pieces (bucket x shard)
+//   K12g k_est_classify: exact child sizes from the cursors, output offsets, K11 lists
+//   K11e k_local_sort_e: persistent K11 over {src in Y, dst in out, len} entries
+// The eflag word: bit 2 = ineligible (a child estimate above kLocalMax, a u8 counter wrap,
+// every sample in one level-3 bucket, or a region total past its buffer): every later kernel
+// returns at once and the runtime takes the exact plan.  ovf: a region overflowed.
+// =======================================================================================
+constexpr uint32_t kEstBlockKeys = kEstBlockKeysHost, kEstSegKeys = 8;
+constexpr uint32_t kEstWG = kEstWGs;  // K1e workgroups (= partial histograms)
+constexpr uint32_t kEstPartWords = kBuckets16 / 4, kEstPart3 = kShards * kRadix;
+
+__device__ __forceinline__ uint32_t est_seg_off(uint32_t j) {  // sample offset in block j
+    return (uint32_t)(mix64((uint64_t)j * kGolden + 0x5EEDull) >> 58) * kEstSegKeys;  // 0 .. 504
+}
+
+// K1e: thread tid samples key tid % 8 of segment tid / 8; workgroup b takes the 512-key
+// blocks j = b * 128 + seg, + kEstWG * 128, ... (so every child's samples spread over all
+// workgroups), four loads in flight per thread.  part8[b][.] = the 65536 u8 child counters
+// (packed 4 per word), part3[b][x * 256 + d] = samples of level-3 bucket d in shard x (tile
+// pair j / 32, shard pair % 8, as K3r deals them), msamp[b] = samples | wrap << 31.
+// Block 0 also zeroes eflag[0..1] (eflag, ovf) for this sort.
+template <bool FIN>
+__global__ __launch_bounds__(1024) void k_est_sample(const uint32_t *__restrict__ in, uint64_t n,
+                                                     uint32_t *__restrict__ part8,
+                                                     uint32_t *__restrict__ part3,
+                                                     uint32_t *__restrict__ msamp,
+                                                     uint32_t *__restrict__ eflag) {
+    __shared__ uint32_t s_h[kEstPartWords];
+    __shared__ uint32_t s_3[kEstPart3];
+    __shared__ uint32_t s_m;
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t i = tid; i < kEstPartWords; i += 1024) s_h[i] = 0;
+    for (uint32_t i = tid; i < kEstPart3; i += 1024) s_3[i] = 0;
+    if (tid == 0) s_m = 0;
+    if (blockIdx.x == 0 && tid < 2) eflag[tid] = 0;
+    __syncthreads();
+    const uint32_t nblk = (uint32_t)((n + kEstBlockKeys - 1) / kEstBlockKeys);
+    constexpr uint32_t SEGS = 1024 / kEstSegKeys;  // segments per workgroup round
+    static_assert(kEstBlockKeys / kEstSegKeys == 64, "64 segment offsets per block");
+    const uint32_t seg = tid / kEstSegKeys, kk = tid % kEstSegKeys, step = gridDim.x * SEGS;
+    constexpr int U = 4;
+    uint32_t cnt = 0, wrap = 0;
+    for (uint32_t j0 = blockIdx.x * SEGS + seg; j0 < nblk; j0 += U * step) {
+        uint32_t key[U], jj[U];
+        bool ok[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            jj[u] = j0 + (uint32_t)u * step;
+            const uint64_t pos = (uint64_t)jj[u] * kEstBlockKeys + est_seg_off(jj[u]) + kk;
+            ok[u] = jj[u] < nblk && pos < n;
+            key[u] = ok[u] ? in[pos] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (!ok[u]) continue;
+            const uint32_t k = FIN ? key[u] ^ kFlip : key[u];
+            const uint32_t b = k >> 16, sh = (b & 3u) << 3;
+            const uint32_t old = atomicAdd(&s_h[b >> 2], 1u << sh);
+            wrap |= ((old >> sh) & 255u) == 255u;
+            constexpr uint32_t kPairBlocks = 2 * kSweepTile / kEstBlockKeys;
+            atomicAdd(&s_3[((jj[u] / kPairBlocks) % kShards) * kRadix + (k >> 24)], 1u);
+            ++cnt;
+        }
+    }
+    atomicAdd(&s_m, cnt | (wrap << 31));
+    __syncthreads();
+    uint32_t *dst = part8 + (uint64_t)blockIdx.x * kEstPartWords;
+    for (uint32_t i = tid; i < kEstPartWords; i += 1024) dst[i] = s_h[i];
+    uint32_t *d3 = part3 + (uint64_t)blockIdx.x * kEstPart3;
+    for (uint32_t i = tid; i < kEstPart3; i += 1024) d3[i] = s_3[i];
+    if (tid == 0) msamp[blockIdx.x] = s_m;
+}
+
+// A region's capacity from its sample count: the estimate + the larger of 6 sigma of the
+// sampling error and two sample blocks (on position-correlated input -- sorted runs -- a
+// region's keys are contiguous and its only error is the two blocks its ends cut) + 64 keys.
+// slack scales the margin (GSORT_EST_SLACK, a test hook: 0 forces overflows).
+__device__ __forceinline__ uint64_t est_cap(uint32_t cnt, double scale, double slack) {
+    const double c = (double)cnt;
+    const double sig = fmax(6.0 * sqrt(c + 1.0) * scale, 2.0 * kEstBlockKeys);
+    return (uint64_t)ceil(c * scale + slack * (sig + 64.0));
+}
+
+// K12e-a: block s (level-3 bucket), thread e (level-2 child).  capc[s*256+e] = the child's
+// capacity (u32), cap3[x*256+s] = shard x's capacity in bucket s; r2[s] / r3[s] = bucket s's
+// level-2 / level-3 region sizes (u64).  Ineligible (eflag bit 2): a child capacity past
+// kLocalMax (K11 could not take it in one pass), a u8 wrap in K1e, or every sample in bucket s
+// (level 3 would copy; the exact plan skips that level).
+__global__ __launch_bounds__(kRadix) void k_est_caps(const uint32_t *__restrict__ part8,
+                                                     const uint32_t *__restrict__ part3,
+                                                     const uint32_t *__restrict__ msamp,
+                                                     uint32_t nwg, uint64_t n, double slack,
+                                                     uint32_t *__restrict__ capc,
+                                                     uint32_t *__restrict__ cap3,
+                                                     unsigned long long *__restrict__ r2,
+                                                     unsigned long long *__restrict__ r3,
+                                                     uint32_t *__restrict__ eflag) {
+    constexpr uint32_t G = kRadix / 64;  // thread groups, each over every G-th partial
+    __shared__ uint32_t s_m, s_bad;
+    __shared__ uint32_t s_c[G][kRadix], s_3[kRadix / kShards][kShards];
+    __shared__ unsigned long long s_w[kRadix / 64], s_c3[kShards];
+    const uint32_t s = blockIdx.x, e = threadIdx.x, g = e >> 6, l = e & 63;
+    if (e == 0) { s_m = 0; s_bad = 0; }
+    __syncthreads();
+    if (e < nwg) {
+        const uint32_t v = msamp[e];
+        atomicAdd(&s_m, v & 0x7fffffffu);
+        if (v >> 31) s_bad = 1;
+    }
+    // bucket s's 64 packed words of every partial: lane l reads word l of the partials
+    // b = g, g + G, ..; four children per word
+    uint32_t c4[4] = {0, 0, 0, 0};
+    const uint32_t *pw = part8 + s * (kRadix / 4) + l;
+#pragma unroll 8
+    for (uint32_t b = g; b < nwg; b += G) {
+        const uint32_t v = pw[(uint64_t)b * kEstPartWords];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) c4[q] += (v >> (8 * q)) & 255u;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) s_c[g][4 * l + q] = c4[q];
+    // shard counts of bucket s: thread (b0 = e >> 3, x = e & 7) over the partials b0, b0 + 32, ..
+    {
+        const uint32_t x = e & 7u, b0 = e >> 3;
+        uint32_t c3 = 0;
+        for (uint32_t b = b0; b < nwg; b += kRadix / 8) c3 += part3[(uint64_t)b * kEstPart3 + x * kRadix + s];
+        s_3[b0][x] = c3;
+    }
+    __syncthreads();
+    uint32_t cnt = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < G; ++q) cnt += s_c[q][e];
+    const uint32_t m = s_m;
+    const double scale = m ? (double)n / (double)m : 0.0;
+    const uint64_t cap = est_cap(cnt, scale, slack);
+    if (cap > kLocalMax) s_bad = 1;
+    capc[s * kRadix + e] = (uint32_t)min(cap, (uint64_t)kLocalMax);
+    unsigned long long tot;
+    block_excl_scan(min(cap, (uint64_t)kLocalMax), s_w, &tot);
+    if (e < kShards) {
+        uint32_t c3 = 0;
+        for (uint32_t r = 0; r < kRadix / kShards; ++r) c3 += s_3[r][e];
+        const uint64_t cp = est_cap(c3, scale, slack);
+        cap3[e * kRadix + s] = (uint32_t)min(cp, (uint64_t)0xffffffffu);
+        s_c3[e] = ((unsigned long long)c3 << 32) | min(cp, (uint64_t)0xffffffffu);
+    }
+    __syncthreads();
+    if (e == 0) {
+        unsigned long long r = 0, samp = 0;
+        for (uint32_t x = 0; x < kShards; ++x) { r += s_c3[x] & 0xffffffffull; samp += s_c3[x] >> 32; }
+        r2[s] = tot;
+        r3[s] = r;
+        if (m && samp == m) s_bad = 1;
+        if (s_bad) atomicOr(eflag, 4u);
+    }
+}
+
+// K12e-b: block s, thread e.  bases3[s] / bases2[s] = exclusive scans of r3 / r2 (the regions
+// of bucket s in X / Y); the child cursors cur2[s*256+e] (u32, offset in bucket s's Y region)
+// with their limits lim2 and start copies init2; the shard cursors cur3[x*256+s] (offset in
+// bucket s's X region), lim3, init3.  Ineligible when X or Y would outgrow its buffer
+// (capx / capy keys).  Block 0 zeroes the nzero work-list counters at zero.
+__global__ __launch_bounds__(kRadix) void k_est_place(
+    const uint32_t *__restrict__ capc, const uint32_t *__restrict__ cap3,
+    const unsigned long long *__restrict__ r2, const unsigned long long *__restrict__ r3,
+    uint64_t capx, uint64_t capy, unsigned long long *__restrict__ bases3,
+    unsigned long long *__restrict__ bases2, uint32_t *__restrict__ cur2,
+    uint32_t *__restrict__ lim2, uint32_t *__restrict__ init2, uint32_t *__restrict__ cur3,
+    uint32_t *__restrict__ lim3, uint32_t *__restrict__ init3,
+    unsigned long long *__restrict__ zero, uint32_t nzero, uint32_t *__restrict__ eflag) {
+    __shared__ unsigned long long s_w[kRadix / 64];
+    const uint32_t s = blockIdx.x, e = threadIdx.x;
+    unsigned long long tx, ty;
+    const unsigned long long b3 = block_excl_scan(r3[e], s_w, &tx);
+    const unsigned long long b2 = block_excl_scan(r2[e], s_w, &ty);
+    if (s == 0) {
+        bases3[e] = b3;
+        bases2[e] = b2;
+        if (e < nzero) zero[e] = 0;
+        if (e == 0 && (tx > capx || ty > capy)) atomicOr(eflag, 4u);
+    }
+    const uint32_t c = capc[s * kRadix + e];
+    unsigned long long t2;
+    const uint32_t off = (uint32_t)block_excl_scan(c, s_w, &t2);
+    const uint32_t i = s * kRadix + e;
+    cur2[i] = off;
+    init2[i] = off;
+    lim2[i] = off + c;
+    if (e == 0) {
+        uint32_t r = 0;
+        for (uint32_t x = 0; x < kShards; ++x) {
+            const uint32_t j = x * kRadix + s, cx = cap3[j];
+            cur3[j] = r;
+            init3[j] = r;
+            lim3[j] = r + cx;
+            r += cx;
+        }
+    }
+}
+
+// K12f: K3a's tile descriptors over the level-3 pieces q = s * 8 + x (bucket s, shard x: keys
+// [bases3[s] + init3[x*256+s], + their count, clamped to the region: an overflowed piece's
+// excess went to the scratch tile)), ceil(count / kSweepTile) tiles each; every
+// block rebuilds the 2048-piece tile prefix in LDS and describes its 256 tiles.  tp[256] =
+// the tile total (K3a's ntile).
+__global__ __launch_bounds__(256) void k_est_tiles(const uint32_t *__restrict__ cur3,
+                                                   const uint32_t *__restrict__ init3,
+                                                   const uint32_t *__restrict__ lim3,
+                                                   const unsigned long long *__restrict__ bases3,
+                                                   uint32_t max_tiles, const uint32_t *eflag,
+                                                   uint32_t *__restrict__ tp,
+                                                   TileDesc *__restrict__ desc) {
+    constexpr uint32_t NQ = kShards * kRadix, PER = NQ / 256;
+    __shared__ uint32_t s_tp[NQ + 1];
+    __shared__ uint32_t s_w[4];
+    if ((*eflag & 4u) || eflag[1]) return;  // ineligible, or level 3 overflowed
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    uint32_t nt[PER], sum = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < PER; ++i) {
+        const uint32_t q = tid * PER + i, s = q / kShards, x = q % kShards;
+        const uint32_t j = x * kRadix + s, c = min(cur3[j], lim3[j]) - init3[j];
+        nt[i] = (c + kSweepTile - 1) / kSweepTile;
+        sum += nt[i];
+    }
+    uint32_t v = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(v, o);
+        if ((int)lane >= o) v += t;
+    }
+    if (lane == 63) s_w[w] = v;
+    __syncthreads();
+    uint32_t run = v - sum;
+    for (uint32_t ww = 0; ww < w; ++ww) run += s_w[ww];
+#pragma unroll
+    for (uint32_t i = 0; i < PER; ++i) { s_tp[tid * PER + i] = run; run += nt[i]; }
+    if (tid == 255) s_tp[NQ] = run;
+    __syncthreads();
+    const uint32_t total = s_tp[NQ];
+    if (blockIdx.x == 0 && tid == 0) tp[kRadix] = total;
+    const uint32_t t = blockIdx.x * 256 + tid;
+    if (t >= total || t >= max_tiles) return;
+    uint32_t lo = 0, hi = NQ;  // s_tp[lo] <= t < s_tp[hi]
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (s_tp[mid] <= t) lo = mid;
+        else hi = mid;
+    }
+    const uint32_t s = lo / kShards, x = lo % kShards, j = x * kRadix + s;
+    const uint32_t c = min(cur3[j], lim3[j]) - init3[j], i0 = (t - s_tp[lo]) * kSweepTile;
+    desc[t] = {bases3[s] + init3[j] + i0, min(c - i0, (uint32_t)kSweepTile), s};
+}
+
+// K12g: block s, thread e.  Exact sizes: child (s, e) holds cur2 - init2 keys, bucket s' holds
+// sum_x (cur3 - init3) keys, so the child's output offset is the scan of the bucket totals
+// before s plus the scan of its siblings before e.  Non-empty children go to the K11e class
+// lists as {src = bases2[s] + init2, dst | len << 40}.  A child past its limit raises ovf and
+// is not listed (K3a has flagged it already).
+__global__ __launch_bounds__(kRadix) void k_est_classify(
+    const uint32_t *__restrict__ cur2, const uint32_t *__restrict__ init2,
+    const uint32_t *__restrict__ lim2, const uint32_t *__restrict__ cur3,
+    const uint32_t *__restrict__ init3, const unsigned long long *__restrict__ bases2,
+    WorkLists wl, uint32_t *__restrict__ eflag) {
+    constexpr int NL = kLocalClasses + 1;
+    __shared__ unsigned long long s_w[kRadix / 64];
+    __shared__ unsigned long long s_fb;
+    __shared__ unsigned int s_n[NL];
+    __shared__ unsigned long long s_keys[NL], s_max[NL], s_base[NL];
+    if (*eflag & 4u) return;
+    const uint32_t s = blockIdx.x, e = threadIdx.x;
+    if (e < NL) { s_n[e] = 0; s_keys[e] = 0; s_max[e] = 0; }
+    unsigned long long te = 0;
+    for (uint32_t x = 0; x < kShards; ++x) te += cur3[x * kRadix + e] - init3[x * kRadix + e];
+    unsigned long long all;
+    const unsigned long long fb = block_excl_scan(te, s_w, &all);
+    if (e == s) s_fb = fb;
+    const uint32_t i = s * kRadix + e;
+    const uint32_t c0 = init2[i], len = cur2[i] - c0;
+    const bool over = cur2[i] > lim2[i];
+    if (over) atomicOr(eflag + 1, 1u);
+    unsigned long long tot;
+    const unsigned long long ex = block_excl_scan(len, s_w, &tot);  // (syncs: s_fb visible)
+    const unsigned long long dst = s_fb + ex;
+    int which = -1;
+    if (len > 0 && !over)
+        for (int k = 1; k < NL; ++k)
+            if (len <= kLocalCap[k]) { which = k; break; }
+    unsigned int idx = 0;
+    if (which > 0) {
+        idx = atomicAdd(&s_n[which], 1u);
+        atomicAdd(&s_keys[which], (unsigned long long)len);
+        atomicMax(&s_max[which], (unsigned long long)len);
+    }
+    __syncthreads();
+    if (e < NL && s_n[e]) {
+        unsigned long long *ctr = reinterpret_cast<unsigned long long *>(wl.ctr) + 3 * e;
+        s_base[e] = atomicAdd(&ctr[0], (unsigned long long)s_n[e]);
+        atomicAdd(&ctr[1], s_keys[e]);
+        atomicMax(&ctr[2], s_max[e]);
+    }
+    __syncthreads();
+    if (which > 0) {
+        unsigned long long *list = reinterpret_cast<unsigned long long *>(wl.list[which]);
+        const unsigned long long j = s_base[which] + idx;
+        list[2 * j] = bases2[s] + c0;
+        list[2 * j + 1] = dst | ((unsigned long long)len << 40);
+    }
+}
+
+// K11e: K11 over a class list of the sampled plan: entry blockIdx.x = {src, dst | len << 40} is
+// loaded from in + src, sorted on its low ndigits digits and stored flipped at out + dst.
+// (A persistent form that read the entry count on the device was tried: inlined into its loop
+// the sort took 177 VGPRs, under launch bounds it spilled; both ran at half speed.)
+template <int BLOCK, int ITEMS, bool ATOMIC>
+__global__ __launch_bounds__(BLOCK) void k_local_sort_e(const uint32_t *__restrict__ in,
+                                                        uint32_t *__restrict__ out,
+                                                        const unsigned long long *__restrict__ list,
+                                                        int ndigits) {
+    constexpr int WAVES = BLOCK / 64;
+    constexpr int TILE = BLOCK * ITEMS;
+    __shared__ uint32_t s_a[TILE];
+    __shared__ uint32_t s_wc[WAVES * kRadix];
+    const uint64_t src = list[2 * blockIdx.x];
+    const uint64_t e = list[2 * blockIdx.x + 1];
+    const uint32_t len = (uint32_t)(e >> 40);
+    if (threadIdx.x < kRadix) s_wc[threadIdx.x] = 0;
+    uint32_t k[ITEMS];
+    load_bucket<BLOCK, ITEMS, false>(in + src, len, k);
+    __syncthreads();
+    sort_bucket<BLOCK, ITEMS, ATOMIC>(k, len, ndigits, out + (e & ((1ull << 40) - 1)), s_a, s_wc);
+}
+
 constexpr int cls_of(int block, int items) {
     return block == 256 ? 1 : block == 1024 ? 4 : items == 18 ? 2 : 3;
 }
@@ -2419,7 +2784,8 @@ hipError_t launch_partition3r(const uint32_t *in, uint32_t *out, uint64_t n, uin
     const uint64_t pairs = (sweep_tiles(n) + 1) / 2;
     launch_k(k_partition_res<B, I, true, true>, (unsigned)pairs, B, 0, s,
         in, out, n, nullptr, nullptr, reinterpret_cast<const ull *>(bases), cur3, flags,
-        (const uint32_t *)nullptr);
+        (const uint32_t *)nullptr, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+        (uint32_t *)nullptr);
     return hipGetLastError();
 }
 
@@ -2439,10 +2805,12 @@ hipError_t launch_partition2r(const uint32_t *in, uint32_t *out, uint16_t *out16
     const unsigned g2 = (max_tiles + 1) / 2;
     if (out16)
         launch_k(k_partition_res<B, I, false, false, uint16_t>, g2, B, 0, s, in, out16, n, tpfx,
-                 desc, bs, cur, flags, raw);
+                 desc, bs, cur, flags, raw, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+                 (uint16_t *)nullptr);
     else
         launch_k(k_partition_res<B, I, false, false>, g2, B, 0, s, in, out, n, tpfx, desc, bs,
-                 cur, flags, raw);
+                 cur, flags, raw, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+                 (uint32_t *)nullptr);
     return hipGetLastError();
 }
 
@@ -2743,6 +3111,79 @@ hipError_t launch_publish(const uint64_t *src, uint32_t n, uint64_t *dst, uint64
     using ull = unsigned long long;
     launch_k(k_publish, 1, 64, 0, s, reinterpret_cast<const ull *>(src), n,
              reinterpret_cast<ull *>(dst), reinterpret_cast<ull *>(flag), (ull)seq);
+    return hipGetLastError();
+}
+
+// ---- sampled plan (K1e, K12e, K3r/K3a EST, K12f, K12g, K11e) ----------------------------
+hipError_t launch_est_front(const EstPlan &p, hipStream_t s) {
+    using ull = unsigned long long;
+    if (p.n == 0 || p.n > kEstMaxKeys) return hipErrorInvalidValue;
+    if (p.flip_in) launch_k(k_est_sample<true>, kEstWG, 1024, 0, s, p.in, p.n, p.part8, p.part3, p.msamp, p.eflag);
+    else launch_k(k_est_sample<false>, kEstWG, 1024, 0, s, p.in, p.n, p.part8, p.part3, p.msamp, p.eflag);
+    launch_k(k_est_caps, kRadix, kRadix, 0, s, p.part8, p.part3, p.msamp, kEstWG, p.n, p.slack,
+             p.capc, p.cap3, reinterpret_cast<ull *>(p.r2), reinterpret_cast<ull *>(p.r3), p.eflag);
+    launch_k(k_est_place, kRadix, kRadix, 0, s, p.capc, p.cap3,
+             reinterpret_cast<const ull *>(p.r2), reinterpret_cast<const ull *>(p.r3), p.capx,
+             p.capy, reinterpret_cast<ull *>(p.bases3), reinterpret_cast<ull *>(p.bases2), p.cur2,
+             p.lim2, p.init2, p.cur3, p.lim3, p.init3, reinterpret_cast<ull *>(p.wl.ctr),
+             (uint32_t)(3 * (kLocalClasses + 1)), p.eflag);
+    return hipGetLastError();
+}
+
+hipError_t launch_est_level3(const EstPlan &p, hipStream_t s) {
+    using ull = unsigned long long;
+    constexpr int B = kPartBlock, I = kSweepTile / kPartBlock;
+    const uint64_t pairs = (sweep_tiles(p.n) + 1) / 2;
+    if (!p.flip_in) return hipErrorInvalidValue;  // K3r loads the int32 input
+    launch_k(k_partition_res<B, I, true, true, uint32_t, true>, (unsigned)pairs, B, 0, s,
+             p.in, p.x, p.n, (const uint32_t *)nullptr, (const TileDesc *)nullptr,
+             reinterpret_cast<const ull *>(p.bases3), p.cur3, (const uint32_t *)p.eflag,
+             (const uint32_t *)nullptr, (const uint32_t *)p.lim3, p.eflag + 1, p.dump);
+    return hipGetLastError();
+}
+
+hipError_t launch_est_level2(const EstPlan &p, hipStream_t s) {
+    using ull = unsigned long long;
+    constexpr int B = kPartBlock, I = kSweepTile / kPartBlock;
+    const uint32_t max_tiles = (uint32_t)est_max_tiles(p.n);
+    TileDesc *desc = static_cast<TileDesc *>(p.tdesc);
+    launch_k(k_est_tiles, (max_tiles + 255) / 256, 256, 0, s, (const uint32_t *)p.cur3,
+             (const uint32_t *)p.init3, (const uint32_t *)p.lim3,
+             reinterpret_cast<const ull *>(p.bases3), max_tiles, (const uint32_t *)p.eflag, p.tp,
+             desc);
+    launch_k(k_partition_res<B, I, false, false, uint32_t, true>, (max_tiles + 1) / 2, B, 0, s,
+             (const uint32_t *)p.x, p.y, p.n, (const uint32_t *)p.tp, (const TileDesc *)desc,
+             reinterpret_cast<const ull *>(p.bases2), p.cur2, (const uint32_t *)p.eflag,
+             (const uint32_t *)nullptr, (const uint32_t *)p.lim2, p.eflag + 1, p.dump);
+    return hipGetLastError();
+}
+
+hipError_t launch_est_classify(const EstPlan &p, hipStream_t s) {
+    using ull = unsigned long long;
+    launch_k(k_est_classify, kRadix, kRadix, 0, s, (const uint32_t *)p.cur2,
+             (const uint32_t *)p.init2, (const uint32_t *)p.lim2, (const uint32_t *)p.cur3,
+             (const uint32_t *)p.init3, reinterpret_cast<const ull *>(p.bases2), p.wl, p.eflag);
+    return hipGetLastError();
+}
+
+hipError_t launch_local_sort_e(const EstPlan &p, int cls, uint32_t nlist, hipStream_t s) {
+    using ull = unsigned long long;
+    if (nlist == 0) return hipSuccess;
+    if (cls < 1 || cls > kLocalClasses) return hipErrorInvalidValue;
+    const ull *l = reinterpret_cast<const ull *>(p.wl.list[cls]);
+    const uint32_t *y = p.y;
+#define GSORT_K11E(B, I)                                                                       \
+    do {                                                                                       \
+        if (p.atomic_rank) launch_k(k_local_sort_e<B, I, true>, nlist, B, 0, s, y, p.out, l, 2); \
+        else launch_k(k_local_sort_e<B, I, false>, nlist, B, 0, s, y, p.out, l, 2);             \
+    } while (0)
+    switch (cls) {
+        case 1: GSORT_K11E(256, 18); break;
+        case 2: GSORT_K11E(512, 18); break;
+        case 3: GSORT_K11E(512, 32); break;
+        default: GSORT_K11E(1024, 32); break;
+    }
+#undef GSORT_K11E
     return hipGetLastError();
 }
 

@@ -11,6 +11,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cmath>
 #include <atomic>
 #include <map>
 #include <mutex>
@@ -74,6 +75,13 @@ struct gsort_ctx {
     DevBuf m_part, m_fix, m_cur, m_local3[kLocalClasses];
     DevBuf m_ccount, m_t3, m_cur3;  // K12a child counts, per-shard level-3 counts + totals, K3r cursors
     DevBuf m_tdesc;                 // K12c: K3a tile descriptors
+    // sampled plan (K1e .. K11e): level-3 / level-2 region buffers, sample partials, plan
+    // arrays, K3a tile descriptors, overflow scratch tile
+    bool plan_est = true;   // GSORT_EST (default 1)
+    double est_slack = 1.0; // GSORT_EST_SLACK (test hook: the sampling-error margin's scale)
+    int ncu = 256;
+    int last_plan = 0;      // gsort_last_plan: 0 exact, 1 sampled, 2 sampled then exact
+    DevBuf m_ex, m_ey, m_epart, m_eplan, m_edesc, m_edump;
     // K12p mailbox: pinned host memory the GPU writes the work-list counters into, then a
     // sequence number (polled by the host: no copy or event on the stream)
     uint64_t *h_mail = nullptr, *d_mail = nullptr;
@@ -564,7 +572,9 @@ void for_each_buf(gsort_ctx *c, F &&f) {
         {"m_cstart", &c->m_cstart}, {"m_next0", &c->m_next[0]}, {"m_next1", &c->m_next[1]},
         {"m_part", &c->m_part}, {"m_fix", &c->m_fix}, {"m_cur", &c->m_cur},
         {"m_ccount", &c->m_ccount}, {"m_t3", &c->m_t3}, {"m_cur3", &c->m_cur3},
-        {"m_tdesc", &c->m_tdesc},
+        {"m_tdesc", &c->m_tdesc}, {"m_ex", &c->m_ex}, {"m_ey", &c->m_ey},
+        {"m_epart", &c->m_epart}, {"m_eplan", &c->m_eplan}, {"m_edesc", &c->m_edesc},
+        {"m_edump", &c->m_edump},
         {"m_split", &c->m_split}, {"m_rpos", &c->m_rpos}, {"m_bsize", &c->m_bsize},
         {"m_bseg", &c->m_bseg}, {"m_blist", &c->m_blist}, {"m_gb", &c->m_gb},
         {"m_pack", &c->m_pack}, {"m_meta", &c->m_meta}, {"m_g16", &c->m_g16},
@@ -910,15 +920,159 @@ gsort_status msd_sort_h16(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
     return GSORT_OK;
 }
 
+// The sampled plan (gsort_kernels.hip, "Sampled plan"): levels 3 and 2 into gapped regions
+// sized from a 1/64 sample, K11e into out.  The host reads the eligibility / overflow words
+// and the K11e list counts K12g leaves in the mailbox (one wait, after level 2), then launches
+// K11e; *ok = false means nothing was written to out and the caller sorts on the exact plan.
+// mailbox words [400] = {eflag, ovf} after level 2, [401] its sequence; [402] / [403] the
+// same after K12e (eligibility only)
+constexpr size_t kEstMailWord = 400;
+
+// Keys of the region buffers the caps of `nreg` regions can add up to (k_est_caps' est_cap:
+// max(a, b) <= a + b, Cauchy-Schwarz on the sigma terms: sum sqrt(cnt + 1) <=
+// sqrt(nreg (m + nreg)); m >= the samples of all full blocks)
+uint64_t est_region_keys(uint64_t n, uint64_t nreg, double slack) {
+    const double m = (double)std::max<uint64_t>((n / kEstBlockKeysHost) * 8, 8);
+    const double sig = 6.0 * ((double)n / m) * std::sqrt((double)nreg * (m + (double)nreg));
+    const double floor2 = 2.0 * kEstBlockKeysHost * (double)nreg;
+    return n + nreg + (uint64_t)std::ceil(slack * (sig + floor2 + 64.0 * (double)nreg)) + 1024;
+}
+
+gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *out,
+                          gsort_stats *stats, bool *ok) {
+    *ok = false;
+    const double slack = std::max(c->est_slack, 0.0);
+    const uint64_t capx = est_region_keys(n, (uint64_t)kH16Shards * kRadix, slack);
+    const uint64_t capy = std::min<uint64_t>(est_region_keys(n, kBuckets16, slack),
+                                             (uint64_t)kBuckets16 * kLocalMax);
+    ST_TRY(ensure(c, c->m_ex, capx * 4));
+    ST_TRY(ensure(c, c->m_ey, capy * 4));
+    ST_TRY(ensure(c, c->m_epart, (size_t)kEstWGs * (kBuckets16 / 4 + kH16Shards * kRadix + 1) * 4));
+    constexpr size_t kPlanWords = (size_t)4 * kBuckets16 + 4 * kH16Shards * kRadix + kRadix + 1;
+    ST_TRY(ensure(c, c->m_eplan, kPlanWords * 4 + 4 * kRadix * 8 + 64));
+    ST_TRY(ensure(c, c->m_edesc, (size_t)est_max_tiles(n) * kTileDescBytes));
+    ST_TRY(ensure(c, c->m_edump, (size_t)kSweepTile * 4));
+    for (int k = 0; k < kLocalClasses; ++k) ST_TRY(ensure_list(c, c->m_local[k], kBuckets16));
+    EstPlan p{};
+    p.in = in;
+    p.n = n;
+    p.flip_in = true;
+    p.x = static_cast<uint32_t *>(c->m_ex.p);
+    p.y = static_cast<uint32_t *>(c->m_ey.p);
+    p.out = out;
+    p.capx = capx;
+    p.capy = capy;
+    p.part8 = static_cast<uint32_t *>(c->m_epart.p);
+    p.part3 = p.part8 + (size_t)kEstWGs * (kBuckets16 / 4);
+    p.msamp = p.part3 + (size_t)kEstWGs * kH16Shards * kRadix;
+    uint64_t *u64 = static_cast<uint64_t *>(c->m_eplan.p);
+    p.r2 = u64;
+    p.r3 = u64 + kRadix;
+    p.bases3 = u64 + 2 * kRadix;
+    p.bases2 = u64 + 3 * kRadix;
+    uint32_t *w = reinterpret_cast<uint32_t *>(u64 + 4 * kRadix);
+    p.capc = w;
+    p.cur2 = w + kBuckets16;
+    p.lim2 = w + 2 * kBuckets16;
+    p.init2 = w + 3 * kBuckets16;
+    w += 4 * kBuckets16;
+    p.cap3 = w;
+    p.cur3 = w + kH16Shards * kRadix;
+    p.lim3 = w + 2 * kH16Shards * kRadix;
+    p.init3 = w + 3 * kH16Shards * kRadix;
+    p.tp = w + 4 * kH16Shards * kRadix;
+    p.eflag = p.tp + kRadix + 2;  // 2 words, 8-B aligned (published as one u64)
+    p.tdesc = c->m_edesc.p;
+    p.dump = static_cast<uint32_t *>(c->m_edump.p);
+    p.wl = work_lists(c, 0);
+    p.slack = slack;
+    p.atomic_rank = c->atomic_rank;
+    hipEvent_t t = tic(c);
+    HIP_TRY(c, launch_est_front(p, c->stream));
+    // the eligibility word as soon as K12e has decided it (words [402], flag [403]); K3r is
+    // queued behind it and returns at once on an ineligible block, while the host reads it
+    const uint64_t seq0 = ++c->mail_seq;
+    HIP_TRY(c, launch_publish(reinterpret_cast<const uint64_t *>(p.eflag), 1,
+                              c->d_mail + kEstMailWord + 2, c->d_mail + kEstMailWord + 3, seq0,
+                              c->stream));
+    toc(c, PH_COUNT, t);
+    t = tic(c);
+    HIP_TRY(c, launch_est_level3(p, c->stream));
+    toc(c, PH_LEVEL3, t);
+    {
+        volatile uint64_t *flag = c->h_mail + kEstMailWord + 3;
+        for (uint64_t spin = 0; *flag != seq0; ++spin) {
+            if ((spin & 1023) == 1023) {
+                const hipError_t q = hipStreamQuery(c->stream);
+                if (q != hipErrorNotReady && *flag != seq0)
+                    return set_err(c, GSORT_EHIP, std::string("sampled plan: eligibility word: ") +
+                                                      hipGetErrorString(q));
+                std::this_thread::yield();
+            }
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
+        if (c->h_mail[kEstMailWord + 2] & 4u) return GSORT_OK;  // ineligible: exact plan
+    }
+    t = tic(c);
+    HIP_TRY(c, launch_est_level2(p, c->stream));
+    toc(c, PH_LEVEL2, t);
+    HIP_TRY(c, launch_est_classify(p, c->stream));
+    // K12p twice: the status words, then the list counters behind the sequence flag the host
+    // polls (the K11e grids are the list lengths)
+    const uint64_t seq = ++c->mail_seq;
+    constexpr uint32_t kCtrWords = (uint32_t)(kCtrBytes / 8);
+    HIP_TRY(c, launch_publish(reinterpret_cast<const uint64_t *>(p.eflag), 1,
+                              c->d_mail + kEstMailWord, c->d_mail + kEstMailWord + 1, seq,
+                              c->stream));
+    HIP_TRY(c, launch_publish(reinterpret_cast<const uint64_t *>(c->d_small + OFF_CTR), kCtrWords,
+                              c->d_mail + 8, c->d_mail, seq, c->stream));
+    ST_TRY(wait_mail(c, seq));
+    volatile uint64_t *mail = c->h_mail;
+    if (mail[kEstMailWord + 1] != seq)
+        return set_err(c, GSORT_EHIP, "sampled plan: status word not published");
+    if (mail[kEstMailWord] != 0) return GSORT_OK;  // ineligible or overflowed: *ok stays false
+    uint64_t h[3 * (kLocalClasses + 1)];
+    memcpy(h, c->h_mail + 8, kCtrBytes);
+    uint64_t keys = 0, ent = 0;
+    for (int k = 1; k <= kLocalClasses; ++k) { keys += h[3 * k + 1]; ent += h[3 * k]; }
+    if (keys != n || ent > kBuckets16)  // every key in exactly one K11e entry
+        return set_err(c, GSORT_EINVAL, "sampled plan: K11e lists hold " + std::to_string(keys) +
+                                            " keys in " + std::to_string(ent) + " entries, want " +
+                                            std::to_string(n) + " keys");
+    t = tic(c);
+    for (int k = 1; k <= kLocalClasses; ++k)
+        HIP_TRY(c, launch_local_sort_e(p, k, (uint32_t)h[3 * k], c->stream));
+    toc(c, PH_BUCKET, t);
+    *ok = true;
+    if (stats) stats->buckets_local += ent;
+    if (*ok && stats) {
+        stats->keys_level[0] += n;
+        stats->keys_level[1] += n;
+        stats->keys_bucket_sort += n;
+        stats->passes_run = 2;
+    }
+    return GSORT_OK;
+}
+
 // group16: stop after level 2 -- out holds the keys (int32) grouped by their top 16 bits
 // (ordered u32) but not sorted inside a group (the sender side of the distributed radix);
 // with out16 and n > kLocalMax, level 2 stores only the low 16 bits of every key, at out16.
 // With the two-level plan (c->plan16) and group16, gb (65537 u64) receives the 16-bit bucket
 // bounds of the grouped block.
+// allow_est: the caller synchronizes after the sort anyway, so the sampled plan (which waits
+// for its own status word) may run.
 gsort_status msd_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *out,
                       uint32_t *tmp, gsort_stats *stats, bool group16 = false,
-                      uint16_t *out16 = nullptr, uint64_t *gb = nullptr) {
+                      uint16_t *out16 = nullptr, uint64_t *gb = nullptr, bool allow_est = false) {
+    c->last_plan = 0;
     if (n == 0) return GSORT_OK;
+    if (allow_est && c->plan_est && c->plan16 && !group16 && n >= kEstMinKeys &&
+        n <= kEstMaxKeys) {
+        bool ok = false;
+        ST_TRY(msd_sort_est(c, in, n, out, stats, &ok));
+        c->last_plan = ok ? 1 : 2;
+        if (ok) return GSORT_OK;
+    }
     uint64_t *ctr = reinterpret_cast<uint64_t *>(c->d_small + OFF_CTR);
     if (n <= kLocalMax) {  // one bucket: all four digits in LDS
         uint64_t *h_one = reinterpret_cast<uint64_t *>(c->h_small + OFF_ONE);
@@ -934,8 +1088,13 @@ gsort_status msd_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *ou
         if (stats) { stats->buckets_local += 1; stats->keys_bucket_sort += n; }
         return GSORT_OK;
     }
-    if (c->plan16 && (!group16 || out16) && n < (1ull << 32))
-        return msd_sort_h16(c, in, n, out, tmp, stats, group16, out16, group16 ? gb : nullptr);
+    if (c->plan16 && (!group16 || out16) && n < (1ull << 32)) {
+        const int lp = c->last_plan;
+        const gsort_status st =
+            msd_sort_h16(c, in, n, out, tmp, stats, group16, out16, group16 ? gb : nullptr);
+        c->last_plan = lp;
+        return st;
+    }
     ST_TRY(ensure_pass_scratch(c, n));
     uint64_t *totals = reinterpret_cast<uint64_t *>(c->d_small + OFF_TOT);
     uint64_t *bases = reinterpret_cast<uint64_t *>(c->d_small + OFF_BASES);
@@ -967,14 +1126,15 @@ gsort_status msd_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *ou
 }
 
 gsort_status local_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *out,
-                        uint32_t *tmp, int *passes_run, gsort_stats *stats = nullptr) {
+                        uint32_t *tmp, int *passes_run, gsort_stats *stats = nullptr,
+                        bool allow_est = false) {
     if (stats) stats->local_algo = c->local_algo;
     if (c->local_algo == GSORT_LOCAL_LSD) return lsd_sort(c, in, n, out, tmp, passes_run);
     gsort_stats tmp_st;
     memset(&tmp_st, 0, sizeof(tmp_st));
     gsort_stats *st = stats ? stats : &tmp_st;
     const int before = st->passes_run;
-    ST_TRY(msd_sort(c, in, n, out, tmp, st));
+    ST_TRY(msd_sort(c, in, n, out, tmp, st, false, nullptr, nullptr, allow_est));
     if (passes_run) *passes_run = st->passes_run;
     if (stats) stats->passes_run = std::max(before, st->passes_run);
     return GSORT_OK;
@@ -1975,6 +2135,9 @@ gsort_status create_common(gsort_ctx *c, int hip_device) {
     HIP_TRY(c, hipMemsetAsync(c->d_small, 0, kSmallBytes, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     if (const char *e = getenv("GSORT_PLAN16")) c->plan16 = atoi(e) != 0;
+    if (const char *e = getenv("GSORT_EST")) c->plan_est = atoi(e) != 0;
+    if (const char *e = getenv("GSORT_EST_SLACK")) c->est_slack = atof(e);
+    HIP_TRY(c, hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, hip_device));
     {
         std::lock_guard<std::mutex> lk(g_ctx_mu);
         g_ctxs.insert(c);
@@ -2150,7 +2313,8 @@ gsort_status gsort_radix(gsort_ctx *c, const int32_t *d_keys, size_t n_local, in
         ST_TRY(ensure(c, c->slot[S_OUT], cap));
         int pr = 0;
         st = local_sort(c, reinterpret_cast<const uint32_t *>(d_keys), n_local,
-                        slot_ptr<uint32_t>(c, S_OUT), slot_ptr<uint32_t>(c, S_TMP), &pr, stats);
+                        slot_ptr<uint32_t>(c, S_OUT), slot_ptr<uint32_t>(c, S_TMP), &pr, stats,
+                        true);
         if (stats) stats->passes_run = pr;
         *d_out = slot_ptr<int32_t>(c, S_OUT);
         nout = n_local;
@@ -2187,7 +2351,8 @@ gsort_status gsort_sample(gsort_ctx *c, const int32_t *d_keys, size_t n_local, i
         ST_TRY(ensure(c, c->slot[S_OUT], cap));
         int pr = 0;
         ST_TRY(local_sort(c, reinterpret_cast<const uint32_t *>(d_keys), n_local,
-                          slot_ptr<uint32_t>(c, S_OUT), slot_ptr<uint32_t>(c, S_TMP), &pr, stats));
+                          slot_ptr<uint32_t>(c, S_OUT), slot_ptr<uint32_t>(c, S_TMP), &pr, stats,
+                          true));
         if (stats) stats->passes_run = pr;
         c->splitters.clear();
         c->bucket_counts.assign(1, n_local);
@@ -2205,6 +2370,8 @@ gsort_status gsort_sample(gsort_ctx *c, const int32_t *d_keys, size_t n_local, i
     if (canary_mode()) ST_TRY(check_all_guards(c, __func__));
     return GSORT_OK;
 }
+
+int gsort_last_plan(const gsort_ctx *c) { return c ? c->last_plan : -1; }
 
 gsort_status gsort_sample_info(const gsort_ctx *c, int32_t *splitters, uint64_t *bucket_counts) {
     if (!c) return GSORT_EINVAL;

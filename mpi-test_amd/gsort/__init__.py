@@ -76,6 +76,7 @@ EXPORTS = [
     "gsort_copy_to_device", "gsort_onesweep_tile", "gsort_plan_radix_route",
     "gsort_plan_splitters", "gsort_plan_split", "gsort_plan_split_balanced", "gsort_parse_text",
     "gsort_format_dump", "gsort_copy_ceiling", "gsort_set_ref_compat", "gsort_plan_ref_digits",
+    "gsort_last_plan",
 ]
 
 _lib = None
@@ -111,6 +112,7 @@ def lib():
     for fn in (L.gsort_radix, L.gsort_sample):
         fn.argtypes = [VP, VP, SZ, P(VP), P(SZ), P(Stats)]
     L.gsort_sample_info.argtypes = [VP, VP, VP]
+    L.gsort_last_plan.argtypes = [VP]
     L.gsort_scatter_from_root.argtypes = [VP, VP, SZ, P(VP), P(SZ)]
     L.gsort_gather_to_root.argtypes = [VP, VP, SZ, VP]
     L.gsort_generate.argtypes = [VP, I, U64, U64, SZ, VP]
@@ -236,6 +238,13 @@ class Context:
         cnt = np.zeros(self.nranks, dtype=np.uint64)
         self._c(lib().gsort_sample_info(self.h, spl.ctypes.data, cnt.ctypes.data))
         return spl[: self.nranks - 1], cnt
+
+    PLAN_EXACT, PLAN_SAMPLED, PLAN_SAMPLED_THEN_EXACT = 0, 1, 2
+
+    def last_plan(self):
+        """Plan of the last one-rank local sort (gsort_last_plan): 0 exact, 1 sampled,
+        2 sampled then re-sorted on the exact plan (ineligible block or a region overflow)."""
+        return lib().gsort_last_plan(self.h)
 
     def generate(self, dist, seed, start, n, d_out):
         self._c(lib().gsort_generate(self.h, dist, seed, start, n, ctypes.c_void_p(d_out)))

@@ -1,0 +1,149 @@
+"""GPU parity tests of the sampled plan: levels 3 and 2 sized from a 1/64
+sample, K11e into exact positions, and the exact-plan re-sort it falls back to.
+
+Bit-exact against numpy's sort (integer keys).  Every case also states which plan ran
+(gsort_last_plan), so a silent fallback cannot pass for the sampled path: uniform and
+sorted inputs must stay on the sampled plan; skewed / dense inputs may be ineligible and
+must then come back sorted through the exact plan; GSORT_EST_SLACK=0 (no sampling-error
+margin) forces region overflows, which must be caught and re-sorted.
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SAMPLED, FALLBACK = 1, 2
+
+
+def _ctx(gsort, **env):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update({k: str(v) for k, v in env.items()})
+    try:
+        return gsort.Context()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k)
+            else:
+                os.environ[k] = v
+
+
+@pytest.fixture(scope="module")
+def ctx(gsort):
+    c = _ctx(gsort, GSORT_EST=1, GSORT_EST_SLACK=1)
+    yield c
+    c.close()
+
+
+def _sort(ctx, keys, algo="radix"):
+    p = ctx.alloc(max(keys.size, 1) * 4)
+    try:
+        ctx.to_device(keys, p)
+        out, n, st = (ctx.radix if algo == "radix" else ctx.sample)(p, keys.size)
+        assert n == keys.size
+        return ctx.to_host(out, n), st
+    finally:
+        ctx.free(p)
+
+
+# the sampled plan starts at 2^22 keys (kEstMinKeys); odd sizes leave a partial last tile,
+# sample block and segment
+SIZES = [1 << 22, (1 << 22) + 12345, (1 << 23) + 8191, (1 << 24) + 1, 3 << 23]
+
+
+@pytest.mark.parametrize("n", SIZES)
+def test_sampled_plan_uniform(ctx, orc, n):
+    keys = orc.gen(orc.UNIFORM, n % 1000 + 5, n)
+    got, st = _sort(ctx, keys)
+    assert ctx.last_plan() == SAMPLED
+    assert np.array_equal(got, np.sort(keys))
+    assert st["passes_run"] == 2
+
+
+def test_sampled_plan_full_range_and_sample_sort(ctx):
+    """Negative and positive keys over the whole int32 range (256 level-3 buckets); the one-rank
+    sample sort takes the same plan."""
+    rng = np.random.default_rng(11)
+    keys = rng.integers(-2**31, 2**31, 1 << 23, dtype=np.int64).astype(np.int32)
+    for algo in ("radix", "sample"):
+        got, _ = _sort(ctx, keys, algo)
+        assert ctx.last_plan() == SAMPLED, algo
+        assert np.array_equal(got, np.sort(keys)), algo
+
+
+def test_sampled_plan_below_threshold_is_exact(ctx, orc):
+    keys = orc.gen(orc.UNIFORM, 3, (1 << 22) - 1)
+    got, _ = _sort(ctx, keys)
+    assert ctx.last_plan() == 0
+    assert np.array_equal(got, np.sort(keys))
+
+
+def _inputs(orc, n):
+    rng = np.random.default_rng(5)
+    u = orc.gen(orc.UNIFORM, 21, n)
+    runs = np.sort(u)
+    return {
+        "sorted": runs,
+        "reversed": runs[::-1].copy(),
+        "sorted_blocks": np.concatenate([np.sort(b) for b in np.array_split(u, 64)]),
+        "zipf": orc.gen(orc.ZIPF, 4, n),
+        "all_equal": np.full(n, -77, dtype=np.int32),
+        "bits16": (u & 0xFFFF).astype(np.int32),
+        "bits24": (u & 0xFFFFFF).astype(np.int32),
+        "bits28": (u & 0xFFFFFFF).astype(np.int32),
+        "half_one_value": np.where(rng.random(n) < 0.5, np.int32(1 << 20), u).astype(np.int32),
+        "two_clusters": np.where(rng.random(n) < 0.5, u >> 12, -(u >> 12)).astype(np.int32),
+    }
+
+
+@pytest.mark.parametrize("name", ["sorted", "reversed", "sorted_blocks", "zipf", "all_equal",
+                                  "bits16", "bits24", "bits28", "half_one_value",
+                                  "two_clusters"])
+def test_sampled_plan_distributions(ctx, orc, name):
+    n = 1 << 23
+    keys = _inputs(orc, n)[name]
+    got, _ = _sort(ctx, keys)
+    plan = ctx.last_plan()
+    assert plan in (SAMPLED, FALLBACK), plan
+    if name in ("sorted", "reversed", "sorted_blocks"):  # uniform keys, position-correlated
+        assert plan == SAMPLED, name
+    if name in ("all_equal", "bits16", "zipf", "half_one_value"):  # a child > kLocalMax
+        assert plan == FALLBACK, name
+    assert np.array_equal(got, np.sort(keys)), name
+
+
+def test_sampled_plan_overflow_falls_back(gsort, orc):
+    """No sampling margin: about half the regions overflow; every overflowed run went to the
+    scratch tile, the runtime sees ovf and the exact plan sorts the block again."""
+    c = _ctx(gsort, GSORT_EST=1, GSORT_EST_SLACK=0)
+    try:
+        for n in ((1 << 22) + 3, 1 << 24):
+            keys = orc.gen(orc.UNIFORM, 99, n)
+            got, _ = _sort(c, keys)
+            assert c.last_plan() == FALLBACK
+            assert np.array_equal(got, np.sort(keys))
+    finally:
+        c.close()
+
+
+def test_sampled_plan_off(gsort, orc):
+    c = _ctx(gsort, GSORT_EST=0)
+    try:
+        keys = orc.gen(orc.UNIFORM, 8, 1 << 23)
+        got, _ = _sort(c, keys)
+        assert c.last_plan() == 0
+        assert np.array_equal(got, np.sort(keys))
+    finally:
+        c.close()
+
+
+def test_sampled_plan_repeated_sorts_reuse_scratch(ctx, orc):
+    """Back-to-back sorts of different sizes on one context (scratch reused, K1e re-zeroes the
+    status words, the class counters are cleared by the front)."""
+    for i, n in enumerate([1 << 24, (1 << 22) + 1, 1 << 24, 5 << 22]):
+        keys = orc.gen(orc.UNIFORM, 100 + i, n)
+        got, _ = _sort(ctx, keys)
+        assert ctx.last_plan() == SAMPLED
+        assert np.array_equal(got, np.sort(keys)), n
