@@ -288,7 +288,13 @@ struct EstPlan {
     WorkLists wl;
     double slack;
     bool atomic_rank;
+    // pinned host mailbox (device pointer) and the sequence numbers K12e-b / K12g publish with:
+    // mail[2] eligibility word, mail[3] = seq_elig; mail[0] status {eflag, ovf}, mail[8 .. 23)
+    // the K11e list counters, mail[1] = seq_done
+    uint64_t *mail;
+    uint64_t seq_elig, seq_done;
 };
+constexpr uint32_t kEstMailWords = 24;
 hipError_t launch_est_front(const EstPlan &p, hipStream_t s);   // K1e + K12e
 hipError_t launch_est_level3(const EstPlan &p, hipStream_t s);  // K3r
 hipError_t launch_est_level2(const EstPlan &p, hipStream_t s);  // K12f + K3a

@@ -2199,7 +2199,7 @@ __device__ __forceinline__ uint32_t est_seg_off(uint32_t j) {  // sample offset 
 // workgroups), four loads in flight per thread.  part8[b][.] = the 65536 u8 child counters
 // (packed 4 per word), part3[b][x * 256 + d] = samples of level-3 bucket d in shard x (tile
 // pair j / 32, shard pair % 8, as K3r deals them), msamp[b] = samples | wrap << 31.
-// Block 0 also zeroes eflag[0..1] (eflag, ovf) for this sort.
+// Block 0 also zeroes eflag[0..2] (eflag, ovf, K12g's finished-block count) for this sort.
 template <bool FIN>
 __global__ __launch_bounds__(1024) void k_est_sample(const uint32_t *__restrict__ in, uint64_t n,
                                                      uint32_t *__restrict__ part8,
@@ -2213,7 +2213,7 @@ __global__ __launch_bounds__(1024) void k_est_sample(const uint32_t *__restrict_
     for (uint32_t i = tid; i < kEstPartWords; i += 1024) s_h[i] = 0;
     for (uint32_t i = tid; i < kEstPart3; i += 1024) s_3[i] = 0;
     if (tid == 0) s_m = 0;
-    if (blockIdx.x == 0 && tid < 2) eflag[tid] = 0;
+    if (blockIdx.x == 0 && tid < 3) eflag[tid] = 0;
     __syncthreads();
     const uint32_t nblk = (uint32_t)((n + kEstBlockKeys - 1) / kEstBlockKeys);
     constexpr uint32_t SEGS = 1024 / kEstSegKeys;  // segments per workgroup round
@@ -2250,6 +2250,16 @@ __global__ __launch_bounds__(1024) void k_est_sample(const uint32_t *__restrict_
     uint32_t *d3 = part3 + (uint64_t)blockIdx.x * kEstPart3;
     for (uint32_t i = tid; i < kEstPart3; i += 1024) d3[i] = s_3[i];
     if (tid == 0) msamp[blockIdx.x] = s_m;
+}
+
+// The sampled plan's words in the pinned host mailbox (relative to the `mail` pointer the
+// runtime passes): the status {eflag, ovf} and its sequence after K12g, the same after K12e
+// (eligibility only), the 15 work-list counters after K12g.
+constexpr uint32_t kMailStatus = 0, kMailSeq = 1, kMailElig = 2, kMailEligSeq = 3, kMailCtr = 8;
+
+__device__ __forceinline__ void mail_release(unsigned long long *flag, unsigned long long seq) {
+    __threadfence_system();
+    __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // A region's capacity from its sample count: the estimate + the larger of 6 sigma of the
@@ -2340,7 +2350,8 @@ __global__ __launch_bounds__(kRadix) void k_est_caps(const uint32_t *__restrict_
 // of bucket s in X / Y); the child cursors cur2[s*256+e] (u32, offset in bucket s's Y region)
 // with their limits lim2 and start copies init2; the shard cursors cur3[x*256+s] (offset in
 // bucket s's X region), lim3, init3.  Ineligible when X or Y would outgrow its buffer
-// (capx / capy keys).  Block 0 zeroes the nzero work-list counters at zero.
+// (capx / capy keys).  Block 0 zeroes the nzero work-list counters at zero and publishes the
+// final eligibility word to the host mailbox (mail[kMailElig], then seq at kMailEligSeq).
 __global__ __launch_bounds__(kRadix) void k_est_place(
     const uint32_t *__restrict__ capc, const uint32_t *__restrict__ cap3,
     const unsigned long long *__restrict__ r2, const unsigned long long *__restrict__ r3,
@@ -2348,7 +2359,8 @@ __global__ __launch_bounds__(kRadix) void k_est_place(
     unsigned long long *__restrict__ bases2, uint32_t *__restrict__ cur2,
     uint32_t *__restrict__ lim2, uint32_t *__restrict__ init2, uint32_t *__restrict__ cur3,
     uint32_t *__restrict__ lim3, uint32_t *__restrict__ init3,
-    unsigned long long *__restrict__ zero, uint32_t nzero, uint32_t *__restrict__ eflag) {
+    unsigned long long *__restrict__ zero, uint32_t nzero, uint32_t *__restrict__ eflag,
+    unsigned long long *mail, unsigned long long seq) {
     __shared__ unsigned long long s_w[kRadix / 64];
     const uint32_t s = blockIdx.x, e = threadIdx.x;
     unsigned long long tx, ty;
@@ -2358,7 +2370,13 @@ __global__ __launch_bounds__(kRadix) void k_est_place(
         bases3[e] = b3;
         bases2[e] = b2;
         if (e < nzero) zero[e] = 0;
-        if (e == 0 && (tx > capx || ty > capy)) atomicOr(eflag, 4u);
+        if (e == 0) {  // the eligibility is final here (K12e-a's flags are in): publish it
+            if (tx > capx || ty > capy) atomicOr(eflag, 4u);
+            __threadfence();
+            mail[kMailElig] = __hip_atomic_load(reinterpret_cast<unsigned long long *>(eflag),
+                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            mail_release(mail + kMailEligSeq, seq);
+        }
     }
     const uint32_t c = capc[s * kRadix + e];
     unsigned long long t2;
@@ -2437,55 +2455,76 @@ __global__ __launch_bounds__(256) void k_est_tiles(const uint32_t *__restrict__ 
 // sum_x (cur3 - init3) keys, so the child's output offset is the scan of the bucket totals
 // before s plus the scan of its siblings before e.  Non-empty children go to the K11e class
 // lists as {src = bases2[s] + init2, dst | len << 40}.  A child past its limit raises ovf and
-// is not listed (K3a has flagged it already).
+// is not listed (K3a has flagged it already).  The last block to finish publishes the list
+// counters and the status words to the host mailbox (mail[kMailCtr ..], mail[kMailStatus],
+// then seq at kMailSeq): the host sizes the K11e grids from them, with no K12p launch behind.
 __global__ __launch_bounds__(kRadix) void k_est_classify(
     const uint32_t *__restrict__ cur2, const uint32_t *__restrict__ init2,
     const uint32_t *__restrict__ lim2, const uint32_t *__restrict__ cur3,
     const uint32_t *__restrict__ init3, const unsigned long long *__restrict__ bases2,
-    WorkLists wl, uint32_t *__restrict__ eflag) {
+    WorkLists wl, uint32_t *__restrict__ eflag, unsigned long long *mail,
+    unsigned long long seq) {
     constexpr int NL = kLocalClasses + 1;
     __shared__ unsigned long long s_w[kRadix / 64];
     __shared__ unsigned long long s_fb;
     __shared__ unsigned int s_n[NL];
     __shared__ unsigned long long s_keys[NL], s_max[NL], s_base[NL];
-    if (*eflag & 4u) return;
+    __shared__ uint32_t s_last;
     const uint32_t s = blockIdx.x, e = threadIdx.x;
-    if (e < NL) { s_n[e] = 0; s_keys[e] = 0; s_max[e] = 0; }
-    unsigned long long te = 0;
-    for (uint32_t x = 0; x < kShards; ++x) te += cur3[x * kRadix + e] - init3[x * kRadix + e];
-    unsigned long long all;
-    const unsigned long long fb = block_excl_scan(te, s_w, &all);
-    if (e == s) s_fb = fb;
-    const uint32_t i = s * kRadix + e;
-    const uint32_t c0 = init2[i], len = cur2[i] - c0;
-    const bool over = cur2[i] > lim2[i];
-    if (over) atomicOr(eflag + 1, 1u);
-    unsigned long long tot;
-    const unsigned long long ex = block_excl_scan(len, s_w, &tot);  // (syncs: s_fb visible)
-    const unsigned long long dst = s_fb + ex;
-    int which = -1;
-    if (len > 0 && !over)
-        for (int k = 1; k < NL; ++k)
-            if (len <= kLocalCap[k]) { which = k; break; }
-    unsigned int idx = 0;
-    if (which > 0) {
-        idx = atomicAdd(&s_n[which], 1u);
-        atomicAdd(&s_keys[which], (unsigned long long)len);
-        atomicMax(&s_max[which], (unsigned long long)len);
+    unsigned long long *ctr = reinterpret_cast<unsigned long long *>(wl.ctr);
+    if (!(*eflag & 4u)) {
+        if (e < NL) { s_n[e] = 0; s_keys[e] = 0; s_max[e] = 0; }
+        unsigned long long te = 0;
+        for (uint32_t x = 0; x < kShards; ++x) te += cur3[x * kRadix + e] - init3[x * kRadix + e];
+        unsigned long long all;
+        const unsigned long long fb = block_excl_scan(te, s_w, &all);
+        if (e == s) s_fb = fb;
+        const uint32_t i = s * kRadix + e;
+        const uint32_t c0 = init2[i], len = cur2[i] - c0;
+        const bool over = cur2[i] > lim2[i];
+        if (over) atomicOr(eflag + 1, 1u);
+        unsigned long long tot;
+        const unsigned long long ex = block_excl_scan(len, s_w, &tot);  // (syncs: s_fb visible)
+        const unsigned long long dst = s_fb + ex;
+        int which = -1;
+        if (len > 0 && !over)
+            for (int k = 1; k < NL; ++k)
+                if (len <= kLocalCap[k]) { which = k; break; }
+        unsigned int idx = 0;
+        if (which > 0) {
+            idx = atomicAdd(&s_n[which], 1u);
+            atomicAdd(&s_keys[which], (unsigned long long)len);
+            atomicMax(&s_max[which], (unsigned long long)len);
+        }
+        __syncthreads();
+        if (e < NL && s_n[e]) {
+            s_base[e] = atomicAdd(&ctr[3 * e], (unsigned long long)s_n[e]);
+            atomicAdd(&ctr[3 * e + 1], s_keys[e]);
+            atomicMax(&ctr[3 * e + 2], s_max[e]);
+        }
+        __syncthreads();
+        if (which > 0) {
+            unsigned long long *list = reinterpret_cast<unsigned long long *>(wl.list[which]);
+            const unsigned long long j = s_base[which] + idx;
+            list[2 * j] = bases2[s] + c0;
+            list[2 * j + 1] = dst | ((unsigned long long)len << 40);
+        }
     }
     __syncthreads();
-    if (e < NL && s_n[e]) {
-        unsigned long long *ctr = reinterpret_cast<unsigned long long *>(wl.ctr) + 3 * e;
-        s_base[e] = atomicAdd(&ctr[0], (unsigned long long)s_n[e]);
-        atomicAdd(&ctr[1], s_keys[e]);
-        atomicMax(&ctr[2], s_max[e]);
+    if (e == 0) {
+        __threadfence();  // this block's counter atomics before its ticket
+        s_last = atomicAdd(eflag + 2, 1u) == gridDim.x - 1;
     }
     __syncthreads();
-    if (which > 0) {
-        unsigned long long *list = reinterpret_cast<unsigned long long *>(wl.list[which]);
-        const unsigned long long j = s_base[which] + idx;
-        list[2 * j] = bases2[s] + c0;
-        list[2 * j + 1] = dst | ((unsigned long long)len << 40);
+    if (s_last) {
+        __threadfence();
+        if (e < 3 * NL)
+            mail[kMailCtr + e] = __hip_atomic_load(ctr + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (e == 3 * NL)
+            mail[kMailStatus] = __hip_atomic_load(reinterpret_cast<unsigned long long *>(eflag),
+                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        if (e == 0) mail_release(mail + kMailSeq, seq);
     }
 }
 
@@ -3126,7 +3165,8 @@ hipError_t launch_est_front(const EstPlan &p, hipStream_t s) {
              reinterpret_cast<const ull *>(p.r2), reinterpret_cast<const ull *>(p.r3), p.capx,
              p.capy, reinterpret_cast<ull *>(p.bases3), reinterpret_cast<ull *>(p.bases2), p.cur2,
              p.lim2, p.init2, p.cur3, p.lim3, p.init3, reinterpret_cast<ull *>(p.wl.ctr),
-             (uint32_t)(3 * (kLocalClasses + 1)), p.eflag);
+             (uint32_t)(3 * (kLocalClasses + 1)), p.eflag, reinterpret_cast<ull *>(p.mail),
+             (ull)p.seq_elig);
     return hipGetLastError();
 }
 
@@ -3162,7 +3202,8 @@ hipError_t launch_est_classify(const EstPlan &p, hipStream_t s) {
     using ull = unsigned long long;
     launch_k(k_est_classify, kRadix, kRadix, 0, s, (const uint32_t *)p.cur2,
              (const uint32_t *)p.init2, (const uint32_t *)p.lim2, (const uint32_t *)p.cur3,
-             (const uint32_t *)p.init3, reinterpret_cast<const ull *>(p.bases2), p.wl, p.eflag);
+             (const uint32_t *)p.init3, reinterpret_cast<const ull *>(p.bases2), p.wl, p.eflag,
+             reinterpret_cast<ull *>(p.mail), (ull)p.seq_done);
     return hipGetLastError();
 }
 

@@ -924,9 +924,9 @@ gsort_status msd_sort_h16(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
 // sized from a 1/64 sample, K11e into out.  The host reads the eligibility / overflow words
 // and the K11e list counts K12g leaves in the mailbox (one wait, after level 2), then launches
 // K11e; *ok = false means nothing was written to out and the caller sorts on the exact plan.
-// mailbox words [400] = {eflag, ovf} after level 2, [401] its sequence; [402] / [403] the
-// same after K12e (eligibility only)
+// the sampled plan's mailbox words start here (EstPlan::mail: kEstMailWords of them)
 constexpr size_t kEstMailWord = 400;
+static_assert((kEstMailWord + kEstMailWords) * 8 <= kMailBytes, "mailbox");
 
 // Keys of the region buffers the caps of `nreg` regions can add up to (k_est_caps' est_cap:
 // max(a, b) <= a + b, Cauchy-Schwarz on the sigma terms: sum sqrt(cnt + 1) <=
@@ -987,52 +987,41 @@ gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
     p.wl = work_lists(c, 0);
     p.slack = slack;
     p.atomic_rank = c->atomic_rank;
-    hipEvent_t t = tic(c);
-    HIP_TRY(c, launch_est_front(p, c->stream));
-    // the eligibility word as soon as K12e has decided it (words [402], flag [403]); K3r is
-    // queued behind it and returns at once on an ineligible block, while the host reads it
-    const uint64_t seq0 = ++c->mail_seq;
-    HIP_TRY(c, launch_publish(reinterpret_cast<const uint64_t *>(p.eflag), 1,
-                              c->d_mail + kEstMailWord + 2, c->d_mail + kEstMailWord + 3, seq0,
-                              c->stream));
-    toc(c, PH_COUNT, t);
-    t = tic(c);
-    HIP_TRY(c, launch_est_level3(p, c->stream));
-    toc(c, PH_LEVEL3, t);
-    {
-        volatile uint64_t *flag = c->h_mail + kEstMailWord + 3;
-        for (uint64_t spin = 0; *flag != seq0; ++spin) {
+    p.mail = c->d_mail + kEstMailWord;
+    p.seq_elig = ++c->mail_seq;
+    p.seq_done = ++c->mail_seq;
+    volatile uint64_t *mail = c->h_mail + kEstMailWord;
+    // poll a sequence word of the mailbox; a stream that goes idle without it is an error
+    auto wait_word = [&](size_t w, uint64_t seq, const char *what) -> gsort_status {
+        for (uint64_t spin = 0; mail[w] != seq; ++spin) {
             if ((spin & 1023) == 1023) {
                 const hipError_t q = hipStreamQuery(c->stream);
-                if (q != hipErrorNotReady && *flag != seq0)
-                    return set_err(c, GSORT_EHIP, std::string("sampled plan: eligibility word: ") +
-                                                      hipGetErrorString(q));
+                if (q != hipErrorNotReady && mail[w] != seq)
+                    return set_err(c, GSORT_EHIP, std::string("sampled plan: ") + what + ": " +
+                                                      (q == hipSuccess ? "stream idle without it"
+                                                                       : hipGetErrorString(q)));
                 std::this_thread::yield();
             }
         }
         std::atomic_thread_fence(std::memory_order_acquire);
-        if (c->h_mail[kEstMailWord + 2] & 4u) return GSORT_OK;  // ineligible: exact plan
-    }
+        return GSORT_OK;
+    };
+    hipEvent_t t = tic(c);
+    HIP_TRY(c, launch_est_front(p, c->stream));  // K12e-b publishes the eligibility word
+    toc(c, PH_COUNT, t);
+    t = tic(c);
+    HIP_TRY(c, launch_est_level3(p, c->stream));  // returns at once on an ineligible block
+    toc(c, PH_LEVEL3, t);
+    ST_TRY(wait_word(3, p.seq_elig, "eligibility word"));
+    if (mail[2] & 4u) return GSORT_OK;  // ineligible: the exact plan sorts
     t = tic(c);
     HIP_TRY(c, launch_est_level2(p, c->stream));
     toc(c, PH_LEVEL2, t);
-    HIP_TRY(c, launch_est_classify(p, c->stream));
-    // K12p twice: the status words, then the list counters behind the sequence flag the host
-    // polls (the K11e grids are the list lengths)
-    const uint64_t seq = ++c->mail_seq;
-    constexpr uint32_t kCtrWords = (uint32_t)(kCtrBytes / 8);
-    HIP_TRY(c, launch_publish(reinterpret_cast<const uint64_t *>(p.eflag), 1,
-                              c->d_mail + kEstMailWord, c->d_mail + kEstMailWord + 1, seq,
-                              c->stream));
-    HIP_TRY(c, launch_publish(reinterpret_cast<const uint64_t *>(c->d_small + OFF_CTR), kCtrWords,
-                              c->d_mail + 8, c->d_mail, seq, c->stream));
-    ST_TRY(wait_mail(c, seq));
-    volatile uint64_t *mail = c->h_mail;
-    if (mail[kEstMailWord + 1] != seq)
-        return set_err(c, GSORT_EHIP, "sampled plan: status word not published");
-    if (mail[kEstMailWord] != 0) return GSORT_OK;  // ineligible or overflowed: *ok stays false
+    HIP_TRY(c, launch_est_classify(p, c->stream));  // its last block publishes the counters
+    ST_TRY(wait_word(1, p.seq_done, "K12g counters"));
+    if (mail[0] != 0) return GSORT_OK;  // a region overflowed: *ok stays false
     uint64_t h[3 * (kLocalClasses + 1)];
-    memcpy(h, c->h_mail + 8, kCtrBytes);
+    for (int i = 0; i < 3 * (kLocalClasses + 1); ++i) h[i] = mail[8 + i];
     uint64_t keys = 0, ent = 0;
     for (int k = 1; k <= kLocalClasses; ++k) { keys += h[3 * k + 1]; ent += h[3 * k]; }
     if (keys != n || ent > kBuckets16)  // every key in exactly one K11e entry
