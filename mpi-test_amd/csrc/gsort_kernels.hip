@@ -2177,7 +2177,7 @@ __global__ __launch_bounds__(512) void k_lds_order_check(const uint32_t *__restr
 //       512-key block: short segments keep the estimate of position-correlated input, e.g.
 //       concatenated sorted runs, close to that of independent samples), 65536 u8 child
 //       counters + 8 x 256 shard counters per workgroup
-//   K12e k_est_caps / k_est_place: region capacities, bases and cursors; eligibility
+//   K12e k_est_plan: region capacities, bases and cursors; eligibility
 //   K3r / K3a (EST): the reservation partitions with region limits
 //   K12f k_est_tiles: K3a tile descriptors over the level-3 pieces (bucket x shard)
 //   K12g k_est_classify: exact child sizes from the cursors, output offsets, K11 lists
@@ -2196,10 +2196,10 @@ __device__ __forceinline__ uint32_t est_seg_off(uint32_t j) {  // sample offset 
 
 // K1e: thread tid samples key tid % 8 of segment tid / 8; workgroup b takes the 512-key
 // blocks j = b * 128 + seg, + kEstWG * 128, ... (so every child's samples spread over all
-// workgroups), four loads in flight per thread.  part8[b][.] = the 65536 u8 child counters
+// workgroups), eight loads in flight per thread.  part8[b][.] = the 65536 u8 child counters
 // (packed 4 per word), part3[b][x * 256 + d] = samples of level-3 bucket d in shard x (tile
 // pair j / 32, shard pair % 8, as K3r deals them), msamp[b] = samples | wrap << 31.
-// Block 0 also zeroes eflag[0..2] (eflag, ovf, K12g's finished-block count) for this sort.
+// Block 0 also zeroes eflag[0..3] (eflag, ovf, K12g's and K12e's finished-block counts).
 template <bool FIN>
 __global__ __launch_bounds__(1024) void k_est_sample(const uint32_t *__restrict__ in, uint64_t n,
                                                      uint32_t *__restrict__ part8,
@@ -2213,13 +2213,13 @@ __global__ __launch_bounds__(1024) void k_est_sample(const uint32_t *__restrict_
     for (uint32_t i = tid; i < kEstPartWords; i += 1024) s_h[i] = 0;
     for (uint32_t i = tid; i < kEstPart3; i += 1024) s_3[i] = 0;
     if (tid == 0) s_m = 0;
-    if (blockIdx.x == 0 && tid < 3) eflag[tid] = 0;
+    if (blockIdx.x == 0 && tid < 4) eflag[tid] = 0;
     __syncthreads();
     const uint32_t nblk = (uint32_t)((n + kEstBlockKeys - 1) / kEstBlockKeys);
     constexpr uint32_t SEGS = 1024 / kEstSegKeys;  // segments per workgroup round
     static_assert(kEstBlockKeys / kEstSegKeys == 64, "64 segment offsets per block");
     const uint32_t seg = tid / kEstSegKeys, kk = tid % kEstSegKeys, step = gridDim.x * SEGS;
-    constexpr int U = 4;
+    constexpr int U = 8;
     uint32_t cnt = 0, wrap = 0;
     for (uint32_t j0 = blockIdx.x * SEGS + seg; j0 < nblk; j0 += U * step) {
         uint32_t key[U], jj[U];
@@ -2272,22 +2272,28 @@ __device__ __forceinline__ uint64_t est_cap(uint32_t cnt, double scale, double s
     return (uint64_t)ceil(c * scale + slack * (sig + 64.0));
 }
 
-// K12e-a: block s (level-3 bucket), thread e (level-2 child).  capc[s*256+e] = the child's
-// capacity (u32), cap3[x*256+s] = shard x's capacity in bucket s; r2[s] / r3[s] = bucket s's
-// level-2 / level-3 region sizes (u64).  Ineligible (eflag bit 2): a child capacity past
-// kLocalMax (K11 could not take it in one pass), a u8 wrap in K1e, or every sample in bucket s
-// (level 3 would copy; the exact plan skips that level).
-__global__ __launch_bounds__(kRadix) void k_est_caps(const uint32_t *__restrict__ part8,
-                                                     const uint32_t *__restrict__ part3,
-                                                     const uint32_t *__restrict__ msamp,
-                                                     uint32_t nwg, uint64_t n, double slack,
-                                                     uint32_t *__restrict__ capc,
-                                                     uint32_t *__restrict__ cap3,
-                                                     unsigned long long *__restrict__ r2,
-                                                     unsigned long long *__restrict__ r3,
-                                                     uint32_t *__restrict__ eflag) {
+// K12e: block s (level-3 bucket), thread e (level-2 child).  capc = the child's capacity,
+// cap3[x*256+s] = shard x's capacity in bucket s; the child cursors cur2[s*256+e] (u32, offset
+// in bucket s's Y region) with their limits lim2 and start copies init2; the shard cursors
+// cur3[x*256+s] (offset in bucket s's X region), lim3, init3; r2[s] / r3[s] = bucket s's
+// region sizes.  The last block to finish scans r3 / r2 into the region bases bases3 / bases2,
+// zeroes the nzero work-list counters at zero and publishes the final eligibility word to the
+// host mailbox (mail[kMailElig], then seq at kMailEligSeq).
+// Ineligible (eflag bit 2): a child capacity past kLocalMax (K11 could not take it in one
+// pass), a u8 wrap in K1e, every sample in one level-3 bucket (level 3 would copy; the exact
+// plan skips that level), or X / Y outgrowing their buffers (capx / capy keys).
+__global__ __launch_bounds__(kRadix) void k_est_plan(
+    const uint32_t *__restrict__ part8, const uint32_t *__restrict__ part3,
+    const uint32_t *__restrict__ msamp, uint32_t nwg, uint64_t n, double slack, uint64_t capx,
+    uint64_t capy, uint32_t *__restrict__ capc, uint32_t *__restrict__ cap3,
+    unsigned long long *__restrict__ r2, unsigned long long *__restrict__ r3,
+    unsigned long long *__restrict__ bases3, unsigned long long *__restrict__ bases2,
+    uint32_t *__restrict__ cur2, uint32_t *__restrict__ lim2, uint32_t *__restrict__ init2,
+    uint32_t *__restrict__ cur3, uint32_t *__restrict__ lim3, uint32_t *__restrict__ init3,
+    unsigned long long *__restrict__ zero, uint32_t nzero, uint32_t *__restrict__ eflag,
+    unsigned long long *mail, unsigned long long seq) {
     constexpr uint32_t G = kRadix / 64;  // thread groups, each over every G-th partial
-    __shared__ uint32_t s_m, s_bad;
+    __shared__ uint32_t s_m, s_bad, s_last;
     __shared__ uint32_t s_c[G][kRadix], s_3[kRadix / kShards][kShards];
     __shared__ unsigned long long s_w[kRadix / 64], s_c3[kShards];
     const uint32_t s = blockIdx.x, e = threadIdx.x, g = e >> 6, l = e & 63;
@@ -2310,8 +2316,7 @@ __global__ __launch_bounds__(kRadix) void k_est_caps(const uint32_t *__restrict_
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) s_c[g][4 * l + q] = c4[q];
-    // shard counts of bucket s: thread (b0 = e >> 3, x = e & 7) over the partials b0, b0 + 32, ..
-    {
+    {  // shard counts of bucket s: thread (b0 = e >> 3, x = e & 7) over partials b0, b0 + 32, ..
         const uint32_t x = e & 7u, b0 = e >> 3;
         uint32_t c3 = 0;
         for (uint32_t b = b0; b < nwg; b += kRadix / 8) c3 += part3[(uint64_t)b * kEstPart3 + x * kRadix + s];
@@ -2325,9 +2330,14 @@ __global__ __launch_bounds__(kRadix) void k_est_caps(const uint32_t *__restrict_
     const double scale = m ? (double)n / (double)m : 0.0;
     const uint64_t cap = est_cap(cnt, scale, slack);
     if (cap > kLocalMax) s_bad = 1;
-    capc[s * kRadix + e] = (uint32_t)min(cap, (uint64_t)kLocalMax);
+    const uint32_t cc = (uint32_t)min(cap, (uint64_t)kLocalMax);
+    const uint32_t i = s * kRadix + e;
+    capc[i] = cc;
     unsigned long long tot;
-    block_excl_scan(min(cap, (uint64_t)kLocalMax), s_w, &tot);
+    const uint32_t off = (uint32_t)block_excl_scan(cc, s_w, &tot);
+    cur2[i] = off;
+    init2[i] = off;
+    lim2[i] = off + cc;
     if (e < kShards) {
         uint32_t c3 = 0;
         for (uint32_t r = 0; r < kRadix / kShards; ++r) c3 += s_3[r][e];
@@ -2338,62 +2348,36 @@ __global__ __launch_bounds__(kRadix) void k_est_caps(const uint32_t *__restrict_
     __syncthreads();
     if (e == 0) {
         unsigned long long r = 0, samp = 0;
-        for (uint32_t x = 0; x < kShards; ++x) { r += s_c3[x] & 0xffffffffull; samp += s_c3[x] >> 32; }
+        for (uint32_t x = 0; x < kShards; ++x) {
+            const uint32_t j = x * kRadix + s, cx = (uint32_t)(s_c3[x] & 0xffffffffull);
+            cur3[j] = (uint32_t)r;
+            init3[j] = (uint32_t)r;
+            lim3[j] = (uint32_t)(r + cx);
+            r += cx;
+            samp += s_c3[x] >> 32;
+        }
         r2[s] = tot;
         r3[s] = r;
         if (m && samp == m) s_bad = 1;
         if (s_bad) atomicOr(eflag, 4u);
+        __threadfence();
+        s_last = atomicAdd(eflag + 3, 1u) == gridDim.x - 1;
     }
-}
-
-// K12e-b: block s, thread e.  bases3[s] / bases2[s] = exclusive scans of r3 / r2 (the regions
-// of bucket s in X / Y); the child cursors cur2[s*256+e] (u32, offset in bucket s's Y region)
-// with their limits lim2 and start copies init2; the shard cursors cur3[x*256+s] (offset in
-// bucket s's X region), lim3, init3.  Ineligible when X or Y would outgrow its buffer
-// (capx / capy keys).  Block 0 zeroes the nzero work-list counters at zero and publishes the
-// final eligibility word to the host mailbox (mail[kMailElig], then seq at kMailEligSeq).
-__global__ __launch_bounds__(kRadix) void k_est_place(
-    const uint32_t *__restrict__ capc, const uint32_t *__restrict__ cap3,
-    const unsigned long long *__restrict__ r2, const unsigned long long *__restrict__ r3,
-    uint64_t capx, uint64_t capy, unsigned long long *__restrict__ bases3,
-    unsigned long long *__restrict__ bases2, uint32_t *__restrict__ cur2,
-    uint32_t *__restrict__ lim2, uint32_t *__restrict__ init2, uint32_t *__restrict__ cur3,
-    uint32_t *__restrict__ lim3, uint32_t *__restrict__ init3,
-    unsigned long long *__restrict__ zero, uint32_t nzero, uint32_t *__restrict__ eflag,
-    unsigned long long *mail, unsigned long long seq) {
-    __shared__ unsigned long long s_w[kRadix / 64];
-    const uint32_t s = blockIdx.x, e = threadIdx.x;
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();
     unsigned long long tx, ty;
-    const unsigned long long b3 = block_excl_scan(r3[e], s_w, &tx);
-    const unsigned long long b2 = block_excl_scan(r2[e], s_w, &ty);
-    if (s == 0) {
-        bases3[e] = b3;
-        bases2[e] = b2;
-        if (e < nzero) zero[e] = 0;
-        if (e == 0) {  // the eligibility is final here (K12e-a's flags are in): publish it
-            if (tx > capx || ty > capy) atomicOr(eflag, 4u);
-            __threadfence();
-            mail[kMailElig] = __hip_atomic_load(reinterpret_cast<unsigned long long *>(eflag),
-                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            mail_release(mail + kMailEligSeq, seq);
-        }
-    }
-    const uint32_t c = capc[s * kRadix + e];
-    unsigned long long t2;
-    const uint32_t off = (uint32_t)block_excl_scan(c, s_w, &t2);
-    const uint32_t i = s * kRadix + e;
-    cur2[i] = off;
-    init2[i] = off;
-    lim2[i] = off + c;
+    const unsigned long long v3 = __hip_atomic_load(r3 + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long v2 = __hip_atomic_load(r2 + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    bases3[e] = block_excl_scan(v3, s_w, &tx);
+    bases2[e] = block_excl_scan(v2, s_w, &ty);
+    if (e < nzero) zero[e] = 0;
     if (e == 0) {
-        uint32_t r = 0;
-        for (uint32_t x = 0; x < kShards; ++x) {
-            const uint32_t j = x * kRadix + s, cx = cap3[j];
-            cur3[j] = r;
-            init3[j] = r;
-            lim3[j] = r + cx;
-            r += cx;
-        }
+        if (tx > capx || ty > capy) atomicOr(eflag, 4u);
+        __threadfence();
+        mail[kMailElig] = __hip_atomic_load(reinterpret_cast<unsigned long long *>(eflag),
+                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        mail_release(mail + kMailEligSeq, seq);
     }
 }
 
@@ -3159,14 +3143,12 @@ hipError_t launch_est_front(const EstPlan &p, hipStream_t s) {
     if (p.n == 0 || p.n > kEstMaxKeys) return hipErrorInvalidValue;
     if (p.flip_in) launch_k(k_est_sample<true>, kEstWG, 1024, 0, s, p.in, p.n, p.part8, p.part3, p.msamp, p.eflag);
     else launch_k(k_est_sample<false>, kEstWG, 1024, 0, s, p.in, p.n, p.part8, p.part3, p.msamp, p.eflag);
-    launch_k(k_est_caps, kRadix, kRadix, 0, s, p.part8, p.part3, p.msamp, kEstWG, p.n, p.slack,
-             p.capc, p.cap3, reinterpret_cast<ull *>(p.r2), reinterpret_cast<ull *>(p.r3), p.eflag);
-    launch_k(k_est_place, kRadix, kRadix, 0, s, p.capc, p.cap3,
-             reinterpret_cast<const ull *>(p.r2), reinterpret_cast<const ull *>(p.r3), p.capx,
-             p.capy, reinterpret_cast<ull *>(p.bases3), reinterpret_cast<ull *>(p.bases2), p.cur2,
-             p.lim2, p.init2, p.cur3, p.lim3, p.init3, reinterpret_cast<ull *>(p.wl.ctr),
-             (uint32_t)(3 * (kLocalClasses + 1)), p.eflag, reinterpret_cast<ull *>(p.mail),
-             (ull)p.seq_elig);
+    launch_k(k_est_plan, kRadix, kRadix, 0, s, p.part8, p.part3, p.msamp, kEstWG, p.n, p.slack,
+             p.capx, p.capy, p.capc, p.cap3, reinterpret_cast<ull *>(p.r2),
+             reinterpret_cast<ull *>(p.r3), reinterpret_cast<ull *>(p.bases3),
+             reinterpret_cast<ull *>(p.bases2), p.cur2, p.lim2, p.init2, p.cur3, p.lim3, p.init3,
+             reinterpret_cast<ull *>(p.wl.ctr), (uint32_t)(3 * (kLocalClasses + 1)), p.eflag,
+             reinterpret_cast<ull *>(p.mail), (ull)p.seq_elig);
     return hipGetLastError();
 }
 

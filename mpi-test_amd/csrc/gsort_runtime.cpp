@@ -928,7 +928,7 @@ gsort_status msd_sort_h16(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
 constexpr size_t kEstMailWord = 400;
 static_assert((kEstMailWord + kEstMailWords) * 8 <= kMailBytes, "mailbox");
 
-// Keys of the region buffers the caps of `nreg` regions can add up to (k_est_caps' est_cap:
+// Keys of the region buffers the caps of `nreg` regions can add up to (k_est_plan's est_cap:
 // max(a, b) <= a + b, Cauchy-Schwarz on the sigma terms: sum sqrt(cnt + 1) <=
 // sqrt(nreg (m + nreg)); m >= the samples of all full blocks)
 uint64_t est_region_keys(uint64_t n, uint64_t nreg, double slack) {
