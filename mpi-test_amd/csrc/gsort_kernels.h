@@ -264,13 +264,14 @@ hipError_t launch_compat_keys(const int32_t *a, uint64_t n, int P, int loop, con
 // exact plan; both are known once K12g has run (the runtime reads them with the K11e list
 // counts).  Sizes (u32 unless noted): part8 kEstWGs x 16384, part3 kEstWGs x 2048, msamp
 // kEstWGs, capc / cur2 / lim2 / init2 65536, cap3 / cur3 / lim3 / init3 2048, r2 / r3 / bases3 /
-// bases2 256 u64, tp 257, tdesc est_max_tiles(n) x kTileDescBytes, dump kSweepTile keys;
+// bases2 256 u64, tp 257, tdesc (est_max_tiles(n) + 2048) x kTileDescBytes (tile descriptors,
+// then the 2048-entry level-3 piece table), dump kSweepTile keys;
 // wl.list[1..4] 65536 entries each, wl.ctr the 15 counters (zeroed by the front).
 constexpr uint32_t kEstWGs = 128;
 constexpr uint32_t kEstBlockKeysHost = 512;  // one 8-key sample segment per block
 constexpr uint64_t kEstMinKeys = 1ull << 22;   // below: too few samples per child
 constexpr uint64_t kEstMaxKeys = 1ull << 31;   // level-3 regions stay below 2^32 keys
-inline uint64_t est_max_tiles(uint64_t n) { return sweep_tiles(n) + 8 * 256; }
+inline uint64_t est_max_tiles(uint64_t n) { return sweep_tiles(n) + 256; }
 struct EstPlan {
     const uint32_t *in;
     uint64_t n;

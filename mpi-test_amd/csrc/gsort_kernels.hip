@@ -1404,6 +1404,7 @@ __global__ __launch_bounds__(kRadix) void k_plan16_place(
 // (tpfx[s] <= t < tpfx[s+1]), first key and length.  K3a then reaches its keys after one
 // (scalar) load instead of a tpfx load, an LDS binary search and two dependent loads of the
 // bucket bounds -- a chain every one of its ~16K single-pair workgroups exposed.
+constexpr uint32_t kStraddle = 0x80000000u;  // K12f: a K3a tile across level-3 pieces
 struct TileDesc {
     unsigned long long t0;
     uint32_t len, seg;
@@ -1459,7 +1460,7 @@ __global__ __launch_bounds__(BLOCK) void k_partition_res(
     const unsigned long long *__restrict__ bases, uint32_t *__restrict__ cur,
     const uint32_t *__restrict__ flags, const uint32_t *__restrict__ raw,
     const uint32_t *__restrict__ lim = nullptr, uint32_t *__restrict__ ovf = nullptr,
-    OT *__restrict__ dump = nullptr) {
+    OT *__restrict__ dump = nullptr, const TileDesc *__restrict__ pieces = nullptr) {
     constexpr int TILE = BLOCK * ITEMS, shift = L3 ? 24 : 16;
     static_assert(TILE == kSweepTile, "reservation tiles are kSweepTile keys");
     uint32_t flip = 0;
@@ -1487,6 +1488,7 @@ __global__ __launch_bounds__(BLOCK) void k_partition_res(
     if (2 * pr >= ntile) return;
     uint32_t seg[2], len[2];
     uint64_t t0[2];
+    bool straddle[2] = {false, false};
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         const uint32_t t = 2 * pr + h;
@@ -1500,6 +1502,7 @@ __global__ __launch_bounds__(BLOCK) void k_partition_res(
                 t0[h] = d.t0;
                 len[h] = d.len;
                 seg[h] = d.seg;
+                if (EST && (d.seg & kStraddle)) { straddle[h] = true; seg[h] = d.seg & ~kStraddle; }
             }
         }
     }
@@ -1510,7 +1513,23 @@ __global__ __launch_bounds__(BLOCK) void k_partition_res(
     uint32_t k[2][ITEMS], r[2][ITEMS];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-        load_tile<BLOCK, ITEMS, FIN>(in + t0[h] + tid, len[h] == (uint32_t)TILE, len[h], k[h]);
+        if (EST && !L3 && straddle[h]) {  // a tile across pieces of bucket seg[h] (K12f)
+            const TileDesc *pc = pieces + seg[h] * kShards;
+            uint64_t pa[kShards];
+            uint32_t pv[kShards];
+#pragma unroll
+            for (uint32_t x = 0; x < kShards; ++x) { pa[x] = pc[x].t0; pv[x] = pc[x].len; }
+#pragma unroll
+            for (int i = 0; i < ITEMS; ++i) {
+                const uint32_t j = (uint32_t)(i * BLOCK) + tid, v = (uint32_t)t0[h] + j;
+                uint32_t x = 0;
+#pragma unroll
+                for (uint32_t q = 1; q < kShards; ++q) x += v >= pv[q];
+                k[h][i] = j < len[h] ? in[pa[x] + (v - pv[x])] : 0u;
+            }
+        } else {
+            load_tile<BLOCK, ITEMS, FIN>(in + t0[h] + tid, len[h] == (uint32_t)TILE, len[h], k[h]);
+        }
         if (!L3) {
 #pragma unroll
             for (int i = 0; i < ITEMS; ++i) k[h][i] ^= flip;
@@ -2381,32 +2400,40 @@ __global__ __launch_bounds__(kRadix) void k_est_plan(
     }
 }
 
-// K12f: K3a's tile descriptors over the level-3 pieces q = s * 8 + x (bucket s, shard x: keys
-// [bases3[s] + init3[x*256+s], + their count, clamped to the region: an overflowed piece's
-// excess went to the scratch tile)), ceil(count / kSweepTile) tiles each; every
-// block rebuilds the 2048-piece tile prefix in LDS and describes its 256 tiles.  tp[256] =
-// the tile total (K3a's ntile).
+// K12f: K3a's tile descriptors.  Level-3 bucket s is the concatenation of its 8 pieces (shard
+// x: keys [bases3[s] + init3[x*256+s], + their count, clamped to the region: an overflowed
+// piece's excess went to the scratch tile)); its tiles cover that concatenation in kSweepTile
+// steps, so a bucket has one partial tile, not one per piece (2048 half-full tiles cost K3a ~3 %).
+// A tile inside one piece gets {first key, length, s}; one that crosses a piece boundary gets
+// {virtual start, length, s | kStraddle} and K3a maps every key through the bucket's piece
+// table pieces[s*8 + x] = {first key, virtual start, virtual end}.  Every block rebuilds the
+// 256-bucket tile prefix in LDS and describes its 256 tiles; tp[256] = the tile total.
 __global__ __launch_bounds__(256) void k_est_tiles(const uint32_t *__restrict__ cur3,
                                                    const uint32_t *__restrict__ init3,
                                                    const uint32_t *__restrict__ lim3,
                                                    const unsigned long long *__restrict__ bases3,
                                                    uint32_t max_tiles, const uint32_t *eflag,
                                                    uint32_t *__restrict__ tp,
-                                                   TileDesc *__restrict__ desc) {
-    constexpr uint32_t NQ = kShards * kRadix, PER = NQ / 256;
-    __shared__ uint32_t s_tp[NQ + 1];
+                                                   TileDesc *__restrict__ desc,
+                                                   TileDesc *__restrict__ pieces) {
+    __shared__ uint32_t s_tp[kRadix + 1];
     __shared__ uint32_t s_w[4];
     if ((*eflag & 4u) || eflag[1]) return;  // ineligible, or level 3 overflowed
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    uint32_t nt[PER], sum = 0;
+    uint32_t vs[kShards + 1];  // bucket tid's piece starts in its concatenation
+    vs[0] = 0;
 #pragma unroll
-    for (uint32_t i = 0; i < PER; ++i) {
-        const uint32_t q = tid * PER + i, s = q / kShards, x = q % kShards;
-        const uint32_t j = x * kRadix + s, c = min(cur3[j], lim3[j]) - init3[j];
-        nt[i] = (c + kSweepTile - 1) / kSweepTile;
-        sum += nt[i];
+    for (uint32_t x = 0; x < kShards; ++x) {
+        const uint32_t j = x * kRadix + tid;
+        vs[x + 1] = vs[x] + (min(cur3[j], lim3[j]) - init3[j]);
     }
-    uint32_t v = sum;
+    if (blockIdx.x == 0) {
+#pragma unroll
+        for (uint32_t x = 0; x < kShards; ++x)
+            pieces[tid * kShards + x] = {bases3[tid] + init3[x * kRadix + tid], vs[x], vs[x + 1]};
+    }
+    const uint32_t nt = (vs[kShards] + kSweepTile - 1) / kSweepTile;
+    uint32_t v = nt;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
         const uint32_t t = __shfl_up(v, o);
@@ -2414,25 +2441,37 @@ __global__ __launch_bounds__(256) void k_est_tiles(const uint32_t *__restrict__ 
     }
     if (lane == 63) s_w[w] = v;
     __syncthreads();
-    uint32_t run = v - sum;
+    uint32_t run = v - nt;
     for (uint32_t ww = 0; ww < w; ++ww) run += s_w[ww];
-#pragma unroll
-    for (uint32_t i = 0; i < PER; ++i) { s_tp[tid * PER + i] = run; run += nt[i]; }
-    if (tid == 255) s_tp[NQ] = run;
+    s_tp[tid] = run;
+    if (tid == 255) s_tp[kRadix] = run + nt;
     __syncthreads();
-    const uint32_t total = s_tp[NQ];
+    const uint32_t total = s_tp[kRadix];
     if (blockIdx.x == 0 && tid == 0) tp[kRadix] = total;
     const uint32_t t = blockIdx.x * 256 + tid;
     if (t >= total || t >= max_tiles) return;
-    uint32_t lo = 0, hi = NQ;  // s_tp[lo] <= t < s_tp[hi]
+    uint32_t lo = 0, hi = kRadix;  // s_tp[lo] <= t < s_tp[hi]
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
         if (s_tp[mid] <= t) lo = mid;
         else hi = mid;
     }
-    const uint32_t s = lo / kShards, x = lo % kShards, j = x * kRadix + s;
-    const uint32_t c = min(cur3[j], lim3[j]) - init3[j], i0 = (t - s_tp[lo]) * kSweepTile;
-    desc[t] = {bases3[s] + init3[j] + i0, min(c - i0, (uint32_t)kSweepTile), s};
+    const uint32_t sb = lo;
+    uint32_t vb[kShards + 1];
+    vb[0] = 0;
+#pragma unroll
+    for (uint32_t x = 0; x < kShards; ++x) {
+        const uint32_t j = x * kRadix + sb;
+        vb[x + 1] = vb[x] + (min(cur3[j], lim3[j]) - init3[j]);
+    }
+    const uint32_t v0 = (t - s_tp[sb]) * kSweepTile, len = min(vb[kShards] - v0, (uint32_t)kSweepTile);
+    uint32_t x = 0;
+#pragma unroll
+    for (uint32_t q = 1; q < kShards; ++q) x += v0 >= vb[q];
+    if (v0 + len <= vb[x + 1])
+        desc[t] = {bases3[sb] + init3[x * kRadix + sb] + (v0 - vb[x]), len, sb};
+    else
+        desc[t] = {v0, len, sb | kStraddle};
 }
 
 // K12g: block s, thread e.  Exact sizes: child (s, e) holds cur2 - init2 keys, bucket s' holds
@@ -2808,7 +2847,7 @@ hipError_t launch_partition3r(const uint32_t *in, uint32_t *out, uint64_t n, uin
     launch_k(k_partition_res<B, I, true, true>, (unsigned)pairs, B, 0, s,
         in, out, n, nullptr, nullptr, reinterpret_cast<const ull *>(bases), cur3, flags,
         (const uint32_t *)nullptr, (const uint32_t *)nullptr, (uint32_t *)nullptr,
-        (uint32_t *)nullptr);
+        (uint32_t *)nullptr, (const TileDesc *)nullptr);
     return hipGetLastError();
 }
 
@@ -2829,11 +2868,11 @@ hipError_t launch_partition2r(const uint32_t *in, uint32_t *out, uint16_t *out16
     if (out16)
         launch_k(k_partition_res<B, I, false, false, uint16_t>, g2, B, 0, s, in, out16, n, tpfx,
                  desc, bs, cur, flags, raw, (const uint32_t *)nullptr, (uint32_t *)nullptr,
-                 (uint16_t *)nullptr);
+                 (uint16_t *)nullptr, (const TileDesc *)nullptr);
     else
         launch_k(k_partition_res<B, I, false, false>, g2, B, 0, s, in, out, n, tpfx, desc, bs,
                  cur, flags, raw, (const uint32_t *)nullptr, (uint32_t *)nullptr,
-                 (uint32_t *)nullptr);
+                 (uint32_t *)nullptr, (const TileDesc *)nullptr);
     return hipGetLastError();
 }
 
@@ -3160,7 +3199,8 @@ hipError_t launch_est_level3(const EstPlan &p, hipStream_t s) {
     launch_k(k_partition_res<B, I, true, true, uint32_t, true>, (unsigned)pairs, B, 0, s,
              p.in, p.x, p.n, (const uint32_t *)nullptr, (const TileDesc *)nullptr,
              reinterpret_cast<const ull *>(p.bases3), p.cur3, (const uint32_t *)p.eflag,
-             (const uint32_t *)nullptr, (const uint32_t *)p.lim3, p.eflag + 1, p.dump);
+             (const uint32_t *)nullptr, (const uint32_t *)p.lim3, p.eflag + 1, p.dump,
+             (const TileDesc *)nullptr);
     return hipGetLastError();
 }
 
@@ -3169,14 +3209,16 @@ hipError_t launch_est_level2(const EstPlan &p, hipStream_t s) {
     constexpr int B = kPartBlock, I = kSweepTile / kPartBlock;
     const uint32_t max_tiles = (uint32_t)est_max_tiles(p.n);
     TileDesc *desc = static_cast<TileDesc *>(p.tdesc);
+    TileDesc *pieces = desc + max_tiles;
     launch_k(k_est_tiles, (max_tiles + 255) / 256, 256, 0, s, (const uint32_t *)p.cur3,
              (const uint32_t *)p.init3, (const uint32_t *)p.lim3,
              reinterpret_cast<const ull *>(p.bases3), max_tiles, (const uint32_t *)p.eflag, p.tp,
-             desc);
+             desc, pieces);
     launch_k(k_partition_res<B, I, false, false, uint32_t, true>, (max_tiles + 1) / 2, B, 0, s,
              (const uint32_t *)p.x, p.y, p.n, (const uint32_t *)p.tp, (const TileDesc *)desc,
              reinterpret_cast<const ull *>(p.bases2), p.cur2, (const uint32_t *)p.eflag,
-             (const uint32_t *)nullptr, (const uint32_t *)p.lim2, p.eflag + 1, p.dump);
+             (const uint32_t *)nullptr, (const uint32_t *)p.lim2, p.eflag + 1, p.dump,
+             (const TileDesc *)pieces);
     return hipGetLastError();
 }
 

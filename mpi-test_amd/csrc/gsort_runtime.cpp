@@ -950,7 +950,7 @@ gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
     ST_TRY(ensure(c, c->m_epart, (size_t)kEstWGs * (kBuckets16 / 4 + kH16Shards * kRadix + 1) * 4));
     constexpr size_t kPlanWords = (size_t)4 * kBuckets16 + 4 * kH16Shards * kRadix + kRadix + 1;
     ST_TRY(ensure(c, c->m_eplan, kPlanWords * 4 + 4 * kRadix * 8 + 64));
-    ST_TRY(ensure(c, c->m_edesc, (size_t)est_max_tiles(n) * kTileDescBytes));
+    ST_TRY(ensure(c, c->m_edesc, ((size_t)est_max_tiles(n) + kH16Shards * kRadix) * kTileDescBytes));
     ST_TRY(ensure(c, c->m_edump, (size_t)kSweepTile * 4));
     for (int k = 0; k < kLocalClasses; ++k) ST_TRY(ensure_list(c, c->m_local[k], kBuckets16));
     EstPlan p{};
