@@ -290,7 +290,8 @@ struct EstPlan {
     double slack;
     bool atomic_rank;
     // pinned host mailbox (device pointer) and the sequence numbers K12e-b / K12g publish with:
-    // mail[2] eligibility word, mail[3] = seq_elig; mail[0] status {eflag, ovf}, mail[8 .. 23)
+    // mail[2] eligibility word, mail[4] the children with samples, mail[3] = seq_elig;
+    // mail[0] status {eflag, ovf}, mail[8 .. 23)
     // the K11e list counters, mail[1] = seq_done
     uint64_t *mail;
     uint64_t seq_elig, seq_done;
@@ -300,8 +301,10 @@ hipError_t launch_est_front(const EstPlan &p, hipStream_t s);   // K1e + K12e
 hipError_t launch_est_level3(const EstPlan &p, hipStream_t s);  // K3r
 hipError_t launch_est_level2(const EstPlan &p, hipStream_t s);  // K12f + K3a
 hipError_t launch_est_classify(const EstPlan &p, hipStream_t s);  // K12g
-// K11e over class list cls (nlist entries: the host reads the counts K12g made)
-hipError_t launch_local_sort_e(const EstPlan &p, int cls, uint32_t nlist, hipStream_t s);
+// K11e over entries [first, first + nlist) of class list cls (those at or past the count K12g
+// made return at once)
+hipError_t launch_local_sort_e(const EstPlan &p, int cls, uint32_t first, uint32_t nlist,
+                               hipStream_t s);
 // Plain device copy kernel (used when a sort has no non-trivial pass).
 hipError_t launch_copy(const uint32_t *in, uint32_t *out, uint64_t n, hipStream_t s);
 

@@ -2218,7 +2218,8 @@ __device__ __forceinline__ uint32_t est_seg_off(uint32_t j) {  // sample offset 
 // workgroups), eight loads in flight per thread.  part8[b][.] = the 65536 u8 child counters
 // (packed 4 per word), part3[b][x * 256 + d] = samples of level-3 bucket d in shard x (tile
 // pair j / 32, shard pair % 8, as K3r deals them), msamp[b] = samples | wrap << 31.
-// Block 0 also zeroes eflag[0..3] (eflag, ovf, K12g's and K12e's finished-block counts).
+// Block 0 also zeroes eflag[0..4] (eflag, ovf, K12g's and K12e's finished-block counts, K12e's
+// count of sampled children).
 template <bool FIN>
 __global__ __launch_bounds__(1024) void k_est_sample(const uint32_t *__restrict__ in, uint64_t n,
                                                      uint32_t *__restrict__ part8,
@@ -2232,7 +2233,7 @@ __global__ __launch_bounds__(1024) void k_est_sample(const uint32_t *__restrict_
     for (uint32_t i = tid; i < kEstPartWords; i += 1024) s_h[i] = 0;
     for (uint32_t i = tid; i < kEstPart3; i += 1024) s_3[i] = 0;
     if (tid == 0) s_m = 0;
-    if (blockIdx.x == 0 && tid < 4) eflag[tid] = 0;
+    if (blockIdx.x == 0 && tid < 5) eflag[tid] = 0;
     __syncthreads();
     const uint32_t nblk = (uint32_t)((n + kEstBlockKeys - 1) / kEstBlockKeys);
     constexpr uint32_t SEGS = 1024 / kEstSegKeys;  // segments per workgroup round
@@ -2274,7 +2275,8 @@ __global__ __launch_bounds__(1024) void k_est_sample(const uint32_t *__restrict_
 // The sampled plan's words in the pinned host mailbox (relative to the `mail` pointer the
 // runtime passes): the status {eflag, ovf} and its sequence after K12g, the same after K12e
 // (eligibility only), the 15 work-list counters after K12g.
-constexpr uint32_t kMailStatus = 0, kMailSeq = 1, kMailElig = 2, kMailEligSeq = 3, kMailCtr = 8;
+constexpr uint32_t kMailStatus = 0, kMailSeq = 1, kMailElig = 2, kMailEligSeq = 3,
+                   kMailChildren = 4, kMailCtr = 8;
 
 __device__ __forceinline__ void mail_release(unsigned long long *flag, unsigned long long seq) {
     __threadfence_system();
@@ -2297,7 +2299,8 @@ __device__ __forceinline__ uint64_t est_cap(uint32_t cnt, double scale, double s
 // cur3[x*256+s] (offset in bucket s's X region), lim3, init3; r2[s] / r3[s] = bucket s's
 // region sizes.  The last block to finish scans r3 / r2 into the region bases bases3 / bases2,
 // zeroes the nzero work-list counters at zero and publishes the final eligibility word to the
-// host mailbox (mail[kMailElig], then seq at kMailEligSeq).
+// host mailbox (mail[kMailElig], the number of children with samples at mail[kMailChildren],
+// then seq at kMailEligSeq).
 // Ineligible (eflag bit 2): a child capacity past kLocalMax (K11 could not take it in one
 // pass), a u8 wrap in K1e, every sample in one level-3 bucket (level 3 would copy; the exact
 // plan skips that level), or X / Y outgrowing their buffers (capx / capy keys).
@@ -2312,11 +2315,11 @@ __global__ __launch_bounds__(kRadix) void k_est_plan(
     unsigned long long *__restrict__ zero, uint32_t nzero, uint32_t *__restrict__ eflag,
     unsigned long long *mail, unsigned long long seq) {
     constexpr uint32_t G = kRadix / 64;  // thread groups, each over every G-th partial
-    __shared__ uint32_t s_m, s_bad, s_last;
+    __shared__ uint32_t s_m, s_bad, s_last, s_ne;
     __shared__ uint32_t s_c[G][kRadix], s_3[kRadix / kShards][kShards];
     __shared__ unsigned long long s_w[kRadix / 64], s_c3[kShards];
     const uint32_t s = blockIdx.x, e = threadIdx.x, g = e >> 6, l = e & 63;
-    if (e == 0) { s_m = 0; s_bad = 0; }
+    if (e == 0) { s_m = 0; s_bad = 0; s_ne = 0; }
     __syncthreads();
     if (e < nwg) {
         const uint32_t v = msamp[e];
@@ -2349,6 +2352,8 @@ __global__ __launch_bounds__(kRadix) void k_est_plan(
     const double scale = m ? (double)n / (double)m : 0.0;
     const uint64_t cap = est_cap(cnt, scale, slack);
     if (cap > kLocalMax) s_bad = 1;
+    const uint64_t sampled = __ballot(cnt > 0);  // (outside the branch: all lanes vote)
+    if ((e & 63) == 0) atomicAdd(&s_ne, (uint32_t)__popcll(sampled));
     const uint32_t cc = (uint32_t)min(cap, (uint64_t)kLocalMax);
     const uint32_t i = s * kRadix + e;
     capc[i] = cc;
@@ -2379,6 +2384,7 @@ __global__ __launch_bounds__(kRadix) void k_est_plan(
         r3[s] = r;
         if (m && samp == m) s_bad = 1;
         if (s_bad) atomicOr(eflag, 4u);
+        atomicAdd(eflag + 4, s_ne);
         __threadfence();
         s_last = atomicAdd(eflag + 3, 1u) == gridDim.x - 1;
     }
@@ -2396,6 +2402,7 @@ __global__ __launch_bounds__(kRadix) void k_est_plan(
         __threadfence();
         mail[kMailElig] = __hip_atomic_load(reinterpret_cast<unsigned long long *>(eflag),
                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        mail[kMailChildren] = __hip_atomic_load(eflag + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         mail_release(mail + kMailEligSeq, seq);
     }
 }
@@ -2555,17 +2562,23 @@ __global__ __launch_bounds__(kRadix) void k_est_classify(
 // loaded from in + src, sorted on its low ndigits digits and stored flipped at out + dst.
 // (A persistent form that read the entry count on the device was tried: inlined into its loop
 // the sort took 177 VGPRs, under launch bounds it spilled; both ran at half speed.)
+// Entry first + blockIdx.x, if below the class's entry count ctr[0]: the runtime launches the
+// class it expects to hold most children right behind K12g with a grid of the sampled children
+// (no host round trip in between), and the rest once it has read the counts.
 template <int BLOCK, int ITEMS, bool ATOMIC>
 __global__ __launch_bounds__(BLOCK) void k_local_sort_e(const uint32_t *__restrict__ in,
                                                         uint32_t *__restrict__ out,
                                                         const unsigned long long *__restrict__ list,
-                                                        int ndigits) {
+                                                        const unsigned long long *__restrict__ ctr,
+                                                        uint32_t first, int ndigits) {
     constexpr int WAVES = BLOCK / 64;
     constexpr int TILE = BLOCK * ITEMS;
     __shared__ uint32_t s_a[TILE];
     __shared__ uint32_t s_wc[WAVES * kRadix];
-    const uint64_t src = list[2 * blockIdx.x];
-    const uint64_t e = list[2 * blockIdx.x + 1];
+    const uint32_t i = first + blockIdx.x;
+    if (i >= (uint32_t)*ctr) return;
+    const uint64_t src = list[2 * i];
+    const uint64_t e = list[2 * i + 1];
     const uint32_t len = (uint32_t)(e >> 40);
     if (threadIdx.x < kRadix) s_wc[threadIdx.x] = 0;
     uint32_t k[ITEMS];
@@ -3231,16 +3244,20 @@ hipError_t launch_est_classify(const EstPlan &p, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_local_sort_e(const EstPlan &p, int cls, uint32_t nlist, hipStream_t s) {
+hipError_t launch_local_sort_e(const EstPlan &p, int cls, uint32_t first, uint32_t nlist,
+                               hipStream_t s) {
     using ull = unsigned long long;
     if (nlist == 0) return hipSuccess;
     if (cls < 1 || cls > kLocalClasses) return hipErrorInvalidValue;
     const ull *l = reinterpret_cast<const ull *>(p.wl.list[cls]);
+    const ull *ctr = reinterpret_cast<const ull *>(p.wl.ctr) + 3 * cls;
     const uint32_t *y = p.y;
 #define GSORT_K11E(B, I)                                                                       \
     do {                                                                                       \
-        if (p.atomic_rank) launch_k(k_local_sort_e<B, I, true>, nlist, B, 0, s, y, p.out, l, 2); \
-        else launch_k(k_local_sort_e<B, I, false>, nlist, B, 0, s, y, p.out, l, 2);             \
+        if (p.atomic_rank)                                                                     \
+            launch_k(k_local_sort_e<B, I, true>, nlist, B, 0, s, y, p.out, l, ctr, first, 2);  \
+        else                                                                                   \
+            launch_k(k_local_sort_e<B, I, false>, nlist, B, 0, s, y, p.out, l, ctr, first, 2); \
     } while (0)
     switch (cls) {
         case 1: GSORT_K11E(256, 18); break;

@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <cmath>
 #include <atomic>
+#include <chrono>
 #include <map>
 #include <mutex>
 #include <set>
@@ -1006,19 +1007,39 @@ gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
         std::atomic_thread_fence(std::memory_order_acquire);
         return GSORT_OK;
     };
+    static const bool etrace = getenv("GSORT_EST_TRACE") != nullptr;  // development
+    const auto h0 = std::chrono::steady_clock::now();
+    auto us = [&] {
+        return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - h0)
+            .count();
+    };
+    double tq = 0, te = 0, tc = 0;
     hipEvent_t t = tic(c);
     HIP_TRY(c, launch_est_front(p, c->stream));  // K12e-b publishes the eligibility word
     toc(c, PH_COUNT, t);
     t = tic(c);
     HIP_TRY(c, launch_est_level3(p, c->stream));  // returns at once on an ineligible block
     toc(c, PH_LEVEL3, t);
-    ST_TRY(wait_word(3, p.seq_elig, "eligibility word"));
-    if (mail[2] & 4u) return GSORT_OK;  // ineligible: the exact plan sorts
+    // K12f, K3a and K12g return at once on an ineligible block too, so they are queued before
+    // the host looks at the eligibility word (waiting first left a launch gap behind K3r)
     t = tic(c);
     HIP_TRY(c, launch_est_level2(p, c->stream));
     toc(c, PH_LEVEL2, t);
     HIP_TRY(c, launch_est_classify(p, c->stream));  // its last block publishes the counters
+    tq = us();
+    ST_TRY(wait_word(3, p.seq_elig, "eligibility word"));
+    te = us();
+    if (mail[2] & 4u) return GSORT_OK;  // ineligible: the exact plan sorts
+    // K11e of the class the average child falls in, queued right behind K12g (a grid of the
+    // sampled children: at least its entries, usually exactly), so no host round trip sits
+    // between K12g and the largest K11e launch; the other classes follow once the counts are in
+    const uint32_t sampled = (uint32_t)std::min<uint64_t>((uint64_t)mail[4], (uint64_t)kBuckets16);
+    const int kspec = sampled ? std::max(local_class(n / sampled), 1) : 0;
+    t = tic(c);
+    if (kspec) HIP_TRY(c, launch_local_sort_e(p, kspec, 0, sampled, c->stream));
     ST_TRY(wait_word(1, p.seq_done, "K12g counters"));
+    tc = us();
+    if (etrace) fprintf(stderr, "est: queued %.1f us, eligibility seen %.1f, counters seen %.1f\n", tq, te, tc);
     if (mail[0] != 0) return GSORT_OK;  // a region overflowed: *ok stays false
     uint64_t h[3 * (kLocalClasses + 1)];
     for (int i = 0; i < 3 * (kLocalClasses + 1); ++i) h[i] = mail[8 + i];
@@ -1028,9 +1049,10 @@ gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
         return set_err(c, GSORT_EINVAL, "sampled plan: K11e lists hold " + std::to_string(keys) +
                                             " keys in " + std::to_string(ent) + " entries, want " +
                                             std::to_string(n) + " keys");
-    t = tic(c);
-    for (int k = 1; k <= kLocalClasses; ++k)
-        HIP_TRY(c, launch_local_sort_e(p, k, (uint32_t)h[3 * k], c->stream));
+    for (int k = 1; k <= kLocalClasses; ++k) {
+        const uint32_t done = k == kspec ? sampled : 0u, cnt = (uint32_t)h[3 * k];
+        if (cnt > done) HIP_TRY(c, launch_local_sort_e(p, k, done, cnt - done, c->stream));
+    }
     toc(c, PH_BUCKET, t);
     *ok = true;
     if (stats) stats->buckets_local += ent;
