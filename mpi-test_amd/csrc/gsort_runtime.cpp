@@ -1070,8 +1070,8 @@ gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
 // with out16 and n > kLocalMax, level 2 stores only the low 16 bits of every key, at out16.
 // With the two-level plan (c->plan16) and group16, gb (65537 u64) receives the 16-bit bucket
 // bounds of the grouped block.
-// allow_est: the caller synchronizes after the sort anyway, so the sampled plan (which waits
-// for its own status word) may run.
+// allow_est: the sampled plan may run (it waits on the host for its mailbox words mid-sort, so
+// callers that must not block -- the distributed sender's grouping -- keep it off).
 gsort_status msd_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *out,
                       uint32_t *tmp, gsort_stats *stats, bool group16 = false,
                       uint16_t *out16 = nullptr, uint64_t *gb = nullptr, bool allow_est = false) {
@@ -1980,7 +1980,8 @@ gsort_status sample_dist(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in, int
     int32_t *sorted = slot_ptr<int32_t>(c, S_SORTED);
     int pr = 0;
     ST_TRY(local_sort(c, reinterpret_cast<const uint32_t *>(d_keys), n_in,
-                      reinterpret_cast<uint32_t *>(sorted), slot_ptr<uint32_t>(c, S_TMP), &pr));
+                      reinterpret_cast<uint32_t *>(sorted), slot_ptr<uint32_t>(c, S_TMP), &pr,
+                      nullptr, true));
 
     // K4 samples -> root (grouped send/recv), K5 on root, broadcast splitters
     hipEvent_t t = tic_rec(c);
