@@ -1467,7 +1467,7 @@ __global__ __launch_bounds__(BLOCK) void k_partition_res(
     if (flags) {
         const uint32_t f = *flags;
         if (f & (L3 ? 5u : 6u)) return;
-        if (EST && !L3 && *ovf) return;  // level 3 overflowed: the exact plan sorts again
+        if (EST && !L3 && ovf && *ovf) return;  // level 3 overflowed: the exact plan sorts again
         if (!L3 && (f & 1u)) { in = raw; flip = kFlip; }
     }
     __shared__ uint32_t s_keys[2][TILE];
@@ -1508,8 +1508,13 @@ __global__ __launch_bounds__(BLOCK) void k_partition_res(
     }
     if (tid < kRadix) { s_cur[0][tid] = 0; s_cur[1][tid] = 0; }
     uint32_t *cursor[2];
+    uint32_t limv[2] = {0, 0};  // EST: the region limits, loaded now (off the reservation path)
 #pragma unroll
-    for (int h = 0; h < 2; ++h) cursor[h] = cur + (L3 ? (pr % kShards) : seg[h]) * kRadix;
+    for (int h = 0; h < 2; ++h) {
+        const uint32_t row = (L3 ? (pr % kShards) : seg[h]) * kRadix;
+        cursor[h] = cur + row;
+        if (EST && tid < kRadix) limv[h] = lim ? lim[row + tid] : ~0u;
+    }
     uint32_t k[2][ITEMS], r[2][ITEMS];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -1579,8 +1584,7 @@ __global__ __launch_bounds__(BLOCK) void k_partition_res(
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             OT *d = out + ((L3 ? bases[tid] : bases[seg[h]]) + pos[h]) - excl[h];
-            if (EST && cnt[h] &&
-                (uint64_t)pos[h] + cnt[h] > lim[(L3 ? (pr % kShards) : seg[h]) * kRadix + tid]) {
+            if (EST && cnt[h] && (uint64_t)pos[h] + cnt[h] > limv[h]) {
                 atomicOr(ovf, 1u);
                 d = dump - excl[h];
             }
