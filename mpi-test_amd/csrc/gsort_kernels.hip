@@ -2219,7 +2219,7 @@ __device__ __forceinline__ uint32_t est_seg_off(uint32_t j) {  // sample offset 
 
 // K1e: thread tid samples key tid % 8 of segment tid / 8; workgroup b takes the 512-key
 // blocks j = b * 128 + seg, + kEstWG * 128, ... (so every child's samples spread over all
-// workgroups), eight loads in flight per thread.  part8[b][.] = the 65536 u8 child counters
+// workgroups), sixteen loads in flight per thread.  part8[b][.] = the 65536 u8 child counters
 // (packed 4 per word), part3[b][x * 256 + d] = samples of level-3 bucket d in shard x (tile
 // pair j / 32, shard pair % 8, as K3r deals them), msamp[b] = samples | wrap << 31.
 // Block 0 also zeroes eflag[0..4] (eflag, ovf, K12g's and K12e's finished-block counts, K12e's
@@ -2243,7 +2243,7 @@ __global__ __launch_bounds__(1024) void k_est_sample(const uint32_t *__restrict_
     constexpr uint32_t SEGS = 1024 / kEstSegKeys;  // segments per workgroup round
     static_assert(kEstBlockKeys / kEstSegKeys == 64, "64 segment offsets per block");
     const uint32_t seg = tid / kEstSegKeys, kk = tid % kEstSegKeys, step = gridDim.x * SEGS;
-    constexpr int U = 8;
+    constexpr int U = 16;
     uint32_t cnt = 0, wrap = 0;
     for (uint32_t j0 = blockIdx.x * SEGS + seg; j0 < nblk; j0 += U * step) {
         uint32_t key[U], jj[U];
@@ -2325,7 +2325,8 @@ __global__ __launch_bounds__(kRadix) void k_est_plan(
     const uint32_t s = blockIdx.x, e = threadIdx.x, g = e >> 6, l = e & 63;
     if (e == 0) { s_m = 0; s_bad = 0; s_ne = 0; }
     __syncthreads();
-    if (e < nwg) {
+    static_assert(kEstWG <= kRadix && kEstWG % (kRadix / 8) == 0, "K12e geometry");
+    if (e < kEstWG) {
         const uint32_t v = msamp[e];
         atomicAdd(&s_m, v & 0x7fffffffu);
         if (v >> 31) s_bad = 1;
@@ -2334,18 +2335,25 @@ __global__ __launch_bounds__(kRadix) void k_est_plan(
     // b = g, g + G, ..; four children per word
     uint32_t c4[4] = {0, 0, 0, 0};
     const uint32_t *pw = part8 + s * (kRadix / 4) + l;
-#pragma unroll 8
-    for (uint32_t b = g; b < nwg; b += G) {
-        const uint32_t v = pw[(uint64_t)b * kEstPartWords];
+    constexpr uint32_t NB = kEstWG / G;  // all of a thread's partial words in flight at once
+    uint32_t pv[NB];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) c4[q] += (v >> (8 * q)) & 255u;
-    }
+    for (uint32_t b = 0; b < NB; ++b) pv[b] = pw[(uint64_t)(g + b * G) * kEstPartWords];
+#pragma unroll
+    for (uint32_t b = 0; b < NB; ++b)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) c4[q] += (pv[b] >> (8 * q)) & 255u;
 #pragma unroll
     for (int q = 0; q < 4; ++q) s_c[g][4 * l + q] = c4[q];
     {  // shard counts of bucket s: thread (b0 = e >> 3, x = e & 7) over partials b0, b0 + 32, ..
         const uint32_t x = e & 7u, b0 = e >> 3;
-        uint32_t c3 = 0;
-        for (uint32_t b = b0; b < nwg; b += kRadix / 8) c3 += part3[(uint64_t)b * kEstPart3 + x * kRadix + s];
+        constexpr uint32_t NB3 = kEstWG / (kRadix / 8);
+        uint32_t pv3[NB3], c3 = 0;
+#pragma unroll
+        for (uint32_t b = 0; b < NB3; ++b)
+            pv3[b] = part3[(uint64_t)(b0 + b * (kRadix / 8)) * kEstPart3 + x * kRadix + s];
+#pragma unroll
+        for (uint32_t b = 0; b < NB3; ++b) c3 += pv3[b];
         s_3[b0][x] = c3;
     }
     __syncthreads();
