@@ -302,9 +302,11 @@ hipError_t launch_est_level3(const EstPlan &p, hipStream_t s);  // K3r
 hipError_t launch_est_level2(const EstPlan &p, hipStream_t s);  // K12f + K3a
 hipError_t launch_est_classify(const EstPlan &p, hipStream_t s);  // K12g
 // K11e over entries [first, first + nlist) of class list cls (those at or past the count K12g
-// made return at once)
+// made return at once); publish: its block 0 first hands K12g's counters and status to the
+// host (mail, seq_done) -- exactly one launch behind K12g must, or launch_est_publish
 hipError_t launch_local_sort_e(const EstPlan &p, int cls, uint32_t first, uint32_t nlist,
-                               hipStream_t s);
+                               bool publish, hipStream_t s);
+hipError_t launch_est_publish(const EstPlan &p, hipStream_t s);
 // Plain device copy kernel (used when a sort has no non-trivial pass).
 hipError_t launch_copy(const uint32_t *in, uint32_t *out, uint64_t n, hipStream_t s);
 

@@ -2497,21 +2497,18 @@ __global__ __launch_bounds__(256) void k_est_tiles(const uint32_t *__restrict__ 
 // sum_x (cur3 - init3) keys, so the child's output offset is the scan of the bucket totals
 // before s plus the scan of its siblings before e.  Non-empty children go to the K11e class
 // lists as {src = bases2[s] + init2, dst | len << 40}.  A child past its limit raises ovf and
-// is not listed (K3a has flagged it already).  The last block to finish publishes the list
-// counters and the status words to the host mailbox (mail[kMailCtr ..], mail[kMailStatus],
-// then seq at kMailSeq): the host sizes the K11e grids from them, with no K12p launch behind.
+// is not listed (K3a has flagged it already).  The list counters and the status words reach
+// the host through publish_lists, run by block 0 of the K11e launch queued behind K12g.
 __global__ __launch_bounds__(kRadix) void k_est_classify(
     const uint32_t *__restrict__ cur2, const uint32_t *__restrict__ init2,
     const uint32_t *__restrict__ lim2, const uint32_t *__restrict__ cur3,
     const uint32_t *__restrict__ init3, const unsigned long long *__restrict__ bases2,
-    WorkLists wl, uint32_t *__restrict__ eflag, unsigned long long *mail,
-    unsigned long long seq) {
+    WorkLists wl, uint32_t *__restrict__ eflag) {
     constexpr int NL = kLocalClasses + 1;
     __shared__ unsigned long long s_w[kRadix / 64];
     __shared__ unsigned long long s_fb;
     __shared__ unsigned int s_n[NL];
     __shared__ unsigned long long s_keys[NL], s_max[NL], s_base[NL];
-    __shared__ uint32_t s_last;
     const uint32_t s = blockIdx.x, e = threadIdx.x;
     unsigned long long *ctr = reinterpret_cast<unsigned long long *>(wl.ctr);
     if (!(*eflag & 4u)) {
@@ -2552,22 +2549,27 @@ __global__ __launch_bounds__(kRadix) void k_est_classify(
             list[2 * j + 1] = dst | ((unsigned long long)len << 40);
         }
     }
+}
+
+// The K12g results for the host: the 15 work-list counters and the status words {eflag, ovf}
+// into the mailbox, then seq (threads 0 .. 15 of one block; K12g has completed).
+__device__ __forceinline__ void publish_lists(unsigned long long *mail,
+                                              const unsigned long long *ctr,
+                                              const uint32_t *eflag, unsigned long long seq) {
+    constexpr uint32_t NC = 3 * (kLocalClasses + 1);
+    const uint32_t e = threadIdx.x;
+    if (e < NC) mail[kMailCtr + e] = ctr[e];
+    if (e == NC) mail[kMailStatus] = *reinterpret_cast<const unsigned long long *>(eflag);
     __syncthreads();
-    if (e == 0) {
-        __threadfence();  // this block's counter atomics before its ticket
-        s_last = atomicAdd(eflag + 2, 1u) == gridDim.x - 1;
-    }
-    __syncthreads();
-    if (s_last) {
-        __threadfence();
-        if (e < 3 * NL)
-            mail[kMailCtr + e] = __hip_atomic_load(ctr + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (e == 3 * NL)
-            mail[kMailStatus] = __hip_atomic_load(reinterpret_cast<unsigned long long *>(eflag),
-                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __syncthreads();
-        if (e == 0) mail_release(mail + kMailSeq, seq);
-    }
+    if (e == 0) mail_release(mail + kMailSeq, seq);
+}
+
+// K12p for the sampled plan when no K11e launch follows K12g directly.
+__global__ __launch_bounds__(64) void k_publish_lists(unsigned long long *mail,
+                                                      const unsigned long long *ctr,
+                                                      const uint32_t *eflag,
+                                                      unsigned long long seq) {
+    publish_lists(mail, ctr, eflag, seq);
 }
 
 // K11e: K11 over a class list of the sampled plan: entry blockIdx.x = {src, dst | len << 40} is
@@ -2576,17 +2578,24 @@ __global__ __launch_bounds__(kRadix) void k_est_classify(
 // the sort took 177 VGPRs, under launch bounds it spilled; both ran at half speed.)
 // Entry first + blockIdx.x, if below the class's entry count ctr[0]: the runtime launches the
 // class it expects to hold most children right behind K12g with a grid of the sampled children
-// (no host round trip in between), and the rest once it has read the counts.
+// (no host round trip in between), and the rest once it has read the counts.  With mail set,
+// block 0 first hands K12g's counters and status to the host (publish_lists), off the kernels'
+// critical path.
 template <int BLOCK, int ITEMS, bool ATOMIC>
 __global__ __launch_bounds__(BLOCK) void k_local_sort_e(const uint32_t *__restrict__ in,
                                                         uint32_t *__restrict__ out,
                                                         const unsigned long long *__restrict__ list,
                                                         const unsigned long long *__restrict__ ctr,
-                                                        uint32_t first, int ndigits) {
+                                                        uint32_t first, int ndigits,
+                                                        unsigned long long *mail,
+                                                        const unsigned long long *ctr_all,
+                                                        const uint32_t *eflag,
+                                                        unsigned long long seq) {
     constexpr int WAVES = BLOCK / 64;
     constexpr int TILE = BLOCK * ITEMS;
     __shared__ uint32_t s_a[TILE];
     __shared__ uint32_t s_wc[WAVES * kRadix];
+    if (mail && blockIdx.x == 0) publish_lists(mail, ctr_all, eflag, seq);  // K12g is done
     const uint32_t i = first + blockIdx.x;
     if (i >= (uint32_t)*ctr) return;
     const uint64_t src = list[2 * i];
@@ -3251,25 +3260,35 @@ hipError_t launch_est_classify(const EstPlan &p, hipStream_t s) {
     using ull = unsigned long long;
     launch_k(k_est_classify, kRadix, kRadix, 0, s, (const uint32_t *)p.cur2,
              (const uint32_t *)p.init2, (const uint32_t *)p.lim2, (const uint32_t *)p.cur3,
-             (const uint32_t *)p.init3, reinterpret_cast<const ull *>(p.bases2), p.wl, p.eflag,
-             reinterpret_cast<ull *>(p.mail), (ull)p.seq_done);
+             (const uint32_t *)p.init3, reinterpret_cast<const ull *>(p.bases2), p.wl, p.eflag);
+    return hipGetLastError();
+}
+
+hipError_t launch_est_publish(const EstPlan &p, hipStream_t s) {
+    using ull = unsigned long long;
+    launch_k(k_publish_lists, 1, 64, 0, s, reinterpret_cast<ull *>(p.mail),
+             reinterpret_cast<const ull *>(p.wl.ctr), (const uint32_t *)p.eflag, (ull)p.seq_done);
     return hipGetLastError();
 }
 
 hipError_t launch_local_sort_e(const EstPlan &p, int cls, uint32_t first, uint32_t nlist,
-                               hipStream_t s) {
+                               bool publish, hipStream_t s) {
     using ull = unsigned long long;
     if (nlist == 0) return hipSuccess;
     if (cls < 1 || cls > kLocalClasses) return hipErrorInvalidValue;
     const ull *l = reinterpret_cast<const ull *>(p.wl.list[cls]);
-    const ull *ctr = reinterpret_cast<const ull *>(p.wl.ctr) + 3 * cls;
-    const uint32_t *y = p.y;
+    const ull *call = reinterpret_cast<const ull *>(p.wl.ctr), *ctr = call + 3 * cls;
+    const uint32_t *y = p.y, *ef = p.eflag;
+    ull *mail = publish ? reinterpret_cast<ull *>(p.mail) : nullptr;
+    const ull seq = (ull)p.seq_done;
 #define GSORT_K11E(B, I)                                                                       \
     do {                                                                                       \
         if (p.atomic_rank)                                                                     \
-            launch_k(k_local_sort_e<B, I, true>, nlist, B, 0, s, y, p.out, l, ctr, first, 2);  \
+            launch_k(k_local_sort_e<B, I, true>, nlist, B, 0, s, y, p.out, l, ctr, first, 2,   \
+                     mail, call, ef, seq);                                                     \
         else                                                                                   \
-            launch_k(k_local_sort_e<B, I, false>, nlist, B, 0, s, y, p.out, l, ctr, first, 2); \
+            launch_k(k_local_sort_e<B, I, false>, nlist, B, 0, s, y, p.out, l, ctr, first, 2,  \
+                     mail, call, ef, seq);                                                     \
     } while (0)
     switch (cls) {
         case 1: GSORT_K11E(256, 18); break;

@@ -1025,7 +1025,7 @@ gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
     t = tic(c);
     HIP_TRY(c, launch_est_level2(p, c->stream));
     toc(c, PH_LEVEL2, t);
-    HIP_TRY(c, launch_est_classify(p, c->stream));  // its last block publishes the counters
+    HIP_TRY(c, launch_est_classify(p, c->stream));
     tq = us();
     ST_TRY(wait_word(3, p.seq_elig, "eligibility word"));
     te = us();
@@ -1036,7 +1036,8 @@ gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
     const uint32_t sampled = (uint32_t)std::min<uint64_t>((uint64_t)mail[4], (uint64_t)kBuckets16);
     const int kspec = sampled ? std::max(local_class(n / sampled), 1) : 0;
     t = tic(c);
-    if (kspec) HIP_TRY(c, launch_local_sort_e(p, kspec, 0, sampled, c->stream));
+    if (kspec) HIP_TRY(c, launch_local_sort_e(p, kspec, 0, sampled, true, c->stream));
+    else HIP_TRY(c, launch_est_publish(p, c->stream));
     ST_TRY(wait_word(1, p.seq_done, "K12g counters"));
     tc = us();
     if (etrace) fprintf(stderr, "est: queued %.1f us, eligibility seen %.1f, counters seen %.1f\n", tq, te, tc);
@@ -1051,7 +1052,7 @@ gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
                                             std::to_string(n) + " keys");
     for (int k = 1; k <= kLocalClasses; ++k) {
         const uint32_t done = k == kspec ? sampled : 0u, cnt = (uint32_t)h[3 * k];
-        if (cnt > done) HIP_TRY(c, launch_local_sort_e(p, k, done, cnt - done, c->stream));
+        if (cnt > done) HIP_TRY(c, launch_local_sort_e(p, k, done, cnt - done, false, c->stream));
     }
     toc(c, PH_BUCKET, t);
     *ok = true;
