@@ -1404,6 +1404,27 @@ __global__ __launch_bounds__(kRadix) void k_plan16_place(
 // (tpfx[s] <= t < tpfx[s+1]), first key and length.  K3a then reaches its keys after one
 // (scalar) load instead of a tpfx load, an LDS binary search and two dependent loads of the
 // bucket bounds -- a chain every one of its ~16K single-pair workgroups exposed.
+// The sampled plan's words in the pinned host mailbox (relative to the `mail` pointer the
+// runtime passes): the status {eflag, ovf} and its sequence after K12g, the same after K12e
+// (eligibility only), the 15 work-list counters after K12g.
+constexpr uint32_t kMailStatus = 0, kMailSeq = 1, kMailElig = 2, kMailEligSeq = 3,
+                   kMailChildren = 4, kMailCtr = 8;
+
+__device__ __forceinline__ void mail_release(unsigned long long *flag, unsigned long long seq) {
+    __threadfence_system();
+    __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// The eligibility word and the count of sampled children for the host (K12e has completed).
+__device__ __forceinline__ void publish_elig(unsigned long long *mail, const uint32_t *eflag,
+                                             unsigned long long seq) {
+    if (threadIdx.x == 0) {
+        mail[kMailElig] = *reinterpret_cast<const unsigned long long *>(eflag);
+        mail[kMailChildren] = eflag[4];
+        mail_release(mail + kMailEligSeq, seq);
+    }
+}
+
 constexpr uint32_t kStraddle = 0x80000000u;  // K12f: a K3a tile across level-3 pieces
 struct TileDesc {
     unsigned long long t0;
@@ -1460,9 +1481,11 @@ __global__ __launch_bounds__(BLOCK) void k_partition_res(
     const unsigned long long *__restrict__ bases, uint32_t *__restrict__ cur,
     const uint32_t *__restrict__ flags, const uint32_t *__restrict__ raw,
     const uint32_t *__restrict__ lim = nullptr, uint32_t *__restrict__ ovf = nullptr,
-    OT *__restrict__ dump = nullptr, const TileDesc *__restrict__ pieces = nullptr) {
+    OT *__restrict__ dump = nullptr, const TileDesc *__restrict__ pieces = nullptr,
+    unsigned long long *mail = nullptr, unsigned long long seq = 0) {
     constexpr int TILE = BLOCK * ITEMS, shift = L3 ? 24 : 16;
     static_assert(TILE == kSweepTile, "reservation tiles are kSweepTile keys");
+    if (EST && L3 && mail && blockIdx.x == 0) publish_elig(mail, flags, seq);  // K12e is done
     uint32_t flip = 0;
     if (flags) {
         const uint32_t f = *flags;
@@ -2276,17 +2299,6 @@ __global__ __launch_bounds__(1024) void k_est_sample(const uint32_t *__restrict_
     if (tid == 0) msamp[blockIdx.x] = s_m;
 }
 
-// The sampled plan's words in the pinned host mailbox (relative to the `mail` pointer the
-// runtime passes): the status {eflag, ovf} and its sequence after K12g, the same after K12e
-// (eligibility only), the 15 work-list counters after K12g.
-constexpr uint32_t kMailStatus = 0, kMailSeq = 1, kMailElig = 2, kMailEligSeq = 3,
-                   kMailChildren = 4, kMailCtr = 8;
-
-__device__ __forceinline__ void mail_release(unsigned long long *flag, unsigned long long seq) {
-    __threadfence_system();
-    __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
 // A region's capacity from its sample count: the estimate + the larger of 6 sigma of the
 // sampling error and two sample blocks (on position-correlated input -- sorted runs -- a
 // region's keys are contiguous and its only error is the two blocks its ends cut) + 64 keys.
@@ -2302,9 +2314,9 @@ __device__ __forceinline__ uint64_t est_cap(uint32_t cnt, double scale, double s
 // in bucket s's Y region) with their limits lim2 and start copies init2; the shard cursors
 // cur3[x*256+s] (offset in bucket s's X region), lim3, init3; r2[s] / r3[s] = bucket s's
 // region sizes.  The last block to finish scans r3 / r2 into the region bases bases3 / bases2,
-// zeroes the nzero work-list counters at zero and publishes the final eligibility word to the
-// host mailbox (mail[kMailElig], the number of children with samples at mail[kMailChildren],
-// then seq at kMailEligSeq).
+// zeroes the nzero work-list counters at zero and sets the last eligibility bit; block 0 of
+// K3r then hands the eligibility word and the number of children with samples to the host
+// (publish_elig).
 // Ineligible (eflag bit 2): a child capacity past kLocalMax (K11 could not take it in one
 // pass), a u8 wrap in K1e, every sample in one level-3 bucket (level 3 would copy; the exact
 // plan skips that level), or X / Y outgrowing their buffers (capx / capy keys).
@@ -2316,8 +2328,7 @@ __global__ __launch_bounds__(kRadix) void k_est_plan(
     unsigned long long *__restrict__ bases3, unsigned long long *__restrict__ bases2,
     uint32_t *__restrict__ cur2, uint32_t *__restrict__ lim2, uint32_t *__restrict__ init2,
     uint32_t *__restrict__ cur3, uint32_t *__restrict__ lim3, uint32_t *__restrict__ init3,
-    unsigned long long *__restrict__ zero, uint32_t nzero, uint32_t *__restrict__ eflag,
-    unsigned long long *mail, unsigned long long seq) {
+    unsigned long long *__restrict__ zero, uint32_t nzero, uint32_t *__restrict__ eflag) {
     constexpr uint32_t G = kRadix / 64;  // thread groups, each over every G-th partial
     __shared__ uint32_t s_m, s_bad, s_last, s_ne;
     __shared__ uint32_t s_c[G][kRadix], s_3[kRadix / kShards][kShards];
@@ -2409,15 +2420,9 @@ __global__ __launch_bounds__(kRadix) void k_est_plan(
     bases3[e] = block_excl_scan(v3, s_w, &tx);
     bases2[e] = block_excl_scan(v2, s_w, &ty);
     if (e < nzero) zero[e] = 0;
-    if (e == 0) {
-        if (tx > capx || ty > capy) atomicOr(eflag, 4u);
-        __threadfence();
-        mail[kMailElig] = __hip_atomic_load(reinterpret_cast<unsigned long long *>(eflag),
-                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        mail[kMailChildren] = __hip_atomic_load(eflag + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        mail_release(mail + kMailEligSeq, seq);
-    }
+    if (e == 0 && (tx > capx || ty > capy)) atomicOr(eflag, 4u);
 }
+
 
 // K12f: K3a's tile descriptors.  Level-3 bucket s is the concatenation of its 8 pieces (shard
 // x: keys [bases3[s] + init3[x*256+s], + their count, clamped to the region: an overflowed
@@ -2881,7 +2886,7 @@ hipError_t launch_partition3r(const uint32_t *in, uint32_t *out, uint64_t n, uin
     launch_k(k_partition_res<B, I, true, true>, (unsigned)pairs, B, 0, s,
         in, out, n, nullptr, nullptr, reinterpret_cast<const ull *>(bases), cur3, flags,
         (const uint32_t *)nullptr, (const uint32_t *)nullptr, (uint32_t *)nullptr,
-        (uint32_t *)nullptr, (const TileDesc *)nullptr);
+        (uint32_t *)nullptr, (const TileDesc *)nullptr, (unsigned long long *)nullptr, 0ull);
     return hipGetLastError();
 }
 
@@ -2902,11 +2907,12 @@ hipError_t launch_partition2r(const uint32_t *in, uint32_t *out, uint16_t *out16
     if (out16)
         launch_k(k_partition_res<B, I, false, false, uint16_t>, g2, B, 0, s, in, out16, n, tpfx,
                  desc, bs, cur, flags, raw, (const uint32_t *)nullptr, (uint32_t *)nullptr,
-                 (uint16_t *)nullptr, (const TileDesc *)nullptr);
+                 (uint16_t *)nullptr, (const TileDesc *)nullptr, (unsigned long long *)nullptr,
+                 0ull);
     else
         launch_k(k_partition_res<B, I, false, false>, g2, B, 0, s, in, out, n, tpfx, desc, bs,
                  cur, flags, raw, (const uint32_t *)nullptr, (uint32_t *)nullptr,
-                 (uint32_t *)nullptr, (const TileDesc *)nullptr);
+                 (uint32_t *)nullptr, (const TileDesc *)nullptr, (unsigned long long *)nullptr, 0ull);
     return hipGetLastError();
 }
 
@@ -3220,8 +3226,7 @@ hipError_t launch_est_front(const EstPlan &p, hipStream_t s) {
              p.capx, p.capy, p.capc, p.cap3, reinterpret_cast<ull *>(p.r2),
              reinterpret_cast<ull *>(p.r3), reinterpret_cast<ull *>(p.bases3),
              reinterpret_cast<ull *>(p.bases2), p.cur2, p.lim2, p.init2, p.cur3, p.lim3, p.init3,
-             reinterpret_cast<ull *>(p.wl.ctr), (uint32_t)(3 * (kLocalClasses + 1)), p.eflag,
-             reinterpret_cast<ull *>(p.mail), (ull)p.seq_elig);
+             reinterpret_cast<ull *>(p.wl.ctr), (uint32_t)(3 * (kLocalClasses + 1)), p.eflag);
     return hipGetLastError();
 }
 
@@ -3234,7 +3239,7 @@ hipError_t launch_est_level3(const EstPlan &p, hipStream_t s) {
              p.in, p.x, p.n, (const uint32_t *)nullptr, (const TileDesc *)nullptr,
              reinterpret_cast<const ull *>(p.bases3), p.cur3, (const uint32_t *)p.eflag,
              (const uint32_t *)nullptr, (const uint32_t *)p.lim3, p.eflag + 1, p.dump,
-             (const TileDesc *)nullptr);
+             (const TileDesc *)nullptr, reinterpret_cast<ull *>(p.mail), (ull)p.seq_elig);
     return hipGetLastError();
 }
 
@@ -3252,7 +3257,7 @@ hipError_t launch_est_level2(const EstPlan &p, hipStream_t s) {
              (const uint32_t *)p.x, p.y, p.n, (const uint32_t *)p.tp, (const TileDesc *)desc,
              reinterpret_cast<const ull *>(p.bases2), p.cur2, (const uint32_t *)p.eflag,
              (const uint32_t *)nullptr, (const uint32_t *)p.lim2, p.eflag + 1, p.dump,
-             (const TileDesc *)pieces);
+             (const TileDesc *)pieces, (ull *)nullptr, (ull)0);
     return hipGetLastError();
 }
 

@@ -1015,10 +1015,10 @@ gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
     };
     double tq = 0, te = 0, tc = 0;
     hipEvent_t t = tic(c);
-    HIP_TRY(c, launch_est_front(p, c->stream));  // K12e-b publishes the eligibility word
+    HIP_TRY(c, launch_est_front(p, c->stream));
     toc(c, PH_COUNT, t);
     t = tic(c);
-    HIP_TRY(c, launch_est_level3(p, c->stream));  // returns at once on an ineligible block
+    HIP_TRY(c, launch_est_level3(p, c->stream));  // block 0 publishes the eligibility word; all return at once on an ineligible block
     toc(c, PH_LEVEL3, t);
     // K12f, K3a and K12g return at once on an ineligible block too, so they are queued before
     // the host looks at the eligibility word (waiting first left a launch gap behind K3r)
