@@ -147,3 +147,15 @@ def test_sampled_plan_repeated_sorts_reuse_scratch(ctx, orc):
         got, _ = _sort(ctx, keys)
         assert ctx.last_plan() == SAMPLED
         assert np.array_equal(got, np.sort(keys)), n
+
+
+@pytest.mark.parametrize("bits,plan", [(27, SAMPLED), (26, SAMPLED), (25, FALLBACK)])
+def test_sampled_plan_child_classes(ctx, bits, plan):
+    """2^24 keys below 2^bits: 16-bit children of 2^(bits-8) keys -- K11e classes 2 and 3
+    (8 192 / 16 384 keys) on the sampled plan; 32 768-key children leave no room for the
+    sampling margin under kLocalMax, so the block goes to the exact plan."""
+    rng = np.random.default_rng(bits)
+    keys = rng.integers(0, 1 << bits, 1 << 24, dtype=np.int64).astype(np.int32)
+    got, _ = _sort(ctx, keys)
+    assert ctx.last_plan() == plan
+    assert np.array_equal(got, np.sort(keys))
