@@ -445,8 +445,9 @@ def main():
         "phases_ms_avg": phases,
         "passes_run": last["passes_run"],
         "local_algo": "lsd" if last["local_algo"] == gsort.LOCAL_LSD else "msd",
-        "local_plan": {0: "exact two-level", 1: "sampled", 2: "sampled, re-sorted exact"}.get(
-            plan, str(plan)),
+        "local_plan": ("lsd passes" if a.local == "lsd" else
+                       {0: "exact two-level", 1: "sampled", 2: "sampled, re-sorted exact"}.get(
+                           plan, str(plan))),
         "verified": bool(ok),
     }
     if last["exchanges"]:
