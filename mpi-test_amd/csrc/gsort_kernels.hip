@@ -1572,12 +1572,27 @@ __global__ __launch_bounds__(BLOCK) void k_partition_res(
                 r[h][i] = agg_rank(s_cur[h], (k[h][i] >> shift) & 255u, s_spare);
     __syncthreads();
     uint32_t excl[2] = {0, 0}, pos[2] = {0, 0}, cnt[2] = {0, 0};
+    // both tiles on one cursor row (always for K3r: one shard; for K3a when both tiles are in
+    // one bucket): ONE reservation of both counts, tile 1's run right behind tile 0's, so the
+    // pair writes one run of twice the length -- half the run boundaries, whose lines are
+    // otherwise written partly by two workgroups (often on two XCDs)
+    const bool merge = 2 * pr + 1 < ntile && cursor[0] == cursor[1];
     if (tid < kRadix) {
+        cnt[0] = s_cur[0][tid];
+        cnt[1] = s_cur[1][tid];
+        if (merge) {
+            if (cnt[0] + cnt[1]) {
+                pos[0] = atomicAdd(&cursor[0][tid], cnt[0] + cnt[1]);
+                pos[1] = pos[0] + cnt[0];
+            }
+        } else {
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+                if (cnt[h]) pos[h] = atomicAdd(&cursor[h][tid], cnt[h]);
+        }
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            const uint32_t c = s_cur[h][tid];
-            cnt[h] = c;
-            if (c) pos[h] = atomicAdd(&cursor[h][tid], c);
+            const uint32_t c = cnt[h];
             uint32_t v = c;
 #pragma unroll
             for (int o = 1; o < 64; o <<= 1) {
