@@ -946,8 +946,18 @@ gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
     const uint64_t capx = est_region_keys(n, (uint64_t)kH16Shards * kRadix, slack);
     const uint64_t capy = std::min<uint64_t>(est_region_keys(n, kBuckets16, slack),
                                              (uint64_t)kBuckets16 * kLocalMax);
-    ST_TRY(ensure(c, c->m_ex, capx * 4));
-    ST_TRY(ensure(c, c->m_ey, capy * 4));
+    // the region buffers are the plan's only large allocations: without room for them the
+    // exact plan sorts (it needs none), and the memory is handed back
+    for (DevBuf *b : {&c->m_ex, &c->m_ey}) {
+        const gsort_status st = ensure(c, *b, (b == &c->m_ex ? capx : capy) * 4);
+        if (st == GSORT_ENOMEM) {
+            (void)dev_free(c->m_ex);
+            (void)dev_free(c->m_ey);
+            c->err.clear();
+            return GSORT_OK;  // *ok stays false
+        }
+        ST_TRY(st);
+    }
     ST_TRY(ensure(c, c->m_epart, (size_t)kEstWGs * (kBuckets16 / 4 + kH16Shards * kRadix + 1) * 4));
     constexpr size_t kPlanWords = (size_t)4 * kBuckets16 + 4 * kH16Shards * kRadix + kRadix + 1;
     ST_TRY(ensure(c, c->m_eplan, kPlanWords * 4 + 4 * kRadix * 8 + 64));

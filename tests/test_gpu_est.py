@@ -8,6 +8,8 @@ must then come back sorted through the exact plan; GSORT_EST_SLACK=0 (no samplin
 margin) forces region overflows, which must be caught and re-sorted.
 """
 import os
+import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -159,3 +161,28 @@ def test_sampled_plan_child_classes(ctx, bits, plan):
     got, _ = _sort(ctx, keys)
     assert ctx.last_plan() == plan
     assert np.array_equal(got, np.sort(keys))
+
+
+def test_sampled_plan_without_room_falls_back():
+    """GSORT_ALLOC_LIMIT below the region buffers' size (but above the block's): the sampled
+    plan cannot allocate Y, hands its memory back, and the exact plan sorts (one child
+    process: the limit is read once per process)."""
+    n = 1 << 23
+    code = f"""
+import sys, numpy as np
+sys.path[:0] = {[os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                 os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                              "mpi-test_amd")]!r}
+import torch, gsort
+keys = np.random.default_rng(3).integers(-2**31, 2**31, {n}, dtype=np.int64).astype(np.int32)
+with gsort.Context() as c:
+    p = c.alloc(keys.size * 4); c.to_device(keys, p)
+    out, m, _ = c.radix(p, keys.size)
+    assert c.last_plan() == 2, c.last_plan()
+    assert np.array_equal(c.to_host(out, m), np.sort(keys))
+print("ok")
+"""
+    env = dict(os.environ, GSORT_EST="1", GSORT_ALLOC_LIMIT=str(n * 4 * 3 // 2))
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
