@@ -446,7 +446,8 @@ def main():
         "passes_run": last["passes_run"],
         "local_algo": "lsd" if last["local_algo"] == gsort.LOCAL_LSD else "msd",
         "local_plan": ("lsd passes" if a.local == "lsd" else
-                       {0: "exact two-level", 1: "sampled", 2: "sampled, re-sorted exact"}.get(
+                       {0: "exact two-level", 1: "sampled", 2: "sampled, re-sorted exact",
+                        3: "sampled below a constant key prefix"}.get(
                            plan, str(plan))),
         "verified": bool(ok),
     }

@@ -141,7 +141,9 @@ gsort_status gsort_sample_info(const gsort_ctx *ctx, int32_t *splitters,
 /* Which plan the last one-rank local sort of ctx took (diagnostics; no reference
  * counterpart): 0 the exact two-level plan (or a small / distributed case), 1 the sampled
  * plan, 2 the sampled plan found the block ineligible or a region overflowed, and the block
- * was sorted again on the exact plan (GSORT_EST=0 turns the sampled plan off). */
+ * was sorted again on the exact plan, 3 the sampled plan on digits below a key prefix every key
+ * shares (e.g. 16- or 24-bit keys in int32) after a first sampled attempt found the block
+ * ineligible (GSORT_EST=0 turns the sampled plan off). */
 int gsort_last_plan(const gsort_ctx *ctx);
 
 /* ---- drop-in staging (replaces MPI_Scatter / MPI_Gather(v) through rank 0) ---------------

@@ -1408,7 +1408,7 @@ __global__ __launch_bounds__(kRadix) void k_plan16_place(
 // runtime passes): the status {eflag, ovf} and its sequence after K12g, the same after K12e
 // (eligibility only), the 15 work-list counters after K12g.
 constexpr uint32_t kMailStatus = 0, kMailSeq = 1, kMailElig = 2, kMailEligSeq = 3,
-                   kMailChildren = 4, kMailCtr = 8;
+                   kMailChildren = 4, kMailVary = 5, kMailCtr = 8;
 
 __device__ __forceinline__ void mail_release(unsigned long long *flag, unsigned long long seq) {
     __threadfence_system();
@@ -1421,6 +1421,7 @@ __device__ __forceinline__ void publish_elig(unsigned long long *mail, const uin
     if (threadIdx.x == 0) {
         mail[kMailElig] = *reinterpret_cast<const unsigned long long *>(eflag);
         mail[kMailChildren] = eflag[4];
+        mail[kMailVary] = eflag[5];
         mail_release(mail + kMailEligSeq, seq);
     }
 }
@@ -1482,8 +1483,9 @@ __global__ __launch_bounds__(BLOCK) void k_partition_res(
     const uint32_t *__restrict__ flags, const uint32_t *__restrict__ raw,
     const uint32_t *__restrict__ lim = nullptr, uint32_t *__restrict__ ovf = nullptr,
     OT *__restrict__ dump = nullptr, const TileDesc *__restrict__ pieces = nullptr,
-    unsigned long long *mail = nullptr, unsigned long long seq = 0) {
-    constexpr int TILE = BLOCK * ITEMS, shift = L3 ? 24 : 16;
+    unsigned long long *mail = nullptr, unsigned long long seq = 0, int sb = 0) {
+    constexpr int TILE = BLOCK * ITEMS;
+    const int shift = (L3 ? 24 : 16) - (EST ? sb : 0);  // EST: digits sb bits lower
     static_assert(TILE == kSweepTile, "reservation tiles are kSweepTile keys");
     if (EST && L3 && mail && blockIdx.x == 0) publish_elig(mail, flags, seq);  // K12e is done
     uint32_t flip = 0;
@@ -1562,6 +1564,16 @@ __global__ __launch_bounds__(BLOCK) void k_partition_res(
 #pragma unroll
             for (int i = 0; i < ITEMS; ++i) k[h][i] ^= flip;
         }
+    }
+    if (EST && L3 && sb) {  // the prefix the sampled digits skip must hold for every key
+        const uint32_t pfx = (in[0] ^ kFlip) >> (32 - sb);
+        bool bad = false;
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int i = 0; i < ITEMS; ++i)
+                bad |= (uint32_t)(i * BLOCK) + tid < len[h] && (k[h][i] >> (32 - sb)) != pfx;
+        if (__ballot(bad) && (tid & 63) == 0) atomicOr(ovf, 1u);
     }
     __syncthreads();  // s_cur zeroed
 #pragma unroll
@@ -2259,30 +2271,34 @@ __device__ __forceinline__ uint32_t est_seg_off(uint32_t j) {  // sample offset 
 // blocks j = b * 128 + seg, + kEstWG * 128, ... (so every child's samples spread over all
 // workgroups), sixteen loads in flight per thread.  part8[b][.] = the 65536 u8 child counters
 // (packed 4 per word), part3[b][x * 256 + d] = samples of level-3 bucket d in shard x (tile
-// pair j / 32, shard pair % 8, as K3r deals them), msamp[b] = samples | wrap << 31.
-// Block 0 also zeroes eflag[0..4] (eflag, ovf, K12g's and K12e's finished-block counts, K12e's
-// count of sampled children).
+// pair j / 32, shard pair % 8, as K3r deals them), msamp[b] = samples | wrap << 31,
+// msamp[kEstWG + b] = the key bits that differ from in[0] among its samples.  sb (0, 8, 16):
+// the plan's digits start sb bits lower (the top sb bits are one constant prefix: the runtime
+// retries a block whose samples share leading bytes that way; K3r verifies the prefix).
+// Block 0 also zeroes eflag[0..5] (eflag, ovf, K12g's and K12e's finished-block counts, K12e's
+// count of sampled children, the samples' varying bits).
 template <bool FIN>
 __global__ __launch_bounds__(1024) void k_est_sample(const uint32_t *__restrict__ in, uint64_t n,
                                                      uint32_t *__restrict__ part8,
                                                      uint32_t *__restrict__ part3,
                                                      uint32_t *__restrict__ msamp,
-                                                     uint32_t *__restrict__ eflag) {
+                                                     uint32_t *__restrict__ eflag, int sb) {
     __shared__ uint32_t s_h[kEstPartWords];
     __shared__ uint32_t s_3[kEstPart3];
-    __shared__ uint32_t s_m;
+    __shared__ uint32_t s_m, s_vary;
     const uint32_t tid = threadIdx.x;
     for (uint32_t i = tid; i < kEstPartWords; i += 1024) s_h[i] = 0;
     for (uint32_t i = tid; i < kEstPart3; i += 1024) s_3[i] = 0;
-    if (tid == 0) s_m = 0;
-    if (blockIdx.x == 0 && tid < 5) eflag[tid] = 0;
+    if (tid == 0) { s_m = 0; s_vary = 0; }
+    if (blockIdx.x == 0 && tid < 6) eflag[tid] = 0;
+    const uint32_t ref = FIN ? in[0] ^ kFlip : in[0];  // bits that vary across the samples
     __syncthreads();
     const uint32_t nblk = (uint32_t)((n + kEstBlockKeys - 1) / kEstBlockKeys);
     constexpr uint32_t SEGS = 1024 / kEstSegKeys;  // segments per workgroup round
     static_assert(kEstBlockKeys / kEstSegKeys == 64, "64 segment offsets per block");
     const uint32_t seg = tid / kEstSegKeys, kk = tid % kEstSegKeys, step = gridDim.x * SEGS;
     constexpr int U = 16;
-    uint32_t cnt = 0, wrap = 0;
+    uint32_t cnt = 0, wrap = 0, vary = 0;
     for (uint32_t j0 = blockIdx.x * SEGS + seg; j0 < nblk; j0 += U * step) {
         uint32_t key[U], jj[U];
         bool ok[U];
@@ -2297,21 +2313,23 @@ __global__ __launch_bounds__(1024) void k_est_sample(const uint32_t *__restrict_
         for (int u = 0; u < U; ++u) {
             if (!ok[u]) continue;
             const uint32_t k = FIN ? key[u] ^ kFlip : key[u];
-            const uint32_t b = k >> 16, sh = (b & 3u) << 3;
+            vary |= k ^ ref;
+            const uint32_t b = (k >> (16 - sb)) & 0xffffu, sh = (b & 3u) << 3;
             const uint32_t old = atomicAdd(&s_h[b >> 2], 1u << sh);
             wrap |= ((old >> sh) & 255u) == 255u;
             constexpr uint32_t kPairBlocks = 2 * kSweepTile / kEstBlockKeys;
-            atomicAdd(&s_3[((jj[u] / kPairBlocks) % kShards) * kRadix + (k >> 24)], 1u);
+            atomicAdd(&s_3[((jj[u] / kPairBlocks) % kShards) * kRadix + ((k >> (24 - sb)) & 255u)], 1u);
             ++cnt;
         }
     }
     atomicAdd(&s_m, cnt | (wrap << 31));
+    if (vary) atomicOr(&s_vary, vary);
     __syncthreads();
     uint32_t *dst = part8 + (uint64_t)blockIdx.x * kEstPartWords;
     for (uint32_t i = tid; i < kEstPartWords; i += 1024) dst[i] = s_h[i];
     uint32_t *d3 = part3 + (uint64_t)blockIdx.x * kEstPart3;
     for (uint32_t i = tid; i < kEstPart3; i += 1024) d3[i] = s_3[i];
-    if (tid == 0) msamp[blockIdx.x] = s_m;
+    if (tid == 0) { msamp[blockIdx.x] = s_m; msamp[kEstWG + blockIdx.x] = s_vary; }
 }
 
 // A region's capacity from its sample count: the estimate + the larger of 6 sigma of the
@@ -2356,6 +2374,7 @@ __global__ __launch_bounds__(kRadix) void k_est_plan(
         const uint32_t v = msamp[e];
         atomicAdd(&s_m, v & 0x7fffffffu);
         if (v >> 31) s_bad = 1;
+        if (s == 0 && msamp[kEstWG + e]) atomicOr(eflag + 5, msamp[kEstWG + e]);
     }
     // bucket s's 64 packed words of every partial: lane l reads word l of the partials
     // b = g, g + G, ..; four children per word
@@ -2601,7 +2620,7 @@ __global__ __launch_bounds__(64) void k_publish_lists(unsigned long long *mail,
 // (no host round trip in between), and the rest once it has read the counts.  With mail set,
 // block 0 first hands K12g's counters and status to the host (publish_lists), off the kernels'
 // critical path.
-template <int BLOCK, int ITEMS, bool ATOMIC>
+template <int BLOCK, int ITEMS, bool ATOMIC, bool COPY = false>
 __global__ __launch_bounds__(BLOCK) void k_local_sort_e(const uint32_t *__restrict__ in,
                                                         uint32_t *__restrict__ out,
                                                         const unsigned long long *__restrict__ list,
@@ -2624,8 +2643,16 @@ __global__ __launch_bounds__(BLOCK) void k_local_sort_e(const uint32_t *__restri
     if (threadIdx.x < kRadix) s_wc[threadIdx.x] = 0;
     uint32_t k[ITEMS];
     load_bucket<BLOCK, ITEMS, false>(in + src, len, k);
+    uint32_t *dst = out + (e & ((1ull << 40) - 1));
+    if (COPY) {  // every key of the child is one value (digits below a constant prefix)
+        const __amdgpu_buffer_rsrc_t rs = bucket_rsrc(dst, len * 4u);
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j)
+            __builtin_amdgcn_raw_buffer_store_b32(k[j] ^ kFlip, rs, (j * BLOCK + (int)threadIdx.x) * 4, 0, 0);
+        return;
+    }
     __syncthreads();
-    sort_bucket<BLOCK, ITEMS, ATOMIC>(k, len, ndigits, out + (e & ((1ull << 40) - 1)), s_a, s_wc);
+    sort_bucket<BLOCK, ITEMS, ATOMIC>(k, len, ndigits, dst, s_a, s_wc);
 }
 
 constexpr int cls_of(int block, int items) {
@@ -2901,7 +2928,7 @@ hipError_t launch_partition3r(const uint32_t *in, uint32_t *out, uint64_t n, uin
     launch_k(k_partition_res<B, I, true, true>, (unsigned)pairs, B, 0, s,
         in, out, n, nullptr, nullptr, reinterpret_cast<const ull *>(bases), cur3, flags,
         (const uint32_t *)nullptr, (const uint32_t *)nullptr, (uint32_t *)nullptr,
-        (uint32_t *)nullptr, (const TileDesc *)nullptr, (unsigned long long *)nullptr, 0ull);
+        (uint32_t *)nullptr, (const TileDesc *)nullptr, (unsigned long long *)nullptr, 0ull, 0);
     return hipGetLastError();
 }
 
@@ -2923,11 +2950,11 @@ hipError_t launch_partition2r(const uint32_t *in, uint32_t *out, uint16_t *out16
         launch_k(k_partition_res<B, I, false, false, uint16_t>, g2, B, 0, s, in, out16, n, tpfx,
                  desc, bs, cur, flags, raw, (const uint32_t *)nullptr, (uint32_t *)nullptr,
                  (uint16_t *)nullptr, (const TileDesc *)nullptr, (unsigned long long *)nullptr,
-                 0ull);
+                 0ull, 0);
     else
         launch_k(k_partition_res<B, I, false, false>, g2, B, 0, s, in, out, n, tpfx, desc, bs,
                  cur, flags, raw, (const uint32_t *)nullptr, (uint32_t *)nullptr,
-                 (uint32_t *)nullptr, (const TileDesc *)nullptr, (unsigned long long *)nullptr, 0ull);
+                 (uint32_t *)nullptr, (const TileDesc *)nullptr, (unsigned long long *)nullptr, 0ull, 0);
     return hipGetLastError();
 }
 
@@ -3235,8 +3262,9 @@ hipError_t launch_publish(const uint64_t *src, uint32_t n, uint64_t *dst, uint64
 hipError_t launch_est_front(const EstPlan &p, hipStream_t s) {
     using ull = unsigned long long;
     if (p.n == 0 || p.n > kEstMaxKeys) return hipErrorInvalidValue;
-    if (p.flip_in) launch_k(k_est_sample<true>, kEstWG, 1024, 0, s, p.in, p.n, p.part8, p.part3, p.msamp, p.eflag);
-    else launch_k(k_est_sample<false>, kEstWG, 1024, 0, s, p.in, p.n, p.part8, p.part3, p.msamp, p.eflag);
+    if (p.sb != 0 && p.sb != 8 && p.sb != 16) return hipErrorInvalidValue;
+    if (p.flip_in) launch_k(k_est_sample<true>, kEstWG, 1024, 0, s, p.in, p.n, p.part8, p.part3, p.msamp, p.eflag, p.sb);
+    else launch_k(k_est_sample<false>, kEstWG, 1024, 0, s, p.in, p.n, p.part8, p.part3, p.msamp, p.eflag, p.sb);
     launch_k(k_est_plan, kRadix, kRadix, 0, s, p.part8, p.part3, p.msamp, kEstWG, p.n, p.slack,
              p.capx, p.capy, p.capc, p.cap3, reinterpret_cast<ull *>(p.r2),
              reinterpret_cast<ull *>(p.r3), reinterpret_cast<ull *>(p.bases3),
@@ -3254,7 +3282,7 @@ hipError_t launch_est_level3(const EstPlan &p, hipStream_t s) {
              p.in, p.x, p.n, (const uint32_t *)nullptr, (const TileDesc *)nullptr,
              reinterpret_cast<const ull *>(p.bases3), p.cur3, (const uint32_t *)p.eflag,
              (const uint32_t *)nullptr, (const uint32_t *)p.lim3, p.eflag + 1, p.dump,
-             (const TileDesc *)nullptr, reinterpret_cast<ull *>(p.mail), (ull)p.seq_elig);
+             (const TileDesc *)nullptr, reinterpret_cast<ull *>(p.mail), (ull)p.seq_elig, p.sb);
     return hipGetLastError();
 }
 
@@ -3272,7 +3300,7 @@ hipError_t launch_est_level2(const EstPlan &p, hipStream_t s) {
              (const uint32_t *)p.x, p.y, p.n, (const uint32_t *)p.tp, (const TileDesc *)desc,
              reinterpret_cast<const ull *>(p.bases2), p.cur2, (const uint32_t *)p.eflag,
              (const uint32_t *)nullptr, (const uint32_t *)p.lim2, p.eflag + 1, p.dump,
-             (const TileDesc *)pieces, (ull *)nullptr, (ull)0);
+             (const TileDesc *)pieces, (ull *)nullptr, (ull)0, p.sb);
     return hipGetLastError();
 }
 
@@ -3299,15 +3327,20 @@ hipError_t launch_local_sort_e(const EstPlan &p, int cls, uint32_t first, uint32
     const ull *l = reinterpret_cast<const ull *>(p.wl.list[cls]);
     const ull *call = reinterpret_cast<const ull *>(p.wl.ctr), *ctr = call + 3 * cls;
     const uint32_t *y = p.y, *ef = p.eflag;
+    const int nd = 2 - p.sb / 8;  // digits below the plan's two levels (sb = 16: a child is
+                                  // one value, K11e copies it)
     ull *mail = publish ? reinterpret_cast<ull *>(p.mail) : nullptr;
     const ull seq = (ull)p.seq_done;
 #define GSORT_K11E(B, I)                                                                       \
     do {                                                                                       \
-        if (p.atomic_rank)                                                                     \
-            launch_k(k_local_sort_e<B, I, true>, nlist, B, 0, s, y, p.out, l, ctr, first, 2,   \
+        if (nd == 0)                                                                           \
+            launch_k(k_local_sort_e<B, I, true, true>, nlist, B, 0, s, y, p.out, l, ctr, first, \
+                     nd, mail, call, ef, seq);                                                 \
+        else if (p.atomic_rank)                                                                \
+            launch_k(k_local_sort_e<B, I, true>, nlist, B, 0, s, y, p.out, l, ctr, first, nd,  \
                      mail, call, ef, seq);                                                     \
         else                                                                                   \
-            launch_k(k_local_sort_e<B, I, false>, nlist, B, 0, s, y, p.out, l, ctr, first, 2,  \
+            launch_k(k_local_sort_e<B, I, false>, nlist, B, 0, s, y, p.out, l, ctr, first, nd, \
                      mail, call, ef, seq);                                                     \
     } while (0)
     switch (cls) {

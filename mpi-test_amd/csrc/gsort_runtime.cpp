@@ -940,8 +940,9 @@ uint64_t est_region_keys(uint64_t n, uint64_t nreg, double slack) {
 }
 
 gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *out,
-                          gsort_stats *stats, bool *ok) {
+                          gsort_stats *stats, bool *ok, int sb = 0, int *retry_sb = nullptr) {
     *ok = false;
+    if (retry_sb) *retry_sb = 0;
     const double slack = std::max(c->est_slack, 0.0);
     const uint64_t capx = est_region_keys(n, (uint64_t)kH16Shards * kRadix, slack);
     const uint64_t capy = std::min<uint64_t>(est_region_keys(n, kBuckets16, slack),
@@ -958,7 +959,7 @@ gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
         }
         ST_TRY(st);
     }
-    ST_TRY(ensure(c, c->m_epart, (size_t)kEstWGs * (kBuckets16 / 4 + kH16Shards * kRadix + 1) * 4));
+    ST_TRY(ensure(c, c->m_epart, (size_t)kEstWGs * (kBuckets16 / 4 + kH16Shards * kRadix + 2) * 4));
     constexpr size_t kPlanWords = (size_t)4 * kBuckets16 + 4 * kH16Shards * kRadix + kRadix + 1;
     ST_TRY(ensure(c, c->m_eplan, kPlanWords * 4 + 4 * kRadix * 8 + 64));
     ST_TRY(ensure(c, c->m_edesc, ((size_t)est_max_tiles(n) + kH16Shards * kRadix) * kTileDescBytes));
@@ -998,6 +999,7 @@ gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
     p.wl = work_lists(c, 0);
     p.slack = slack;
     p.atomic_rank = c->atomic_rank;
+    p.sb = sb;
     p.mail = c->d_mail + kEstMailWord;
     p.seq_elig = ++c->mail_seq;
     p.seq_done = ++c->mail_seq;
@@ -1039,7 +1041,20 @@ gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
     tq = us();
     ST_TRY(wait_word(3, p.seq_elig, "eligibility word"));
     te = us();
-    if (mail[2] & 4u) return GSORT_OK;  // ineligible: the exact plan sorts
+    if (mail[2] & 4u) {  // ineligible: the exact plan sorts -- unless the samples share leading
+        // key bytes whose removal leaves children K11e can take (16- / 24-bit keys in int32):
+        // then the caller retries with the digits that many bits lower
+        const uint32_t vary = (uint32_t)mail[5];
+        const int lead = vary ? __builtin_clz(vary) : 32;
+        const int nsb = sb == 0 ? (lead >= 16 ? 16 : lead >= 8 ? 8 : 0) : 0;
+        if (retry_sb && nsb && lead < 32) {
+            // distinct children once the digits start nsb bits lower, and their average size
+            const int fixed = std::max(0, std::min(lead - nsb, 16));
+            const uint64_t children = 1ull << (16 - fixed);
+            if (n / children <= kLocalMax / 2) *retry_sb = nsb;
+        }
+        return GSORT_OK;
+    }
     // K11e of the class the average child falls in, queued right behind K12g (a grid of the
     // sampled children: at least its entries, usually exactly), so no host round trip sits
     // between K12g and the largest K11e launch; the other classes follow once the counts are in
@@ -1091,8 +1106,10 @@ gsort_status msd_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *ou
     if (allow_est && c->plan_est && c->plan16 && !group16 && n >= kEstMinKeys &&
         n <= kEstMaxKeys) {
         bool ok = false;
-        ST_TRY(msd_sort_est(c, in, n, out, stats, &ok));
-        c->last_plan = ok ? 1 : 2;
+        int retry_sb = 0;
+        ST_TRY(msd_sort_est(c, in, n, out, stats, &ok, 0, &retry_sb));
+        if (!ok && retry_sb) ST_TRY(msd_sort_est(c, in, n, out, stats, &ok, retry_sb));
+        c->last_plan = ok ? (retry_sb ? 3 : 1) : 2;
         if (ok) return GSORT_OK;
     }
     uint64_t *ctr = reinterpret_cast<uint64_t *>(c->d_small + OFF_CTR);

@@ -239,11 +239,12 @@ class Context:
         self._c(lib().gsort_sample_info(self.h, spl.ctypes.data, cnt.ctypes.data))
         return spl[: self.nranks - 1], cnt
 
-    PLAN_EXACT, PLAN_SAMPLED, PLAN_SAMPLED_THEN_EXACT = 0, 1, 2
+    PLAN_EXACT, PLAN_SAMPLED, PLAN_SAMPLED_THEN_EXACT, PLAN_SAMPLED_SHIFTED = 0, 1, 2, 3
 
     def last_plan(self):
         """Plan of the last one-rank local sort (gsort_last_plan): 0 exact, 1 sampled,
-        2 sampled then re-sorted on the exact plan (ineligible block or a region overflow)."""
+        2 sampled then re-sorted on the exact plan (ineligible block or a region overflow),
+        3 sampled on the digits below a constant key prefix."""
         return lib().gsort_last_plan(self.h)
 
     def generate(self, dist, seed, start, n, d_out):

@@ -16,7 +16,7 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-SAMPLED, FALLBACK = 1, 2
+SAMPLED, FALLBACK, SHIFTED = 1, 2, 3
 
 
 def _ctx(gsort, **env):
@@ -108,11 +108,13 @@ def test_sampled_plan_distributions(ctx, orc, name):
     keys = _inputs(orc, n)[name]
     got, _ = _sort(ctx, keys)
     plan = ctx.last_plan()
-    assert plan in (SAMPLED, FALLBACK), plan
+    assert plan in (SAMPLED, FALLBACK, SHIFTED), plan
     if name in ("sorted", "reversed", "sorted_blocks"):  # uniform keys, position-correlated
         assert plan == SAMPLED, name
-    if name in ("all_equal", "bits16", "zipf", "half_one_value"):  # a child > kLocalMax
+    if name in ("all_equal", "zipf", "half_one_value"):  # a child > kLocalMax
         assert plan == FALLBACK, name
+    if name in ("bits16", "bits24"):  # one constant key prefix: the digits below it
+        assert plan == SHIFTED, name
     assert np.array_equal(got, np.sort(keys)), name
 
 
@@ -186,3 +188,28 @@ print("ok")
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
                        timeout=240)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("case", ["prefix_broken_late", "prefix_broken_first", "negative_16bit"])
+def test_sampled_plan_shifted_prefix_check(ctx, case):
+    """The shifted retry trusts the samples' common prefix only after K3r has checked it on every
+    key: a block of 16-bit keys with a few keys outside the prefix (at unsampled positions or at
+    position 0, the reference key) must still come back sorted (exact plan), and negative 16-bit
+    keys (prefix 0x7fff after the sign flip) take the shifted plan."""
+    rng = np.random.default_rng(17)
+    n = 1 << 23
+    keys = rng.integers(0, 1 << 16, n, dtype=np.int64).astype(np.int32)
+    if case == "prefix_broken_late":
+        keys[[n - 1, n // 2 + 3, 12345]] = [1 << 30, -5, 70000]
+    elif case == "prefix_broken_first":
+        keys[0] = 1 << 20
+    else:
+        keys = (keys - (1 << 16)).astype(np.int32)
+    got, _ = _sort(ctx, keys)
+    plan = ctx.last_plan()
+    if case == "negative_16bit":
+        assert plan == SHIFTED
+    else:
+        assert plan in (FALLBACK, SHIFTED, SAMPLED)
+        assert plan != SHIFTED or case != "prefix_broken_late"
+    assert np.array_equal(got, np.sort(keys)), case
