@@ -2272,9 +2272,9 @@ __device__ __forceinline__ uint32_t est_seg_off(uint32_t j) {  // sample offset 
 // workgroups), sixteen loads in flight per thread.  part8[b][.] = the 65536 u8 child counters
 // (packed 4 per word), part3[b][x * 256 + d] = samples of level-3 bucket d in shard x (tile
 // pair j / 32, shard pair % 8, as K3r deals them), msamp[b] = samples | wrap << 31,
-// msamp[kEstWG + b] = the key bits that differ from in[0] among its samples.  sb (0, 8, 16):
+// msamp[kEstWG + b] = the key bits that differ from in[0] among its samples.  sb (0 .. 16):
 // the plan's digits start sb bits lower (the top sb bits are one constant prefix: the runtime
-// retries a block whose samples share leading bytes that way; K3r verifies the prefix).
+// retries a block whose samples share leading bits that way; K3r verifies the prefix).
 // Block 0 also zeroes eflag[0..5] (eflag, ovf, K12g's and K12e's finished-block counts, K12e's
 // count of sampled children, the samples' varying bits).
 template <bool FIN>
@@ -3262,7 +3262,7 @@ hipError_t launch_publish(const uint64_t *src, uint32_t n, uint64_t *dst, uint64
 hipError_t launch_est_front(const EstPlan &p, hipStream_t s) {
     using ull = unsigned long long;
     if (p.n == 0 || p.n > kEstMaxKeys) return hipErrorInvalidValue;
-    if (p.sb != 0 && p.sb != 8 && p.sb != 16) return hipErrorInvalidValue;
+    if (p.sb < 0 || p.sb > 16) return hipErrorInvalidValue;
     if (p.flip_in) launch_k(k_est_sample<true>, kEstWG, 1024, 0, s, p.in, p.n, p.part8, p.part3, p.msamp, p.eflag, p.sb);
     else launch_k(k_est_sample<false>, kEstWG, 1024, 0, s, p.in, p.n, p.part8, p.part3, p.msamp, p.eflag, p.sb);
     launch_k(k_est_plan, kRadix, kRadix, 0, s, p.part8, p.part3, p.msamp, kEstWG, p.n, p.slack,
@@ -3327,8 +3327,8 @@ hipError_t launch_local_sort_e(const EstPlan &p, int cls, uint32_t first, uint32
     const ull *l = reinterpret_cast<const ull *>(p.wl.list[cls]);
     const ull *call = reinterpret_cast<const ull *>(p.wl.ctr), *ctr = call + 3 * cls;
     const uint32_t *y = p.y, *ef = p.eflag;
-    const int nd = 2 - p.sb / 8;  // digits below the plan's two levels (sb = 16: a child is
-                                  // one value, K11e copies it)
+    const int nd = (16 - p.sb + 7) / 8;  // digits for the bits below the plan's two levels
+                                         // (sb = 16: a child is one value, K11e copies it)
     ull *mail = publish ? reinterpret_cast<ull *>(p.mail) : nullptr;
     const ull seq = (ull)p.seq_done;
 #define GSORT_K11E(B, I)                                                                       \

@@ -1042,12 +1042,15 @@ gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
     ST_TRY(wait_word(3, p.seq_elig, "eligibility word"));
     te = us();
     if (mail[2] & 4u) {  // ineligible: the exact plan sorts -- unless the samples share leading
-        // key bytes whose removal leaves children K11e can take (16- / 24-bit keys in int32):
-        // then the caller retries with the digits that many bits lower
+        // key bits (a key range narrower than int32: 16-, 20-, 24-, 28-bit keys, dense or
+        // sorted ranges) whose removal leaves children K11e can take: then the caller retries
+        // with every digit that many bits lower (at most 16, the plan's two levels).  One or
+        // two shared bits (Zipf, any non-negative keys) rarely turn an ineligible block
+        // eligible and are not worth a second sample.
         const uint32_t vary = (uint32_t)mail[5];
         const int lead = vary ? __builtin_clz(vary) : 32;
-        const int nsb = sb == 0 ? (lead >= 16 ? 16 : lead >= 8 ? 8 : 0) : 0;
-        if (retry_sb && nsb && lead < 32) {
+        const int nsb = sb == 0 && lead >= 3 && lead < 32 ? std::min(lead, 16) : 0;
+        if (retry_sb && nsb) {
             // distinct children once the digits start nsb bits lower, and their average size
             const int fixed = std::max(0, std::min(lead - nsb, 16));
             const uint64_t children = 1ull << (16 - fixed);

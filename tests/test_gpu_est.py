@@ -153,11 +153,12 @@ def test_sampled_plan_repeated_sorts_reuse_scratch(ctx, orc):
         assert np.array_equal(got, np.sort(keys)), n
 
 
-@pytest.mark.parametrize("bits,plan", [(27, SAMPLED), (26, SAMPLED), (25, FALLBACK)])
+@pytest.mark.parametrize("bits,plan", [(27, SAMPLED), (26, SAMPLED), (25, SHIFTED)])
 def test_sampled_plan_child_classes(ctx, bits, plan):
     """2^24 keys below 2^bits: 16-bit children of 2^(bits-8) keys -- K11e classes 2 and 3
     (8 192 / 16 384 keys) on the sampled plan; 32 768-key children leave no room for the
-    sampling margin under kLocalMax, so the block goes to the exact plan."""
+    sampling margin under kLocalMax, so the block is retried with its digits below the 7
+    leading bits every key shares."""
     rng = np.random.default_rng(bits)
     keys = rng.integers(0, 1 << bits, 1 << 24, dtype=np.int64).astype(np.int32)
     got, _ = _sort(ctx, keys)
@@ -213,3 +214,18 @@ def test_sampled_plan_shifted_prefix_check(ctx, case):
         assert plan in (FALLBACK, SHIFTED, SAMPLED)
         assert plan != SHIFTED or case != "prefix_broken_late"
     assert np.array_equal(got, np.sort(keys)), case
+
+
+@pytest.mark.parametrize("lo,hi,n", [(0, 1 << 20, 1 << 23), (-(1 << 27), 0, 1 << 26),
+                                     (5 << 24, (5 << 24) + (1 << 26), 1 << 26),
+                                     (1 << 28, 3 << 27, 1 << 26), (-(1 << 14), 1 << 14, 1 << 23)])
+def test_sampled_plan_shifted_ranges(ctx, lo, hi, n):
+    """Key ranges narrower than int32 at any bit offset (20-, 27-, 26-, 27-bit spans, and one
+    across zero: its ordered keys share no leading bit) with children too large for the first
+    attempt: the retry shifts every digit by the samples' shared leading bits (not only whole
+    bytes); the range across zero stays on the exact plan."""
+    rng = np.random.default_rng(hi & 0xffff)
+    keys = rng.integers(lo, hi, n, dtype=np.int64).astype(np.int32)
+    got, _ = _sort(ctx, keys)
+    assert np.array_equal(got, np.sort(keys)), (lo, hi)
+    assert ctx.last_plan() == (FALLBACK if lo < 0 < hi else SHIFTED), (lo, hi, ctx.last_plan())
