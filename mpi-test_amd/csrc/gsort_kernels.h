@@ -263,7 +263,7 @@ hipError_t launch_compat_keys(const int32_t *a, uint64_t n, int P, int loop, con
 // eflag[1]: a region overflowed (the output is wrong).  Either way the caller re-sorts on the
 // exact plan; both are known once K12g has run (the runtime reads them with the K11e list
 // counts).  Sizes (u32 unless noted): part8 kEstWGs x 16384, part3 kEstWGs x 2048, msamp
-// 2 x kEstWGs, capc / cur2 / lim2 / init2 65536, cap3 / cur3 / lim3 / init3 2048, r2 / r3 / bases3 /
+// 4 x kEstWGs, capc / cur2 / lim2 / init2 65536, cap3 / cur3 / lim3 / init3 2048, r2 / r3 / bases3 /
 // bases2 256 u64, tp 257, tdesc (est_max_tiles(n) + 2048) x kTileDescBytes (tile descriptors,
 // then the 2048-entry level-3 piece table), dump kSweepTile keys;
 // wl.list[1..4] 65536 entries each, wl.ctr the 15 counters (zeroed by the front).
@@ -291,12 +291,14 @@ struct EstPlan {
     bool atomic_rank;
     // pinned host mailbox (device pointer) and the sequence numbers K12e-b / K12g publish with:
     // mail[2] eligibility word, mail[4] the children with samples, mail[5] the key bits that
-    // vary among the samples, mail[3] = seq_elig;
+    // vary among the samples, mail[6] / mail[7] their min / max, mail[23] the samples of the
+    // largest child, mail[3] = seq_elig;
     // mail[0] status {eflag, ovf}, mail[8 .. 23)
     // the K11e list counters, mail[1] = seq_done
     uint64_t *mail;
     uint64_t seq_elig, seq_done;
-    int sb;  // 0, 8, 16: the levels' digits start sb bits lower (a constant key prefix)
+    int sb;         // 0 .. 16: the levels' digits start sb bits lower (a constant key prefix)
+    uint32_t koff;  // keys taken as ordered u32 minus koff (the offset retry; 0 otherwise)
 };
 constexpr uint32_t kEstMailWords = 24;
 hipError_t launch_est_front(const EstPlan &p, hipStream_t s);   // K1e + K12e

@@ -1408,7 +1408,8 @@ __global__ __launch_bounds__(kRadix) void k_plan16_place(
 // runtime passes): the status {eflag, ovf} and its sequence after K12g, the same after K12e
 // (eligibility only), the 15 work-list counters after K12g.
 constexpr uint32_t kMailStatus = 0, kMailSeq = 1, kMailElig = 2, kMailEligSeq = 3,
-                   kMailChildren = 4, kMailVary = 5, kMailCtr = 8;
+                   kMailChildren = 4, kMailVary = 5, kMailLo = 6, kMailHi = 7, kMailCtr = 8,
+                   kMailMaxChild = 23;
 
 __device__ __forceinline__ void mail_release(unsigned long long *flag, unsigned long long seq) {
     __threadfence_system();
@@ -1422,6 +1423,9 @@ __device__ __forceinline__ void publish_elig(unsigned long long *mail, const uin
         mail[kMailElig] = *reinterpret_cast<const unsigned long long *>(eflag);
         mail[kMailChildren] = eflag[4];
         mail[kMailVary] = eflag[5];
+        mail[kMailLo] = eflag[6];
+        mail[kMailHi] = eflag[7];
+        mail[kMailMaxChild] = eflag[8];
         mail_release(mail + kMailEligSeq, seq);
     }
 }
@@ -1483,7 +1487,8 @@ __global__ __launch_bounds__(BLOCK) void k_partition_res(
     const uint32_t *__restrict__ flags, const uint32_t *__restrict__ raw,
     const uint32_t *__restrict__ lim = nullptr, uint32_t *__restrict__ ovf = nullptr,
     OT *__restrict__ dump = nullptr, const TileDesc *__restrict__ pieces = nullptr,
-    unsigned long long *mail = nullptr, unsigned long long seq = 0, int sb = 0) {
+    unsigned long long *mail = nullptr, unsigned long long seq = 0, int sb = 0,
+    uint32_t koff = 0) {
     constexpr int TILE = BLOCK * ITEMS;
     const int shift = (L3 ? 24 : 16) - (EST ? sb : 0);  // EST: digits sb bits lower
     static_assert(TILE == kSweepTile, "reservation tiles are kSweepTile keys");
@@ -1565,8 +1570,14 @@ __global__ __launch_bounds__(BLOCK) void k_partition_res(
             for (int i = 0; i < ITEMS; ++i) k[h][i] ^= flip;
         }
     }
+    if (EST && L3 && koff) {  // the offset retry: keys relative to the block's minimum
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int i = 0; i < ITEMS; ++i) k[h][i] -= koff;
+    }
     if (EST && L3 && sb) {  // the prefix the sampled digits skip must hold for every key
-        const uint32_t pfx = (in[0] ^ kFlip) >> (32 - sb);
+        const uint32_t pfx = ((in[0] ^ kFlip) - koff) >> (32 - sb);
         bool bad = false;
 #pragma unroll
         for (int h = 0; h < 2; ++h)
@@ -1695,7 +1706,7 @@ __device__ __forceinline__ uint32_t wave_rank(uint32_t *wc, uint32_t d, bool val
 template <int BLOCK, int ITEMS, bool ATOMIC>
 __device__ __forceinline__ void sort_bucket(uint32_t (&k)[ITEMS], uint32_t len, int ndigits,
                                             uint32_t *__restrict__ dst, uint32_t *s_a,
-                                            uint32_t *s_wc) {
+                                            uint32_t *s_wc, uint32_t koff = 0) {
     constexpr int WAVES = BLOCK / 64;
     constexpr int TILE = BLOCK * ITEMS;
     static_assert(TILE <= 65536, "ranks fit 16 bits");
@@ -1790,7 +1801,7 @@ __device__ __forceinline__ void sort_bucket(uint32_t (&k)[ITEMS], uint32_t len, 
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
         const uint32_t j = (uint32_t)(i * BLOCK + tid);
-        __builtin_amdgcn_raw_buffer_store_b32(s_a[j] ^ kFlip, rs, (int)(j * 4u), 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32((s_a[j] + koff) ^ kFlip, rs, (int)(j * 4u), 0, 0);
     }
 }
 
@@ -2272,33 +2283,37 @@ __device__ __forceinline__ uint32_t est_seg_off(uint32_t j) {  // sample offset 
 // workgroups), sixteen loads in flight per thread.  part8[b][.] = the 65536 u8 child counters
 // (packed 4 per word), part3[b][x * 256 + d] = samples of level-3 bucket d in shard x (tile
 // pair j / 32, shard pair % 8, as K3r deals them), msamp[b] = samples | wrap << 31,
-// msamp[kEstWG + b] = the key bits that differ from in[0] among its samples.  sb (0 .. 16):
+// msamp[kEstWG + b] = the key bits that differ from in[0] among its samples, msamp[2 / 3 *
+// kEstWG + b] = their min / max.  koff: keys are taken as ordered u32 minus koff (the
+// runtime's offset retry; 0 otherwise).  sb (0 .. 16):
 // the plan's digits start sb bits lower (the top sb bits are one constant prefix: the runtime
 // retries a block whose samples share leading bits that way; K3r verifies the prefix).
-// Block 0 also zeroes eflag[0..5] (eflag, ovf, K12g's and K12e's finished-block counts, K12e's
-// count of sampled children, the samples' varying bits).
+// Block 0 also initializes eflag[0..8] (eflag, ovf, K12g's and K12e's finished-block counts,
+// K12e's count of sampled children, the samples' varying bits, min, max, largest child).
 template <bool FIN>
 __global__ __launch_bounds__(1024) void k_est_sample(const uint32_t *__restrict__ in, uint64_t n,
                                                      uint32_t *__restrict__ part8,
                                                      uint32_t *__restrict__ part3,
                                                      uint32_t *__restrict__ msamp,
-                                                     uint32_t *__restrict__ eflag, int sb) {
+                                                     uint32_t *__restrict__ eflag, int sb,
+                                                     uint32_t koff) {
     __shared__ uint32_t s_h[kEstPartWords];
     __shared__ uint32_t s_3[kEstPart3];
-    __shared__ uint32_t s_m, s_vary;
+    __shared__ uint32_t s_m, s_vary, s_lo, s_hi;
     const uint32_t tid = threadIdx.x;
     for (uint32_t i = tid; i < kEstPartWords; i += 1024) s_h[i] = 0;
     for (uint32_t i = tid; i < kEstPart3; i += 1024) s_3[i] = 0;
-    if (tid == 0) { s_m = 0; s_vary = 0; }
-    if (blockIdx.x == 0 && tid < 6) eflag[tid] = 0;
-    const uint32_t ref = FIN ? in[0] ^ kFlip : in[0];  // bits that vary across the samples
+    if (tid == 0) { s_m = 0; s_vary = 0; s_lo = ~0u; s_hi = 0; }
+    if (blockIdx.x == 0 && tid < 9) eflag[tid] = tid == 6 ? ~0u : 0u;
+    // bits that vary across the samples (against key 0), and the samples' range
+    const uint32_t ref = (FIN ? in[0] ^ kFlip : in[0]) - koff;
     __syncthreads();
     const uint32_t nblk = (uint32_t)((n + kEstBlockKeys - 1) / kEstBlockKeys);
     constexpr uint32_t SEGS = 1024 / kEstSegKeys;  // segments per workgroup round
     static_assert(kEstBlockKeys / kEstSegKeys == 64, "64 segment offsets per block");
     const uint32_t seg = tid / kEstSegKeys, kk = tid % kEstSegKeys, step = gridDim.x * SEGS;
     constexpr int U = 16;
-    uint32_t cnt = 0, wrap = 0, vary = 0;
+    uint32_t cnt = 0, wrap = 0, vary = 0, lo = ~0u, hi = 0;
     for (uint32_t j0 = blockIdx.x * SEGS + seg; j0 < nblk; j0 += U * step) {
         uint32_t key[U], jj[U];
         bool ok[U];
@@ -2312,8 +2327,10 @@ __global__ __launch_bounds__(1024) void k_est_sample(const uint32_t *__restrict_
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if (!ok[u]) continue;
-            const uint32_t k = FIN ? key[u] ^ kFlip : key[u];
+            const uint32_t k = (FIN ? key[u] ^ kFlip : key[u]) - koff;
             vary |= k ^ ref;
+            lo = min(lo, k);
+            hi = max(hi, k);
             const uint32_t b = (k >> (16 - sb)) & 0xffffu, sh = (b & 3u) << 3;
             const uint32_t old = atomicAdd(&s_h[b >> 2], 1u << sh);
             wrap |= ((old >> sh) & 255u) == 255u;
@@ -2324,12 +2341,18 @@ __global__ __launch_bounds__(1024) void k_est_sample(const uint32_t *__restrict_
     }
     atomicAdd(&s_m, cnt | (wrap << 31));
     if (vary) atomicOr(&s_vary, vary);
+    if (cnt) { atomicMin(&s_lo, lo); atomicMax(&s_hi, hi); }
     __syncthreads();
     uint32_t *dst = part8 + (uint64_t)blockIdx.x * kEstPartWords;
     for (uint32_t i = tid; i < kEstPartWords; i += 1024) dst[i] = s_h[i];
     uint32_t *d3 = part3 + (uint64_t)blockIdx.x * kEstPart3;
     for (uint32_t i = tid; i < kEstPart3; i += 1024) d3[i] = s_3[i];
-    if (tid == 0) { msamp[blockIdx.x] = s_m; msamp[kEstWG + blockIdx.x] = s_vary; }
+    if (tid == 0) {
+        msamp[blockIdx.x] = s_m;
+        msamp[kEstWG + blockIdx.x] = s_vary;
+        msamp[2 * kEstWG + blockIdx.x] = s_lo;
+        msamp[3 * kEstWG + blockIdx.x] = s_hi;
+    }
 }
 
 // A region's capacity from its sample count: the estimate + the larger of 6 sigma of the
@@ -2374,7 +2397,9 @@ __global__ __launch_bounds__(kRadix) void k_est_plan(
         const uint32_t v = msamp[e];
         atomicAdd(&s_m, v & 0x7fffffffu);
         if (v >> 31) s_bad = 1;
+        if (s == 0 && (v >> 31)) atomicMax(eflag + 8, ~0u);  // wrapped: the counts say nothing
         if (s == 0 && msamp[kEstWG + e]) atomicOr(eflag + 5, msamp[kEstWG + e]);
+        if (s == 0) { atomicMin(eflag + 6, msamp[2 * kEstWG + e]); atomicMax(eflag + 7, msamp[3 * kEstWG + e]); }
     }
     // bucket s's 64 packed words of every partial: lane l reads word l of the partials
     // b = g, g + G, ..; four children per word
@@ -2409,6 +2434,10 @@ __global__ __launch_bounds__(kRadix) void k_est_plan(
     const double scale = m ? (double)n / (double)m : 0.0;
     const uint64_t cap = est_cap(cnt, scale, slack);
     if (cap > kLocalMax) s_bad = 1;
+    uint32_t wmax = cnt;  // the largest child's samples (the runtime's retry): one atomic a wave
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) wmax = max(wmax, (uint32_t)__shfl_xor((int)wmax, o));
+    if ((e & 63) == 0 && wmax) atomicMax(eflag + 8, wmax);
     const uint64_t sampled = __ballot(cnt > 0);  // (outside the branch: all lanes vote)
     if ((e & 63) == 0) atomicAdd(&s_ne, (uint32_t)__popcll(sampled));
     const uint32_t cc = (uint32_t)min(cap, (uint64_t)kLocalMax);
@@ -2629,7 +2658,7 @@ __global__ __launch_bounds__(BLOCK) void k_local_sort_e(const uint32_t *__restri
                                                         unsigned long long *mail,
                                                         const unsigned long long *ctr_all,
                                                         const uint32_t *eflag,
-                                                        unsigned long long seq) {
+                                                        unsigned long long seq, uint32_t koff) {
     constexpr int WAVES = BLOCK / 64;
     constexpr int TILE = BLOCK * ITEMS;
     __shared__ uint32_t s_a[TILE];
@@ -2648,11 +2677,11 @@ __global__ __launch_bounds__(BLOCK) void k_local_sort_e(const uint32_t *__restri
         const __amdgpu_buffer_rsrc_t rs = bucket_rsrc(dst, len * 4u);
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j)
-            __builtin_amdgcn_raw_buffer_store_b32(k[j] ^ kFlip, rs, (j * BLOCK + (int)threadIdx.x) * 4, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32((k[j] + koff) ^ kFlip, rs, (j * BLOCK + (int)threadIdx.x) * 4, 0, 0);
         return;
     }
     __syncthreads();
-    sort_bucket<BLOCK, ITEMS, ATOMIC>(k, len, ndigits, dst, s_a, s_wc);
+    sort_bucket<BLOCK, ITEMS, ATOMIC>(k, len, ndigits, dst, s_a, s_wc, koff);
 }
 
 constexpr int cls_of(int block, int items) {
@@ -2928,7 +2957,7 @@ hipError_t launch_partition3r(const uint32_t *in, uint32_t *out, uint64_t n, uin
     launch_k(k_partition_res<B, I, true, true>, (unsigned)pairs, B, 0, s,
         in, out, n, nullptr, nullptr, reinterpret_cast<const ull *>(bases), cur3, flags,
         (const uint32_t *)nullptr, (const uint32_t *)nullptr, (uint32_t *)nullptr,
-        (uint32_t *)nullptr, (const TileDesc *)nullptr, (unsigned long long *)nullptr, 0ull, 0);
+        (uint32_t *)nullptr, (const TileDesc *)nullptr, (unsigned long long *)nullptr, 0ull, 0, 0u);
     return hipGetLastError();
 }
 
@@ -2950,11 +2979,11 @@ hipError_t launch_partition2r(const uint32_t *in, uint32_t *out, uint16_t *out16
         launch_k(k_partition_res<B, I, false, false, uint16_t>, g2, B, 0, s, in, out16, n, tpfx,
                  desc, bs, cur, flags, raw, (const uint32_t *)nullptr, (uint32_t *)nullptr,
                  (uint16_t *)nullptr, (const TileDesc *)nullptr, (unsigned long long *)nullptr,
-                 0ull, 0);
+                 0ull, 0, 0u);
     else
         launch_k(k_partition_res<B, I, false, false>, g2, B, 0, s, in, out, n, tpfx, desc, bs,
                  cur, flags, raw, (const uint32_t *)nullptr, (uint32_t *)nullptr,
-                 (uint32_t *)nullptr, (const TileDesc *)nullptr, (unsigned long long *)nullptr, 0ull, 0);
+                 (uint32_t *)nullptr, (const TileDesc *)nullptr, (unsigned long long *)nullptr, 0ull, 0, 0u);
     return hipGetLastError();
 }
 
@@ -3263,8 +3292,8 @@ hipError_t launch_est_front(const EstPlan &p, hipStream_t s) {
     using ull = unsigned long long;
     if (p.n == 0 || p.n > kEstMaxKeys) return hipErrorInvalidValue;
     if (p.sb < 0 || p.sb > 16) return hipErrorInvalidValue;
-    if (p.flip_in) launch_k(k_est_sample<true>, kEstWG, 1024, 0, s, p.in, p.n, p.part8, p.part3, p.msamp, p.eflag, p.sb);
-    else launch_k(k_est_sample<false>, kEstWG, 1024, 0, s, p.in, p.n, p.part8, p.part3, p.msamp, p.eflag, p.sb);
+    if (p.flip_in) launch_k(k_est_sample<true>, kEstWG, 1024, 0, s, p.in, p.n, p.part8, p.part3, p.msamp, p.eflag, p.sb, p.koff);
+    else launch_k(k_est_sample<false>, kEstWG, 1024, 0, s, p.in, p.n, p.part8, p.part3, p.msamp, p.eflag, p.sb, p.koff);
     launch_k(k_est_plan, kRadix, kRadix, 0, s, p.part8, p.part3, p.msamp, kEstWG, p.n, p.slack,
              p.capx, p.capy, p.capc, p.cap3, reinterpret_cast<ull *>(p.r2),
              reinterpret_cast<ull *>(p.r3), reinterpret_cast<ull *>(p.bases3),
@@ -3282,7 +3311,8 @@ hipError_t launch_est_level3(const EstPlan &p, hipStream_t s) {
              p.in, p.x, p.n, (const uint32_t *)nullptr, (const TileDesc *)nullptr,
              reinterpret_cast<const ull *>(p.bases3), p.cur3, (const uint32_t *)p.eflag,
              (const uint32_t *)nullptr, (const uint32_t *)p.lim3, p.eflag + 1, p.dump,
-             (const TileDesc *)nullptr, reinterpret_cast<ull *>(p.mail), (ull)p.seq_elig, p.sb);
+             (const TileDesc *)nullptr, reinterpret_cast<ull *>(p.mail), (ull)p.seq_elig, p.sb,
+             p.koff);
     return hipGetLastError();
 }
 
@@ -3300,7 +3330,7 @@ hipError_t launch_est_level2(const EstPlan &p, hipStream_t s) {
              (const uint32_t *)p.x, p.y, p.n, (const uint32_t *)p.tp, (const TileDesc *)desc,
              reinterpret_cast<const ull *>(p.bases2), p.cur2, (const uint32_t *)p.eflag,
              (const uint32_t *)nullptr, (const uint32_t *)p.lim2, p.eflag + 1, p.dump,
-             (const TileDesc *)pieces, (ull *)nullptr, (ull)0, p.sb);
+             (const TileDesc *)pieces, (ull *)nullptr, (ull)0, p.sb, 0u);
     return hipGetLastError();
 }
 
@@ -3327,6 +3357,7 @@ hipError_t launch_local_sort_e(const EstPlan &p, int cls, uint32_t first, uint32
     const ull *l = reinterpret_cast<const ull *>(p.wl.list[cls]);
     const ull *call = reinterpret_cast<const ull *>(p.wl.ctr), *ctr = call + 3 * cls;
     const uint32_t *y = p.y, *ef = p.eflag;
+    const uint32_t ko = p.koff;
     const int nd = (16 - p.sb + 7) / 8;  // digits for the bits below the plan's two levels
                                          // (sb = 16: a child is one value, K11e copies it)
     ull *mail = publish ? reinterpret_cast<ull *>(p.mail) : nullptr;
@@ -3335,13 +3366,13 @@ hipError_t launch_local_sort_e(const EstPlan &p, int cls, uint32_t first, uint32
     do {                                                                                       \
         if (nd == 0)                                                                           \
             launch_k(k_local_sort_e<B, I, true, true>, nlist, B, 0, s, y, p.out, l, ctr, first, \
-                     nd, mail, call, ef, seq);                                                 \
+                     nd, mail, call, ef, seq, ko);                                             \
         else if (p.atomic_rank)                                                                \
             launch_k(k_local_sort_e<B, I, true>, nlist, B, 0, s, y, p.out, l, ctr, first, nd,  \
-                     mail, call, ef, seq);                                                     \
+                     mail, call, ef, seq, ko);                                                 \
         else                                                                                   \
             launch_k(k_local_sort_e<B, I, false>, nlist, B, 0, s, y, p.out, l, ctr, first, nd, \
-                     mail, call, ef, seq);                                                     \
+                     mail, call, ef, seq, ko);                                                 \
     } while (0)
     switch (cls) {
         case 1: GSORT_K11E(256, 18); break;

@@ -125,6 +125,7 @@ namespace {
 constexpr size_t OFF_HIST = 0, OFF_TOT = 8192, OFF_BASES = 10240, OFF_CTR = 12288,
                  OFF_ONE = 12416, OFF_CTR3 = 12544, OFF_PLAN = 20480;
 constexpr size_t OFF_FLAGS = 12408;  // K12b's trivial-level word, inside the published range
+constexpr size_t OFF_MINMAX = 12480;  // the offset retry's exact min / max (2 int32)
 
 gsort_status set_err(gsort_ctx *c, gsort_status st, const std::string &msg) {
     if (c) c->err = msg;
@@ -939,10 +940,21 @@ uint64_t est_region_keys(uint64_t n, uint64_t nreg, double slack) {
     return n + nreg + (uint64_t)std::ceil(slack * (sig + floor2 + 64.0 * (double)nreg)) + 1024;
 }
 
+// What an ineligible first attempt saw: the key bits that vary among the samples (against key
+// 0) and the samples' min / max, all as ordered u32.
+struct EstRetry {
+    bool valid = false;
+    uint32_t vary = 0, lo = 0, hi = 0, maxc = 0;  // maxc: samples of the largest child
+};
+
+// Leading bits shared by every key of a range (clz of its span), 32 for a single value.
+int span_lead(uint32_t lo, uint32_t hi) { return hi > lo ? __builtin_clz(hi - lo) : 32; }
+
 gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *out,
-                          gsort_stats *stats, bool *ok, int sb = 0, int *retry_sb = nullptr) {
+                          gsort_stats *stats, bool *ok, int sb = 0, uint32_t koff = 0,
+                          EstRetry *retry = nullptr) {
     *ok = false;
-    if (retry_sb) *retry_sb = 0;
+    if (retry) *retry = EstRetry{};
     const double slack = std::max(c->est_slack, 0.0);
     const uint64_t capx = est_region_keys(n, (uint64_t)kH16Shards * kRadix, slack);
     const uint64_t capy = std::min<uint64_t>(est_region_keys(n, kBuckets16, slack),
@@ -959,7 +971,7 @@ gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
         }
         ST_TRY(st);
     }
-    ST_TRY(ensure(c, c->m_epart, (size_t)kEstWGs * (kBuckets16 / 4 + kH16Shards * kRadix + 2) * 4));
+    ST_TRY(ensure(c, c->m_epart, (size_t)kEstWGs * (kBuckets16 / 4 + kH16Shards * kRadix + 4) * 4));
     constexpr size_t kPlanWords = (size_t)4 * kBuckets16 + 4 * kH16Shards * kRadix + kRadix + 1;
     ST_TRY(ensure(c, c->m_eplan, kPlanWords * 4 + 4 * kRadix * 8 + 64));
     ST_TRY(ensure(c, c->m_edesc, ((size_t)est_max_tiles(n) + kH16Shards * kRadix) * kTileDescBytes));
@@ -1000,6 +1012,7 @@ gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
     p.slack = slack;
     p.atomic_rank = c->atomic_rank;
     p.sb = sb;
+    p.koff = koff;
     p.mail = c->d_mail + kEstMailWord;
     p.seq_elig = ++c->mail_seq;
     p.seq_done = ++c->mail_seq;
@@ -1047,14 +1060,12 @@ gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
         // with every digit that many bits lower (at most 16, the plan's two levels).  One or
         // two shared bits (Zipf, any non-negative keys) rarely turn an ineligible block
         // eligible and are not worth a second sample.
-        const uint32_t vary = (uint32_t)mail[5];
-        const int lead = vary ? __builtin_clz(vary) : 32;
-        const int nsb = sb == 0 && lead >= 3 && lead < 32 ? std::min(lead, 16) : 0;
-        if (retry_sb && nsb) {
-            // distinct children once the digits start nsb bits lower, and their average size
-            const int fixed = std::max(0, std::min(lead - nsb, 16));
-            const uint64_t children = 1ull << (16 - fixed);
-            if (n / children <= kLocalMax / 2) *retry_sb = nsb;
+        if (retry) {
+            retry->vary = (uint32_t)mail[5];
+            retry->lo = (uint32_t)mail[6];
+            retry->hi = (uint32_t)mail[7];
+            retry->maxc = (uint32_t)mail[23];
+            retry->valid = true;
         }
         return GSORT_OK;
     }
@@ -1109,11 +1120,59 @@ gsort_status msd_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *ou
     if (allow_est && c->plan_est && c->plan16 && !group16 && n >= kEstMinKeys &&
         n <= kEstMaxKeys) {
         bool ok = false;
-        int retry_sb = 0;
-        ST_TRY(msd_sort_est(c, in, n, out, stats, &ok, 0, &retry_sb));
-        if (!ok && retry_sb) ST_TRY(msd_sort_est(c, in, n, out, stats, &ok, retry_sb));
-        c->last_plan = ok ? (retry_sb ? 3 : 1) : 2;
+        EstRetry r;
+        ST_TRY(msd_sort_est(c, in, n, out, stats, &ok, 0, 0, &r));
+        c->last_plan = ok ? 1 : 2;
         if (ok) return GSORT_OK;
+        // An ineligible block whose keys span a narrow range: retry with every digit below the
+        // bits the range's keys share (children of at most kLocalMax / 2 on average), either
+        // a prefix the samples share (free: K3r checks it on every key) or -- when the range
+        // crosses a power of two, e.g. around zero -- the exact min / max (one read pass) as an
+        // offset.  One or two shared bits (Zipf, any non-negative keys) rarely make a block
+        // eligible and are not worth a second sample.
+        // fits: the children after a shift by min(lead, 16) bits average at most kLocalMax / 2,
+        // and -- when the first sample's child counts are known (no u8 counter wrapped) -- the
+        // largest one now (~64 keys per sample) split 2^shift ways stays below 5/8 of it.  The
+        // prefix retry costs a failed sample when wrong; the offset retry also a read pass, so
+        // it needs known counts (peaked inputs -- Gaussian keys -- fail it: their densest
+        // child stays too large after any shift).
+        const bool known = r.maxc != 0xffffffffu;
+        auto fits = [&](int lead) {
+            const int sb = std::min(lead, 16);
+            const int fixed = std::max(0, std::min(lead - sb, 16));  // bits fixed below the shift
+            return n / (1ull << (16 - fixed)) <= kLocalMax / 2 &&
+                   (!known || ((uint64_t)r.maxc * 64) >> sb <= kLocalMax * 5 / 8);
+        };
+        if (r.valid) {
+            const int lead = r.vary ? __builtin_clz(r.vary) : 32;
+            const int slead = span_lead(r.lo, r.hi);
+            if (lead >= 3 && lead < 32 && fits(lead)) {
+                ST_TRY(msd_sort_est(c, in, n, out, stats, &ok, std::min(lead, 16)));
+            } else if (slead == 32 || (known && slead >= 4 && fits(slead - 1))) {
+                // (the samples' span, one bit of margin: the block's may be wider)
+                int *mm = reinterpret_cast<int *>(c->d_small + OFF_MINMAX);
+                int *hmm = reinterpret_cast<int *>(c->h_small + OFF_MINMAX);
+                HIP_TRY(c, hipStreamSynchronize(c->stream));  // hmm may feed an earlier copy
+                hmm[0] = 2147483647;
+                hmm[1] = -2147483647 - 1;
+                HIP_TRY(c, hipMemcpyAsync(mm, hmm, 8, hipMemcpyHostToDevice, c->stream));
+                HIP_TRY(c, launch_minmax(reinterpret_cast<const int32_t *>(in), n, mm, c->stream));
+                HIP_TRY(c, hipMemcpyAsync(hmm, mm, 8, hipMemcpyDeviceToHost, c->stream));
+                HIP_TRY(c, hipStreamSynchronize(c->stream));
+                const uint32_t lo = (uint32_t)hmm[0] ^ 0x80000000u, hi = (uint32_t)hmm[1] ^ 0x80000000u;
+                const int lead = span_lead(lo, hi);
+                if (lead == 32) {  // one value: the sorted block is the block
+                    HIP_TRY(c, hipMemcpyAsync(out, in, n * 4, hipMemcpyDeviceToDevice, c->stream));
+                    ok = true;
+                } else if (lead >= 3 && fits(lead)) {
+                    ST_TRY(msd_sort_est(c, in, n, out, stats, &ok, std::min(lead, 16), lo));
+                }
+            }
+        }
+        if (ok) {
+            c->last_plan = 3;
+            return GSORT_OK;
+        }
     }
     uint64_t *ctr = reinterpret_cast<uint64_t *>(c->d_small + OFF_CTR);
     if (n <= kLocalMax) {  // one bucket: all four digits in LDS

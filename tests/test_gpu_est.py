@@ -111,10 +111,10 @@ def test_sampled_plan_distributions(ctx, orc, name):
     assert plan in (SAMPLED, FALLBACK, SHIFTED), plan
     if name in ("sorted", "reversed", "sorted_blocks"):  # uniform keys, position-correlated
         assert plan == SAMPLED, name
-    if name in ("all_equal", "zipf", "half_one_value"):  # a child > kLocalMax
+    if name in ("zipf", "half_one_value"):  # a child > kLocalMax, keys over the whole range
         assert plan == FALLBACK, name
-    if name in ("bits16", "bits24"):  # one constant key prefix: the digits below it
-        assert plan == SHIFTED, name
+    if name in ("bits16", "bits24", "all_equal"):  # a narrow key range: the digits below its
+        assert plan == SHIFTED, name  # shared bits (all-equal: a copy)
     assert np.array_equal(got, np.sort(keys)), name
 
 
@@ -223,9 +223,32 @@ def test_sampled_plan_shifted_ranges(ctx, lo, hi, n):
     """Key ranges narrower than int32 at any bit offset (20-, 27-, 26-, 27-bit spans, and one
     across zero: its ordered keys share no leading bit) with children too large for the first
     attempt: the retry shifts every digit by the samples' shared leading bits (not only whole
-    bytes); the range across zero stays on the exact plan."""
+    bytes)."""
     rng = np.random.default_rng(hi & 0xffff)
     keys = rng.integers(lo, hi, n, dtype=np.int64).astype(np.int32)
     got, _ = _sort(ctx, keys)
     assert np.array_equal(got, np.sort(keys)), (lo, hi)
+    # across zero the shared bits are the keys' minus the exact minimum: that read pass is only
+    # spent when the first sample's child counts are known (here two children wrapped them)
     assert ctx.last_plan() == (FALLBACK if lo < 0 < hi else SHIFTED), (lo, hi, ctx.last_plan())
+
+
+@pytest.mark.parametrize("case", ["gauss", "gauss_outliers", "two_values_across_zero"])
+def test_sampled_plan_offset_retry(ctx, case):
+    """Clustered keys around zero (no shared prefix) go through the offset retry: the exact
+    min / max, every key taken minus the minimum.  Outliers the samples miss only widen that
+    range (the plan still has to be right); two values across zero make many one-value
+    children."""
+    rng = np.random.default_rng(23)
+    n = 1 << 24
+    if case == "two_values_across_zero":
+        keys = rng.choice(np.array([-3, 4], dtype=np.int32), n)
+    else:
+        keys = np.clip(rng.normal(0, 3e5, n), -2**31, 2**31 - 1).astype(np.int32)
+        if case == "gauss_outliers":
+            keys[[7, n // 3, n - 2]] = [-2**31, 2**31 - 1, 123456789]
+    got, _ = _sort(ctx, keys)
+    assert np.array_equal(got, np.sort(keys)), case
+    assert ctx.last_plan() in (FALLBACK, SHIFTED), ctx.last_plan()
+    if case == "gauss":
+        assert ctx.last_plan() == SHIFTED

@@ -50,6 +50,7 @@ for name, make in cases.items():
     lv = [sum(s["ms_level"][i] for s in st) / len(st) for i in range(4)]
     print(f"{name:22s} {f('ms_total'):8.3f} ms  ({n / f('ms_total') / 1e6:6.1f} GKeys/s)  "
           f"hist {f('ms_hist'):.3f} levels {' '.join(f'{x:.3f}' for x in lv)} "
-          f"K11 {f('ms_bucket_sort'):.3f} passes {st[-1]['passes_run']}", flush=True)
+          f"K11 {f('ms_bucket_sort'):.3f} passes {st[-1]['passes_run']} plan {ctx.last_plan()}",
+          flush=True)
 ctx.free(p)
 ctx.close()
