@@ -2339,9 +2339,20 @@ __global__ __launch_bounds__(1024) void k_est_sample(const uint32_t *__restrict_
             ++cnt;
         }
     }
-    atomicAdd(&s_m, cnt | (wrap << 31));
-    if (vary) atomicOr(&s_vary, vary);
-    if (cnt) { atomicMin(&s_lo, lo); atomicMax(&s_hi, hi); }
+    // wave reductions first: 64 lanes on one LDS word serialize
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        cnt += (uint32_t)__shfl_xor((int)cnt, o);
+        wrap |= (uint32_t)__shfl_xor((int)wrap, o);
+        vary |= (uint32_t)__shfl_xor((int)vary, o);
+        lo = min(lo, (uint32_t)__shfl_xor((int)lo, o));
+        hi = max(hi, (uint32_t)__shfl_xor((int)hi, o));
+    }
+    if ((tid & 63) == 0) {
+        atomicAdd(&s_m, cnt | (wrap << 31));
+        if (vary) atomicOr(&s_vary, vary);
+        if (cnt) { atomicMin(&s_lo, lo); atomicMax(&s_hi, hi); }
+    }
     __syncthreads();
     uint32_t *dst = part8 + (uint64_t)blockIdx.x * kEstPartWords;
     for (uint32_t i = tid; i < kEstPartWords; i += 1024) dst[i] = s_h[i];
@@ -2386,20 +2397,39 @@ __global__ __launch_bounds__(kRadix) void k_est_plan(
     uint32_t *__restrict__ cur3, uint32_t *__restrict__ lim3, uint32_t *__restrict__ init3,
     unsigned long long *__restrict__ zero, uint32_t nzero, uint32_t *__restrict__ eflag) {
     constexpr uint32_t G = kRadix / 64;  // thread groups, each over every G-th partial
-    __shared__ uint32_t s_m, s_bad, s_last, s_ne;
+    __shared__ uint32_t s_m, s_bad, s_last, s_ne, s_maxc;
     __shared__ uint32_t s_c[G][kRadix], s_3[kRadix / kShards][kShards];
     __shared__ unsigned long long s_w[kRadix / 64], s_c3[kShards];
     const uint32_t s = blockIdx.x, e = threadIdx.x, g = e >> 6, l = e & 63;
-    if (e == 0) { s_m = 0; s_bad = 0; s_ne = 0; }
+    if (e == 0) { s_m = 0; s_bad = 0; s_ne = 0; s_maxc = 0; }
     __syncthreads();
     static_assert(kEstWG <= kRadix && kEstWG % (kRadix / 8) == 0, "K12e geometry");
     if (e < kEstWG) {
         const uint32_t v = msamp[e];
         atomicAdd(&s_m, v & 0x7fffffffu);
         if (v >> 31) s_bad = 1;
-        if (s == 0 && (v >> 31)) atomicMax(eflag + 8, ~0u);  // wrapped: the counts say nothing
-        if (s == 0 && msamp[kEstWG + e]) atomicOr(eflag + 5, msamp[kEstWG + e]);
-        if (s == 0) { atomicMin(eflag + 6, msamp[2 * kEstWG + e]); atomicMax(eflag + 7, msamp[3 * kEstWG + e]); }
+    }
+    if (s == 0) {  // block 0: the samples' varying bits, min, max and any wrap, one atomic a wave
+        uint32_t vy = 0, lo = ~0u, hi = 0, wr = 0;
+        for (uint32_t b = e; b < kEstWG; b += kRadix) {
+            vy |= msamp[kEstWG + b];
+            lo = min(lo, msamp[2 * kEstWG + b]);
+            hi = max(hi, msamp[3 * kEstWG + b]);
+            wr |= msamp[b] >> 31;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            vy |= (uint32_t)__shfl_xor((int)vy, o);
+            lo = min(lo, (uint32_t)__shfl_xor((int)lo, o));
+            hi = max(hi, (uint32_t)__shfl_xor((int)hi, o));
+            wr |= (uint32_t)__shfl_xor((int)wr, o);
+        }
+        if ((e & 63) == 0) {
+            if (vy) atomicOr(eflag + 5, vy);
+            atomicMin(eflag + 6, lo);
+            atomicMax(eflag + 7, hi);
+            if (wr) atomicMax(eflag + 8, ~0u);  // wrapped: the child counts say nothing
+        }
     }
     // bucket s's 64 packed words of every partial: lane l reads word l of the partials
     // b = g, g + G, ..; four children per word
@@ -2434,10 +2464,10 @@ __global__ __launch_bounds__(kRadix) void k_est_plan(
     const double scale = m ? (double)n / (double)m : 0.0;
     const uint64_t cap = est_cap(cnt, scale, slack);
     if (cap > kLocalMax) s_bad = 1;
-    uint32_t wmax = cnt;  // the largest child's samples (the runtime's retry): one atomic a wave
+    uint32_t wmax = cnt;  // the largest child's samples (the runtime's retry), per block
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) wmax = max(wmax, (uint32_t)__shfl_xor((int)wmax, o));
-    if ((e & 63) == 0 && wmax) atomicMax(eflag + 8, wmax);
+    if ((e & 63) == 0) atomicMax(&s_maxc, wmax);
     const uint64_t sampled = __ballot(cnt > 0);  // (outside the branch: all lanes vote)
     if ((e & 63) == 0) atomicAdd(&s_ne, (uint32_t)__popcll(sampled));
     const uint32_t cc = (uint32_t)min(cap, (uint64_t)kLocalMax);
@@ -2471,6 +2501,7 @@ __global__ __launch_bounds__(kRadix) void k_est_plan(
         if (m && samp == m) s_bad = 1;
         if (s_bad) atomicOr(eflag, 4u);
         atomicAdd(eflag + 4, s_ne);
+        if (s_maxc) atomicMax(eflag + 8, s_maxc);
         __threadfence();
         s_last = atomicAdd(eflag + 3, 1u) == gridDim.x - 1;
     }
