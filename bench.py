@@ -56,6 +56,10 @@ def parse():
     ap.add_argument("--dist", choices=["uniform", "zipf"], default="uniform")
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-cpu-large", action="store_true",
+                    help="skip the reference's 2^28-key point (~1 min of host time)")
+    ap.add_argument("--no-dist-p1", action="store_true",
+                    help="skip the one-rank distributed-path block")
     ap.add_argument("--no-stats", action="store_true",
                     help="experiment: time the steps without per-phase events")
     ap.add_argument("--local", choices=["msd", "lsd"], default="msd",
@@ -112,12 +116,12 @@ def host_cpu():
     return {"cpu_model": model, "host_logical_cpus": os.cpu_count(), "usable_cpus": usable}
 
 
-def run_reference(prog, np_, path, mpirun):
+def run_reference(prog, np_, path, mpirun, bind=True, timeout=300):
     """One reference program under mpirun; (program-timer seconds, wall seconds, stdout)."""
     ref = os.path.join(ROOT, "oracle", "_ref", prog)
     t0 = time.time()
-    r = subprocess.run([mpirun, "-np", str(np_), ref, path], capture_output=True, text=True,
-                       timeout=300)
+    cmd = [mpirun] + (["-bind-to", "core"] if bind else []) + ["-np", str(np_), ref, path]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout)
     wall = time.time() - t0
     m = re.search(r"Endtime\(\)-Starttime\(\) = ([0-9.]+) sec", r.stderr)
     if r.returncode != 0 or not m:
@@ -125,40 +129,82 @@ def run_reference(prog, np_, path, mpirun):
     return float(m.group(1)), wall, r.stdout.strip().splitlines()[-1]
 
 
-def cpu_baseline(dist, seed):
+def median3(prog, np_, path, mpirun, bind):
+    """Median of 3 runs (program timer), with every run's figures."""
+    runs = [run_reference(prog, np_, path, mpirun, bind) for _ in range(3)]
+    ts = sorted(r[0] for r in runs)
+    meds = {r[2] for r in runs}
+    if len(meds) != 1:
+        raise RuntimeError(f"{prog} median lines differ between runs: {meds}")
+    return ts[1], [round(r[0], 4) for r in runs], round(sum(r[1] for r in runs) / 3, 2), meds.pop()
+
+
+def cpu_baseline(dist, seed, large=True):
     """The reference itself (oracle/_ref: radix_sort and sample_sort built unchanged from their
-    sources with their own flags, -O0) under mpirun -np 4 on BASELINE configs[0]'s 2^24 keys,
-    timed by their own stderr timers (mpi_radix_sort.c:98,197,203; mpi_sample_sort.c:61,201,
-    207), which exclude the text read.  The 2^28 point is not run by default: the survey
-    measured ref-radix at 2^28 (P=8) at 25.8 s plus a ~25 s text read, past the bench budget."""
+    sources with their own flags, -O0) under `mpirun -bind-to core -np P`, P = 4 (BASELINE
+    configs[0]) and 8, on 2^24 keys of the same stream, median of 3, timed by the programs' own
+    stderr timers (mpi_radix_sort.c:98,197,203; mpi_sample_sort.c:61,201,207), which exclude
+    the text read; then the largest feasible point, 2^28 keys, radix at P = 8, one run (the
+    reference's int N stops at 2^31 - 1, mpi_radix_sort.c:65).  `value` is the P = 4 radix
+    figure; `cores` the ranks it ran on (one core each)."""
     keys_log2, np_ = 24, 4  # BASELINE configs[0]: reference radix, mpirun -np 4, 2^24 keys
     n = 1 << keys_log2
     gen = os.path.join(PKG, "bin", "gen_keys")
     mpirun = shutil.which("mpirun") or "/opt/conda/bin/mpirun"
     tmp = tempfile.mkdtemp(prefix="gsort_cpu_")
     host = host_cpu()
+    t_start = time.time()
     try:
         path = os.path.join(tmp, "keys.txt")
         subprocess.run([gen, dist, str(n), str(seed), path], check=True)
         if os.path.exists(os.path.join(ROOT, "oracle", "_ref", "radix_sort")) and \
                 os.path.exists(mpirun):
-            t, wall, med = run_reference("radix_sort", np_, path, mpirun)
-            out = {"value": n / t / 1e9, "unit": "GKeys/s", "cores": np_, "kind": "reference",
-                   "sample": f"reference radix_sort (oracle/_ref, -O0 as shipped) under "
-                             f"mpirun -np {np_} (one core per rank), 2^{keys_log2} {dist} keys "
-                             f"seed {seed}; program timer {t:.3f} s (excludes its text read), "
-                             f"wall {wall:.1f} s",
-                   "median_line": med, **host,
-                   "large_point": "2^28 not run by default (ref-radix 2^28 P=8: 25.8 s + "
-                                  "~25 s read, SURVEY.md 6); N >= 2^31: n/a, the reference's "
-                                  "int N overflows (mpi_radix_sort.c:65)"}
+            bind = True
             try:
-                ts, walls, meds = run_reference("sample_sort", np_, path, mpirun)
-                out["sample_sort"] = {"value": n / ts / 1e9, "unit": "GKeys/s", "cores": np_,
-                                      "program_s": ts, "wall_s": round(walls, 1),
-                                      "median_line": meds}
-            except Exception as e:  # reported, never fatal
-                out["sample_sort"] = {"value": None, "error": repr(e)}
+                run_reference("radix_sort", 2, path, mpirun, True)
+            except Exception:  # binding refused on this host: run unbound, and say so
+                bind = False
+            points = {}
+            for prog in ("radix_sort", "sample_sort"):
+                for p in (4, 8):
+                    try:
+                        t, runs, wall, med = median3(prog, p, path, mpirun, bind)
+                        points[f"{prog}_np{p}"] = {"value": n / t / 1e9, "program_s": t,
+                                                    "runs_s": runs, "wall_s_avg": wall,
+                                                    "median_line": med}
+                    except Exception as e:  # reported, never fatal
+                        points[f"{prog}_np{p}"] = {"value": None, "error": repr(e)}
+            r4 = points["radix_sort_np4"]
+            if r4.get("value") is None:
+                raise RuntimeError(r4.get("error"))
+            out = {"value": r4["value"], "unit": "GKeys/s", "cores": np_, "kind": "reference",
+                   "sample": f"reference radix_sort (oracle/_ref, -O0 as shipped) under mpirun "
+                             f"{'-bind-to core ' if bind else '(unbound) '}-np {np_}, 2^{keys_log2} "
+                             f"{dist} keys seed {seed}; median of 3 program timers "
+                             f"{r4['runs_s']} s (exclude the text read)",
+                   "median_line": r4["median_line"], "bind_to_core": bind,
+                   "points_2p24": points, **host}
+            if large and time.time() - t_start < 120:
+                nl = 1 << 28
+                try:
+                    lpath = os.path.join(tmp, "keys28.txt")
+                    os.remove(path)
+                    subprocess.run([gen, dist, str(nl), str(seed), lpath], check=True)
+                    t, wall, med = run_reference("radix_sort", 8, lpath, mpirun, bind, 600)
+                    out["large_point"] = {"value": nl / t / 1e9, "keys": nl, "np": 8,
+                                          "program_s": t, "wall_s": round(wall, 1),
+                                          "median_line": med, "runs": 1}
+                except Exception as e:
+                    out["large_point"] = {"value": None, "error": repr(e)}
+                finally:
+                    shutil.rmtree(tmp, ignore_errors=True)
+            else:
+                out["large_point"] = {"value": None,
+                                      "skipped": "--no-cpu-large" if not large else
+                                      "2^24 points took > 120 s"}
+            out["beyond_reference"] = ("N >= 2^31: n/a, the reference's int N overflows "
+                                       "(mpi_radix_sort.c:65)")
+            out["wall_s_total"] = round(time.time() - t_start, 1)
             return out
         # fallback: the oracle's scalar port of the build's algorithm, one core
         from oracle import orc
@@ -174,6 +220,85 @@ def cpu_baseline(dist, seed):
                 "sample": f"cpu baseline failed: {e!r}"}
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
+
+
+def median_check(ctx, fn, dist_id, seed, cpu):
+    """The GPU's sort of the CPU baseline's 2^24-key stream (same generator, seed, order)
+    against the reference's own output on it: its median line (measured beside us in
+    cpu_baseline) and, when tests/golden/ref_large.json holds this stream, the sha256 of the
+    reference's full sorted dump."""
+    import hashlib
+    import numpy as np
+    n = 1 << 24
+    d = ctx.alloc(n * 4)
+    try:
+        ctx.generate(dist_id, seed, 0, n, d)
+        out, m, _ = fn(d, n, stats=False)
+        plan = ctx.last_plan()
+        h = ctx.to_host(out, m)
+    finally:
+        ctx.free(d)
+    res = {"keys": n, "gpu_median_line": f"The n/2-th sorted element: {h[n // 2 - 1]}",
+           "local_plan": plan}
+    ref_med = (cpu or {}).get("median_line")
+    res["reference_median_line"] = ref_med
+    res["median_matches_reference"] = (None if ref_med is None
+                                       else ref_med == res["gpu_median_line"])
+    try:
+        cases = json.load(open(os.path.join(ROOT, "tests", "golden", "ref_large.json")))["cases"]
+        gen = "uniform" if dist_id == 0 else "zipf"
+        want = [c["output_sha256"] for c in cases if c["input"] == {"gen": gen, "n": n,
+                                                                     "seed": seed}
+                and c.get("output_is_sorted_input")]
+        if want:
+            got = hashlib.sha256(np.ascontiguousarray(h, dtype="<i4").tobytes()).hexdigest()
+            res["dump_sha256_matches_reference"] = got == want[0]
+    except (OSError, ValueError, KeyError):
+        pass
+    return res
+
+
+def dist_p1(gsort, n_local, dist_id, seed, steps=5):
+    """The distributed radix path at N = 1 (one-rank RCCL communicator, GSORT_FORCE_DIST):
+    sender grouping, radix select, packed self-exchange through RCCL, receive sort -- the
+    per-GPU cost the weak-scaling points pay before any xGMI time."""
+    os.environ["GSORT_FORCE_DIST"] = "1"
+    try:
+        ctx = gsort.Context(rank=0, nranks=1, device=0, uid=gsort.get_uid())
+    finally:
+        del os.environ["GSORT_FORCE_DIST"]
+    try:
+        d = ctx.alloc(n_local * 4)
+        ctx.generate(dist_id, seed, 0, n_local, d)
+        ctx.reserve(n_local)
+        for _ in range(2):
+            ctx.radix(d, n_local, stats=False)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            ctx.radix(d, n_local, stats=False)
+        ms = (time.perf_counter() - t0) * 1e3 / steps
+        st = [ctx.radix(d, n_local)[2] for _ in range(3)]
+        out, m, _ = ctx.radix(d, n_local, stats=False)
+        fp, fin = ctx.fingerprint(out, m), ctx.fingerprint(d, n_local)
+        ok = fp["sorted"] and fp["sum"] == fin["sum"] and fp["xor"] == fin["xor"]
+        ctx.free(d)
+    finally:
+        ctx.close()
+    avg = {k: round(sum(s[k] for s in st) / len(st), 4)
+           for k in ("ms_total", "ms_hist", "ms_sample", "ms_exchange", "ms_place", "ms_merge",
+                     "ms_bucket_sort")}
+    avg["ms_level"] = [round(sum(s["ms_level"][i] for s in st) / len(st), 4) for i in range(2)]
+    merge = avg["ms_merge"]
+    return {"ms_per_step": round(ms, 4), "GKeys_s": round(n_local / (ms * 1e-3) / 1e9, 2),
+            "phases_ms_avg": avg, "verified": bool(ok),
+            "receive_sort": {"ms": merge, "bytes_per_key": 6,
+                             "achieved_GBps": (round(n_local * 6 / (merge * 1e-3) / 1e9, 1)
+                                               if merge else None),
+                             "frac": (round(n_local * 6 / (merge * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
+                                      if merge else None),
+                             "note": "K11g + K18: read the 2-B packed key, write the 4-B key"},
+            "note": "GSORT_FORCE_DIST=1, one-rank RCCL communicator (self-exchange = HBM copy); "
+                    "untimed steps, then 3 timed for phases"}
 
 
 def kernel_rooflines(stats, n_local, plan=0):
@@ -318,7 +443,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baseline(dist_name, a.seed)
+        cpu = cpu_baseline(dist_name, a.seed, large=not a.no_cpu_large)
 
     import torch
     import torch.distributed as dist
@@ -392,6 +517,8 @@ def main():
 
     ceiling = copy_ceiling(ctx, n_local) if rank == 0 else None
     drop_in = drop_in_e2e(ctx, fn, d_in, n_local) if world == 1 else None
+    dist_id = gsort.UNIFORM if dist_name == "uniform" else gsort.ZIPF
+    med = median_check(ctx, fn, dist_id, a.seed, cpu) if world == 1 else None
 
     rooflines = kernel_rooflines(stats, n_local, plan)
     dom = max(rooflines, key=lambda r: r["total_ms"])
@@ -450,6 +577,7 @@ def main():
                         3: "sampled below a constant key prefix"}.get(
                            plan, str(plan))),
         "verified": bool(ok),
+        "reference_check_2p24": med,
     }
     if last["exchanges"]:
         ex = sum(s["ms_exchange"] for s in stats) / len(stats) / max(last["exchanges"], 1)
@@ -459,10 +587,16 @@ def main():
                             "achieved_link_GBps": round(pair / (ex * 1e-3) / 1e9, 2) if ex else None,
                             "peak_link_GBps": XGMI_LINK_GBPS,
                             "frac": round(pair / (ex * 1e-3) / 1e9 / XGMI_LINK_GBPS, 4) if ex else None}
-    if rank == 0:
-        os.write(json_fd, (json.dumps(line) + "\n").encode())
     ctx.free(d_in)
     ctx.close()
+    if world == 1 and a.algo == "radix" and not a.no_dist_p1 and \
+            os.environ.get("GSORT_FORCE_DIST") != "1":
+        try:
+            line["dist_p1"] = dist_p1(gsort, n_local, dist_id, a.seed)
+        except Exception as e:  # reported, never fatal
+            line["dist_p1"] = {"error": repr(e)}
+    if rank == 0:
+        os.write(json_fd, (json.dumps(line) + "\n").encode())
     if world > 1:
         dist.destroy_process_group()
     if not ok:

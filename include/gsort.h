@@ -38,7 +38,7 @@ typedef enum {
     GSORT_ENOSAMPLE = 5, /* sample sort: a block is too small for 2P-1 regular samples;
                             the reference aborts with "no enough sample"
                             (mpi_sample_sort.c:94-99)                                      */
-    GSORT_ECOMM = 6      /* in-process rank group misuse / peer failure                   */
+    GSORT_ECOMM = 6      /* rank group (in-process or IPC) misuse / peer failure           */
 } gsort_status;
 
 /* Wraps an ncclUniqueId (rccl.h:43).  Rank 0 creates it, the host broadcasts it (MPI_Bcast in
@@ -75,8 +75,16 @@ typedef struct {
 enum { GSORT_LOCAL_MSD = 0, GSORT_LOCAL_LSD = 1 };
 
 /* ---- context -------------------------------------------------------------------------- */
+/* gsort_get_uid: an RCCL unique id (one process per GPU, xGMI between GPUs).
+ * gsort_get_uid_ipc: the id of a same-node process group of nranks processes that exchange
+ * through HIP IPC handles -- any number of ranks per GPU (RCCL refuses two ranks on one device),
+ * e.g. `mpirun -np 8` on a one-GPU node.  Rank 0 makes either id; every rank passes it to
+ * gsort_create.  gsort_visible_devices: HIP devices this process sees (0 on error). */
 gsort_status gsort_get_uid(gsort_uid *out);
-/* RCCL-backed context (one process per GPU).  nranks == 1 needs no uid (uid may be NULL).
+gsort_status gsort_get_uid_ipc(int nranks, gsort_uid *out);
+int gsort_visible_devices(void);
+/* Context of one rank (one process); the uid's kind picks the transport (RCCL or IPC group).
+ * nranks == 1 needs no uid (uid may be NULL).
  * hip_device >= 0 selects that GPU; hip_device = -1 - local_rank selects
  * local_rank % (visible GPUs), the usual one-rank-per-GPU placement.
  * Replaces MPI_Init/MPI_Comm_size/MPI_Comm_rank + the MPI communicator
@@ -166,7 +174,10 @@ gsort_status gsort_generate(gsort_ctx *ctx, int dist, uint64_t seed, uint64_t st
                             int32_t *d_out);
 gsort_status gsort_fingerprint(gsort_ctx *ctx, const int32_t *d_keys, size_t n, uint64_t *sum,
                                uint64_t *xr, int *sorted, int32_t *first, int32_t *last);
-/* Copy helpers for hosts that have no HIP headers (the C CLIs, ctypes). */
+/* Copy helpers for hosts that have no HIP headers (the C CLIs, ctypes).  Buffers from
+ * gsort_device_alloc belong to ctx: gsort_destroy releases every one still allocated (do not use
+ * them afterwards), and gsort_device_free accepts only pointers gsort_device_alloc returned on
+ * the same ctx (anything else returns GSORT_EINVAL and frees nothing). */
 gsort_status gsort_device_alloc(gsort_ctx *ctx, size_t bytes, void **d_ptr);
 gsort_status gsort_device_free(gsort_ctx *ctx, void *d_ptr);
 gsort_status gsort_copy_to_host(gsort_ctx *ctx, void *h_dst, const void *d_src, size_t bytes);
@@ -192,6 +203,32 @@ long long gsort_parse_text(const char *buf, size_t len, int32_t *out, size_t cap
  * Returns the byte count (out == NULL: only count), or -1 if cap is too small. */
 long long gsort_format_dump(const int32_t *keys, size_t n, uint64_t first_index, char *out,
                             size_t cap, int threads);
+
+/* gsort_write_report: the drop-in programs' stdout contract lines for one rank, written to fd
+ * (write(2); flush any stdio buffer on fd first), in the reference's order:
+ *   sample, rank 0:       "Each bucket will be put %llu items.\n", B = ceil(N/P)
+ *                         (mpi_sample_sort.c:72-74)
+ *   sample, debug >= 1:   rank 0 "[MASTER] Splitter: %u.\n" x (P-1) (:124); then every rank
+ *                         "[COMMON] r: Bucket j=len\n" for j < P (:156-158)
+ *   rank 0, the dump:     "%u|%u\n" index|key of sorted[0 .. N) at radix debug > 2
+ *                         (mpi_radix_sort.c:198-200) or sample debug >= 1 (sample:202-204)
+ *   rank 0:               "The n/2-th sorted element: %d\n" = sorted[N/2 - 1], sorted[0] for
+ *                         N = 1 (radix:201, sample:205; quirk Q14)
+ * The reference's other debug lines are free-form progress output, not reproduced.  splitters
+ * (rank 0, P-1) and bucket_counts (P) come from gsort_sample_info; sorted is rank 0's gathered
+ * array (gsort_gather_to_root).  Replaces the printf calls listed above. */
+enum { GSORT_REPORT_RADIX = 0, GSORT_REPORT_SAMPLE = 1 };
+typedef struct {
+    int algo;                      /* GSORT_REPORT_RADIX / GSORT_REPORT_SAMPLE               */
+    int rank, nranks, debug;       /* debug: the programs' argv[2] (0 when absent)            */
+    uint64_t n_total;              /* N                                                       */
+    const int32_t *splitters;      /* sample, debug >= 1, rank 0: P-1 splitters               */
+    const uint64_t *bucket_counts; /* sample, debug >= 1: this rank's P bucket lengths        */
+    const int32_t *sorted;         /* rank 0: the N sorted keys                               */
+    int stage;                     /* 0: every line; 1: only what the reference prints before
+                                      its sort ("Each bucket", sample:74); 2: only the rest     */
+} gsort_report;
+gsort_status gsort_write_report(const gsort_report *r, int fd);
 
 /* ---- host-only planning (no GPU; exported so CPU tests can check it) ----------------------
  * gsort_plan_radix_route: the K8 routing of one distributed LSD pass.  hist = P x 256 per-rank

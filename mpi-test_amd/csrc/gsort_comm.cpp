@@ -3,12 +3,19 @@
 
 #include "gsort_debug.h"
 
+#include <errno.h>
+#include <fcntl.h>
 #include <rccl/rccl.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <time.h>
+#include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <mutex>
@@ -273,5 +280,266 @@ class GroupComm : public Comm {
 };
 
 Comm *make_group_comm(GroupState *g, int rank) { return new GroupComm(g, rank); }
+
+}  // namespace gsort
+
+// ---------------------------------------------------------------------------------------
+// Same-node process group over HIP IPC (one process per rank, any number of ranks per GPU).
+// RCCL refuses two ranks on one device, so this is how `mpirun -np P radix_sort` runs the
+// distributed algorithm on a node with fewer GPUs than ranks (a one-GPU box in particular),
+// each rank its own process and context as with RCCL.  Keys move GPU to GPU: every collective
+// publishes the IPC handle of each rank's send buffer (+ offset, counts) in a POSIX shared-memory
+// control block, meets the others at a barrier, pulls what it needs with hipMemcpyAsync from the
+// opened peer buffers, synchronises, closes them and meets the others again (so no sender
+// reuses a buffer a peer is still reading) -- GroupComm's protocol across processes.  The uid
+// carries the control block's name; rank 0 creates it (gsort_get_uid_ipc) and unlinks it once
+// every rank has attached.
+// ---------------------------------------------------------------------------------------
+namespace gsort {
+namespace {
+
+constexpr char kIpcMagic[8] = {'G', 'S', 'I', 'P', 'C', 0, 0, 1};
+constexpr int kIpcMaxRanks = 64;
+constexpr size_t kIpcNameOff = 8, kIpcNameMax = 88, kIpcRanksOff = 96;
+
+struct IpcSlot {
+    hipIpcMemHandle_t handle;
+    uint64_t off;    // send pointer - allocation base
+    uint64_t valid;  // handle published (the rank sends something)
+    uint64_t count[kIpcMaxRanks], displ[kIpcMaxRanks];  // bytes to / offsets for each rank
+};
+struct IpcShared {
+    std::atomic<uint32_t> arrived, generation, broken, attached;
+    int32_t n;
+    IpcSlot slot[kIpcMaxRanks];
+};
+static_assert(std::atomic<uint32_t>::is_always_lock_free, "shared-memory atomics");
+
+std::mutex g_shm_mu;
+std::vector<std::string> g_shm_pending;  // created here, not yet unlinked (unlinked at exit)
+
+void unlink_pending() {
+    std::lock_guard<std::mutex> lk(g_shm_mu);
+    for (const auto &n : g_shm_pending) shm_unlink(n.c_str());
+    g_shm_pending.clear();
+}
+
+void forget_pending(const std::string &name) {
+    std::lock_guard<std::mutex> lk(g_shm_mu);
+    g_shm_pending.erase(std::remove(g_shm_pending.begin(), g_shm_pending.end(), name),
+                        g_shm_pending.end());
+}
+
+IpcShared *map_shared(const char *name, bool create, std::string *err) {
+    const int fd = shm_open(name, create ? O_RDWR | O_CREAT | O_EXCL : O_RDWR, 0600);
+    if (fd < 0) {
+        *err = std::string("shm_open ") + name + ": " + strerror(errno);
+        return nullptr;
+    }
+    if (create && ftruncate(fd, sizeof(IpcShared)) != 0) {
+        *err = std::string("ftruncate: ") + strerror(errno);
+        close(fd);
+        return nullptr;
+    }
+    void *p = mmap(nullptr, sizeof(IpcShared), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (p == MAP_FAILED) {
+        *err = std::string("mmap: ") + strerror(errno);
+        return nullptr;
+    }
+    return static_cast<IpcShared *>(p);
+}
+
+class IpcComm : public Comm {
+  public:
+    IpcComm(IpcShared *sh, int rank, int n) : sh_(sh) { rank_ = rank; size_ = n; }
+    ~IpcComm() override { munmap(sh_, sizeof(IpcShared)); }
+
+    // generation barrier in shared memory; a peer that does not arrive within 120 s breaks the
+    // group (every later collective fails instead of hanging)
+    bool barrier() {
+        if (sh_->broken.load()) return false;
+        const uint32_t gen = sh_->generation.load(std::memory_order_acquire);
+        if (sh_->arrived.fetch_add(1, std::memory_order_acq_rel) + 1 == (uint32_t)size_) {
+            sh_->arrived.store(0, std::memory_order_relaxed);
+            sh_->generation.fetch_add(1, std::memory_order_acq_rel);
+            return true;
+        }
+        const auto t0 = std::chrono::steady_clock::now();
+        for (uint64_t spin = 0; sh_->generation.load(std::memory_order_acquire) == gen; ++spin) {
+            if (sh_->broken.load()) return false;
+            if (spin < 2000) continue;
+            struct timespec ts = {0, 20000};
+            nanosleep(&ts, nullptr);
+            if ((spin & 1023) == 0 &&
+                std::chrono::steady_clock::now() - t0 > std::chrono::seconds(120)) {
+                sh_->broken.store(1);
+                return false;
+            }
+        }
+        return true;
+    }
+    gsort_status fail(const std::string &what) {
+        err = "ipc group: " + what;
+        return GSORT_ECOMM;
+    }
+    gsort_status hip(hipError_t e, const char *what) {
+        if (e == hipSuccess) return GSORT_OK;
+        err = std::string("ipc group: ") + what + ": " + hipGetErrorString(e);
+        return GSORT_EHIP;
+    }
+    // publish this rank's send buffer (the allocation's IPC handle + the offset into it)
+    gsort_status publish(const void *send, const size_t *count, const size_t *displ,
+                         size_t all_bytes) {
+        IpcSlot &me = sh_->slot[rank_];
+        me.valid = 0;
+        bool any = all_bytes != 0;
+        for (int q = 0; q < size_ && count; ++q) {
+            me.count[q] = count[q];
+            me.displ[q] = displ ? displ[q] : 0;
+            any = any || count[q];
+        }
+        if (!any || !send) return GSORT_OK;
+        void *base = nullptr;
+        size_t len = 0;
+        gsort_status st = hip(hipMemGetAddressRange(&base, &len, const_cast<void *>(send)),
+                              "hipMemGetAddressRange");
+        if (st == GSORT_OK) st = hip(hipIpcGetMemHandle(&me.handle, base), "hipIpcGetMemHandle");
+        if (st != GSORT_OK) return st;
+        me.off = (uint64_t)((const char *)send - (const char *)base);
+        me.valid = 1;
+        return GSORT_OK;
+    }
+    // the bytes [a, a + len) of rank r's send buffer into dst (opened peer buffers collected in
+    // opened, closed after the copies complete)
+    gsort_status pull(int r, const void *own, uint64_t a, size_t len, void *dst, hipStream_t s,
+                      std::vector<std::pair<int, void *>> &opened) {
+        if (!len) return GSORT_OK;
+        const char *src = nullptr;
+        if (r == rank_) {
+            src = static_cast<const char *>(own);
+        } else {
+            const IpcSlot &ps = sh_->slot[r];
+            if (!ps.valid) return fail("peer published no buffer");
+            void *p = nullptr;
+            for (auto &o : opened)
+                if (o.first == r) p = o.second;
+            if (!p) {
+                gsort_status st = hip(hipIpcOpenMemHandle(&p, ps.handle,
+                                                          hipIpcMemLazyEnablePeerAccess),
+                                      "hipIpcOpenMemHandle");
+                if (st != GSORT_OK) return st;
+                opened.push_back({r, p});
+            }
+            src = static_cast<const char *>(p) + ps.off;
+        }
+        return hip(hipMemcpyAsync(dst, src + a, len, hipMemcpyDeviceToDevice, s), "hipMemcpyAsync");
+    }
+    gsort_status finish(hipStream_t s, std::vector<std::pair<int, void *>> &opened,
+                        gsort_status st) {
+        gsort_status st2 = hip(hipStreamSynchronize(s), "hipStreamSynchronize");
+        for (auto &o : opened) (void)hipIpcCloseMemHandle(o.second);
+        if (!barrier()) return fail("barrier timeout");
+        return st != GSORT_OK ? st : st2;
+    }
+
+    gsort_status allgather(const void *send, void *recv, size_t bytes, hipStream_t s) override {
+        gsort_status st = hip(hipStreamSynchronize(s), "hipStreamSynchronize");
+        if (st == GSORT_OK) st = publish(send, nullptr, nullptr, bytes);
+        if (!barrier()) return fail("barrier timeout");
+        std::vector<std::pair<int, void *>> opened;
+        for (int r = 0; r < size_ && st == GSORT_OK; ++r)
+            st = pull(r, send, 0, bytes, (char *)recv + (size_t)r * bytes, s, opened);
+        return finish(s, opened, st);
+    }
+    gsort_status alltoallv(const void *send, const size_t *scount, const size_t *sdispl,
+                           void *recv, const size_t *rcount, const size_t *rdispl,
+                           hipStream_t s) override {
+        if (size_ > kIpcMaxRanks) return fail("too many ranks");
+        gsort_status st = hip(hipStreamSynchronize(s), "hipStreamSynchronize");
+        if (st == GSORT_OK) st = publish(send, scount, sdispl, 0);
+        if (!barrier()) return fail("barrier timeout");
+        std::vector<std::pair<int, void *>> opened;
+        for (int r = 0; r < size_ && st == GSORT_OK; ++r) {
+            const IpcSlot &ps = sh_->slot[r];
+            if (ps.count[rank_] != rcount[r]) { st = fail("send/recv count mismatch"); break; }
+            st = pull(r, send, ps.displ[rank_], rcount[r], (char *)recv + rdispl[r], s, opened);
+        }
+        return finish(s, opened, st);
+    }
+    gsort_status bcast(void *buf, size_t bytes, int root, hipStream_t s) override {
+        gsort_status st = hip(hipStreamSynchronize(s), "hipStreamSynchronize");
+        if (st == GSORT_OK && rank_ == root) st = publish(buf, nullptr, nullptr, bytes);
+        if (!barrier()) return fail("barrier timeout");
+        std::vector<std::pair<int, void *>> opened;
+        if (st == GSORT_OK && rank_ != root) st = pull(root, buf, 0, bytes, buf, s, opened);
+        return finish(s, opened, st);
+    }
+    // every rank has mapped the control block: its name can go
+    gsort_status attach(const std::string &name) {
+        sh_->attached.fetch_add(1);
+        if (!barrier()) return fail("not every rank attached within 120 s");
+        if (rank_ == 0) {
+            shm_unlink(name.c_str());
+            forget_pending(name);
+        }
+        return GSORT_OK;
+    }
+
+  private:
+    IpcShared *sh_;
+};
+
+}  // namespace
+
+bool is_ipc_uid(const gsort_uid *uid) {
+    return uid && memcmp(uid->internal, kIpcMagic, sizeof kIpcMagic) == 0;
+}
+
+gsort_status ipc_get_uid(int nranks, gsort_uid *out) {
+    if (nranks < 1 || nranks > kIpcMaxRanks) return GSORT_EINVAL;
+    static std::atomic<int> seq{0};
+    char name[kIpcNameMax];
+    const unsigned long long t =
+        (unsigned long long)std::chrono::steady_clock::now().time_since_epoch().count();
+    snprintf(name, sizeof name, "/gsort_ipc_%d_%d_%llx", (int)getpid(), seq++, t & 0xffffffffull);
+    std::string err;
+    IpcShared *sh = map_shared(name, true, &err);
+    if (!sh) return GSORT_ECOMM;
+    {
+        std::lock_guard<std::mutex> lk(g_shm_mu);
+        if (g_shm_pending.empty()) atexit(unlink_pending);
+        g_shm_pending.push_back(name);
+    }
+    memset(static_cast<void *>(sh), 0, sizeof(IpcShared));
+    sh->n = nranks;
+    munmap(sh, sizeof(IpcShared));
+    memset(out, 0, sizeof(*out));
+    memcpy(out->internal, kIpcMagic, sizeof kIpcMagic);
+    memcpy(out->internal + kIpcNameOff, name, strlen(name) + 1);
+    memcpy(out->internal + kIpcRanksOff, &nranks, sizeof nranks);
+    return GSORT_OK;
+}
+
+Comm *make_ipc_comm(int rank, int nranks, const gsort_uid *uid, std::string *err) {
+    int n = 0;
+    memcpy(&n, uid->internal + kIpcRanksOff, sizeof n);
+    if (n != nranks) {
+        *err = "ipc uid made for " + std::to_string(n) + " ranks, not " + std::to_string(nranks);
+        return nullptr;
+    }
+    char name[kIpcNameMax];
+    memcpy(name, uid->internal + kIpcNameOff, kIpcNameMax);
+    name[kIpcNameMax - 1] = 0;
+    IpcShared *sh = map_shared(name, false, err);
+    if (!sh) return nullptr;
+    IpcComm *c = new IpcComm(sh, rank, nranks);
+    if (c->attach(name) != GSORT_OK) {
+        *err = c->err;
+        delete c;
+        return nullptr;
+    }
+    return c;
+}
 
 }  // namespace gsort

@@ -1,12 +1,15 @@
 // gsort_comm.h -- the rank-to-rank transport of libgsort (internal).
 //
 // Replaces the reference's MPI point-to-point loops (mpi_radix_sort.c:150-173,
-// mpi_sample_sort.c:100-133, :160-170) and its rank-0 Scatter/Gather(v).  Two transports:
+// mpi_sample_sort.c:100-133, :160-170) and its rank-0 Scatter/Gather(v).  Three transports:
 //   RcclComm   one process per GPU, RCCL over xGMI: grouped ncclSend/ncclRecv for the
 //              all-to-all-v and the gather, ncclAllGather, ncclBroadcast.
 //   GroupComm  P contexts driven by P threads of one process (in-process rank group),
 //              moving bytes with device-to-device hipMemcpyAsync; lets the distributed
 //              algorithm run with P ranks on a single GPU.
+//   IpcComm    one process per rank on one node, any number of ranks per GPU: peers' buffers
+//              opened through HIP IPC handles, a POSIX shared-memory control block; lets the
+//              drop-in programs run under `mpirun -np P` with fewer GPUs than ranks.
 // Every call is collective over the P ranks and blocking on return w.r.t. `stream` ordering
 // (data is valid on `stream` when the call returns).  Byte counts are size_t.
 #pragma once
@@ -41,6 +44,11 @@ class Comm {
 
 Comm *make_rccl_comm(int rank, int nranks, const gsort_uid *uid, std::string *err);
 gsort_status rccl_get_uid(gsort_uid *out);
+// Same-node process group over HIP IPC (gsort_get_uid_ipc): one process per rank, any number
+// of ranks per GPU.
+bool is_ipc_uid(const gsort_uid *uid);
+gsort_status ipc_get_uid(int nranks, gsort_uid *out);
+Comm *make_ipc_comm(int rank, int nranks, const gsort_uid *uid, std::string *err);
 
 struct GroupState;  // opaque; gsort_group wraps it
 Comm *make_group_comm(GroupState *g, int rank);

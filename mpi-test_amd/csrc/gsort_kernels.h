@@ -218,15 +218,12 @@ hipError_t launch_pos_from_meta(const uint32_t *meta, const uint64_t *moff, uint
 // wl (next level: {bstart, len} segments; K11g classes: {h, len}).
 hipError_t launch_recv_classify(const uint64_t *pos, int P, uint64_t *bsize, uint64_t *bstart,
                                 const WorkLists &wl, uint64_t *scratch, hipStream_t s);
-// The two halves of launch_recv_classify, for the chunked receive of the distributed radix:
-// bucket sizes + starts, then the work lists of the buckets [h0, h1) only.
+// The two halves of launch_recv_classify (the distributed radix classifies only its own bucket
+// range): bucket sizes + starts, then the work lists of the buckets [h0, h1) only.
 hipError_t launch_recv_bounds(const uint64_t *pos, int P, uint64_t *bsize, uint64_t *bstart,
                               uint64_t *scratch, hipStream_t s);
 hipError_t launch_classify_range(const uint64_t *bsize, const uint64_t *bstart,
                                  const WorkLists &wl, uint32_t h0, uint32_t h1, hipStream_t s);
-// dst[i] = src[idx[i]], i < n
-hipError_t launch_pick_u64(const uint64_t *src, const uint64_t *idx, uint32_t n, uint64_t *dst,
-                           hipStream_t s);
 // K11g: gather the P pieces of every listed bucket (int32 keys, or packed16: the low 16 bits),
 // sort its low 16 bits in LDS, store int32 at out[bstart[h] ..).
 hipError_t launch_gather_sort(const void *recv, bool packed16, const uint64_t *pos,

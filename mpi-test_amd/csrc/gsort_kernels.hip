@@ -3162,22 +3162,6 @@ hipError_t launch_recv_classify(const uint64_t *pos, int P, uint64_t *bsize, uin
     return launch_classify_range(bsize, bstart, wl, 0, kBuckets16, s);
 }
 
-__global__ __launch_bounds__(256) void k_pick_u64(const unsigned long long *__restrict__ src,
-                                                  const unsigned long long *__restrict__ idx,
-                                                  uint32_t n, unsigned long long *__restrict__ dst) {
-    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-    if (i < n) dst[i] = src[idx[i]];
-}
-
-hipError_t launch_pick_u64(const uint64_t *src, const uint64_t *idx, uint32_t n, uint64_t *dst,
-                           hipStream_t s) {
-    using ull = unsigned long long;
-    if (n == 0) return hipSuccess;
-    launch_k(k_pick_u64, (n + 255) / 256, 256, 0, s, reinterpret_cast<const ull *>(src),
-             reinterpret_cast<const ull *>(idx), n, reinterpret_cast<ull *>(dst));
-    return hipGetLastError();
-}
-
 hipError_t launch_gather_sort(const void *recv, bool packed16, const uint64_t *pos,
                               const uint64_t *roff, int P, const uint64_t *bstart,
                               const uint64_t *list, uint32_t nlist, int cls, bool atomic_rank,

@@ -40,7 +40,6 @@ enum Phase { PH_COUNT, PH_PASS0, PH_PASS1, PH_PASS2, PH_PASS3, PH_EXCH, PH_PLACE
 
 constexpr size_t kSmallBytes = 256 * 1024;  // device + pinned scratch for counts, plans
 constexpr size_t kMailBytes = 4096;          // K12p mailbox: flag, then the counters (u64)
-constexpr int kMaxXChunks = 8;               // chunks of the distributed radix exchange
 
 struct DevBuf {
     void *p = nullptr;     // what the kernels use
@@ -83,6 +82,8 @@ struct gsort_ctx {
     int ncu = 256;
     int last_plan = 0;      // gsort_last_plan: 0 exact, 1 sampled, 2 sampled then exact
     DevBuf m_ex, m_ey, m_epart, m_eplan, m_edesc, m_edump;
+    bool est_busy = false;   // msd_sort_est is using m_ex / m_ey (not reclaimable)
+    size_t scratch_bytes = 0;  // device bytes held by ensure()-managed scratch
     // K12p mailbox: pinned host memory the GPU writes the work-list counters into, then a
     // sequence number (polled by the host: no copy or event on the stream)
     uint64_t *h_mail = nullptr, *d_mail = nullptr;
@@ -92,10 +93,6 @@ struct gsort_ctx {
     DevBuf m_rpos, m_bsize;  // receive side: run bucket bounds (P x 65537), bucket size/start
     DevBuf m_bseg, m_blist;  // boundary groups of the distributed radix: scratch, K11 list
     DevBuf m_gb, m_pack, m_meta, m_g16;  // packed exchange: bucket bounds, low 16 bits, counts
-    // chunked exchange of the distributed radix: the stream the chunks' RCCL transfers run on
-    // (high priority) and the event each chunk's arrival sets (created on first use)
-    hipStream_t xstream = nullptr;
-    hipEvent_t ev_x[kMaxXChunks + 1] = {};
     // device small area: [0, 8K) hist4 (4x256 u64) | [8K, 10K) pass digit totals (256 u64) |
     // [10K, 12K) pass digit bases (256 u64) | [20K, 256K) plans / samples / routing tables
     DevBuf small;               // kSmallBytes; d_small aliases small.p
@@ -167,7 +164,9 @@ gsort_status comm_try(gsort_ctx *c, gsort_status st) {
     return st;
 }
 
-// GSORT_ALLOC_LIMIT=bytes (diagnostics): refuse any larger scratch allocation, naming the buffer
+// GSORT_ALLOC_LIMIT=bytes (diagnostics): refuse any larger scratch allocation, naming the buffer;
+// GSORT_ALLOC_TOTAL=bytes: refuse a scratch allocation that would take the context's scratch
+// past that many bytes (a device with less free memory, for tests)
 std::string buf_name(gsort_ctx *c, const DevBuf &b);
 
 // Device allocation of `want` usable bytes (+ guards with GSORT_CANARY).  Returns the HIP error.
@@ -371,23 +370,58 @@ gsort_status alloc_err(gsort_ctx *c, hipError_t e, size_t want, const std::strin
     return set_err(c, e == hipErrorOutOfMemory ? GSORT_ENOMEM : GSORT_EHIP, msg);
 }
 
+// The sampled plan's region buffers (~2.9x the block) stay allocated between sorts; when some
+// other scratch allocation finds no room they are dropped (and re-made by the next sampled
+// sort), unless the plan is using them right now.
+bool reclaim_regions(gsort_ctx *c, const DevBuf &asking) {
+    if (c->est_busy) return false;
+    bool freed = false;
+    for (DevBuf *r : {&c->m_ex, &c->m_ey}) {
+        if (r == &asking || !r->p) continue;
+        c->scratch_bytes -= std::min(c->scratch_bytes, r->cap);
+        (void)dev_free(*r);
+        freed = true;
+    }
+    return freed;
+}
+
 gsort_status ensure(gsort_ctx *c, DevBuf &b, size_t bytes) {
     if (bytes <= b.cap) return GSORT_OK;
     static const unsigned long long limit =
         getenv("GSORT_ALLOC_LIMIT") ? strtoull(getenv("GSORT_ALLOC_LIMIT"), nullptr, 0) : 0ull;
+    static const unsigned long long total =
+        getenv("GSORT_ALLOC_TOTAL") ? strtoull(getenv("GSORT_ALLOC_TOTAL"), nullptr, 0) : 0ull;
     if (limit && bytes > limit)
         return set_err(c, GSORT_ENOMEM, "allocation of " + std::to_string(bytes) +
                                             " bytes for " + buf_name(c, b) +
                                             " over GSORT_ALLOC_LIMIT (rank " +
                                             std::to_string(c->rank) + ")");
+    c->scratch_bytes -= std::min(c->scratch_bytes, b.cap);
     hipError_t e = dev_free(b);
     if (e != hipSuccess)
         return set_err(c, GSORT_EHIP, "hipFree of " + buf_name(c, b) + " (rank " +
                                           std::to_string(c->rank) + "): " + hipGetErrorString(e));
     const size_t want = (bytes + alloc_align() - 1) & ~(alloc_align() - 1);
-    e = dev_malloc(b, want, buf_name(c, b));
-    if (e != hipSuccess) return alloc_err(c, e, want, buf_name(c, b));
-    return GSORT_OK;
+    for (int attempt = 0;; ++attempt) {
+        const bool refused = total && c->scratch_bytes + want > total;
+        if (!refused) {
+            e = dev_malloc(b, want, buf_name(c, b));
+            if (e == hipSuccess) {
+                c->scratch_bytes += want;
+                return GSORT_OK;
+            }
+        }
+        if ((refused || e == hipErrorOutOfMemory) && attempt == 0 && reclaim_regions(c, b)) {
+            (void)hipGetLastError();
+            continue;
+        }
+        if (refused)
+            return set_err(c, GSORT_ENOMEM, "allocation of " + std::to_string(want) +
+                                                " bytes for " + buf_name(c, b) +
+                                                " over GSORT_ALLOC_TOTAL (rank " +
+                                                std::to_string(c->rank) + ")");
+        return alloc_err(c, e, want, buf_name(c, b));
+    }
 }
 
 template <class T>
@@ -646,15 +680,6 @@ gsort_status check_all_guards(gsort_ctx *c, const char *where) {
 
 // GSORT_CHECK=1 (diagnostics): host-side invariant checks between the distributed phases, so
 // a broken count fails the call with a message instead of sizing buffers or launches from it
-// GSORT_XCHUNKS: chunks of the distributed radix exchange (1 .. kMaxXChunks, the same on every
-// rank).  Default 1: on one MI355X (1-rank RCCL) 4 chunks overlapped with the receive sort took
-// 2.91 ms per 2^28 keys against 2.36 ms unchunked -- the RCCL copies starve beside K11g
-// (DESIGN.md 6); chunking stays selectable for multi-GPU nodes, where it is unmeasured.
-int x_chunks() {
-    const char *e = getenv("GSORT_XCHUNKS");  // read per sort (tests switch it in-process)
-    return std::min(std::max(e ? atoi(e) : 1, 1), kMaxXChunks);
-}
-
 bool check_mode() {
     static const bool on = getenv("GSORT_CHECK") && atoi(getenv("GSORT_CHECK"));
     return on;
@@ -959,24 +984,36 @@ gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
     const uint64_t capx = est_region_keys(n, (uint64_t)kH16Shards * kRadix, slack);
     const uint64_t capy = std::min<uint64_t>(est_region_keys(n, kBuckets16, slack),
                                              (uint64_t)kBuckets16 * kLocalMax);
-    // the region buffers are the plan's only large allocations: without room for them the
-    // exact plan sorts (it needs none), and the memory is handed back
-    for (DevBuf *b : {&c->m_ex, &c->m_ey}) {
-        const gsort_status st = ensure(c, *b, (b == &c->m_ex ? capx : capy) * 4);
+    // the region buffers are the plan's only large allocations: without room for them (or for
+    // its small plan arrays) the exact plan sorts (it needs none of them), and the regions are
+    // handed back
+    constexpr size_t kPlanWords = (size_t)4 * kBuckets16 + 4 * kH16Shards * kRadix + kRadix + 1;
+    {
+        gsort_status st = GSORT_OK;
+        for (DevBuf *b : {&c->m_ex, &c->m_ey})
+            if (st == GSORT_OK) st = ensure(c, *b, (b == &c->m_ex ? capx : capy) * 4);
+        if (st == GSORT_OK)
+            st = ensure(c, c->m_epart,
+                        (size_t)kEstWGs * (kBuckets16 / 4 + kH16Shards * kRadix + 4) * 4);
+        if (st == GSORT_OK) st = ensure(c, c->m_eplan, kPlanWords * 4 + 4 * kRadix * 8 + 64);
+        if (st == GSORT_OK)
+            st = ensure(c, c->m_edesc,
+                        ((size_t)est_max_tiles(n) + kH16Shards * kRadix) * kTileDescBytes);
+        if (st == GSORT_OK) st = ensure(c, c->m_edump, (size_t)kSweepTile * 4);
+        for (int k = 0; k < kLocalClasses && st == GSORT_OK; ++k)
+            st = ensure_list(c, c->m_local[k], kBuckets16);
         if (st == GSORT_ENOMEM) {
-            (void)dev_free(c->m_ex);
-            (void)dev_free(c->m_ey);
+            (void)reclaim_regions(c, DevBuf{});
             c->err.clear();
             return GSORT_OK;  // *ok stays false
         }
         ST_TRY(st);
     }
-    ST_TRY(ensure(c, c->m_epart, (size_t)kEstWGs * (kBuckets16 / 4 + kH16Shards * kRadix + 4) * 4));
-    constexpr size_t kPlanWords = (size_t)4 * kBuckets16 + 4 * kH16Shards * kRadix + kRadix + 1;
-    ST_TRY(ensure(c, c->m_eplan, kPlanWords * 4 + 4 * kRadix * 8 + 64));
-    ST_TRY(ensure(c, c->m_edesc, ((size_t)est_max_tiles(n) + kH16Shards * kRadix) * kTileDescBytes));
-    ST_TRY(ensure(c, c->m_edump, (size_t)kSweepTile * 4));
-    for (int k = 0; k < kLocalClasses; ++k) ST_TRY(ensure_list(c, c->m_local[k], kBuckets16));
+    struct Busy {
+        bool &f;
+        explicit Busy(bool &x) : f(x) { f = true; }
+        ~Busy() { f = false; }
+    } busy(c->est_busy);
     EstPlan p{};
     p.in = in;
     p.n = n;
@@ -1134,8 +1171,9 @@ gsort_status msd_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *ou
         // and -- when the first sample's child counts are known (no u8 counter wrapped) -- the
         // largest one now (~64 keys per sample) split 2^shift ways stays below 5/8 of it.  The
         // prefix retry costs a failed sample when wrong; the offset retry also a read pass, so
-        // it needs known counts (peaked inputs -- Gaussian keys -- fail it: their densest
-        // child stays too large after any shift).
+        // it needs known counts (no u8 counter wrapped) and a fit after the shift -- e.g.
+        // Gaussian keys pass it (profiles/r02_v18_dist_probe.txt, plan 3), Zipf keys, whose
+        // densest child holds ~29 % of the block, do not.
         const bool known = r.maxc != 0xffffffffu;
         auto fits = [&](int lead) {
             const int sb = std::min(lead, 16);
@@ -1164,6 +1202,11 @@ gsort_status msd_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *ou
                 if (lead == 32) {  // one value: the sorted block is the block
                     HIP_TRY(c, hipMemcpyAsync(out, in, n * 4, hipMemcpyDeviceToDevice, c->stream));
                     ok = true;
+                    if (stats) {  // one bucket, finished without a partition level
+                        stats->passes_run = 0;
+                        stats->buckets_local += 1;
+                        stats->keys_bucket_sort += n;
+                    }
                 } else if (lead >= 3 && fits(lead)) {
                     ST_TRY(msd_sort_est(c, in, n, out, stats, &ok, std::min(lead, 16), lo));
                 }
@@ -1188,6 +1231,10 @@ gsort_status msd_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *ou
         toc(c, PH_BUCKET, t);
         if (stats) { stats->buckets_local += 1; stats->keys_bucket_sort += n; }
         return GSORT_OK;
+    }
+    if (!tmp) {  // the exact plans' ping-pong buffer, allocated only when one of them runs
+        ST_TRY(ensure(c, c->slot[S_TMP], n * 4));
+        tmp = slot_ptr<uint32_t>(c, S_TMP);
     }
     if (c->plan16 && (!group16 || out16) && n < (1ull << 32)) {
         const int lp = c->last_plan;
@@ -1226,11 +1273,18 @@ gsort_status msd_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *ou
     return GSORT_OK;
 }
 
+// tmp == nullptr: S_TMP, ensured only if the plan that runs needs a second buffer
 gsort_status local_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *out,
                         uint32_t *tmp, int *passes_run, gsort_stats *stats = nullptr,
                         bool allow_est = false) {
     if (stats) stats->local_algo = c->local_algo;
-    if (c->local_algo == GSORT_LOCAL_LSD) return lsd_sort(c, in, n, out, tmp, passes_run);
+    if (c->local_algo == GSORT_LOCAL_LSD) {
+        if (!tmp) {
+            ST_TRY(ensure(c, c->slot[S_TMP], std::max<uint64_t>(n, 1) * 4));
+            tmp = slot_ptr<uint32_t>(c, S_TMP);
+        }
+        return lsd_sort(c, in, n, out, tmp, passes_run);
+    }
     gsort_stats tmp_st;
     memset(&tmp_st, 0, sizeof(tmp_st));
     gsort_stats *st = stats ? stats : &tmp_st;
@@ -1613,34 +1667,8 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
             if (recv[q]) { rc[q] = nh[me] * 4; rd[q] = ro * 4; ro += nh[me]; }
         }
     }
-    // (5a) the chunk plan.  Chunk k of destination q = its buckets [hbq(q, k), hbq(q, k + 1)):
-    // the sender and the receiver split q's bucket range identically, so chunk k of the run
-    // p -> q is pack[max(cut, gb[hbq]) ..) on the sender and pos[p][hbq] on the receiver.
-    const int C = x_chunks();
-    auto hbq = [&](int q, int k) -> uint64_t { return hlo[q] + nh[q] * (uint64_t)k / C; };
     std::vector<uint64_t> roffs(P + 1, 0);
     for (int p = 0; p < P; ++p) roffs[p + 1] = roffs[p] + recv[p];
-    uint64_t *h_pl = reinterpret_cast<uint64_t *>(c->h_small + OFF_PLAN);
-    uint64_t *d_pl = reinterpret_cast<uint64_t *>(c->d_small + OFF_PLAN);
-    // OFF_PLAN: [0, 2P) run offsets + lengths (u64) | +1 KiB: pick indices | +8 KiB: picked
-    // values | +16 KiB: the chunks' work-list counters
-    constexpr size_t kPickIdx = 1024 / 8, kPicked = 8192 / 8, kChunkCtr = 16384;
-    uint64_t *d_r = d_pl;
-    uint32_t npick_s = 0, npick = 0;
-    {
-        for (int p = 0; p < P; ++p) { h_pl[p] = roffs[p]; h_pl[P + p] = recv[p]; }
-        uint64_t *idx = h_pl + kPickIdx;
-        for (int q = 0; q < P; ++q)
-            if (send[q])
-                for (int k = 1; k < C; ++k) idx[npick++] = hbq(q, k);
-        npick_s = npick;
-        for (int p = 0; p < P; ++p)
-            if (recv[p])
-                for (int k = 1; k < C; ++k) idx[npick++] = (uint64_t)p * (kBuckets16 + 1) + hbq(me, k);
-        static_assert(2 * 64 * (kMaxXChunks - 1) <= kPicked - kPickIdx, "pick area");
-        HIP_TRY(c, hipMemcpyAsync(d_pl, h_pl, (kPickIdx + npick) * 8, hipMemcpyHostToDevice,
-                                  c->stream));
-    }
     t = tic_rec(c);
     ST_TRY(comm_try(c, c->comm->alltoallv(meta_s, sc.data(), sd.data(), meta_r, rc.data(),
                                           rd.data(), c->stream)));
@@ -1651,21 +1679,21 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
             stats->max_pair_bytes = std::max<uint64_t>(stats->max_pair_bytes, send[q] * 2);
         }
     if (roffs[P] != mine) return set_err(c, GSORT_EINVAL, "exchange plan does not fill the block");
+    // the payload, queued right behind the counts: the receive plan below overlaps it
     uint16_t *rbuf = slot_ptr<uint16_t>(c, S_RECV);
-    if (C == 1) {  // one exchange, queued behind the counts: the plan below overlaps it
-        t = tic_rec(c);
-        for (int q = 0; q < P; ++q) {
-            sc[q] = send[q] * 2;
-            sd[q] = cut[q] * 2;
-            rc[q] = recv[q] * 2;
-            rd[q] = roffs[q] * 2;
-        }
-        ST_TRY(comm_try(c, c->comm->alltoallv(pack, sc.data(), sd.data(), rbuf, rc.data(),
-                                              rd.data(), c->stream)));
-        toc_rec(c, PH_EXCH, t);
+    t = tic_rec(c);
+    for (int q = 0; q < P; ++q) {
+        sc[q] = send[q] * 2;
+        sd[q] = cut[q] * 2;
+        rc[q] = recv[q] * 2;
+        rd[q] = roffs[q] * 2;
     }
-    // (5b) the receive plan from the counts alone: run bounds, bucket starts, and the K11g / K18
-    // work lists of every chunk (list entries of chunk k from entry hbq(me, k) - hlo[me] on)
+    ST_TRY(comm_try(c, c->comm->alltoallv(pack, sc.data(), sd.data(), rbuf, rc.data(), rd.data(),
+                                          c->stream)));
+    toc_rec(c, PH_EXCH, t);
+    if (stats) stats->exchanges = 1;
+    // (5) the receive plan from the counts alone: run bounds, bucket starts, the K11g / K18
+    // work lists of this rank's bucket range
     t = tic(c);
     ST_TRY(ensure(c, c->m_rpos, (size_t)P * (kBuckets16 + 1) * 8));
     ST_TRY(ensure(c, c->m_bsize, kBsizeBytes));
@@ -1673,127 +1701,52 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
     for (auto &b : c->m_local) ST_TRY(ensure_list(c, b, kBuckets16));
     uint64_t *pos = reinterpret_cast<uint64_t *>(c->m_rpos.p);
     uint64_t *bsize = reinterpret_cast<uint64_t *>(c->m_bsize.p), *bstart = bsize + kBuckets16;
-    uint64_t *cctr = reinterpret_cast<uint64_t *>(c->d_small + OFF_PLAN + kChunkCtr);
+    uint64_t *h_r = reinterpret_cast<uint64_t *>(c->h_small + OFF_PLAN);
+    uint64_t *d_r = reinterpret_cast<uint64_t *>(c->d_small + OFF_PLAN);
+    HIP_TRY(c, hipStreamSynchronize(c->stream));  // h_r may still feed an earlier copy
+    for (int p = 0; p < P; ++p) { h_r[p] = roffs[p]; h_r[P + p] = recv[p]; }
+    HIP_TRY(c, hipMemcpyAsync(d_r, h_r, (size_t)2 * P * 8, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(c, launch_pos_from_meta(meta_r, d_moff, (uint32_t)hlo[me], (uint32_t)nh[me], P, pos,
                                     bstart + kBuckets16 + 1, c->stream));
-    HIP_TRY(c, hipMemsetAsync(cctr, 0, (size_t)C * kCtrBytes, c->stream));
+    HIP_TRY(c, hipMemsetAsync(c->d_small + OFF_CTR, 0, kCtrBytes, c->stream));
     HIP_TRY(c, launch_recv_bounds(pos, P, bsize, bstart, bstart + kBuckets16 + 1, c->stream));
-    auto chunk_lists = [&](int k) {
-        WorkLists wl = work_lists(c, 0);
-        const uint64_t off = 2 * (hbq(me, k) - hlo[me]);
-        for (auto &l : wl.list) l += off;
-        wl.ctr = cctr + (size_t)k * (kCtrBytes / 8);
-        return wl;
-    };
-    for (int k = 0; k < C; ++k)
-        HIP_TRY(c, launch_classify_range(bsize, bstart, chunk_lists(k), (uint32_t)hbq(me, k),
-                                         (uint32_t)hbq(me, k + 1), c->stream));
-    HIP_TRY(c, launch_pick_u64(gb, d_pl + kPickIdx, npick_s, d_pl + kPicked, c->stream));
-    HIP_TRY(c, launch_pick_u64(pos, d_pl + kPickIdx + npick_s, npick - npick_s,
-                               d_pl + kPicked + npick_s, c->stream));
+    const WorkLists wl = work_lists(c, 0);
+    HIP_TRY(c, launch_classify_range(bsize, bstart, wl, (uint32_t)hlo[me],
+                                     (uint32_t)(hlo[me] + nh[me]), c->stream));
     toc(c, PH_COUNT, t);
-    HIP_TRY(c, hipMemcpyAsync(h_pl + kPicked, d_pl + kPicked, npick * 8, hipMemcpyDeviceToHost,
-                              c->stream));
-    HIP_TRY(c, hipMemcpyAsync(c->h_small + OFF_PLAN + kChunkCtr, cctr, (size_t)C * kCtrBytes,
-                              hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
-    std::vector<uint64_t> hc((size_t)C * (kCtrBytes / 8));
-    memcpy(hc.data(), c->h_small + OFF_PLAN + kChunkCtr, (size_t)C * kCtrBytes);
+    uint64_t h[3 * (kLocalClasses + 1)];
+    ST_TRY(read_counters(c, h));
     if (check_mode()) {
         for (int p = 0; p < P; ++p)
             ST_TRY(check_bounds(c, pos + (size_t)p * (kBuckets16 + 1), kBuckets16 + 1, recv[p],
                                 "received run bounds"));
         uint64_t keys = 0;
-        for (int k = 0; k < C; ++k)
-            for (int l = 0; l <= kLocalClasses; ++l) keys += hc[(size_t)k * (kCtrBytes / 8) + 3 * l + 1];
+        for (int l = 0; l <= kLocalClasses; ++l) keys += h[3 * l + 1];
         if (keys != mine)
-            return set_err(c, GSORT_EINVAL, "GSORT_CHECK chunk lists hold " + std::to_string(keys) +
-                                                " keys, want " + std::to_string(mine) + " (rank " +
+            return set_err(c, GSORT_EINVAL, "GSORT_CHECK receive lists hold " +
+                                                std::to_string(keys) + " keys, want " +
+                                                std::to_string(mine) + " (rank " +
                                                 std::to_string(me) + ")");
     }
-    bool big = false;  // a bucket past K18's reach: the unchunked receive (MSD levels 1, 0)
-    for (int k = 0; k < C; ++k) {
-        const uint64_t *h = &hc[(size_t)k * (kCtrBytes / 8)];
-        big = big || (h[0] && h[2] > kHxMax);
-    }
-    // the cut of every destination's run per chunk (sender) and of every source's (receiver)
-    std::vector<uint64_t> s_off((size_t)P * (C + 1)), r_off((size_t)P * (C + 1));
-    {
-        const uint64_t *pk = h_pl + kPicked;
-        uint32_t i = 0;
-        for (int q = 0; q < P; ++q) {
-            uint64_t *so = &s_off[(size_t)q * (C + 1)];
-            so[0] = cut[q];
-            so[C] = cut[q + 1];
-            for (int k = 1; k < C; ++k)
-                so[k] = send[q] ? std::min(std::max(pk[i++], so[k - 1]), cut[q + 1]) : cut[q];
-        }
-        for (int p = 0; p < P; ++p) {
-            uint64_t *ro = &r_off[(size_t)p * (C + 1)];
-            ro[0] = 0;
-            ro[C] = recv[p];
-            for (int k = 1; k < C; ++k)
-                ro[k] = recv[p] ? std::min(std::max(pk[i++], ro[k - 1]), recv[p]) : 0;
-        }
-    }
-    const int CX = C == 1 ? 0 : big ? 1 : C;  // exchanges still to issue on xstream
-    if (CX && !c->xstream) {
-        int lo = 0, hi = 0;
-        HIP_TRY(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
-        HIP_TRY(c, hipStreamCreateWithPriority(&c->xstream, hipStreamNonBlocking, hi));
-        for (auto &e : c->ev_x) HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    }
-    // (4) the keys' low 16 bits, chunk by chunk on xstream once the pack and the plan are done
-    hipEvent_t xa = nullptr;
-    if (CX) {
-        HIP_TRY(c, hipEventRecord(c->ev_x[kMaxXChunks], c->stream));
-        HIP_TRY(c, hipStreamWaitEvent(c->xstream, c->ev_x[kMaxXChunks], 0));
-        if (c->timing && (xa = next_event(c))) HIP_TRY(c, hipEventRecord(xa, c->xstream));
-    }
-    for (int k = 0; k < CX; ++k) {
-        const int k1 = big ? C : k + 1;
-        for (int q = 0; q < P; ++q) {
-            const uint64_t *so = &s_off[(size_t)q * (C + 1)], *ro = &r_off[(size_t)q * (C + 1)];
-            sc[q] = (so[k1] - so[k]) * 2;
-            sd[q] = so[k] * 2;
-            rc[q] = (ro[k1] - ro[k]) * 2;
-            rd[q] = (roffs[q] + ro[k]) * 2;
-        }
-        ST_TRY(comm_try(c, c->comm->alltoallv(pack, sc.data(), sd.data(), rbuf, rc.data(),
-                                              rd.data(), c->xstream)));
-        if (xa && k == CX - 1) {  // before the last arrival event, so complete when it is
-            hipEvent_t xb = next_event(c);
-            if (xb && hipEventRecord(xb, c->xstream) == hipSuccess)
-                c->spans.push_back({PH_EXCH, xa, xb});
-        }
-        HIP_TRY(c, hipEventRecord(c->ev_x[k], c->xstream));
-    }
-    if (stats) stats->exchanges = 1;
-    // (5c) chunk k's buckets are sorted (K11g by size class, K18 past kLocalMax) as soon as
-    // chunk k has arrived, while the next chunks are in flight
+    // (6) every bucket sorted from its P pieces: K11g by size class, K18 past kLocalMax; a
+    // bucket past K18's reach sends the block through recv_sort's MSD levels 1 and 0
     t = tic(c);
     uint32_t *out = slot_ptr<uint32_t>(c, S_OUT);
-    if (big) {
-        if (CX) HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_x[0], 0));
+    if (h[0] && h[2] > kHxMax) {
         ST_TRY(recv_sort(c, rbuf, true, recv, mine, out, slot_ptr<uint32_t>(c, S_TMP), stats));
     } else {
-        for (int k = 0; k < C; ++k) {
-            if (CX) HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_x[k], 0));
-            const uint64_t *h = &hc[(size_t)k * (kCtrBytes / 8)];
-            const WorkLists wl = chunk_lists(k);
-            for (int cl = 0; cl < kLocalClasses; ++cl) {
-                const uint64_t *hk = h + 3 * (cl + 1);
-                if (!hk[0]) continue;
-                HIP_TRY(c, launch_gather_sort(rbuf, true, pos, d_r, P, bstart, wl.list[cl + 1],
-                                              (uint32_t)hk[0], cl + 1, c->atomic_rank, out,
-                                              c->stream));
-                if (stats) { stats->buckets_local += hk[0]; stats->keys_bucket_sort += hk[1]; }
-            }
-            if (h[0]) {
-                HIP_TRY(c, launch_hist_expand(rbuf, true, pos, d_r, P, bstart, wl.list[0],
-                                              (uint32_t)h[0], out, c->stream));
-                if (stats) { stats->buckets_local += h[0]; stats->keys_bucket_sort += h[1]; }
-            }
+        for (int cl = 0; cl < kLocalClasses; ++cl) {
+            const uint64_t *hk = h + 3 * (cl + 1);
+            if (!hk[0]) continue;
+            HIP_TRY(c, launch_gather_sort(rbuf, true, pos, d_r, P, bstart, wl.list[cl + 1],
+                                          (uint32_t)hk[0], cl + 1, c->atomic_rank, out,
+                                          c->stream));
+            if (stats) { stats->buckets_local += hk[0]; stats->keys_bucket_sort += hk[1]; }
+        }
+        if (h[0]) {
+            HIP_TRY(c, launch_hist_expand(rbuf, true, pos, d_r, P, bstart, wl.list[0],
+                                          (uint32_t)h[0], out, c->stream));
+            if (stats) { stats->buckets_local += h[0]; stats->keys_bucket_sort += h[1]; }
         }
     }
     toc(c, PH_MERGE, t);
@@ -2066,12 +2019,10 @@ gsort_status sample_dist(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in, int
                                std::to_string((uint64_t)(k - 1) * interval));
     const uint64_t cap = std::max<uint64_t>(n_in, 1);
     ST_TRY(ensure(c, c->slot[S_SORTED], cap * 4));
-    ST_TRY(ensure(c, c->slot[S_TMP], cap * 4));
     int32_t *sorted = slot_ptr<int32_t>(c, S_SORTED);
     int pr = 0;
     ST_TRY(local_sort(c, reinterpret_cast<const uint32_t *>(d_keys), n_in,
-                      reinterpret_cast<uint32_t *>(sorted), slot_ptr<uint32_t>(c, S_TMP), &pr,
-                      nullptr, true));
+                      reinterpret_cast<uint32_t *>(sorted), nullptr, &pr, nullptr, true));
 
     // K4 samples -> root (grouped send/recv), K5 on root, broadcast splitters
     hipEvent_t t = tic_rec(c);
@@ -2262,7 +2213,7 @@ const char *gsort_strerror(gsort_status st) {
         case GSORT_EHIP: return "HIP error";
         case GSORT_ERCCL: return "RCCL error";
         case GSORT_ENOSAMPLE: return "not enough keys for regular sampling";
-        case GSORT_ECOMM: return "in-process group error";
+        case GSORT_ECOMM: return "rank group error";
     }
     return "unknown status";
 }
@@ -2286,6 +2237,20 @@ gsort_status gsort_get_uid(gsort_uid *out) {
     return rccl_get_uid(out);
 }
 
+gsort_status gsort_get_uid_ipc(int nranks, gsort_uid *out) {
+    if (!out) return GSORT_EINVAL;
+    return ipc_get_uid(nranks, out);
+}
+
+int gsort_visible_devices(void) {
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return count;
+}
+
 gsort_status gsort_create(gsort_ctx **ctx, int rank, int nranks, int hip_device,
                           const gsort_uid *uid) {
     if (!ctx || nranks < 1 || rank < 0 || rank >= nranks || (nranks > 1 && !uid))
@@ -2297,8 +2262,9 @@ gsort_status gsort_create(gsort_ctx **ctx, int rank, int nranks, int hip_device,
     gsort_status st = create_common(c, hip_device);
     if (st == GSORT_OK && (nranks > 1 || (force_dist() && uid))) {
         std::string e;
-        c->comm = make_rccl_comm(rank, nranks, uid, &e);
-        if (!c->comm) st = set_err(c, GSORT_ERCCL, e);
+        const bool ipc = is_ipc_uid(uid);
+        c->comm = ipc ? make_ipc_comm(rank, nranks, uid, &e) : make_rccl_comm(rank, nranks, uid, &e);
+        if (!c->comm) st = set_err(c, ipc ? GSORT_ECOMM : GSORT_ERCCL, e);
     }
     if (st != GSORT_OK) {
         fprintf(stderr, "gsort_create: %s\n", c->err.c_str());
@@ -2344,7 +2310,6 @@ gsort_status gsort_destroy(gsort_ctx *c) {
     }
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    if (c->xstream) (void)hipStreamSynchronize(c->xstream);
     delete c->comm;
     for_each_buf(c, [](const std::string &, DevBuf &b) { (void)dev_free(b); });
     c->d_small = nullptr;
@@ -2355,9 +2320,6 @@ gsort_status gsort_destroy(gsort_ctx *c) {
     if (c->h_small) (void)hipHostFree(c->h_small);
     if (c->h_mail) (void)hipHostFree(c->h_mail);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
-    for (auto e : c->ev_x)
-        if (e) (void)hipEventDestroy(e);
-    if (c->xstream) (void)hipStreamDestroy(c->xstream);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return GSORT_OK;
@@ -2410,13 +2372,10 @@ gsort_status gsort_radix(gsort_ctx *c, const int32_t *d_keys, size_t n_local, in
     if (c->ref_compat) {
         st = radix_compat(c, d_keys, n_local, d_out, &nout, stats);
     } else if (!c->comm) {
-        const size_t cap = std::max<size_t>(n_local, 1) * 4;
-        ST_TRY(ensure(c, c->slot[S_TMP], cap));
-        ST_TRY(ensure(c, c->slot[S_OUT], cap));
+        ST_TRY(ensure(c, c->slot[S_OUT], std::max<size_t>(n_local, 1) * 4));
         int pr = 0;
         st = local_sort(c, reinterpret_cast<const uint32_t *>(d_keys), n_local,
-                        slot_ptr<uint32_t>(c, S_OUT), slot_ptr<uint32_t>(c, S_TMP), &pr, stats,
-                        true);
+                        slot_ptr<uint32_t>(c, S_OUT), nullptr, &pr, stats, true);
         if (stats) stats->passes_run = pr;
         *d_out = slot_ptr<int32_t>(c, S_OUT);
         nout = n_local;
@@ -2448,13 +2407,10 @@ gsort_status gsort_sample(gsort_ctx *c, const int32_t *d_keys, size_t n_local, i
     uint64_t nout = 0;
     if (!c->comm) {
         // one rank: no splitters, one bucket (the reference reads splitters[-1] here, Q10)
-        const size_t cap = std::max<size_t>(n_local, 1) * 4;
-        ST_TRY(ensure(c, c->slot[S_TMP], cap));
-        ST_TRY(ensure(c, c->slot[S_OUT], cap));
+        ST_TRY(ensure(c, c->slot[S_OUT], std::max<size_t>(n_local, 1) * 4));
         int pr = 0;
         ST_TRY(local_sort(c, reinterpret_cast<const uint32_t *>(d_keys), n_local,
-                          slot_ptr<uint32_t>(c, S_OUT), slot_ptr<uint32_t>(c, S_TMP), &pr, stats,
-                          true));
+                          slot_ptr<uint32_t>(c, S_OUT), nullptr, &pr, stats, true));
         if (stats) stats->passes_run = pr;
         c->splitters.clear();
         c->bucket_counts.assign(1, n_local);

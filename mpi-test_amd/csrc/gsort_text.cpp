@@ -12,6 +12,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -146,4 +147,84 @@ extern "C" long long gsort_format_dump(const int32_t *keys, size_t n, uint64_t f
     dump_write(keys, cut[0], cut[1], first_index, out);
     for (auto &x : th) x.join();
     return (long long)off[threads];
+}
+
+// ---- the drop-in programs' stdout contract ----------------------------------
+// Everything the reference programs print to stdout that is part of their contract, for one
+// rank, in the reference's order: sample's "Each bucket" line (mpi_sample_sort.c:74), at debug
+// its splitters (rank 0, :124) and bucket lengths (every rank, :157), the sorted dump (rank 0;
+// radix at debug > 2, radix:198-200; sample at debug >= 1, sample:202-204) and the median
+// (rank 0, radix:201, sample:205).  The reference's other debug lines are free-form progress
+// output and are not reproduced.  Written with write(2) so a C host and a test harness get the
+// same bytes; the dump goes in blocks rendered by gsort_format_dump.
+#include <errno.h>
+#include <stdio.h>
+#include <unistd.h>
+
+namespace {
+
+bool write_all(int fd, const char *p, size_t n) {
+    while (n) {
+        const ssize_t w = ::write(fd, p, n);
+        if (w < 0 && errno == EINTR) continue;
+        if (w <= 0) return false;
+        p += w;
+        n -= (size_t)w;
+    }
+    return true;
+}
+
+}  // namespace
+
+extern "C" gsort_status gsort_write_report(const gsort_report *r, int fd) {
+    if (!r || r->nranks < 1 || r->rank < 0 || r->rank >= r->nranks ||
+        (r->algo != GSORT_REPORT_RADIX && r->algo != GSORT_REPORT_SAMPLE))
+        return GSORT_EINVAL;
+    const bool sample = r->algo == GSORT_REPORT_SAMPLE, root = r->rank == 0;
+    const bool lines = sample && r->debug >= 1;
+    const bool dump = root && (sample ? r->debug >= 1 : r->debug > 2);
+    const bool before = r->stage != 2, after = r->stage != 1;
+    if (r->stage < 0 || r->stage > 2 ||
+        (after && lines && !r->bucket_counts) ||
+        (after && lines && root && r->nranks > 1 && !r->splitters) ||
+        (after && root && r->n_total && !r->sorted))
+        return GSORT_EINVAL;
+    std::string head;
+    char ln[96];
+    if (sample && root && before) {
+        // size_bucket = ceil(N / P) (mpi_sample_sort.c:72), printed as %u there
+        const unsigned long long B = (r->n_total + (uint64_t)r->nranks - 1) / (uint64_t)r->nranks;
+        snprintf(ln, sizeof ln, "Each bucket will be put %llu items.\n", B);
+        head += ln;
+    }
+    if (lines && after) {
+        if (root)
+            for (int i = 0; i < r->nranks - 1; ++i) {
+                snprintf(ln, sizeof ln, "[MASTER] Splitter: %u.\n", (unsigned)r->splitters[i]);
+                head += ln;
+            }
+        for (int j = 0; j < r->nranks; ++j) {
+            snprintf(ln, sizeof ln, "[COMMON] %d: Bucket %d=%llu\n", r->rank, j,
+                     (unsigned long long)r->bucket_counts[j]);
+            head += ln;
+        }
+    }
+    if (!write_all(fd, head.data(), head.size())) return GSORT_EINVAL;
+    if (!root || !after) return GSORT_OK;
+    if (dump && r->n_total) {
+        constexpr size_t kBlock = 1u << 21, kMaxLine = 32;  // "%llu|%u\n" <= 32 bytes
+        std::vector<char> buf(kBlock * kMaxLine);
+        for (uint64_t a = 0; a < r->n_total; a += kBlock) {
+            const size_t m = (size_t)std::min<uint64_t>(kBlock, r->n_total - a);
+            const long long len = gsort_format_dump(r->sorted + a, m, a, buf.data(), buf.size(), 16);
+            if (len < 0 || !write_all(fd, buf.data(), (size_t)len)) return GSORT_EINVAL;
+        }
+    }
+    if (r->n_total) {
+        // index N/2 - 1 (radix:201); N = 1 would read int_buf[-1] in the reference (quirk Q14)
+        const uint64_t med = r->n_total >= 2 ? r->n_total / 2 - 1 : 0;
+        snprintf(ln, sizeof ln, "The n/2-th sorted element: %d\n", r->sorted[med]);
+        if (!write_all(fd, ln, strlen(ln))) return GSORT_EINVAL;
+    }
+    return GSORT_OK;
 }

@@ -66,7 +66,7 @@ class Uid(ctypes.Structure):
 
 
 EXPORTS = [
-    "gsort_get_uid", "gsort_create", "gsort_group_create", "gsort_group_destroy",
+    "gsort_get_uid", "gsort_get_uid_ipc", "gsort_visible_devices", "gsort_create", "gsort_group_create", "gsort_group_destroy",
     "gsort_create_in_group", "gsort_destroy", "gsort_reserve", "gsort_set_local_algo",
     "gsort_set_sample_balanced",
     "gsort_strerror",
@@ -76,8 +76,17 @@ EXPORTS = [
     "gsort_copy_to_device", "gsort_onesweep_tile", "gsort_plan_radix_route",
     "gsort_plan_splitters", "gsort_plan_split", "gsort_plan_split_balanced", "gsort_parse_text",
     "gsort_format_dump", "gsort_copy_ceiling", "gsort_set_ref_compat", "gsort_plan_ref_digits",
-    "gsort_last_plan",
+    "gsort_last_plan", "gsort_write_report",
 ]
+REPORT_RADIX, REPORT_SAMPLE = 0, 1
+
+
+class Report(ctypes.Structure):
+    """gsort_report: what one rank of the drop-in programs prints to stdout."""
+    _fields_ = [("algo", ctypes.c_int), ("rank", ctypes.c_int), ("nranks", ctypes.c_int),
+                ("debug", ctypes.c_int), ("n_total", ctypes.c_uint64),
+                ("splitters", ctypes.c_void_p), ("bucket_counts", ctypes.c_void_p),
+                ("sorted", ctypes.c_void_p), ("stage", ctypes.c_int)]
 
 _lib = None
 
@@ -98,6 +107,9 @@ def lib():
     L.gsort_last_error.restype = ctypes.c_char_p
     L.gsort_onesweep_tile.restype = SZ
     L.gsort_get_uid.argtypes = [P(Uid)]
+    L.gsort_get_uid_ipc.argtypes = [I, P(Uid)]
+    L.gsort_visible_devices.argtypes = []
+    L.gsort_write_report.argtypes = [P(Report), I]
     L.gsort_create.argtypes = [P(VP), I, I, I, P(Uid)]
     L.gsort_group_create.argtypes = [P(VP), I]
     L.gsort_group_destroy.argtypes = [VP]
@@ -138,10 +150,43 @@ def lib():
     return L
 
 
-def get_uid():
+def get_uid(ipc_ranks=None):
+    """An RCCL unique id, or with ipc_ranks=P the id of a P-process IPC group (any number of
+    ranks per GPU; gsort_get_uid_ipc)."""
     u = Uid()
-    _check(lib().gsort_get_uid(ctypes.byref(u)), None)
+    if ipc_ranks is None:
+        _check(lib().gsort_get_uid(ctypes.byref(u)), None)
+    else:
+        _check(lib().gsort_get_uid_ipc(ipc_ranks, ctypes.byref(u)), None)
     return u.to_bytes()
+
+
+def write_report(fd, algo, rank, nranks, debug, n_total, splitters=None, bucket_counts=None,
+                 sorted_keys=None, stage=0):
+    """gsort_write_report: rank `rank`'s stdout contract lines (the drop-in programs' output)
+    written to the file descriptor fd."""
+    import numpy as np
+    keep = []
+
+    def arr(a, dt):
+        if a is None:
+            return None
+        a = np.ascontiguousarray(a, dtype=dt)
+        keep.append(a)
+        return a.ctypes.data if a.size else None
+
+    r = Report(algo, rank, nranks, debug, n_total, arr(splitters, np.int32),
+               arr(bucket_counts, np.uint64), arr(sorted_keys, np.int32), stage)
+    _check(lib().gsort_write_report(ctypes.byref(r), fd), None)
+
+
+def report_bytes(*args, **kw):
+    """write_report into a pipe-free temporary file; returns the bytes written."""
+    import tempfile
+    with tempfile.TemporaryFile() as f:
+        write_report(f.fileno(), *args, **kw)
+        f.seek(0)
+        return f.read()
 
 
 def _check(st, ctx):

@@ -11,12 +11,14 @@
  *                             sample at debug >= 1 (sample:202-204); sample debug also prints
  *                             "[MASTER] Splitter: %u.\n" and "[COMMON] r: Bucket j=len"
  *   stdout                 -> "The n/2-th sorted element: %d\n" = sorted[N/2-1] (radix:201)
+ *   (every stdout line above comes from gsort_write_report, which the tests call too)
  *   stderr                 -> "Endtime()-Starttime() = %.5f sec\n" (radix:203)
  * The timer spans what the reference's spans -- from after the rank-0 read to after the final
  * gather (radix:98,197; sample:61,201) -- and, like the reference's, excludes process setup
  * (MPI_Init there; MPI_Init + GPU context + RCCL communicator here).
- * MPI carries only the bootstrap: N and the RCCL unique id.  Keys move H2D on rank 0, over
- * xGMI between GPUs (RCCL), and D2H on rank 0 -- never over MPI.
+ * MPI carries only the bootstrap: N and the group id (RCCL unique id, or the IPC process
+ * group's when there are more ranks than GPUs).  Keys move H2D on rank 0, GPU to GPU between
+ * ranks (RCCL over xGMI, or HIP IPC copies), and D2H on rank 0 -- never over MPI.
  */
 #include <mpi.h>
 #include <stdint.h>
@@ -24,6 +26,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <sys/stat.h>
+#include <unistd.h>
 
 #include "gsort.h"
 #include "gsort_cli.h"
@@ -72,24 +75,6 @@ static int32_t *read_keys(const char *file, size_t *n_out, int phantom)
     return keys;
 }
 
-/* the full sorted dump (radix:198-200, sample:202-204) in blocks of kDumpBlock keys, each
- * rendered on 16 threads by gsort_format_dump and written with one fwrite */
-static void print_dump(const int32_t *keys, unsigned long long n)
-{
-    enum { kDumpBlock = 1 << 21, kMaxLine = 32 };
-    char *buf = malloc((size_t)kDumpBlock * kMaxLine);
-    if (!buf) die("print_dump: out of host memory");
-    fflush(stdout);
-    for (unsigned long long a = 0; a < n; a += kDumpBlock) {
-        const size_t m = n - a < kDumpBlock ? (size_t)(n - a) : (size_t)kDumpBlock;
-        const long long len =
-            gsort_format_dump(keys + a, m, a, buf, (size_t)kDumpBlock * kMaxLine, 16);
-        if (len < 0 || fwrite(buf, 1, (size_t)len, stdout) != (size_t)len)
-            die("print_dump: write failed");
-    }
-    free(buf);
-}
-
 static int local_rank(int rank)
 {
     const char *vars[] = {"MPI_LOCALRANKID", "OMPI_COMM_WORLD_LOCAL_RANK", "LOCAL_RANK"};
@@ -127,11 +112,18 @@ int gsort_cli_main(int argc, char **argv, int algo)
         n_total = n;
     }
 
-    /* bootstrap: one context per rank == one GPU; RCCL id broadcast over MPI */
+    /* bootstrap: one context per rank; the group's id broadcast over MPI.  One GPU per rank:
+     * RCCL over xGMI.  More ranks than GPUs (RCCL refuses two ranks on one device): the same-node
+     * IPC process group.  GSORT_TRANSPORT=rccl|ipc overrides the choice. */
     gsort_uid uid;
     memset(&uid, 0, sizeof uid);
     if (size > 1) {
-        if (rank == 0) check(gsort_get_uid(&uid), NULL, "gsort_get_uid");
+        if (rank == 0) {
+            const char *tr = getenv("GSORT_TRANSPORT");
+            const int ipc = tr && *tr ? strcmp(tr, "ipc") == 0 : gsort_visible_devices() < size;
+            if (ipc) check(gsort_get_uid_ipc(size, &uid), NULL, "gsort_get_uid_ipc");
+            else check(gsort_get_uid(&uid), NULL, "gsort_get_uid");
+        }
         MPI_Bcast(&uid, (int)sizeof uid, MPI_BYTE, 0, MPI_COMM_WORLD);
     }
     gsort_ctx *ctx = NULL;
@@ -146,16 +138,28 @@ int gsort_cli_main(int argc, char **argv, int algo)
     MPI_Barrier(MPI_COMM_WORLD);
     const double start = MPI_Wtime();
     MPI_Bcast(&n_total, 1, MPI_UNSIGNED_LONG_LONG, 0, MPI_COMM_WORLD);
-    const unsigned long long B = (n_total + (unsigned long long)size - 1) / (unsigned long long)size;
-    if (algo == CLI_SAMPLE && rank == 0) printf("Each bucket will be put %llu items.\n", B);
+    /* stdout: the reference's contract lines (gsort_write_report), "Each bucket" before the sort
+     * as there (mpi_sample_sort.c:74), the rest after the final gather */
+    gsort_report rep;
+    memset(&rep, 0, sizeof rep);
+    rep.algo = algo == CLI_RADIX ? GSORT_REPORT_RADIX : GSORT_REPORT_SAMPLE;
+    rep.rank = rank;
+    rep.nranks = size;
+    rep.debug = debug;
+    rep.n_total = n_total;
+    rep.stage = 1;
+    fflush(stdout);
+    check(gsort_write_report(&rep, STDOUT_FILENO), ctx, "gsort_write_report");
 
     int32_t *d_keys = NULL, *d_out = NULL;
     size_t n_local = 0, n_out = 0;
+    int32_t *spl = calloc((size_t)size, sizeof(int32_t));
+    uint64_t *cnt = calloc((size_t)size, sizeof(uint64_t));
+    if (!spl || !cnt) die("out of host memory");
     check(gsort_scatter_from_root(ctx, int_buf, n_total, &d_keys, &n_local), ctx,
           "gsort_scatter_from_root");
     if (algo == CLI_RADIX) {
         check(gsort_radix(ctx, d_keys, n_local, &d_out, &n_out, NULL), ctx, "gsort_radix");
-        if (debug) printf("[COMMON] %d: sorted block of %zu keys\n", rank, n_out);
     } else {
         gsort_status st = gsort_sample(ctx, d_keys, n_local, &d_out, &n_out, NULL);
         if (st == GSORT_ENOSAMPLE) {
@@ -167,31 +171,19 @@ int gsort_cli_main(int argc, char **argv, int algo)
             MPI_Abort(MPI_COMM_WORLD, EXIT_FAILURE);
         }
         check(st, ctx, "gsort_sample");
-        if (debug) {
-            int32_t *spl = calloc((size_t)size, sizeof(int32_t));
-            uint64_t *cnt = calloc((size_t)size, sizeof(uint64_t));
-            check(gsort_sample_info(ctx, spl, cnt), ctx, "gsort_sample_info");
-            if (rank == 0)
-                for (int i = 0; i < size - 1; i++)
-                    printf("[MASTER] Splitter: %u.\n", (unsigned)spl[i]);
-            for (int j = 0; j < size; j++)
-                printf("[COMMON] %d: Bucket %d=%llu\n", rank, j, (unsigned long long)cnt[j]);
-            free(spl);
-            free(cnt);
-        }
+        check(gsort_sample_info(ctx, spl, cnt), ctx, "gsort_sample_info");
     }
     check(gsort_gather_to_root(ctx, d_out, n_out, int_buf), ctx, "gsort_gather_to_root");
-    if (rank == 0) {
-        const double end = MPI_Wtime();
-        if ((algo == CLI_RADIX && debug > 2) || (algo == CLI_SAMPLE && debug))
-            print_dump(int_buf, n_total);
-        /* index N/2-1 (radix:201); N = 1 would read int_buf[-1] in the reference (Q14) */
-        const long long med = n_total >= 2 ? (long long)(n_total / 2) - 1 : 0;
-        printf("The n/2-th sorted element: %d\n", int_buf[med]);
-        fflush(stdout);
-        free(int_buf);
-        fprintf(stderr, "Endtime()-Starttime() = %.5f sec\n", end - start);
-    }
+    const double end = MPI_Wtime();
+    rep.splitters = spl;
+    rep.bucket_counts = cnt;
+    rep.sorted = int_buf;
+    rep.stage = 2;
+    check(gsort_write_report(&rep, STDOUT_FILENO), ctx, "gsort_write_report");
+    if (rank == 0) fprintf(stderr, "Endtime()-Starttime() = %.5f sec\n", end - start);
+    free(spl);
+    free(cnt);
+    free(int_buf);
     gsort_destroy(ctx);
     MPI_Finalize();
     return EXIT_SUCCESS;

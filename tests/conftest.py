@@ -79,3 +79,25 @@ def _gsort_memlog(request):
     free, total = torch.cuda.mem_get_info()
     with open(path, "a") as f:
         f.write(f"{request.node.nodeid} {free} {total}\n")
+
+
+@pytest.fixture(scope="session")
+def ref_large():
+    """Reference runs at >= 2^22 keys (tests/golden/make_golden.py --large): digests only."""
+    path = os.path.join(GOLDEN, "ref_large.json")
+    if not os.path.exists(path):
+        pytest.skip("tests/golden/ref_large.json not generated")
+    with open(path) as f:
+        return json.load(f)["cases"]
+
+
+GOLDEN_DEBUG = {"radix_sort": 3, "sample_sort": 1}  # the debug level every fixture was run at
+
+
+def contract_split(data):
+    """A rank's stdout bytes -> (lines before the dump, dump line count, lines after)."""
+    lines = data.decode().splitlines()
+    is_dump = [("|" in ln and ln.replace("|", "").isdigit()) for ln in lines]
+    first = is_dump.index(True) if any(is_dump) else len(lines)
+    last = len(lines) - is_dump[::-1].index(True) if any(is_dump) else len(lines)
+    return lines[:first], last - first, lines[last:]

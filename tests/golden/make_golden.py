@@ -33,10 +33,31 @@ OUT = os.path.join(ROOT, "tests", "golden")
 DUMP = re.compile(r"^(\d+)\|(\d+)$")
 SPLIT = re.compile(r"^\[MASTER\] Splitter: (\d+)\.$")
 BUCKET = re.compile(r"^\[COMMON\] (\d+): Bucket (\d+)=(\d+)$")
+# the program-contract lines of a rank's stdout: "Each bucket" (sample:74),
+# splitters (sample:124), bucket lengths (sample:157), the sorted dump (radix:199, sample:203)
+# and the median (radix:201, sample:205); every other line is free-form progress output
+CONTRACT = re.compile(r"^(Each bucket will be put [0-9]+ items\.|\[MASTER\] Splitter: [0-9]+\.|"
+                      r"\[COMMON\] [0-9]+: Bucket [0-9]+=[0-9]+|[0-9]+\|[0-9]+|"
+                      r"The n/2-th sorted element: -?[0-9]+)$")
 
 
 def sha(a):
     return hashlib.sha256(np.ascontiguousarray(a, dtype="<i4").tobytes()).hexdigest()
+
+
+def contract_of(lines):
+    """{sha256 of the contract lines joined by '\\n' with a final '\\n', the lines before and
+    after the dump block, dump length} for one rank's stdout lines"""
+    keep = [ln for ln in lines if CONTRACT.match(ln)]
+    h = hashlib.sha256()
+    for ln in keep:
+        h.update(ln.encode() + b"\n")
+    is_dump = [bool(DUMP.match(ln)) for ln in keep]
+    first = is_dump.index(True) if any(is_dump) else len(keep)
+    last = len(keep) - is_dump[::-1].index(True) if any(is_dump) else len(keep)
+    assert all(is_dump[first:last]), "dump lines are not one block"
+    return {"sha256": h.hexdigest(), "head": keep[:first], "tail": keep[last:],
+            "n_dump": last - first}
 
 
 def resign(u):
@@ -82,7 +103,97 @@ def run_ref(prog, P, path, debug, timeout=120):
                 mat[(int(m.group(1)), int(m.group(2)))] = int(m.group(3))
     if mat:
         res["bucket_matrix"] = [[mat.get((r, j), 0) for j in range(P)] for r in range(P)]
+    res["contract"] = [contract_of(lines) for lines in [out0] + others]
     return res
+
+
+def run_ref_stream(prog, P, path, debug, timeout=1800):
+    """run_ref for large inputs: at debug 3 the reference's radix prints every key of every
+    pass ("DUMP: LOOP", radix:175-178; ~13 GB of text at 2^24 keys, P = 2), so the merged
+    stdout (-prepend-rank) is filtered to the contract lines by grep on the fly and only the
+    filtered stream is parsed."""
+    tmp = tempfile.mkdtemp(prefix="goldL_")
+    filt, err = os.path.join(tmp, "f"), os.path.join(tmp, "e")
+    cmd = (f"{MPIRUN} -prepend-rank -np {P} {os.path.join(orc.REF_DIR, prog)} {path} {debug} "
+           f"2>{err} | LC_ALL=C grep -a -E '^\\[[0-9]+\\] ({CONTRACT.pattern[2:-2]})$' > {filt}")
+    try:
+        rc = subprocess.run(["bash", "-o", "pipefail", "-c", cmd], timeout=timeout).returncode
+    except subprocess.TimeoutExpired:
+        rc = "timeout"
+    per = [[] for _ in range(P)]
+    with open(filt, "rb") as f:
+        for raw in f:
+            r, _, ln = raw.decode().rstrip("\n").partition("] ")
+            per[int(r[1:])].append(ln)
+    err0 = [ln.partition("] ")[2] for ln in open(err, errors="replace").read().splitlines()
+            if ln.startswith("[0] ")]
+    subprocess.run(["rm", "-rf", tmp])
+    out0 = per[0]
+    dump = [DUMP.match(ln) for ln in out0]
+    vals = np.array([int(m.group(2)) for m in dump if m], dtype=np.uint64)
+    idx = np.array([int(m.group(1)) for m in dump if m], dtype=np.int64)
+    assert idx.size == 0 or np.array_equal(idx, np.arange(idx.size)), "dump index order"
+    res = {
+        "rc": rc,
+        "dump": vals.astype(np.uint32).view(np.int32),
+        "median_line": next((l for l in out0 if l.startswith("The n/2-th")), None),
+        "each_bucket_line": next((l for l in out0 if l.startswith("Each bucket")), None),
+        "stderr0": [re.sub(r"= [0-9.]+ sec", "= <t> sec", l) for l in err0],
+        "splitters": [resign(SPLIT.match(l).group(1)) for l in out0 if SPLIT.match(l)],
+        "contract": [contract_of(lines) for lines in per],
+    }
+    mat = {}
+    for lines in per:
+        for ln in lines:
+            m = BUCKET.match(ln)
+            if m:
+                mat[(int(m.group(1)), int(m.group(2)))] = int(m.group(3))
+    if mat:
+        res["bucket_matrix"] = [[mat.get((r, j), 0) for j in range(P)] for r in range(P)]
+    return res
+
+
+def main_large():
+    """tests/golden/ref_large.json: the reference's output at the sizes the build's default
+    (sampled) local plan runs at, >= 2^22 keys.  Data only: sha256 of the full
+    sorted dump, median / "Each bucket" lines, splitters, bucket matrices and per-rank contract
+    transcripts (sha256 + the non-dump lines); no arrays."""
+    orc.build()
+    tmpdir = tempfile.mkdtemp(prefix="goldLin_")
+    cases = []
+    plan = [(orc.UNIFORM, "uniform", 1 << 22, 42, (2, 4, 8), (2, 4, 8)),
+            (orc.UNIFORM, "uniform", 1 << 24, 42, (2, 4, 8), (2, 4, 8)),
+            (orc.ZIPF, "zipf", 1 << 22, 7, (2, 4, 8), (2, 4)),
+            (orc.ZIPF, "zipf", 1 << 24, 7, (8,), (2,))]
+    for dist, dname, n, seed, radix_ps, sample_ps in plan:
+        keys = orc.gen(dist, seed, n)
+        want = sha(np.sort(keys))
+        path = os.path.join(tmpdir, "in.txt")
+        orc.write_text(path, keys)
+        spec = {"gen": dname, "n": n, "seed": seed}
+        for prog, ps, debug in (("radix_sort", radix_ps, 3), ("sample_sort", sample_ps, 1)):
+            for P in ps:
+                r = run_ref_stream(prog, P, path, debug)
+                c = {"id": f"{dname}{n}s{seed}__{prog}__P{P}", "prog": prog, "P": P,
+                     "input": spec, "input_sha256": sha(keys), "rc": r["rc"],
+                     "median_line": r["median_line"], "each_bucket_line": r["each_bucket_line"],
+                     "stderr0": r["stderr0"], "n_dump": int(r["dump"].size),
+                     "output_sha256": sha(r["dump"]) if r["dump"].size else None,
+                     "contract": r["contract"]}
+                # the reference's sample sort overflows its fixed receive buffers on skewed
+                # inputs (SURVEY.md 8 Q12): record whether this run produced the sorted array
+                c["output_is_sorted_input"] = c["output_sha256"] == want
+                if prog == "sample_sort":
+                    c["splitters"] = r["splitters"]
+                    c["bucket_matrix"] = r.get("bucket_matrix")
+                cases.append(c)
+                print(c["id"], "rc", c["rc"], "n", c["n_dump"], "sorted",
+                      c["output_is_sorted_input"], flush=True)
+    with open(os.path.join(OUT, "ref_large.json"), "w") as f:
+        json.dump({"generator": "tests/golden/make_golden.py --large", "mpirun": MPIRUN,
+                   "cases": cases}, f, indent=1)
+    subprocess.run(["rm", "-rf", tmpdir])
+    print("wrote", len(cases), "large cases")
 
 
 def main():
@@ -112,6 +223,7 @@ def main():
         if prog == "sample_sort":
             c["splitters"] = r["splitters"]
             c["bucket_matrix"] = r.get("bucket_matrix")
+        c["contract"] = r["contract"]
         cases.append(c)
         print(key, "rc", r["rc"], "n", r["dump"].size, flush=True)
 
@@ -165,4 +277,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main_large() if "--large" in sys.argv[1:] else main()

@@ -1,0 +1,80 @@
+"""The drop-in programs as the reference is run: `mpirun -np P radix_sort|sample_sort <file>
+<debug>`, one process per rank.  This box has one GPU, so the P processes share it through the
+same-node IPC process group (gsort_get_uid_ipc; RCCL refuses two ranks on one device): the
+CLI's MPI bootstrap, per-process contexts, scatter / sort / gather across processes and the
+report all run for real.  Each rank's stdout is compared byte for byte with the reference's
+own (tests/golden: contract lines of `mpirun -np P` runs of the reference binaries)."""
+import hashlib
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN_DEBUG, ROOT, case_input, contract_split
+
+pytestmark = pytest.mark.gpu
+BIN = os.path.join(ROOT, "mpi-test_amd", "bin")
+MPIRUN = "/opt/conda/bin/mpirun"
+
+
+def mpirun(prog, P, path, debug, tmp, timeout=150, env=None):
+    cmd = [MPIRUN, "-np", str(P), "-outfile-pattern", f"{tmp}/o.%r", "-errfile-pattern",
+           f"{tmp}/e.%r", os.path.join(BIN, prog), path] + ([str(debug)] if debug is not None else [])
+    e = dict(os.environ, **(env or {}))
+    r = subprocess.run(cmd, timeout=timeout, capture_output=True, text=True, env=e)
+    outs = []
+    for q in range(P):
+        p = os.path.join(tmp, f"o.{q}")
+        outs.append(open(p, "rb").read() if os.path.exists(p) else b"")
+    err0 = open(os.path.join(tmp, "e.0")).read() if os.path.exists(os.path.join(tmp, "e.0")) else ""
+    return r.returncode, outs, err0
+
+
+CASES = [("uniform65536s42", "radix_sort", P) for P in (2, 4, 8)] + \
+        [("uniform65536s42", "sample_sort", P) for P in (2, 4, 8)] + \
+        [("zipf65536s7", "radix_sort", 8), ("zipf65536s7", "sample_sort", 4),
+         ("uniform1024s42", "sample_sort", 8)]
+
+
+@pytest.mark.parametrize("name,prog,P", CASES)
+def test_mpirun_stdout_equals_reference(orc, ref_cases, tmp_path, name, prog, P):
+    c = next(x for x in ref_cases if x["id"] == f"{name}__{prog}__P{P}")
+    keys = case_input(orc, c["input"])
+    path = str(tmp_path / "in.txt")
+    orc.write_text(path, keys)
+    rc, outs, err0 = mpirun(prog, P, path, GOLDEN_DEBUG[prog], tmp_path)
+    assert rc == 0, err0
+    for r in range(P):
+        want = c["contract"][r]
+        assert contract_split(outs[r]) == (want["head"], want["n_dump"], want["tail"]), (c["id"], r)
+        assert hashlib.sha256(outs[r]).hexdigest() == want["sha256"], (c["id"], r)
+    assert err0.startswith("Endtime()-Starttime() = ") and err0.endswith(" sec\n")
+
+
+def test_mpirun_default_debug_and_ragged(orc, tmp_path):
+    """No debug argument, N % P != 0: only the median (radix) / "Each bucket" + median
+    (sample) lines, from rank 0; the other ranks print nothing."""
+    n = 100003
+    keys = orc.gen(orc.UNIFORM, 3, n)
+    path = str(tmp_path / "in.txt")
+    orc.write_text(path, keys)
+    med = f"The n/2-th sorted element: {np.sort(keys)[n // 2 - 1]}\n".encode()
+    rc, outs, err0 = mpirun("radix_sort", 4, path, None, tmp_path)
+    assert rc == 0, err0
+    assert outs == [med, b"", b"", b""]
+    rc, outs, err0 = mpirun("sample_sort", 4, path, None, tmp_path)
+    assert rc == 0, err0
+    assert outs[0] == f"Each bucket will be put {-(-n // 4)} items.\n".encode() + med
+    assert outs[1:] == [b"", b"", b""]
+
+
+def test_mpirun_no_enough_sample(orc, ref_cases, tmp_path):
+    """N = 9 at P = 4: the reference prints "Each bucket" and aborts with "no enough sample"."""
+    c = next(x for x in ref_cases if x["id"] == "q9_n9__sample_sort__P4")
+    path = str(tmp_path / "in.txt")
+    orc.write_text(path, case_input(orc, c["input"]))
+    rc, outs, err0 = mpirun("sample_sort", 4, path, 1, tmp_path)
+    assert rc != 0
+    assert outs[0].decode().splitlines() == c["contract"][0]["head"]
+    assert "no enough sample" in err0

@@ -282,17 +282,13 @@ def test_radix_multirank_balanced_blocks(gsort, orc, P, local):
             assert all(r[1]["exchanges"] == 1 for r in res)
 
 
-@pytest.mark.parametrize("chunks", [2, 3, 8])
 @pytest.mark.parametrize("P", [1, 2, 4, 8])
-def test_radix_multirank_chunked_exchange(gsort, orc, monkeypatch, P, chunks):
-    """GSORT_XCHUNKS > 1: the packed exchange goes in bucket-range chunks on its own stream and
-    each chunk's receive sort waits only for its chunk; rank q still gets [qB, (q+1)B).  Cases:
-    uniform and Zipf keys, a few distinct values (destination ranges of fewer buckets than
-    chunks: empty chunks), uneven blocks with an empty one."""
-    monkeypatch.setenv("GSORT_XCHUNKS", str(chunks))
+def test_radix_multirank_mixed_inputs(gsort, orc, monkeypatch, P):
+    """The packed exchange on uniform and Zipf keys, a few distinct values (destination ranges
+    of very few buckets) and uneven blocks with empty ones; rank q gets [qB, (q+1)B)."""
     if P == 1:  # a one-rank group still takes the distributed path
         monkeypatch.setenv("GSORT_FORCE_DIST", "1")
-    rng = np.random.default_rng(P * 10 + chunks)
+    rng = np.random.default_rng(P * 10)
     cases = [orc.gen(orc.UNIFORM, P, 300007), orc.gen(orc.ZIPF, P + 1, 150000),
              rng.integers(-3, 4, 120000).astype(np.int32)]
     for keys in cases:
@@ -301,7 +297,7 @@ def test_radix_multirank_chunked_exchange(gsort, orc, monkeypatch, P, chunks):
         res = run_group(gsort, blocks, "radix")
         ref = np.sort(keys)
         for q in range(P):
-            assert np.array_equal(res[q][0], ref[q * B:(q + 1) * B]), (P, chunks, q)
+            assert np.array_equal(res[q][0], ref[q * B:(q + 1) * B]), (P, q)
     if P > 2:
         keys = orc.gen(orc.UNIFORM, 7, 90000)
         blocks = [keys[:0], keys[:50000], keys[50000:50001]] + [keys[50001:]] + \
@@ -310,7 +306,7 @@ def test_radix_multirank_chunked_exchange(gsort, orc, monkeypatch, P, chunks):
         ref = np.sort(keys)
         B = -(-keys.size // P)
         for q in range(P):
-            assert np.array_equal(res[q][0], ref[q * B:(q + 1) * B]), (P, chunks, q, "uneven")
+            assert np.array_equal(res[q][0], ref[q * B:(q + 1) * B]), (P, q, "uneven")
 
 
 @pytest.mark.parametrize("local", ["msd", "lsd"])
