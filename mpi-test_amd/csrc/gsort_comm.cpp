@@ -97,6 +97,24 @@ class RcclComm : public Comm {
     gsort_status alltoallv(const void *send, const size_t *scount, const size_t *sdispl,
                            void *recv, const size_t *rcount, const size_t *rdispl,
                            hipStream_t s) override {
+        // the rank's own piece is a device copy on its stream, not an RCCL self send/recv:
+        // RCCL's copy moved a 512 MiB self-message at ~2.2 TB/s of HBM traffic (0.49 ms at
+        // 2^28 keys, forced-distributed P = 1), hipMemcpyAsync at the copy ceiling (~5.8 TB/s).
+        // GSORT_RCCL_SELF=1 keeps it in RCCL (tests/test_gpu_rccl.py pins RCCL's own limits)
+        const bool self_rccl = rccl_self();
+        if (!self_rccl && scount[rank_]) {
+            if (scount[rank_] != rcount[rank_]) {
+                err = "alltoallv: self send / receive counts differ";
+                return GSORT_EINVAL;
+            }
+            const hipError_t e = hipMemcpyAsync((char *)recv + rdispl[rank_],
+                                                (const char *)send + sdispl[rank_],
+                                                scount[rank_], hipMemcpyDeviceToDevice, s);
+            if (e != hipSuccess) {
+                err = std::string("hipMemcpyAsync (self piece): ") + hipGetErrorString(e);
+                return GSORT_EHIP;
+            }
+        }
         gsort_status st = check(ncclGroupStart(), "ncclGroupStart");
         if (st != GSORT_OK) return st;
         // messages go in pieces of at most max_msg_ = 2^30 bytes (matched in order on both
@@ -105,6 +123,7 @@ class RcclComm : public Comm {
         // exact (tests/test_gpu_rccl.py pins both sides of the boundary;
         // GSORT_RCCL_MAX_MSG overrides the piece size for that test)
         for (int q = 0; q < size_ && st == GSORT_OK; ++q) {
+            if (q == rank_ && !self_rccl) continue;
             for (size_t o = 0; o < scount[q] && st == GSORT_OK; o += max_msg_)
                 st = check(ncclSend((const char *)send + sdispl[q] + o,
                                     std::min(max_msg_, scount[q] - o), ncclChar, q, comm_, s),
@@ -122,6 +141,10 @@ class RcclComm : public Comm {
     }
 
   private:
+    static bool rccl_self() {
+        const char *e = getenv("GSORT_RCCL_SELF");
+        return e && e[0] == '1';
+    }
     static size_t max_msg() {
         const char *e = getenv("GSORT_RCCL_MAX_MSG");
         const size_t v = e ? (size_t)strtoull(e, nullptr, 0) : 0;
@@ -287,13 +310,16 @@ Comm *make_group_comm(GroupState *g, int rank) { return new GroupComm(g, rank); 
 // Same-node process group over HIP IPC (one process per rank, any number of ranks per GPU).
 // RCCL refuses two ranks on one device, so this is how `mpirun -np P radix_sort` runs the
 // distributed algorithm on a node with fewer GPUs than ranks (a one-GPU box in particular),
-// each rank its own process and context as with RCCL.  Keys move GPU to GPU: every collective
-// publishes the IPC handle of each rank's send buffer (+ offset, counts) in a POSIX shared-memory
-// control block, meets the others at a barrier, pulls what it needs with hipMemcpyAsync from the
-// opened peer buffers, synchronises, closes them and meets the others again (so no sender
-// reuses a buffer a peer is still reading) -- GroupComm's protocol across processes.  The uid
-// carries the control block's name; rank 0 creates it (gsort_get_uid_ipc) and unlinks it once
-// every rank has attached.
+// each rank its own process and context as with RCCL.  Keys move GPU to GPU: every rank owns
+// one exported staging buffer; a collective copies the rank's send range into it, publishes its
+// counts in a POSIX shared-memory control block, meets the others at a barrier, pulls what it
+// needs from the peers' staging buffers (opened once through their IPC handles, again only when
+// a peer grew its buffer), synchronises and meets them again (so no rank overwrites a staging
+// buffer a peer is still reading) -- GroupComm's protocol across processes.  (Exporting and
+// opening every send buffer per collective instead failed intermittently on MI355X / ROCm 7.2:
+// hipIpcOpenMemHandle "invalid device pointer" on buffers exported many times.)  The uid carries
+// the control block's name; rank 0 creates it (gsort_get_uid_ipc) and unlinks it once every
+// rank has attached.
 // ---------------------------------------------------------------------------------------
 namespace gsort {
 namespace {
@@ -303,9 +329,8 @@ constexpr int kIpcMaxRanks = 64;
 constexpr size_t kIpcNameOff = 8, kIpcNameMax = 88, kIpcRanksOff = 96;
 
 struct IpcSlot {
-    hipIpcMemHandle_t handle;
-    uint64_t off;    // send pointer - allocation base
-    uint64_t valid;  // handle published (the rank sends something)
+    hipIpcMemHandle_t handle;  // the rank's staging buffer
+    uint64_t gen;              // bumped whenever the staging buffer is replaced
     uint64_t count[kIpcMaxRanks], displ[kIpcMaxRanks];  // bytes to / offsets for each rank
 };
 struct IpcShared {
@@ -352,8 +377,16 @@ IpcShared *map_shared(const char *name, bool create, std::string *err) {
 
 class IpcComm : public Comm {
   public:
-    IpcComm(IpcShared *sh, int rank, int n) : sh_(sh) { rank_ = rank; size_ = n; }
-    ~IpcComm() override { munmap(sh_, sizeof(IpcShared)); }
+    IpcComm(IpcShared *sh, int rank, int n)
+        : sh_(sh), peer_(n, nullptr), peer_gen_(n, 0) { rank_ = rank; size_ = n; }
+    ~IpcComm() override {
+        for (void *p : peer_)
+            if (p) (void)hipIpcCloseMemHandle(p);
+        // peers may still hold this rank's staging buffers open; the memory goes with the
+        // process (or with their close), so the buffers are freed last
+        for (void *p : stages_) (void)hipFree(p);
+        munmap(sh_, sizeof(IpcShared));
+    }
 
     // generation barrier in shared memory; a peer that does not arrive within 120 s breaks the
     // group (every later collective fails instead of hanging)
@@ -388,92 +421,93 @@ class IpcComm : public Comm {
         err = std::string("ipc group: ") + what + ": " + hipGetErrorString(e);
         return GSORT_EHIP;
     }
-    // publish this rank's send buffer (the allocation's IPC handle + the offset into it)
-    gsort_status publish(const void *send, const size_t *count, const size_t *displ,
-                         size_t all_bytes) {
+    // the send range [0, span) into this rank's staging buffer (grown and re-exported as
+    // needed), the counts into the control block
+    gsort_status publish(const void *send, size_t span, const size_t *count, const size_t *displ,
+                         hipStream_t s) {
         IpcSlot &me = sh_->slot[rank_];
-        me.valid = 0;
-        bool any = all_bytes != 0;
         for (int q = 0; q < size_ && count; ++q) {
             me.count[q] = count[q];
-            me.displ[q] = displ ? displ[q] : 0;
-            any = any || count[q];
+            me.displ[q] = displ[q];
         }
-        if (!any || !send) return GSORT_OK;
-        void *base = nullptr;
-        size_t len = 0;
-        gsort_status st = hip(hipMemGetAddressRange(&base, &len, const_cast<void *>(send)),
-                              "hipMemGetAddressRange");
-        if (st == GSORT_OK) st = hip(hipIpcGetMemHandle(&me.handle, base), "hipIpcGetMemHandle");
-        if (st != GSORT_OK) return st;
-        me.off = (uint64_t)((const char *)send - (const char *)base);
-        me.valid = 1;
-        return GSORT_OK;
+        if (span > cap_) {
+            size_t cap = size_t(1) << 20;
+            while (cap < span) cap <<= 1;
+            void *p = nullptr;
+            gsort_status st = hip(hipMalloc(&p, cap), "hipMalloc (staging)");
+            if (st == GSORT_OK) st = hip(hipIpcGetMemHandle(&me.handle, p), "hipIpcGetMemHandle");
+            if (st != GSORT_OK) {
+                if (p) (void)hipFree(p);
+                return st;
+            }
+            stages_.push_back(p);  // the old one may still be open in a peer
+            stage_ = p;
+            cap_ = cap;
+            me.gen = ++gen_;
+        }
+        gsort_status st = GSORT_OK;
+        if (span) st = hip(hipMemcpyAsync(stage_, send, span, hipMemcpyDeviceToDevice, s),
+                           "hipMemcpyAsync (stage)");
+        if (st == GSORT_OK) st = hip(hipStreamSynchronize(s), "hipStreamSynchronize");
+        return st;
     }
-    // the bytes [a, a + len) of rank r's send buffer into dst (opened peer buffers collected in
-    // opened, closed after the copies complete)
-    gsort_status pull(int r, const void *own, uint64_t a, size_t len, void *dst, hipStream_t s,
-                      std::vector<std::pair<int, void *>> &opened) {
+    // bytes [a, a + len) of rank r's send range into dst
+    gsort_status pull(int r, const void *own, uint64_t a, size_t len, void *dst, hipStream_t s) {
         if (!len) return GSORT_OK;
         const char *src = nullptr;
         if (r == rank_) {
             src = static_cast<const char *>(own);
         } else {
             const IpcSlot &ps = sh_->slot[r];
-            if (!ps.valid) return fail("peer published no buffer");
-            void *p = nullptr;
-            for (auto &o : opened)
-                if (o.first == r) p = o.second;
-            if (!p) {
+            if (peer_gen_[r] != ps.gen) {
+                if (peer_[r]) (void)hipIpcCloseMemHandle(peer_[r]);
+                peer_[r] = nullptr;
+                void *p = nullptr;
                 gsort_status st = hip(hipIpcOpenMemHandle(&p, ps.handle,
                                                           hipIpcMemLazyEnablePeerAccess),
                                       "hipIpcOpenMemHandle");
                 if (st != GSORT_OK) return st;
-                opened.push_back({r, p});
+                peer_[r] = p;
+                peer_gen_[r] = ps.gen;
             }
-            src = static_cast<const char *>(p) + ps.off;
+            src = static_cast<const char *>(peer_[r]);
         }
         return hip(hipMemcpyAsync(dst, src + a, len, hipMemcpyDeviceToDevice, s), "hipMemcpyAsync");
     }
-    gsort_status finish(hipStream_t s, std::vector<std::pair<int, void *>> &opened,
-                        gsort_status st) {
+    gsort_status finish(hipStream_t s, gsort_status st) {
         gsort_status st2 = hip(hipStreamSynchronize(s), "hipStreamSynchronize");
-        for (auto &o : opened) (void)hipIpcCloseMemHandle(o.second);
         if (!barrier()) return fail("barrier timeout");
         return st != GSORT_OK ? st : st2;
     }
 
     gsort_status allgather(const void *send, void *recv, size_t bytes, hipStream_t s) override {
-        gsort_status st = hip(hipStreamSynchronize(s), "hipStreamSynchronize");
-        if (st == GSORT_OK) st = publish(send, nullptr, nullptr, bytes);
+        gsort_status st = publish(send, bytes, nullptr, nullptr, s);
         if (!barrier()) return fail("barrier timeout");
-        std::vector<std::pair<int, void *>> opened;
         for (int r = 0; r < size_ && st == GSORT_OK; ++r)
-            st = pull(r, send, 0, bytes, (char *)recv + (size_t)r * bytes, s, opened);
-        return finish(s, opened, st);
+            st = pull(r, send, 0, bytes, (char *)recv + (size_t)r * bytes, s);
+        return finish(s, st);
     }
     gsort_status alltoallv(const void *send, const size_t *scount, const size_t *sdispl,
                            void *recv, const size_t *rcount, const size_t *rdispl,
                            hipStream_t s) override {
         if (size_ > kIpcMaxRanks) return fail("too many ranks");
-        gsort_status st = hip(hipStreamSynchronize(s), "hipStreamSynchronize");
-        if (st == GSORT_OK) st = publish(send, scount, sdispl, 0);
+        size_t span = 0;  // what the peers read of this rank's send buffer
+        for (int q = 0; q < size_; ++q)
+            if (q != rank_ && scount[q]) span = std::max(span, sdispl[q] + scount[q]);
+        gsort_status st = publish(send, span, scount, sdispl, s);
         if (!barrier()) return fail("barrier timeout");
-        std::vector<std::pair<int, void *>> opened;
         for (int r = 0; r < size_ && st == GSORT_OK; ++r) {
             const IpcSlot &ps = sh_->slot[r];
             if (ps.count[rank_] != rcount[r]) { st = fail("send/recv count mismatch"); break; }
-            st = pull(r, send, ps.displ[rank_], rcount[r], (char *)recv + rdispl[r], s, opened);
+            st = pull(r, send, ps.displ[rank_], rcount[r], (char *)recv + rdispl[r], s);
         }
-        return finish(s, opened, st);
+        return finish(s, st);
     }
     gsort_status bcast(void *buf, size_t bytes, int root, hipStream_t s) override {
-        gsort_status st = hip(hipStreamSynchronize(s), "hipStreamSynchronize");
-        if (st == GSORT_OK && rank_ == root) st = publish(buf, nullptr, nullptr, bytes);
+        gsort_status st = publish(buf, rank_ == root ? bytes : 0, nullptr, nullptr, s);
         if (!barrier()) return fail("barrier timeout");
-        std::vector<std::pair<int, void *>> opened;
-        if (st == GSORT_OK && rank_ != root) st = pull(root, buf, 0, bytes, buf, s, opened);
-        return finish(s, opened, st);
+        if (st == GSORT_OK && rank_ != root) st = pull(root, buf, 0, bytes, buf, s);
+        return finish(s, st);
     }
     // every rank has mapped the control block: its name can go
     gsort_status attach(const std::string &name) {
@@ -488,6 +522,12 @@ class IpcComm : public Comm {
 
   private:
     IpcShared *sh_;
+    void *stage_ = nullptr;
+    size_t cap_ = 0;
+    uint64_t gen_ = 0;
+    std::vector<void *> stages_;            // every staging buffer this rank made
+    std::vector<void *> peer_;              // the peers' staging buffers, opened
+    std::vector<uint64_t> peer_gen_;        // ... at these generations
 };
 
 }  // namespace

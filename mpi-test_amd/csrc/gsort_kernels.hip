@@ -1502,9 +1502,12 @@ __global__ __launch_bounds__(BLOCK) void k_partition_res(
     }
     __shared__ uint32_t s_keys[2][TILE];
     __shared__ uint32_t s_cur[2][kRadix];
-    __shared__ OT *s_dst[2][kRadix];
+    // each digit's run as a u32 index into out minus its LDS start (out holds < 2^32 keys): one
+    // 4-B random LDS read per key on the way out instead of an 8-B pointer
+    __shared__ uint32_t s_off[2][kRadix];
     __shared__ uint32_t s_wsum[2][kRadix / 64];
     __shared__ uint32_t s_spare[kAggSpare];
+    __shared__ uint32_t s_ovf[2];  // EST: a run of this tile overflowed its region
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     uint32_t pr, ntile, last_len = 0;
     if (L3) {
@@ -1537,6 +1540,7 @@ __global__ __launch_bounds__(BLOCK) void k_partition_res(
         }
     }
     if (tid < kRadix) { s_cur[0][tid] = 0; s_cur[1][tid] = 0; }
+    if (EST && tid < 2) s_ovf[tid] = 0;
     uint32_t *cursor[2];
     uint32_t limv[2] = {0, 0};  // EST: the region limits, loaded now (off the reservation path)
 #pragma unroll
@@ -1644,25 +1648,29 @@ __global__ __launch_bounds__(BLOCK) void k_partition_res(
     if (tid < kRadix) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            OT *d = out + ((L3 ? bases[tid] : bases[seg[h]]) + pos[h]) - excl[h];
+            s_off[h][tid] = (uint32_t)((L3 ? bases[tid] : bases[seg[h]]) + pos[h]) - excl[h];
             if (EST && cnt[h] && (uint64_t)pos[h] + cnt[h] > limv[h]) {
                 atomicOr(ovf, 1u);
-                d = dump - excl[h];
+                s_ovf[h] = 1;  // the block is re-sorted on the exact plan: the tile goes to dump
             }
-            s_dst[h][tid] = d;
         }
     }
     __syncthreads();
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+    for (int h = 0; h < 2; ++h) {
+        OT *o = out;
+        bool to_dump = false;
+        if (EST && s_ovf[h]) { o = dump; to_dump = true; }
 #pragma unroll
         for (int i = 0; i < ITEMS; ++i) {
             const uint32_t j = (uint32_t)(i * BLOCK) + tid;
             if (j < len[h]) {
                 const uint32_t key = s_keys[h][j];
-                s_dst[h][(key >> shift) & 255u][j] = (OT)key;
+                const uint32_t at = to_dump ? j : s_off[h][(key >> shift) & 255u] + j;
+                o[at] = (OT)key;
             }
         }
+    }
 }
 
 // Stable wave-level rank of one round (64 keys, lane order = key order) against the wave's

@@ -15,7 +15,8 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(HERE)
-LIB_PATH = os.path.join(PKG, "lib", "libgsort.so")
+# GSORT_LIB (development, same-box A/B of two builds: tools/ab_lib.sh) loads another build
+LIB_PATH = os.environ.get("GSORT_LIB") or os.path.join(PKG, "lib", "libgsort.so")
 
 OK, EINVAL, ENOMEM, EHIP, ERCCL, ENOSAMPLE, ECOMM = range(7)
 UNIFORM, ZIPF = 0, 1

@@ -23,12 +23,17 @@ def mpirun(prog, P, path, debug, tmp, timeout=150, env=None):
            f"{tmp}/e.%r", os.path.join(BIN, prog), path] + ([str(debug)] if debug is not None else [])
     e = dict(os.environ, **(env or {}))
     r = subprocess.run(cmd, timeout=timeout, capture_output=True, text=True, env=e)
-    outs = []
+    outs, errs = [], []
     for q in range(P):
         p = os.path.join(tmp, f"o.{q}")
         outs.append(open(p, "rb").read() if os.path.exists(p) else b"")
-    err0 = open(os.path.join(tmp, "e.0")).read() if os.path.exists(os.path.join(tmp, "e.0")) else ""
-    return r.returncode, outs, err0
+        p = os.path.join(tmp, f"e.{q}")
+        errs.append(open(p, errors="replace").read() if os.path.exists(p) else "")
+    if r.returncode != 0:  # every rank's stderr and mpirun's own output, for the failure report
+        print(f"mpirun rc={r.returncode}\nstdout: {r.stdout[-2000:]}\nstderr: {r.stderr[-2000:]}")
+        for q in range(P):
+            print(f"--- rank {q} stderr:\n{errs[q][-2000:]}")
+    return r.returncode, outs, errs[0]
 
 
 CASES = [("uniform65536s42", "radix_sort", P) for P in (2, 4, 8)] + \

@@ -106,10 +106,11 @@ def test_dropin_group_sample_ragged_and_too_small(gsort, orc, P):
     assert sum(i[2] for i in infos) == n
     head, nd, _ = contract_split(outs[0])
     assert head[0] == f"Each bucket will be put {-(-n // P)} items." and nd == n
-    # too few keys for 2P - 1 regular samples: every rank fails with GSORT_ENOSAMPLE (the
-    # reference aborts with "no enough sample", mpi_sample_sort.c:94-99)
+    # a block too small for the 2P - 1 regular samples (N = P - 1: the last block is empty):
+    # every rank fails with GSORT_ENOSAMPLE (the reference aborts with "no enough sample",
+    # mpi_sample_sort.c:94-99)
     with pytest.raises(gsort.GsortError) as e:
-        run_dropin(gsort, keys[: 2 * P - 1], P, "sample", 0, report=False)
+        run_dropin(gsort, keys[: P - 1], P, "sample", 0, report=False)
     assert e.value.status == gsort.ENOSAMPLE
 
 
