@@ -574,7 +574,8 @@ def main():
         "local_algo": "lsd" if last["local_algo"] == gsort.LOCAL_LSD else "msd",
         "local_plan": ("lsd passes" if a.local == "lsd" else
                        {0: "exact two-level", 1: "sampled", 2: "sampled, re-sorted exact",
-                        3: "sampled below a constant key prefix"}.get(
+                        3: "sampled below a constant key prefix",
+                        4: "one dominant 16-bit child counted"}.get(
                            plan, str(plan))),
         "verified": bool(ok),
         "reference_check_2p24": med,

@@ -151,7 +151,9 @@ gsort_status gsort_sample_info(const gsort_ctx *ctx, int32_t *splitters,
  * plan, 2 the sampled plan found the block ineligible or a region overflowed, and the block
  * was sorted again on the exact plan, 3 the sampled plan on digits below a key prefix every key
  * shares (e.g. 16- or 24-bit keys in int32) after a first sampled attempt found the block
- * ineligible (GSORT_EST=0 turns the sampled plan off). */
+ * ineligible, 4 one 16-bit child held at least half of the keys (Zipf, 8- or 16-bit keys, one
+ * frequent value): its keys were sorted by counting their low 16 bits, the others apart
+ * (GSORT_EST=0 turns the sampled plan off, GSORT_GIANT=0 the counted child). */
 int gsort_last_plan(const gsort_ctx *ctx);
 
 /* ---- drop-in staging (replaces MPI_Scatter / MPI_Gather(v) through rank 0) ---------------

@@ -308,6 +308,31 @@ hipError_t launch_est_classify(const EstPlan &p, hipStream_t s);  // K12g
 hipError_t launch_local_sort_e(const EstPlan &p, int cls, uint32_t first, uint32_t nlist,
                                bool publish, hipStream_t s);
 hipError_t launch_est_publish(const EstPlan &p, hipStream_t s);
+// ---- one dominant 16-bit child (gsort_kernels.hip, "giant child") -----------
+// K1m: res[0] = the most frequent top-16-bit child (ordered u32) of min(n, 16384) evenly
+// strided keys, res[1] = its sample count, res[2] = the samples (u64 each).
+hipError_t launch_est_mode(const uint32_t *in, uint64_t n, uint64_t *res, hipStream_t s);
+// K1g: child `child`'s keys (int32 input) into per-workgroup packed histograms of their low 16
+// bits (part: nblk x kH16PartWords u32; fix: kH16Shards x 65536 u64, zero on entry, as K1h),
+// every other key copied to cold + x * shard_cap (x = XCD shard, 8 of them) at a position
+// reserved on ctr[x]; ctr[8 + x] counts the cold keys below the child.  ctr (16 u64) zeroed by
+// the caller; cold holds kH16Shards * giant_shard_cap(n) keys.
+inline uint64_t giant_shard_cap(uint64_t n) {
+    const uint64_t pairs = (sweep_tiles(n) + 1) / 2;
+    return (pairs + kH16Shards - 1) / kH16Shards * 2 * kSweepTile;
+}
+hipError_t launch_giant_hist(const uint32_t *in, uint64_t n, uint32_t child, uint32_t *part,
+                             uint64_t *fix, uint32_t *cold, uint64_t *ctr, uint32_t *nblk,
+                             uint64_t *shard_cap, hipStream_t s);
+// K12m + K12s: counts (65536 u64) of the child's low 16 bits (fix zeroed again), starts (65537
+// u64) = their exclusive scan + the cold keys below the child (output positions).
+hipError_t launch_giant_plan(const uint32_t *part, uint32_t nblk, uint64_t *fix,
+                             const uint64_t *ctr, uint64_t *counts, uint64_t *starts,
+                             hipStream_t s);
+// K12w + K18g: the child's n_child keys written sorted at out[starts[0] .. starts[65536]) from
+// the counts; chunk_bin: scratch of ceil(n_child / 8192) u32.
+hipError_t launch_giant_expand(const uint64_t *starts, uint64_t n_child, uint32_t child,
+                               uint32_t *chunk_bin, uint32_t *out, hipStream_t s);
 // Plain device copy kernel (used when a sort has no non-trivial pass).
 hipError_t launch_copy(const uint32_t *in, uint32_t *out, uint64_t n, hipStream_t s);
 

@@ -3407,6 +3407,354 @@ hipError_t launch_local_sort_e(const EstPlan &p, int cls, uint32_t first, uint32
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------------------
+// One dominant 16-bit child ("giant child").  When at least half of a block's
+// keys share their top 16 bits c (Zipf keys: ~99.6 % are below 2^16; 8- or 16-bit keys; one
+// frequent value), every MSD level moves nearly every key again (the exact plan walks all four
+// levels with buckets of up to the whole block; the sampled plan's children outgrow K11).  Keys
+// carry no payload, so child c is sorted by COUNTING its low 16 bits: K1g reads the block once
+// -- child c's keys into a 65536-bin histogram per workgroup (K1h's packed u16 pairs and wrap
+// repair), every other ("cold") key compacted into its XCD shard's region of a scratch buffer
+// -- K12m sums the partials, K12s scans them into output starts (after the cold keys below c),
+// K12w maps every 8192-key output chunk to its first bin, and K18g writes child c's keys
+// straight from the counts.  The cold keys are sorted by the regular local sort.  4 B/key read
+// + 4 B/key write for the child, instead of 8 B/key per MSD level.
+// ---------------------------------------------------------------------------------------
+namespace {
+
+// K1m: the mode of the top 16 bits (ordered u32) over min(n, kModeSamples) keys at an even
+// stride, one workgroup: res[0] = the child, res[1] = its sample count, res[2] = samples.
+constexpr uint32_t kModeSamples = 16384;
+__global__ __launch_bounds__(1024) void k_est_mode(const uint32_t *__restrict__ in, uint64_t n,
+                                                   unsigned long long *__restrict__ res) {
+    constexpr uint32_t kWords = kBuckets16 / 2, PER = kModeSamples / 1024;
+    __shared__ uint32_t s_h[kWords];
+    __shared__ unsigned long long s_best[16];
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t i = tid; i < kWords; i += 1024) s_h[i] = 0;
+    const uint32_t S = n < kModeSamples ? (uint32_t)n : kModeSamples;
+    uint32_t k[PER];
+#pragma unroll
+    for (uint32_t j = 0; j < PER; ++j) {
+        const uint32_t i = j * 1024 + tid;
+        k[j] = i < S ? in[(uint64_t)i * n / S] ^ kFlip : 0u;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t j = 0; j < PER; ++j) {
+        const uint32_t b = k[j] >> 16;
+        if (j * 1024 + tid < S) atomicAdd(&s_h[b >> 1], 1u << ((b & 1u) << 4));  // < 2^16 each
+    }
+    __syncthreads();
+    unsigned long long best = 0;  // count << 32 | child
+    for (uint32_t w = tid * 32; w < tid * 32 + 32; ++w) {
+        const uint32_t v = s_h[w];
+        best = max(best, ((unsigned long long)(v & 0xffffu) << 32) | (2 * w));
+        best = max(best, ((unsigned long long)(v >> 16) << 32) | (2 * w + 1));
+    }
+#pragma unroll
+    for (int o = 32; o; o >>= 1) best = max(best, (unsigned long long)__shfl_xor(best, o));
+    if ((tid & 63) == 0) s_best[tid >> 6] = best;
+    __syncthreads();
+    if (tid == 0) {
+        for (int i = 1; i < 16; ++i) best = max(best, s_best[i]);
+        best = max(best, s_best[0]);
+        res[0] = best & 0xffffffffull;
+        res[1] = best >> 32;
+        res[2] = S;
+    }
+}
+
+// K1g: K1h's loop (tile pairs b, b + G, .. with the next tile prefetched) over the block; keys of
+// child c go into the workgroup's packed histogram of their LOW 16 bits (part, fix as K1h);
+// every other key is written (as the input int32) to cold + shard * shard_cap at a position
+// reserved per tile on ctr[shard] (8 XCD shards: tile pair p runs on workgroup p % G, shard
+// p % 8); ctr[8 + shard] counts the cold keys below child c.
+template <int BLOCK, bool FIN>
+__global__ __launch_bounds__(BLOCK) void k_giant_hist(const uint32_t *__restrict__ in, uint64_t n,
+                                                      uint32_t child, uint32_t *__restrict__ part,
+                                                      unsigned long long *__restrict__ fix,
+                                                      uint32_t *__restrict__ cold,
+                                                      unsigned long long shard_cap,
+                                                      unsigned long long *__restrict__ ctr) {
+    constexpr int ITEMS = kSweepTile / BLOCK;
+    constexpr uint32_t kWords = kBuckets16 / 2;
+    __shared__ uint32_t s_h[kWords + kAggSpare];
+    __shared__ uint32_t s_cnt[2];
+    __shared__ unsigned long long s_base;
+    uint32_t *spare = s_h + kWords;
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    for (uint32_t i = tid; i < kWords; i += BLOCK) s_h[i] = 0;
+    if (tid < 2) s_cnt[tid] = 0;
+    const uint32_t ntiles = (uint32_t)((n + kSweepTile - 1) / kSweepTile);
+    const uint32_t last_len = (uint32_t)(n - (uint64_t)(ntiles - 1) * kSweepTile);
+    auto tile_len = [&](uint32_t t) -> uint32_t {
+        return t == ntiles - 1 ? last_len : (uint32_t)kSweepTile;
+    };
+    auto tile_of = [&](uint32_t i) -> uint32_t {
+        return 2 * (blockIdx.x + (i >> 1) * gridDim.x) + (i & 1);
+    };
+    const uint32_t shard = blockIdx.x % kShards;
+    unsigned long long *fx = fix + (uint64_t)shard * kBuckets16;
+    uint32_t *cs = cold + (uint64_t)shard * shard_cap;
+    uint32_t t = tile_of(0);
+    uint32_t k[ITEMS];
+    if (t < ntiles) {
+        const uint32_t len = tile_len(t);
+        load_tile<BLOCK, ITEMS, FIN>(in + (uint64_t)t * kSweepTile + tid,
+                                     len == (uint32_t)kSweepTile, len, k);
+    }
+    __syncthreads();  // zeroing done
+    for (uint32_t i = 1; t < ntiles; ++i) {
+        const uint32_t len = tile_len(t);
+        const uint32_t tn = tile_of(i);
+        uint32_t kn[ITEMS];
+        if (tn < ntiles) {
+            const uint32_t lenn = tile_len(tn);
+            load_tile<BLOCK, ITEMS, FIN>(in + (uint64_t)tn * kSweepTile + tid,
+                                         lenn == (uint32_t)kSweepTile, lenn, kn);
+        }
+        bool g[ITEMS];
+        uint32_t old[ITEMS];
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j)
+            g[j] = (uint32_t)(j * BLOCK) + tid < len && (k[j] >> 16) == child;
+        // skewed wave (its first item all child c keys on one packed word): aggregated adds
+        const uint32_t w0 = __builtin_amdgcn_readfirstlane((k[0] & 0xffffu) >> 1);
+        const bool skew = __ballot(g[0] && ((k[0] & 0xffffu) >> 1) == w0) ==
+                          __builtin_amdgcn_read_exec();
+        bool wrap = false;
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            const uint32_t b = k[j] & 0xffffu;
+            old[j] = 0;
+            if (g[j]) old[j] = skew ? agg_add_pair(s_h, b, spare)
+                                    : atomicAdd(&s_h[b >> 1], 1u << ((b & 1u) << 4));
+        }
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j)
+            wrap |= g[j] && ((old[j] >> ((k[j] & 1u) << 4)) & 0xffffu) == 0xffffu;
+        if (__builtin_expect(wrap, 0)) {
+#pragma unroll
+            for (int j = 0; j < ITEMS; ++j)
+                if (g[j] && ((old[j] >> ((k[j] & 1u) << 4)) & 0xffffu) == 0xffffu)
+                    h16_wrap(fx, k[j] & 0xffffu, old[j]);
+        }
+        // cold keys: per-wave counts, one reservation per tile on the shard's counter
+        uint64_t m[ITEMS];
+        uint32_t wc = 0, wl = 0;
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            const bool cj = (uint32_t)(j * BLOCK) + tid < len && !g[j];
+            m[j] = __ballot(cj);
+            wc += (uint32_t)__popcll(m[j]);
+            wl += (uint32_t)__popcll(__ballot(cj && (k[j] >> 16) < child));
+        }
+        uint32_t woff = 0;
+        if (lane == 0 && wc) woff = atomicAdd(&s_cnt[0], wc);
+        if (lane == 0 && wl) atomicAdd(&s_cnt[1], wl);
+        woff = __shfl(woff, 0);
+        __syncthreads();
+        if (tid == 0) {
+            const uint32_t tc = s_cnt[0], tl = s_cnt[1];
+            s_base = tc ? atomicAdd(&ctr[shard], (unsigned long long)tc) : 0ull;
+            if (tl) atomicAdd(&ctr[kShards + shard], (unsigned long long)tl);
+            s_cnt[0] = 0;
+            s_cnt[1] = 0;
+        }
+        __syncthreads();
+        if (wc) {
+            const unsigned long long base = s_base + woff;
+            uint32_t run = 0;
+#pragma unroll
+            for (int j = 0; j < ITEMS; ++j) {
+                if ((m[j] >> lane) & 1ull) cs[base + run + lane_rank(m[j])] = k[j] ^ (FIN ? kFlip : 0u);
+                run += (uint32_t)__popcll(m[j]);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) k[j] = kn[j];
+        t = tn;
+    }
+    __syncthreads();
+    uint32_t *dst = part + (uint64_t)blockIdx.x * kWords;
+    for (uint32_t i = tid; i < kWords; i += BLOCK) dst[i] = s_h[i];
+}
+
+// K12m: counts[b] = child c's keys with low 16 bits b: the b-half of word b/2 over the nblk
+// partials + the wrap repairs of all shards (which it zeroes for the next K1h / K1g).  One thread
+// per packed word.
+__global__ __launch_bounds__(256) void k_giant_count(const uint32_t *__restrict__ part,
+                                                     uint32_t nblk,
+                                                     unsigned long long *__restrict__ fix,
+                                                     unsigned long long *__restrict__ counts) {
+    constexpr uint32_t kWords = kBuckets16 / 2;
+    const uint32_t w = blockIdx.x * 256 + threadIdx.x;
+    unsigned long long lo = 0, hi = 0;
+#pragma unroll 8
+    for (uint32_t b = 0; b < nblk; ++b) {
+        const uint32_t v = part[(uint64_t)b * kWords + w];
+        lo += v & 0xffffu;
+        hi += v >> 16;
+    }
+#pragma unroll
+    for (uint32_t x = 0; x < kShards; ++x) {
+        unsigned long long *f = fix + (uint64_t)x * kBuckets16 + 2 * w;
+        lo += f[0];
+        hi += f[1];
+        f[0] = 0;
+        f[1] = 0;
+    }
+    counts[2 * w] = lo;
+    counts[2 * w + 1] = hi;
+}
+
+// K12s: starts[b] = (cold keys below the child: sum of ctr[8 .. 16)) + the exclusive scan of
+// counts; starts[65536] = the child's end.  One workgroup, 64 bins per thread.
+__global__ __launch_bounds__(1024) void k_giant_scan(const unsigned long long *__restrict__ counts,
+                                                     const unsigned long long *__restrict__ ctr,
+                                                     unsigned long long *__restrict__ starts) {
+    __shared__ unsigned long long s_w[16];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    unsigned long long sum = 0;
+    for (uint32_t b = tid * 64; b < tid * 64 + 64; ++b) sum += counts[b];
+    unsigned long long x = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned long long v = __shfl_up(x, o);
+        if ((int)lane >= o) x += v;
+    }
+    if (lane == 63) s_w[w] = x;
+    __syncthreads();
+    unsigned long long run = x - sum, total = 0;
+    for (uint32_t ww = 0; ww < 16; ++ww) {
+        if (ww < w) run += s_w[ww];
+        total += s_w[ww];
+    }
+    unsigned long long lo = 0;
+#pragma unroll
+    for (uint32_t x8 = 0; x8 < kShards; ++x8) lo += ctr[kShards + x8];
+    run += lo;
+    for (uint32_t b = tid * 64; b < tid * 64 + 64; ++b) {
+        starts[b] = run;
+        run += counts[b];
+    }
+    if (tid == 0) starts[kBuckets16] = lo + total;
+}
+
+// K12w: chunk_bin[w] = the bin holding output position starts[0] + w * kExpandChunk (the last
+// bin b with starts[b] <= that position), one thread per chunk.
+constexpr uint32_t kExpandChunk = 8192;
+__global__ __launch_bounds__(256) void k_giant_chunks(const unsigned long long *__restrict__ starts,
+                                                      uint32_t nchunks, uint32_t *__restrict__ chunk_bin) {
+    const uint32_t w = blockIdx.x * 256 + threadIdx.x;
+    if (w >= nchunks) return;
+    const unsigned long long q = starts[0] + (unsigned long long)w * kExpandChunk;
+    uint32_t lo = 0, hi = kBuckets16;  // starts[lo] <= q < starts[hi]
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (starts[mid] <= q) lo = mid;
+        else hi = mid;
+    }
+    chunk_bin[w] = lo;
+}
+
+// K18g: chunk w = output positions [q0, q0 + 8192) of child c: every non-empty bin b starting
+// in it marks its first position with b + 1 (the chunk's first bin marks position 0), an
+// inclusive max-scan gives every position its bin, and the keys (c << 16 | bin) go out as int32
+// in coalesced stores.
+__global__ __launch_bounds__(1024) void k_giant_expand(const unsigned long long *__restrict__ starts,
+                                                       const uint32_t *__restrict__ chunk_bin,
+                                                       uint32_t nchunks, uint32_t child,
+                                                       uint32_t *__restrict__ out) {
+    constexpr uint32_t C = kExpandChunk, PER = C / 1024;
+    __shared__ uint32_t s_m[C];
+    __shared__ uint32_t s_w[16];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6, ch = blockIdx.x;
+    const unsigned long long end = starts[kBuckets16];
+    const unsigned long long q0 = starts[0] + (unsigned long long)ch * C;
+    const uint32_t len = (uint32_t)min((unsigned long long)C, end - q0);
+#pragma unroll
+    for (uint32_t i = 0; i < PER; ++i) s_m[i * 1024 + tid] = 0;
+    const uint32_t b0 = chunk_bin[ch];
+    const uint32_t b1 = ch + 1 < nchunks ? chunk_bin[ch + 1] : kBuckets16 - 1;
+    __syncthreads();
+    for (uint32_t b = b0 + tid; b <= b1; b += 1024) {
+        const unsigned long long st = starts[b], en = starts[b + 1];
+        if (en > st && (b == b0 || st < q0 + len))
+            atomicMax(&s_m[st > q0 ? (uint32_t)(st - q0) : 0u], b + 1);
+    }
+    __syncthreads();
+    uint32_t v[PER], mx = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < PER; ++i) { v[i] = max(mx, s_m[tid * PER + i]); mx = v[i]; }
+    uint32_t x = mx;  // inclusive max over the threads of the wave
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(x, o);
+        if ((int)lane >= o) x = max(x, t);
+    }
+    if (lane == 63) s_w[w] = x;
+    uint32_t pre = __shfl_up(x, 1);
+    if (lane == 0) pre = 0;
+    __syncthreads();
+    for (uint32_t ww = 0; ww < w; ++ww) pre = max(pre, s_w[ww]);
+#pragma unroll
+    for (uint32_t i = 0; i < PER; ++i) s_m[tid * PER + i] = max(v[i], pre);
+    __syncthreads();
+    uint32_t *o = out + q0;
+#pragma unroll
+    for (uint32_t i = 0; i < PER; ++i) {
+        const uint32_t j = i * 1024 + tid;
+        if (j < len) o[j] = ((child << 16) | (s_m[j] - 1u)) ^ kFlip;
+    }
+}
+
+}  // namespace
+
+hipError_t launch_est_mode(const uint32_t *in, uint64_t n, uint64_t *res, hipStream_t s) {
+    if (n == 0) return hipErrorInvalidValue;
+    launch_k(k_est_mode, 1, 1024, 0, s, in, n, reinterpret_cast<unsigned long long *>(res));
+    return hipGetLastError();
+}
+
+hipError_t launch_giant_hist(const uint32_t *in, uint64_t n, uint32_t child, uint32_t *part,
+                             uint64_t *fix, uint32_t *cold, uint64_t *ctr, uint32_t *nblk,
+                             uint64_t *shard_cap, hipStream_t s) {
+    if (n == 0) return hipErrorInvalidValue;
+    const uint64_t pairs = (sweep_tiles(n) + 1) / 2;
+    const uint64_t g = std::min<uint64_t>((pairs + kShards - 1) / kShards * kShards, kH16Blocks);
+    *nblk = (uint32_t)g;
+    *shard_cap = giant_shard_cap(n);
+    using ull = unsigned long long;
+    launch_k(k_giant_hist<1024, true>, (unsigned)g, 1024, 0, s, in, n, child, part,
+             reinterpret_cast<ull *>(fix), cold, (ull)*shard_cap, reinterpret_cast<ull *>(ctr));
+    return hipGetLastError();
+}
+
+hipError_t launch_giant_plan(const uint32_t *part, uint32_t nblk, uint64_t *fix,
+                             const uint64_t *ctr, uint64_t *counts, uint64_t *starts,
+                             hipStream_t s) {
+    using ull = unsigned long long;
+    launch_k(k_giant_count, kBuckets16 / 2 / 256, 256, 0, s, part, nblk,
+             reinterpret_cast<ull *>(fix), reinterpret_cast<ull *>(counts));
+    launch_k(k_giant_scan, 1, 1024, 0, s, reinterpret_cast<const ull *>(counts),
+             reinterpret_cast<const ull *>(ctr), reinterpret_cast<ull *>(starts));
+    return hipGetLastError();
+}
+
+hipError_t launch_giant_expand(const uint64_t *starts, uint64_t n_child, uint32_t child,
+                               uint32_t *chunk_bin, uint32_t *out, hipStream_t s) {
+    if (n_child == 0) return hipSuccess;
+    const uint64_t nch = (n_child + kExpandChunk - 1) / kExpandChunk;
+    using ull = unsigned long long;
+    launch_k(k_giant_chunks, (unsigned)((nch + 255) / 256), 256, 0, s,
+             reinterpret_cast<const ull *>(starts), (uint32_t)nch, chunk_bin);
+    launch_k(k_giant_expand, (unsigned)nch, 1024, 0, s, reinterpret_cast<const ull *>(starts),
+             chunk_bin, (uint32_t)nch, child, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_copy(const uint32_t *in, uint32_t *out, uint64_t n, hipStream_t s) {
     if (n == 0) return hipSuccess;
     launch_k(k_copy, grid_for(n, 256, 8192), 256, 0, s, in, out, n);

@@ -78,10 +78,12 @@ struct gsort_ctx {
     // sampled plan (K1e .. K11e): level-3 / level-2 region buffers, sample partials, plan
     // arrays, K3a tile descriptors, overflow scratch tile
     bool plan_est = true;   // GSORT_EST (default 1)
+    bool plan_giant = true; // GSORT_GIANT (default 1): the one-dominant-child path
     double est_slack = 1.0; // GSORT_EST_SLACK (test hook: the sampling-error margin's scale)
     int ncu = 256;
     int last_plan = 0;      // gsort_last_plan: 0 exact, 1 sampled, 2 sampled then exact
     DevBuf m_ex, m_ey, m_epart, m_eplan, m_edesc, m_edump;
+    DevBuf m_gplan;  // one dominant child: counts (65536 u64), starts (65537 u64), chunk bins
     bool est_busy = false;   // msd_sort_est is using m_ex / m_ey (not reclaimable)
     size_t scratch_bytes = 0;  // device bytes held by ensure()-managed scratch
     // K12p mailbox: pinned host memory the GPU writes the work-list counters into, then a
@@ -123,6 +125,7 @@ constexpr size_t OFF_HIST = 0, OFF_TOT = 8192, OFF_BASES = 10240, OFF_CTR = 1228
                  OFF_ONE = 12416, OFF_CTR3 = 12544, OFF_PLAN = 20480;
 constexpr size_t OFF_FLAGS = 12408;  // K12b's trivial-level word, inside the published range
 constexpr size_t OFF_MINMAX = 12480;  // the offset retry's exact min / max (2 int32)
+constexpr size_t OFF_GIANT = 16384;   // K1m result (3 u64) + K1g counters (16 u64)
 
 gsort_status set_err(gsort_ctx *c, gsort_status st, const std::string &msg) {
     if (c) c->err = msg;
@@ -610,7 +613,7 @@ void for_each_buf(gsort_ctx *c, F &&f) {
         {"m_ccount", &c->m_ccount}, {"m_t3", &c->m_t3}, {"m_cur3", &c->m_cur3},
         {"m_tdesc", &c->m_tdesc}, {"m_ex", &c->m_ex}, {"m_ey", &c->m_ey},
         {"m_epart", &c->m_epart}, {"m_eplan", &c->m_eplan}, {"m_edesc", &c->m_edesc},
-        {"m_edump", &c->m_edump},
+        {"m_edump", &c->m_edump}, {"m_gplan", &c->m_gplan},
         {"m_split", &c->m_split}, {"m_rpos", &c->m_rpos}, {"m_bsize", &c->m_bsize},
         {"m_bseg", &c->m_bseg}, {"m_blist", &c->m_blist}, {"m_gb", &c->m_gb},
         {"m_pack", &c->m_pack}, {"m_meta", &c->m_meta}, {"m_g16", &c->m_g16},
@@ -1142,6 +1145,93 @@ gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
     return GSORT_OK;
 }
 
+gsort_status msd_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *out,
+                      uint32_t *tmp, gsort_stats *stats, bool group16, uint16_t *out16,
+                      uint64_t *gb, bool allow_est, bool allow_giant);
+
+// One dominant 16-bit child (gsort_kernels.hip, "giant child"): K1m found child `child` in at
+// least half of the samples.  K1g histograms its keys' low 16 bits and compacts the other
+// (cold) keys per XCD shard into S_TMP; K12m / K12s turn the partials into output starts; the
+// cold keys are gathered, sorted by the regular local sort into out + n_child (below-child keys
+// then move to the front) and K18g writes the child's keys from the counts.  *ok = false: the
+// child held fewer than half of the keys after all (nothing is written; the caller goes on).
+gsort_status giant_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *out,
+                        uint32_t child, gsort_stats *stats, bool *ok) {
+    *ok = false;
+    const uint64_t cap = (uint64_t)kH16Shards * giant_shard_cap(n);
+    ST_TRY(ensure(c, c->slot[S_TMP], cap * 4));
+    ST_TRY(ensure(c, c->m_part, (size_t)kH16Blocks * kH16PartWords * 4));
+    constexpr size_t kFixBytes = (size_t)kH16Shards * kBuckets16 * 8;
+    ST_TRY(ensure(c, c->m_fix, kFixBytes));
+    const uint64_t nchunks_max = n / 8192 + 2;
+    ST_TRY(ensure(c, c->m_gplan, ((size_t)2 * kBuckets16 + 1) * 8 + nchunks_max * 4));
+    if (c->fix_clean != c->m_fix.p) HIP_TRY(c, hipMemsetAsync(c->m_fix.p, 0, kFixBytes, c->stream));
+    c->fix_clean = nullptr;
+    uint64_t *d_ctr = reinterpret_cast<uint64_t *>(c->d_small + OFF_GIANT) + 4;
+    uint64_t *h_ctr = reinterpret_cast<uint64_t *>(c->h_small + OFF_GIANT) + 4;
+    uint64_t *counts = static_cast<uint64_t *>(c->m_gplan.p), *starts = counts + kBuckets16;
+    uint32_t *chunk_bin = reinterpret_cast<uint32_t *>(starts + kBuckets16 + 1);
+    uint32_t *cold = slot_ptr<uint32_t>(c, S_TMP);
+    HIP_TRY(c, hipMemsetAsync(d_ctr, 0, 2 * kH16Shards * 8, c->stream));
+    uint32_t nblk = 0;
+    uint64_t shard_cap = 0;
+    hipEvent_t t = tic(c);
+    HIP_TRY(c, launch_giant_hist(in, n, child, reinterpret_cast<uint32_t *>(c->m_part.p),
+                                 reinterpret_cast<uint64_t *>(c->m_fix.p), cold, d_ctr, &nblk,
+                                 &shard_cap, c->stream));
+    HIP_TRY(c, launch_giant_plan(reinterpret_cast<uint32_t *>(c->m_part.p), nblk,
+                                 reinterpret_cast<uint64_t *>(c->m_fix.p), d_ctr, counts, starts,
+                                 c->stream));
+    c->fix_clean = c->m_fix.p;  // K12m left it zeroed
+    toc(c, PH_COUNT, t);
+    HIP_TRY(c, hipMemcpyAsync(h_ctr, d_ctr, 2 * kH16Shards * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    uint64_t shard_cold[kH16Shards], n_cold = 0, n_lo = 0;
+    for (uint32_t x = 0; x < kH16Shards; ++x) {
+        shard_cold[x] = h_ctr[x];
+        n_cold += h_ctr[x];
+        n_lo += h_ctr[kH16Shards + x];
+    }
+    const uint64_t n_child = n - n_cold;
+    if (n_cold > n || n_lo > n_cold)
+        return set_err(c, GSORT_EINVAL, "giant child: inconsistent cold counts");
+    if (n_child < n / 2) return GSORT_OK;  // the sample misjudged: not worth it
+    // the cold keys: gathered from their shard regions into out[0, n_cold), sorted into
+    // out[n_child, n) (disjoint: n_cold <= n_child) with S_TMP as scratch, and their part below
+    // the child moved to the front (n_lo <= n_cold <= n_child: no overlap either); the child's
+    // keys then fill [n_lo, n_lo + n_child)
+    if (n_cold) {
+        uint64_t at = 0;
+        for (uint32_t x = 0; x < kH16Shards; ++x) {
+            if (shard_cold[x])
+                HIP_TRY(c, hipMemcpyAsync(out + at, cold + (uint64_t)x * shard_cap,
+                                          shard_cold[x] * 4, hipMemcpyDeviceToDevice, c->stream));
+            at += shard_cold[x];
+        }
+        gsort_stats cst;
+        memset(&cst, 0, sizeof(cst));
+        const int lp = c->last_plan;
+        ST_TRY(msd_sort(c, out, n_cold, out + n_child, cold, &cst, false, nullptr, nullptr, true,
+                        false));
+        c->last_plan = lp;
+        if (n_lo)
+            HIP_TRY(c, hipMemcpyAsync(out, out + n_child, n_lo * 4, hipMemcpyDeviceToDevice,
+                                      c->stream));
+        if (stats) stats->keys_bucket_sort += n_cold;
+    }
+    t = tic(c);
+    HIP_TRY(c, launch_giant_expand(starts, n_child, child, chunk_bin, out, c->stream));
+    toc(c, PH_BUCKET, t);
+    if (stats) {
+        stats->passes_run = 1;
+        stats->keys_level[0] += n;
+        stats->keys_bucket_sort += n_child;
+        stats->buckets_local += 1;
+    }
+    *ok = true;
+    return GSORT_OK;
+}
+
 // group16: stop after level 2 -- out holds the keys (int32) grouped by their top 16 bits
 // (ordered u32) but not sorted inside a group (the sender side of the distributed radix);
 // with out16 and n > kLocalMax, level 2 stores only the low 16 bits of every key, at out16.
@@ -1149,9 +1239,12 @@ gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
 // bounds of the grouped block.
 // allow_est: the sampled plan may run (it waits on the host for its mailbox words mid-sort, so
 // callers that must not block -- the distributed sender's grouping -- keep it off).
+// allow_giant: an ineligible block may take the one-dominant-child path (its cold keys are
+// sorted with allow_giant off).
 gsort_status msd_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *out,
                       uint32_t *tmp, gsort_stats *stats, bool group16 = false,
-                      uint16_t *out16 = nullptr, uint64_t *gb = nullptr, bool allow_est = false) {
+                      uint16_t *out16 = nullptr, uint64_t *gb = nullptr, bool allow_est = false,
+                      bool allow_giant = true) {
     c->last_plan = 0;
     if (n == 0) return GSORT_OK;
     if (allow_est && c->plan_est && c->plan16 && !group16 && n >= kEstMinKeys &&
@@ -1161,6 +1254,22 @@ gsort_status msd_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *ou
         ST_TRY(msd_sort_est(c, in, n, out, stats, &ok, 0, 0, &r));
         c->last_plan = ok ? 1 : 2;
         if (ok) return GSORT_OK;
+        // one 16-bit child holding at least half of the keys (Zipf, 8- / 16-bit keys, one
+        // frequent value): counted, not partitioned (K1m decides from 16384 strided samples)
+        if (allow_giant && c->plan_giant && r.valid) {
+            uint64_t *d_res = reinterpret_cast<uint64_t *>(c->d_small + OFF_GIANT);
+            uint64_t *h_res = reinterpret_cast<uint64_t *>(c->h_small + OFF_GIANT);
+            HIP_TRY(c, launch_est_mode(in, n, d_res, c->stream));
+            HIP_TRY(c, hipMemcpyAsync(h_res, d_res, 24, hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(c, hipStreamSynchronize(c->stream));
+            if (h_res[2] && 2 * h_res[1] >= h_res[2]) {
+                ST_TRY(giant_sort(c, in, n, out, (uint32_t)h_res[0], stats, &ok));
+                if (ok) {
+                    c->last_plan = 4;
+                    return GSORT_OK;
+                }
+            }
+        }
         // An ineligible block whose keys span a narrow range: retry with every digit below the
         // bits the range's keys share (children of at most kLocalMax / 2 on average), either
         // a prefix the samples share (free: K3r checks it on every key) or -- when the range
@@ -2189,6 +2298,7 @@ gsort_status create_common(gsort_ctx *c, int hip_device) {
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     if (const char *e = getenv("GSORT_PLAN16")) c->plan16 = atoi(e) != 0;
     if (const char *e = getenv("GSORT_EST")) c->plan_est = atoi(e) != 0;
+    if (const char *e = getenv("GSORT_GIANT")) c->plan_giant = atoi(e) != 0;
     if (const char *e = getenv("GSORT_EST_SLACK")) c->est_slack = atof(e);
     HIP_TRY(c, hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, hip_device));
     {

@@ -285,12 +285,14 @@ class Context:
         self._c(lib().gsort_sample_info(self.h, spl.ctypes.data, cnt.ctypes.data))
         return spl[: self.nranks - 1], cnt
 
-    PLAN_EXACT, PLAN_SAMPLED, PLAN_SAMPLED_THEN_EXACT, PLAN_SAMPLED_SHIFTED = 0, 1, 2, 3
+    PLAN_EXACT, PLAN_SAMPLED, PLAN_SAMPLED_THEN_EXACT, PLAN_SAMPLED_SHIFTED, PLAN_GIANT = \
+        0, 1, 2, 3, 4
 
     def last_plan(self):
         """Plan of the last one-rank local sort (gsort_last_plan): 0 exact, 1 sampled,
         2 sampled then re-sorted on the exact plan (ineligible block or a region overflow),
-        3 sampled on the digits below a constant key prefix."""
+        3 sampled on the digits below a constant key prefix, 4 one dominant 16-bit child
+        counted (its low 16 bits), the other keys sorted apart."""
         return lib().gsort_last_plan(self.h)
 
     def generate(self, dist, seed, start, n, d_out):

@@ -16,7 +16,7 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-SAMPLED, FALLBACK, SHIFTED = 1, 2, 3
+SAMPLED, FALLBACK, SHIFTED, GIANT = 1, 2, 3, 4
 
 
 def _ctx(gsort, **env):
@@ -108,13 +108,15 @@ def test_sampled_plan_distributions(ctx, orc, name):
     keys = _inputs(orc, n)[name]
     got, _ = _sort(ctx, keys)
     plan = ctx.last_plan()
-    assert plan in (SAMPLED, FALLBACK, SHIFTED), plan
+    assert plan in (SAMPLED, FALLBACK, SHIFTED, GIANT), plan
     if name in ("sorted", "reversed", "sorted_blocks"):  # uniform keys, position-correlated
         assert plan == SAMPLED, name
-    if name in ("zipf", "half_one_value"):  # a child > kLocalMax, keys over the whole range
-        assert plan == FALLBACK, name
-    if name in ("bits16", "bits24", "all_equal"):  # a narrow key range: the digits below its
-        assert plan == SHIFTED, name  # shared bits (all-equal: a copy)
+    if name in ("zipf", "bits16", "all_equal"):  # one 16-bit child holds (nearly) every key:
+        assert plan == GIANT, name  # counted, not partitioned
+    if name == "half_one_value":  # the child holds about half: either way is right
+        assert plan in (FALLBACK, GIANT), name
+    if name == "bits24":  # a narrow key range: the digits below its shared bits
+        assert plan == SHIFTED, name
     assert np.array_equal(got, np.sort(keys)), name
 
 
@@ -208,11 +210,10 @@ def test_sampled_plan_shifted_prefix_check(ctx, case):
         keys = (keys - (1 << 16)).astype(np.int32)
     got, _ = _sort(ctx, keys)
     plan = ctx.last_plan()
-    if case == "negative_16bit":
-        assert plan == SHIFTED
-    else:
-        assert plan in (FALLBACK, SHIFTED, SAMPLED)
-        assert plan != SHIFTED or case != "prefix_broken_late"
+    if case == "negative_16bit":  # every key in child 0x7fff: counted
+        assert plan == GIANT
+    else:  # one child holds all but a few keys: counted, the outliers sorted as cold keys
+        assert plan == GIANT, plan
     assert np.array_equal(got, np.sort(keys)), case
 
 
@@ -230,7 +231,9 @@ def test_sampled_plan_shifted_ranges(ctx, lo, hi, n):
     assert np.array_equal(got, np.sort(keys)), (lo, hi)
     # across zero the shared bits are the keys' minus the exact minimum: that read pass is only
     # spent when the first sample's child counts are known (here two children wrapped them)
-    assert ctx.last_plan() == (FALLBACK if lo < 0 < hi else SHIFTED), (lo, hi, ctx.last_plan())
+    # (across zero two children hold half the keys each: the one-child count may take them)
+    assert ctx.last_plan() in ((FALLBACK, GIANT) if lo < 0 < hi else (SHIFTED,)), \
+        (lo, hi, ctx.last_plan())
 
 
 @pytest.mark.parametrize("case", ["gauss", "gauss_outliers", "two_values_across_zero"])
@@ -249,6 +252,71 @@ def test_sampled_plan_offset_retry(ctx, case):
             keys[[7, n // 3, n - 2]] = [-2**31, 2**31 - 1, 123456789]
     got, _ = _sort(ctx, keys)
     assert np.array_equal(got, np.sort(keys)), case
-    assert ctx.last_plan() in (FALLBACK, SHIFTED), ctx.last_plan()
+    assert ctx.last_plan() in (FALLBACK, SHIFTED, GIANT), ctx.last_plan()
     if case == "gauss":
         assert ctx.last_plan() == SHIFTED
+
+
+# ---- one dominant 16-bit child ("giant child") -------------------------------
+def _giant_inputs(orc, n):
+    rng = np.random.default_rng(31)
+    u = orc.gen(orc.UNIFORM, 32, n)
+    r = rng.random(n)
+    return {
+        # Zipf s = 1.5 (configs[4]'s distribution): ~99.6 % below 2^16, the rest cold
+        "zipf": orc.gen(orc.ZIPF, 33, n),
+        "bits8": (u & 0xFF).astype(np.int32),
+        "bits16_negative": ((u & 0xFFFF) - (1 << 16)).astype(np.int32),
+        # 60 % in one child, 20 % below it (negative keys) and 20 % above: the cold keys below
+        # the child move to the front, those above go after it
+        "child_in_middle": np.where(r < 0.6, (u & 0xFFFF) + (7 << 16),
+                                    np.where(r < 0.8, -(u >> 8) - 1, u | (1 << 30))).astype(np.int32),
+        "one_hot_value": np.where(r < 0.7, np.int32(-123456), u).astype(np.int32),
+        "all_equal_min": np.full(n, -2**31, dtype=np.int32),
+    }
+
+
+@pytest.mark.parametrize("name", ["zipf", "bits8", "bits16_negative", "child_in_middle",
+                                  "one_hot_value", "all_equal_min"])
+@pytest.mark.parametrize("n", [1 << 22, (1 << 24) + 777])
+def test_giant_child_counted(ctx, orc, name, n):
+    keys = _giant_inputs(orc, n)[name]
+    for algo in ("radix", "sample"):
+        got, st = _sort(ctx, keys, algo)
+        assert ctx.last_plan() == GIANT, (name, algo, ctx.last_plan())
+        assert np.array_equal(got, np.sort(keys)), (name, algo)
+        assert st["passes_run"] == 1 and st["buckets_local"] >= 1
+
+
+def test_giant_child_sample_misjudged(ctx):
+    """Every strided sample lands on one value but only 1/256 of the keys hold it: the exact
+    count after K1g sees the child is not dominant, writes nothing, and the block is sorted on
+    another plan."""
+    n = 1 << 22
+    keys = np.random.default_rng(41).integers(-2**31, 2**31, n, dtype=np.int64).astype(np.int32)
+    keys[:: n // 16384] = 5  # exactly the K1m sample positions (i * n / 16384)
+    got, _ = _sort(ctx, keys)
+    assert ctx.last_plan() in (SAMPLED, FALLBACK), ctx.last_plan()
+    assert np.array_equal(got, np.sort(keys))
+
+
+def test_giant_child_off(gsort, orc):
+    c = _ctx(gsort, GSORT_GIANT=0)
+    try:
+        keys = orc.gen(orc.ZIPF, 34, 1 << 22)
+        got, _ = _sort(c, keys)
+        assert c.last_plan() == FALLBACK
+        assert np.array_equal(got, np.sort(keys))
+    finally:
+        c.close()
+
+
+def test_giant_then_sampled_reuses_scratch(ctx, orc):
+    """Giant, uniform, giant on one context: K12m leaves K1h's wrap repairs zeroed, the region
+    buffers and S_TMP are shared."""
+    for i, (dist, n) in enumerate([(orc.ZIPF, 1 << 24), (orc.UNIFORM, 1 << 23),
+                                   (orc.ZIPF, (1 << 22) + 5)]):
+        keys = orc.gen(dist, 60 + i, n)
+        got, _ = _sort(ctx, keys)
+        assert ctx.last_plan() == (GIANT if dist == orc.ZIPF else SAMPLED)
+        assert np.array_equal(got, np.sort(keys))
