@@ -3422,10 +3422,19 @@ hipError_t launch_local_sort_e(const EstPlan &p, int cls, uint32_t first, uint32
 // ---------------------------------------------------------------------------------------
 namespace {
 
+// Workgroup barrier that waits only for this wave's LDS operations: a __syncthreads() also
+// drains the global loads in flight (s_waitcnt vmcnt(0)), which would cost K1g its prefetch of
+// the next tile at every per-tile reservation.
+__device__ __forceinline__ void lds_barrier() {
+    __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // K1m: the mode of the top 16 bits (ordered u32) over min(n, kModeSamples) keys at an even
-// stride, one workgroup: res[0] = the child, res[1] = its sample count, res[2] = samples.
+// stride (floor(n / kModeSamples)), one workgroup: res[0] = the child, res[1] = its sample
+// count, res[2] = samples.
 constexpr uint32_t kModeSamples = 16384;
 __global__ __launch_bounds__(1024) void k_est_mode(const uint32_t *__restrict__ in, uint64_t n,
+                                                   uint64_t stride,
                                                    unsigned long long *__restrict__ res) {
     constexpr uint32_t kWords = kBuckets16 / 2, PER = kModeSamples / 1024;
     __shared__ uint32_t s_h[kWords];
@@ -3437,7 +3446,7 @@ __global__ __launch_bounds__(1024) void k_est_mode(const uint32_t *__restrict__ 
 #pragma unroll
     for (uint32_t j = 0; j < PER; ++j) {
         const uint32_t i = j * 1024 + tid;
-        k[j] = i < S ? in[(uint64_t)i * n / S] ^ kFlip : 0u;
+        k[j] = i < S ? in[(uint64_t)i * stride] ^ kFlip : 0u;  // (no 64-bit division)
     }
     __syncthreads();
 #pragma unroll
@@ -3554,7 +3563,7 @@ __global__ __launch_bounds__(BLOCK) void k_giant_hist(const uint32_t *__restrict
         if (lane == 0 && wc) woff = atomicAdd(&s_cnt[0], wc);
         if (lane == 0 && wl) atomicAdd(&s_cnt[1], wl);
         woff = __shfl(woff, 0);
-        __syncthreads();
+        lds_barrier();
         if (tid == 0) {
             const uint32_t tc = s_cnt[0], tl = s_cnt[1];
             s_base = tc ? atomicAdd(&ctr[shard], (unsigned long long)tc) : 0ull;
@@ -3562,7 +3571,7 @@ __global__ __launch_bounds__(BLOCK) void k_giant_hist(const uint32_t *__restrict
             s_cnt[0] = 0;
             s_cnt[1] = 0;
         }
-        __syncthreads();
+        lds_barrier();
         if (wc) {
             const unsigned long long base = s_base + woff;
             uint32_t run = 0;
@@ -3678,6 +3687,14 @@ __global__ __launch_bounds__(1024) void k_giant_expand(const unsigned long long 
     for (uint32_t i = 0; i < PER; ++i) s_m[i * 1024 + tid] = 0;
     const uint32_t b0 = chunk_bin[ch];
     const uint32_t b1 = ch + 1 < nchunks ? chunk_bin[ch + 1] : kBuckets16 - 1;
+    if (starts[b0 + 1] >= q0 + len) {  // one bin covers the chunk (a frequent value)
+        const uint32_t key = ((child << 16) | b0) ^ kFlip;
+        uint32_t *o = out + q0;
+#pragma unroll
+        for (uint32_t i = 0; i < PER; ++i)
+            if (i * 1024 + tid < len) o[i * 1024 + tid] = key;
+        return;
+    }
     __syncthreads();
     for (uint32_t b = b0 + tid; b <= b1; b += 1024) {
         const unsigned long long st = starts[b], en = starts[b + 1];
@@ -3714,7 +3731,8 @@ __global__ __launch_bounds__(1024) void k_giant_expand(const unsigned long long 
 
 hipError_t launch_est_mode(const uint32_t *in, uint64_t n, uint64_t *res, hipStream_t s) {
     if (n == 0) return hipErrorInvalidValue;
-    launch_k(k_est_mode, 1, 1024, 0, s, in, n, reinterpret_cast<unsigned long long *>(res));
+    const uint64_t stride = n < kModeSamples ? 1 : n / kModeSamples;  // sample i at i * stride
+    launch_k(k_est_mode, 1, 1024, 0, s, in, n, stride, reinterpret_cast<unsigned long long *>(res));
     return hipGetLastError();
 }
 

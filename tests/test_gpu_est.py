@@ -294,7 +294,7 @@ def test_giant_child_sample_misjudged(ctx):
     another plan."""
     n = 1 << 22
     keys = np.random.default_rng(41).integers(-2**31, 2**31, n, dtype=np.int64).astype(np.int32)
-    keys[:: n // 16384] = 5  # exactly the K1m sample positions (i * n / 16384)
+    keys[:: n // 16384] = 5  # exactly the K1m sample positions (i * floor(n / 16384))
     got, _ = _sort(ctx, keys)
     assert ctx.last_plan() in (SAMPLED, FALLBACK), ctx.last_plan()
     assert np.array_equal(got, np.sort(keys))

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""dist_probe.py [log2 n] -- local sort time across key distributions (development tool, GPU):
+"""dist_probe.py [log2 n] [case,case,...] -- local sort time across key distributions (development tool, GPU):
 looks for performance cliffs of the MSD plan (bucket sizes that fall between K11 classes or
 past kLocalMax, skewed digits, duplicates).  Prints ms per sort and the per-phase split."""
 import os
@@ -37,7 +37,10 @@ cases = {
     "reverse": lambda: np.arange(n, 0, -1, dtype=np.int32),
     "gauss": lambda: np.clip(rng.normal(0, 1e6, n), -2**31, 2**31 - 1).astype(np.int32),
 }
+only = set(sys.argv[2].split(",")) if len(sys.argv) > 2 else None  # e.g. zipf,bits16
 for name, make in cases.items():
+    if only and name.split()[0] not in only:
+        continue
     if make is None:
         ctx.generate(gsort.UNIFORM, 42, 0, n, p)
     elif make == "zipf":

@@ -13,7 +13,7 @@ ARGS=("$@")
 run() {  # name, rocprof options...
     local name=$1; shift
     timeout -k 10 120 rocprofv3 "$@" -f csv -d "$OUT/$name" -o run -- \
-        python3 bench.py --no-cpu-baseline "${ARGS[@]}" > "$OUT/$name.json" 2> "$OUT/$name.err"
+        python3 bench.py --no-cpu-baseline --no-dist-p1 "${ARGS[@]}" > "$OUT/$name.json" 2> "$OUT/$name.err"
 }
 run stats --kernel-trace --stats
 run fetch --pmc FETCH_SIZE
