@@ -24,6 +24,16 @@ namespace gsort {
 namespace {
 
 constexpr uint32_t kFlip = 0x80000000u;
+
+// GSORT_SWZ (A/B builds only): XOR-swizzle the LDS key arrays of K3r / K3a and
+// K11 / K11e -- word i at i ^ ((i >> 6) & 63), a permutation inside every 64-word row, so the
+// sequential reads stay conflict-free while the random scatter writes land on other banks.
+#ifndef GSORT_SWZ
+#define GSORT_SWZ 0
+#endif
+__device__ __forceinline__ uint32_t swz(uint32_t i) {
+    return GSORT_SWZ ? i ^ ((i >> 6) & 63u) : i;
+}
 constexpr uint64_t kGolden = 0x9E3779B97F4A7C15ULL;
 
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
@@ -1644,7 +1654,7 @@ __global__ __launch_bounds__(BLOCK) void k_partition_res(
 #pragma unroll
         for (int i = 0; i < ITEMS; ++i)
             if ((uint32_t)(i * BLOCK) + tid < len[h])
-                s_keys[h][s_cur[h][(k[h][i] >> shift) & 255u] + r[h][i]] = k[h][i];
+                s_keys[h][swz(s_cur[h][(k[h][i] >> shift) & 255u] + r[h][i])] = k[h][i];
     if (tid < kRadix) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -1665,7 +1675,7 @@ __global__ __launch_bounds__(BLOCK) void k_partition_res(
         for (int i = 0; i < ITEMS; ++i) {
             const uint32_t j = (uint32_t)(i * BLOCK) + tid;
             if (j < len[h]) {
-                const uint32_t key = s_keys[h][j];
+                const uint32_t key = s_keys[h][swz(j)];
                 const uint32_t at = to_dump ? j : s_off[h][(key >> shift) & 255u] + j;
                 o[at] = (OT)key;
             }
@@ -1757,7 +1767,7 @@ __device__ __forceinline__ void sort_bucket(uint32_t (&k)[ITEMS], uint32_t len, 
         __syncthreads();
 #pragma unroll
         for (int i = 0; i < ITEMS; ++i)
-            if ((uint32_t)tid < lim(i)) s_a[cnt[k[i] & 255u] + r[i]] = k[i];
+            if ((uint32_t)tid < lim(i)) s_a[swz(cnt[k[i] & 255u] + r[i])] = k[i];
         __syncthreads();
     }
 
@@ -1773,7 +1783,7 @@ __device__ __forceinline__ void sort_bucket(uint32_t (&k)[ITEMS], uint32_t len, 
 #pragma unroll
         for (int i = 0; i < ITEMS; ++i)
             if ((uint32_t)i < R && (uint32_t)(i * 64 + lane) < wlen)
-                k[i] = s_a[base + i * 64 + lane];
+                k[i] = s_a[swz(base + i * 64 + lane)];
         __syncthreads();
         uint32_t rk[ITEMS];
 #pragma unroll
@@ -1802,14 +1812,14 @@ __device__ __forceinline__ void sort_bucket(uint32_t (&k)[ITEMS], uint32_t len, 
 #pragma unroll
         for (int i = 0; i < ITEMS; ++i)
             if ((uint32_t)i < R && (uint32_t)(i * 64 + lane) < wlen)
-                s_a[wc[(k[i] >> shift) & 255u] + rk[i]] = k[i];
+                s_a[swz(wc[(k[i] >> shift) & 255u] + rk[i])] = k[i];
         __syncthreads();
     }
     const __amdgpu_buffer_rsrc_t rs = bucket_rsrc(dst, len * 4u);  // stores past len dropped
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
         const uint32_t j = (uint32_t)(i * BLOCK + tid);
-        __builtin_amdgcn_raw_buffer_store_b32((s_a[j] + koff) ^ kFlip, rs, (int)(j * 4u), 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32((s_a[swz(j)] + koff) ^ kFlip, rs, (int)(j * 4u), 0, 0);
     }
 }
 

@@ -173,18 +173,9 @@ gsort_status comm_try(gsort_ctx *c, gsort_status st) {
 std::string buf_name(gsort_ctx *c, const DevBuf &b);
 
 // Device allocation of `want` usable bytes (+ guards with GSORT_CANARY).  Returns the HIP error.
-// Allocation granularity (GSORT_ALLOC_ALIGN bytes, a power of two >= 4096).
+// Allocation granularity: 4 KiB (256 B with GSORT_EFENCE, so buffers end at the unmapped page).
 bool efence_mode();
-size_t alloc_align() {
-    if (efence_mode()) return 256;  // buffers end exactly (to 256 B) at the unmapped page
-    static const size_t a = [] {
-        const char *e = getenv("GSORT_ALLOC_ALIGN");
-        size_t v = e ? (size_t)strtoull(e, nullptr, 0) : 4096;
-        if (v < 4096 || (v & (v - 1))) v = 4096;
-        return v;
-    }();
-    return a;
-}
+size_t alloc_align() { return efence_mode() ? 256 : 4096; }
 
 // GSORT_EFENCE=1 (diagnostics): every buffer ends flush against an unmapped VA page (HIP VMM:
 // reserve a range with a free granule on each side, map physical memory only in the middle,
@@ -204,10 +195,7 @@ hipError_t efence_malloc(DevBuf &b, size_t want) {
     prop.location.type = hipMemLocationTypeDevice;
     prop.location.id = dev;
     size_t gran = 0;
-    static const bool rec = getenv("GSORT_EFENCE_REC") && atoi(getenv("GSORT_EFENCE_REC"));
-    e = hipMemGetAllocationGranularity(&gran, &prop,
-                                       rec ? hipMemAllocationGranularityRecommended
-                                           : hipMemAllocationGranularityMinimum);
+    e = hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityMinimum);
     if (e != hipSuccess) return e;
     static bool said = false;
     if (!said) { said = true; fprintf(stderr, "GSORT_EFENCE: granularity %zu\n", gran); }
@@ -434,11 +422,7 @@ T *slot_ptr(gsort_ctx *c, Slot s) { return reinterpret_cast<T *>(c->slot[s].p); 
 hipEvent_t next_event(gsort_ctx *c) {
     if (c->ev_used == c->ev_pool.size()) {
         hipEvent_t e;
-        // GSORT_EVENT_FLAGS (experiment): hipEventCreateWithFlags flags of the timing events
-        static const unsigned fl = getenv("GSORT_EVENT_FLAGS")
-                                       ? (unsigned)strtoul(getenv("GSORT_EVENT_FLAGS"), nullptr, 0)
-                                       : 0u;
-        if (hipEventCreateWithFlags(&e, fl) != hipSuccess) return nullptr;
+        if (hipEventCreateWithFlags(&e, 0u) != hipSuccess) return nullptr;
         c->ev_pool.push_back(e);
     }
     return c->ev_pool[c->ev_used++];
@@ -1072,13 +1056,6 @@ gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
         std::atomic_thread_fence(std::memory_order_acquire);
         return GSORT_OK;
     };
-    static const bool etrace = getenv("GSORT_EST_TRACE") != nullptr;  // development
-    const auto h0 = std::chrono::steady_clock::now();
-    auto us = [&] {
-        return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - h0)
-            .count();
-    };
-    double tq = 0, te = 0, tc = 0;
     hipEvent_t t = tic(c);
     HIP_TRY(c, launch_est_front(p, c->stream));
     toc(c, PH_COUNT, t);
@@ -1091,9 +1068,7 @@ gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
     HIP_TRY(c, launch_est_level2(p, c->stream));
     toc(c, PH_LEVEL2, t);
     HIP_TRY(c, launch_est_classify(p, c->stream));
-    tq = us();
     ST_TRY(wait_word(3, p.seq_elig, "eligibility word"));
-    te = us();
     if (mail[2] & 4u) {  // ineligible: the exact plan sorts -- unless the samples share leading
         // key bits (a key range narrower than int32: 16-, 20-, 24-, 28-bit keys, dense or
         // sorted ranges) whose removal leaves children K11e can take: then the caller retries
@@ -1118,8 +1093,6 @@ gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
     if (kspec) HIP_TRY(c, launch_local_sort_e(p, kspec, 0, sampled, true, c->stream));
     else HIP_TRY(c, launch_est_publish(p, c->stream));
     ST_TRY(wait_word(1, p.seq_done, "K12g counters"));
-    tc = us();
-    if (etrace) fprintf(stderr, "est: queued %.1f us, eligibility seen %.1f, counters seen %.1f\n", tq, te, tc);
     if (mail[0] != 0) return GSORT_OK;  // a region overflowed: *ok stays false
     uint64_t h[3 * (kLocalClasses + 1)];
     for (int i = 0; i < 3 * (kLocalClasses + 1); ++i) h[i] = mail[8 + i];
@@ -1416,12 +1389,23 @@ gsort_status local_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *
 // bucket sizes (65536) + starts (65537) + row-scan partials (64 x 64), u64
 constexpr size_t kBsizeBytes = ((size_t)2 * kBuckets16 + 1 + 64 * 64) * 8;
 
+// self (int32 runs only): run `self_rank` was not received -- it lies at self_src (the
+// sender's sorted block), and the kernels read it there through a run offset taken relative to
+// recv (mod 2^64); the MSD fallback, which needs the runs back to back, copies it in first.
 gsort_status recv_sort(gsort_ctx *c, const void *recv, bool packed16,
                        const std::vector<uint64_t> &rlen, uint64_t n, uint32_t *out,
-                       uint32_t *tmp, gsort_stats *stats) {
+                       uint32_t *tmp, gsort_stats *stats, int self_rank = -1,
+                       const int32_t *self_src = nullptr) {
     const int P = (int)rlen.size();
     if (n == 0) return GSORT_OK;
     if (!packed16 && (P > 64 || c->local_algo == GSORT_LOCAL_LSD)) {  // K11g: <= 64 pieces
+        if (self_src && rlen[self_rank]) {
+            uint64_t o = 0;
+            for (int p = 0; p < self_rank; ++p) o += rlen[p];
+            HIP_TRY(c, hipMemcpyAsync(static_cast<int32_t *>(const_cast<void *>(recv)) + o,
+                                      self_src, rlen[self_rank] * 4, hipMemcpyDeviceToDevice,
+                                      c->stream));
+        }
         int pr = 0;
         return local_sort(c, reinterpret_cast<const uint32_t *>(recv), n, out, tmp, &pr, stats);
     }
@@ -1436,6 +1420,8 @@ gsort_status recv_sort(gsort_ctx *c, const void *recv, bool packed16,
     HIP_TRY(c, hipStreamSynchronize(c->stream));  // h_r may still feed an earlier copy
     uint64_t off = 0;
     for (int p = 0; p < P; ++p) { h_r[p] = off; h_r[P + p] = rlen[p]; off += rlen[p]; }
+    if (self_src)
+        h_r[self_rank] = (uint64_t)(self_src - static_cast<const int32_t *>(recv));
     HIP_TRY(c, hipMemcpyAsync(d_r, h_r, (size_t)2 * P * 8, hipMemcpyHostToDevice, c->stream));
     uint64_t *pos = reinterpret_cast<uint64_t *>(c->m_rpos.p);
     uint64_t *bsize = reinterpret_cast<uint64_t *>(c->m_bsize.p), *bstart = bsize + kBuckets16;
@@ -1788,13 +1774,17 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
             stats->max_pair_bytes = std::max<uint64_t>(stats->max_pair_bytes, send[q] * 2);
         }
     if (roffs[P] != mine) return set_err(c, GSORT_EINVAL, "exchange plan does not fill the block");
-    // the payload, queued right behind the counts: the receive plan below overlaps it
+    // the payload, queued right behind the counts: the receive plan below overlaps it.  The
+    // rank's own piece is not moved at all: the receive kernels read it where it lies in the
+    // send buffer (its run offset below is taken relative to rbuf, mod 2^64) -- at P = 1 that is
+    // the whole 512 MiB of a 2^28-key block, at P = 8 an eighth of it
     uint16_t *rbuf = slot_ptr<uint16_t>(c, S_RECV);
     t = tic_rec(c);
     for (int q = 0; q < P; ++q) {
-        sc[q] = send[q] * 2;
+        const bool self = q == me;
+        sc[q] = self ? 0 : send[q] * 2;
         sd[q] = cut[q] * 2;
-        rc[q] = recv[q] * 2;
+        rc[q] = self ? 0 : recv[q] * 2;
         rd[q] = roffs[q] * 2;
     }
     ST_TRY(comm_try(c, c->comm->alltoallv(pack, sc.data(), sd.data(), rbuf, rc.data(), rd.data(),
@@ -1814,6 +1804,7 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
     uint64_t *d_r = reinterpret_cast<uint64_t *>(c->d_small + OFF_PLAN);
     HIP_TRY(c, hipStreamSynchronize(c->stream));  // h_r may still feed an earlier copy
     for (int p = 0; p < P; ++p) { h_r[p] = roffs[p]; h_r[P + p] = recv[p]; }
+    h_r[me] = (uint64_t)((pack + cut[me]) - rbuf);  // the self piece, in place (see above)
     HIP_TRY(c, hipMemcpyAsync(d_r, h_r, (size_t)2 * P * 8, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(c, launch_pos_from_meta(meta_r, d_moff, (uint32_t)hlo[me], (uint32_t)nh[me], P, pos,
                                     bstart + kBuckets16 + 1, c->stream));
@@ -1841,7 +1832,10 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
     // bucket past K18's reach sends the block through recv_sort's MSD levels 1 and 0
     t = tic(c);
     uint32_t *out = slot_ptr<uint32_t>(c, S_OUT);
-    if (h[0] && h[2] > kHxMax) {
+    if (h[0] && h[2] > kHxMax) {  // recv_sort wants the P runs back to back in rbuf
+        if (recv[me])
+            HIP_TRY(c, hipMemcpyAsync(rbuf + roffs[me], pack + cut[me], recv[me] * 2,
+                                      hipMemcpyDeviceToDevice, c->stream));
         ST_TRY(recv_sort(c, rbuf, true, recv, mine, out, slot_ptr<uint32_t>(c, S_TMP), stats));
     } else {
         for (int cl = 0; cl < kLocalClasses; ++cl) {
@@ -2223,6 +2217,10 @@ gsort_status sample_dist(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in, int
     ST_TRY(ensure(c, c->slot[S_OUT], cap2 * 4));
     ST_TRY(ensure(c, c->slot[S_TMP], cap2 * 4));
     int32_t *rbuf = slot_ptr<int32_t>(c, S_RECV);
+    // the rank's own bucket stays where it is (recv_sort reads it in place)
+    const size_t self_off = sd[me];
+    sc[me] = 0;
+    rc[me] = 0;
     t = tic_rec(c);
     ST_TRY(comm_try(c, c->comm->alltoallv(sorted, sc.data(), sd.data(), rbuf, rc.data(),
                                           rd.data(), c->stream)));
@@ -2234,7 +2232,7 @@ gsort_status sample_dist(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in, int
     for (int q = 0; q < P; ++q) rlen[q] = M[(size_t)q * P + me];
     t = tic(c);
     ST_TRY(recv_sort(c, rbuf, false, rlen, total, slot_ptr<uint32_t>(c, S_OUT),
-                     slot_ptr<uint32_t>(c, S_TMP), stats));
+                     slot_ptr<uint32_t>(c, S_TMP), stats, me, sorted + self_off / 4));
     toc(c, PH_MERGE, t);
     if (stats) stats->passes_run = pr;
     *d_out = slot_ptr<int32_t>(c, S_OUT);

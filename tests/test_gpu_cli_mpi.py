@@ -83,3 +83,30 @@ def test_mpirun_no_enough_sample(orc, ref_cases, tmp_path):
     assert rc != 0
     assert outs[0].decode().splitlines() == c["contract"][0]["head"]
     assert "no enough sample" in err0
+
+
+def test_mpirun_sample_balanced(orc, ref_cases, tmp_path):
+    """GSORT_SAMPLE_BALANCED=1 (duplicate-aware buckets): on Zipf keys the sorted dump and
+    the median stay the reference's, the bucket lines differ (the copies of a splitter value
+    are shared out instead of all going to the lower bucket)."""
+    c = next(x for x in ref_cases if x["id"] == "zipf65536s7__sample_sort__P4")
+    keys = case_input(orc, c["input"])
+    path = str(tmp_path / "in.txt")
+    orc.write_text(path, keys)
+    rc, outs, err0 = mpirun("sample_sort", 4, path, 1, tmp_path,
+                            env={"GSORT_SAMPLE_BALANCED": "1"})
+    assert rc == 0, err0
+    head, nd, tail = contract_split(outs[0])
+    want = c["contract"][0]
+    assert nd == want["n_dump"] and tail == want["tail"]
+    lines = outs[0].decode().splitlines()
+    dump = np.array([int(ln.split("|")[1]) for ln in lines if "|" in ln], dtype=np.int64)
+    assert np.array_equal(dump.astype(np.uint32).view(np.int32), np.sort(keys))
+    sizes = [sum(int(ln.split("=")[1]) for ln in o.decode().splitlines() if "Bucket" in ln)
+             for o in outs]
+    assert sum(sizes) == keys.size
+    ref_sizes = [sum(c["bucket_matrix"][r]) for r in range(4)]
+    assert sizes == ref_sizes  # each rank still sends its whole block
+    recv = [sum(int(ln.split("=")[1]) for o in outs for ln in o.decode().splitlines()
+                if f"Bucket {q}=" in ln) for q in range(4)]
+    assert max(recv) < max(sum(c["bucket_matrix"][r][q] for r in range(4)) for q in range(4))

@@ -320,3 +320,35 @@ def test_giant_then_sampled_reuses_scratch(ctx, orc):
         got, _ = _sort(ctx, keys)
         assert ctx.last_plan() == (GIANT if dist == orc.ZIPF else SAMPLED)
         assert np.array_equal(got, np.sort(keys))
+
+
+def test_region_buffers_reclaimed_for_a_later_call():
+    """the sampled plan's region buffers (~2.9x the block) outlive its call.  Under
+    GSORT_ALLOC_TOTAL (a cap on the context's scratch bytes) a sampled-plan sort of 2^23 keys
+    fits (~145 MB), and a following LSD sort of 2^24 keys needs ~145 MB of its own: only with the
+    regions dropped on demand (reclaim_regions) does it fit under 190 MB."""
+    code = f"""
+import sys, numpy as np
+sys.path[:0] = {[os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                 os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                              "mpi-test_amd")]!r}
+import torch, gsort
+rng = np.random.default_rng(4)
+with gsort.Context() as c:
+    # the third call finds S_TMP grown: its regions no longer fit, so it sorts on the exact plan
+    for i, (n, algo) in enumerate(((1 << 23, gsort.LOCAL_MSD), (1 << 24, gsort.LOCAL_LSD),
+                                   (1 << 23, gsort.LOCAL_MSD))):
+        keys = rng.integers(-2**31, 2**31, n, dtype=np.int64).astype(np.int32)
+        c.set_local_algo(algo)
+        p = c.alloc(n * 4); c.to_device(keys, p)
+        out, m, _ = c.radix(p, n)
+        assert np.array_equal(c.to_host(out, m), np.sort(keys)), n
+        if i == 0:
+            assert c.last_plan() == 1, c.last_plan()
+        c.free(p)
+print("ok")
+"""
+    env = dict(os.environ, GSORT_EST="1", GSORT_ALLOC_TOTAL=str(190 << 20))
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
