@@ -264,7 +264,10 @@ hipError_t launch_compat_keys(const int32_t *a, uint64_t n, int P, int loop, con
 // bases2 256 u64, tp 257, tdesc (est_max_tiles(n) + 2048) x kTileDescBytes (tile descriptors,
 // then the 2048-entry level-3 piece table), dump kSweepTile keys;
 // wl.list[1..4] 65536 entries each, wl.ctr the 15 counters (zeroed by the front).
-constexpr uint32_t kEstWGs = 128;
+#ifndef GSORT_EST_WGS
+#define GSORT_EST_WGS 128
+#endif
+constexpr uint32_t kEstWGs = GSORT_EST_WGS;
 constexpr uint32_t kEstBlockKeysHost = 512;  // one 8-key sample segment per block
 constexpr uint64_t kEstMinKeys = 1ull << 22;   // below: too few samples per child
 constexpr uint64_t kEstMaxKeys = 1ull << 31;   // level-3 regions stay below 2^32 keys
