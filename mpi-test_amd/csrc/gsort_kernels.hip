@@ -2054,6 +2054,246 @@ __global__ __launch_bounds__(1024) void k_hist_expand(const T *__restrict__ recv
     }
 }
 
+// ---- K18c: one-read counting sort of a receive bucket's low 16 bits -----------------------
+// Wave-wide inclusive scans through DPP (row shifts 1/2/4/8, then the row-15 and row-31
+// broadcasts): VALU only, where __shfl_up costs an LDS-crossbar op per step.
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ uint32_t dpp0(uint32_t x) {  // lanes outside the pattern read 0
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWS, 0xf, true);
+}
+__device__ __forceinline__ uint32_t wave_incl_add(uint32_t x) {
+    x += dpp0<0x111>(x);
+    x += dpp0<0x112>(x);
+    x += dpp0<0x114>(x);
+    x += dpp0<0x118>(x);
+    x += dpp0<0x142, 0xa>(x);
+    x += dpp0<0x143, 0xc>(x);
+    return x;
+}
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
+    x = max(x, dpp0<0x111>(x));
+    x = max(x, dpp0<0x112>(x));
+    x = max(x, dpp0<0x114>(x));
+    x = max(x, dpp0<0x118>(x));
+    x = max(x, dpp0<0x142, 0xa>(x));
+    x = max(x, dpp0<0x143, 0xc>(x));
+    return x;
+}
+
+// Bin counters: 65 536 u16 halves in 32 768 words (128 KiB).  A half that wraps (>= 65 536
+// copies of one value: buckets past 65 535 keys only) is seen by the one lane whose returning
+// atomic read 0xffff; it records the correction (bin, delta): +65 536 for the wrapped bin,
+// and for a low half the carry into its neighbour (-1, and +65 536 more if that carry wrapped
+// the high half too).  kHxMax bounds the wraps: 3 entries per 65 536 keys at most.
+constexpr uint32_t kCxWrapMax = 64;
+static_assert(3 * (kHxMax >> 16) <= kCxWrapMax, "K18c wrap list too small for kHxMax");
+
+template <bool WRAP>
+__device__ __forceinline__ void cx_count(uint32_t *s_h, uint32_t v, uint32_t *s_nw,
+                                         uint32_t *s_wb, int32_t *s_wd) {
+    const uint32_t sh = (v & 1u) << 4;
+    if (!WRAP) {
+        atomicAdd(&s_h[v >> 1], 1u << sh);
+        return;
+    }
+    const uint32_t o = atomicAdd(&s_h[v >> 1], 1u << sh);
+    if (((o >> sh) & 0xFFFFu) == 0xFFFFu) {
+        const bool lo = sh == 0, both = lo && (o >> 16) == 0xFFFFu;
+        const uint32_t e = atomicAdd(s_nw, lo ? (both ? 3u : 2u) : 1u);
+        if (e < kCxWrapMax) { s_wb[e] = v; s_wd[e] = 65536; }
+        if (lo && e + 1 < kCxWrapMax) { s_wb[e + 1] = v + 1; s_wd[e + 1] = -1; }
+        if (both && e + 2 < kCxWrapMax) { s_wb[e + 2] = v + 1; s_wd[e + 2] = 65536; }
+    }
+}
+
+template <bool WRAP, typename T>
+__device__ __forceinline__ void cx_count_piece(const T *src, uint32_t np, uint32_t *s_h,
+                                               uint32_t *s_nw, uint32_t *s_wb, int32_t *s_wd) {
+    constexpr uint32_t NT = 1024, E = 16 / sizeof(T), U = 8;
+    const uint32_t tid = threadIdx.x;
+    // elements before the first 16-B boundary, whole 16-B vectors, the rest
+    const uint32_t mis = (uint32_t)((reinterpret_cast<uintptr_t>(src) / sizeof(T)) & (E - 1));
+    const uint32_t head = min(mis ? E - mis : 0u, np);
+    const uint32_t nv = (np - head) / E, t0 = head + nv * E;
+    if (tid < head) cx_count<WRAP>(s_h, (uint32_t)src[tid] & 0xFFFFu, s_nw, s_wb, s_wd);
+    if (tid < np - t0) cx_count<WRAP>(s_h, (uint32_t)src[t0 + tid] & 0xFFFFu, s_nw, s_wb, s_wd);
+    if (nv == 0) return;
+    const uint4 *vs = reinterpret_cast<const uint4 *>(src + head);
+#pragma unroll 1
+    for (uint32_t v0 = 0; v0 < nv; v0 += U * NT) {
+        uint4 x[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) x[u] = vs[min(v0 + u * NT + tid, nv - 1)];  // all in flight
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            if (v0 + u * NT + tid >= nv) continue;
+            const uint32_t w4[4] = {x[u].x, x[u].y, x[u].z, x[u].w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (sizeof(T) == 2) {
+                    cx_count<WRAP>(s_h, w4[q] & 0xFFFFu, s_nw, s_wb, s_wd);
+                    cx_count<WRAP>(s_h, w4[q] >> 16, s_nw, s_wb, s_wd);
+                } else {
+                    cx_count<WRAP>(s_h, w4[q] & 0xFFFFu, s_nw, s_wb, s_wd);
+                }
+            }
+        }
+    }
+}
+
+// K18c (receive side; list {h, len}, one 1024-thread workgroup per bucket): the bucket's keys
+// are the P pieces recv[roff[p] + pos[p][h] .. roff[p] + pos[p][h + 1]); keys carry no
+// payload, so sorting them is counting them.
+// 1) One read of the pieces (16-B loads) into the 65 536 packed u16 bin counters (one LDS
+//    atomic per key).
+// 2) Wave w owns bins [4096 w, +4096) as 16 chunks of 256 bins, lane L the 4 bins of words
+//    128 j + 2 L, +1 (one ds_read_b64); the chunk totals are scanned block-wide into output
+//    bases.
+// 3) Each wave writes its chunks' keys in windows of 256 output slots aligned to 16 B in out:
+//    every non-empty bin starting in the window marks its first slot (LDS), lane L reads slots
+//    4 L .. 4 L + 3 (ds_read_b128), a running max inside the lane + a wave max-scan (DPP) hand
+//    every slot its bin (the marks grow with the slot), and the lane stores the 4 keys with ONE
+//    16-B store: a window is 1 KiB written by one instruction.  A frequent value is windows
+//    without marks (the bin carried over).
+// 2 B read (16-bit packed pieces; 4 B for int32 pieces) + 4 B written per key.
+template <typename T>
+__global__ __launch_bounds__(1024) void k_count_expand(const T *__restrict__ recv,
+                                                       const unsigned long long *__restrict__ pos,
+                                                       const unsigned long long *__restrict__ roff,
+                                                       int P,
+                                                       const unsigned long long *__restrict__ bstart,
+                                                       const unsigned long long *__restrict__ list,
+                                                       uint32_t *__restrict__ out) {
+    constexpr uint32_t NT = 1024, NW = NT / 64, WORDS = 32768, CW = 128;  // words per chunk
+    constexpr uint32_t CH = WORDS / NW / CW;                               // 16 chunks per wave
+    __shared__ uint32_t s_h[WORDS];
+    __shared__ uint4 s_mark[NW * 64];  // 256 slots per wave
+    __shared__ uint32_t s_base[NW * CH];
+    __shared__ uint32_t s_wsum[NW];
+    __shared__ uint64_t s_src[64];
+    __shared__ uint32_t s_len[64];
+    __shared__ uint32_t s_wb[kCxWrapMax];
+    __shared__ int32_t s_wd[kCxWrapMax];
+    __shared__ uint32_t s_nw;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint32_t h = (uint32_t)list[2 * blockIdx.x];
+    const uint32_t len = (uint32_t)list[2 * blockIdx.x + 1];
+    if ((int)tid < P) {
+        const uint64_t a = pos[(uint64_t)tid * (kBuckets16 + 1) + h];
+        const uint64_t b = pos[(uint64_t)tid * (kBuckets16 + 1) + h + 1];
+        s_src[tid] = roff[tid] + a;
+        s_len[tid] = (uint32_t)(b - a);
+    }
+    if (tid == 0) s_nw = 0;
+    {
+        uint4 *z = reinterpret_cast<uint4 *>(s_h);
+#pragma unroll
+        for (uint32_t i = 0; i < WORDS / 4 / NT; ++i) z[i * NT + tid] = make_uint4(0, 0, 0, 0);
+    }
+    __syncthreads();
+    const bool wrap = len >= 65536u;  // below that no half can wrap
+#pragma unroll 1
+    for (int p = 0; p < P; ++p) {
+        if (wrap) cx_count_piece<true>(recv + s_src[p], s_len[p], s_h, &s_nw, s_wb, s_wd);
+        else cx_count_piece<false>(recv + s_src[p], s_len[p], s_h, &s_nw, s_wb, s_wd);
+    }
+    __syncthreads();
+    const uint32_t nw = min(s_nw, kCxWrapMax);  // uniform; 0 unless a half wrapped
+    const uint32_t w0 = w * (WORDS / NW);
+    // lane's 4 bins of chunk j: counts (wrap corrections applied)
+    auto counts = [&](uint32_t j, uint32_t (&c)[4]) {
+        const uint32_t wd = w0 + CW * j + 2 * lane;
+        const uint2 x = *reinterpret_cast<const uint2 *>(s_h + wd);
+        c[0] = x.x & 0xFFFFu;
+        c[1] = x.x >> 16;
+        c[2] = x.y & 0xFFFFu;
+        c[3] = x.y >> 16;
+        for (uint32_t e = 0; e < nw; ++e) {
+            const uint32_t b = s_wb[e] - 2 * wd;  // bin relative to the lane's first
+            if (b < 4u) {
+                const uint32_t d = (uint32_t)s_wd[e];
+                c[0] += b == 0 ? d : 0u;
+                c[1] += b == 1 ? d : 0u;
+                c[2] += b == 2 ? d : 0u;
+                c[3] += b == 3 ? d : 0u;
+            }
+        }
+    };
+    // chunk totals
+#pragma unroll 1
+    for (uint32_t j = 0; j < CH; ++j) {
+        uint32_t c[4];
+        counts(j, c);
+        const uint32_t x = wave_incl_add(c[0] + c[1] + c[2] + c[3]);
+        if (lane == 63) s_base[w * CH + j] = x;
+    }
+    __syncthreads();
+    // exclusive scan of the 256 chunk totals in (wave, chunk) = bin order
+    {
+        uint32_t v = 0, x = 0;
+        if (tid < NW * CH) { v = s_base[tid]; x = wave_incl_add(v); }
+        if (tid < NW * CH && lane == 63) s_wsum[w] = x;
+        __syncthreads();
+        if (tid < NW * CH) {
+            uint32_t off = 0;
+            for (uint32_t ww = 0; ww < w; ++ww) off += s_wsum[ww];
+            s_base[tid] = off + x - v;
+        }
+        __syncthreads();
+    }
+    uint4 *mk4 = s_mark + 64 * w;
+    uint32_t *mk = reinterpret_cast<uint32_t *>(mk4);
+    uint32_t *dst = out + bstart[h];
+    const uint32_t hk = (h << 16) ^ kFlip;
+#pragma unroll 1
+    for (uint32_t j = 0; j < CH; ++j) {
+        uint32_t c[4];
+        counts(j, c);
+        const uint32_t t = c[0] + c[1] + c[2] + c[3];
+        const uint32_t x = wave_incl_add(t);
+        const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+        if (tot == 0) continue;
+        uint32_t st[4];  // first slot of each of the lane's bins
+        st[0] = x - t;
+        st[1] = st[0] + c[0];
+        st[2] = st[1] + c[1];
+        st[3] = st[2] + c[2];
+        const uint32_t b0 = 2 * (w0 + CW * j + 2 * lane) + 1;  // mark = bin + 1
+        uint32_t *d = dst + s_base[w * CH + j];
+        // windows aligned to 16 B in out: window r covers slots [256 r - off, +256)
+        const uint32_t off = (uint32_t)(reinterpret_cast<uintptr_t>(d) >> 2) & 3u;
+        uint32_t carry = 0;
+#pragma unroll 1
+        for (uint32_t r0 = 0; r0 < tot + off; r0 += 256) {
+            const uint32_t ws = r0 - off;  // window start slot (mod 2^32)
+            mk4[lane] = make_uint4(0, 0, 0, 0);
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (c[i] && st[i] - ws < 256u) mk[st[i] - ws] = b0 + i;
+            __builtin_amdgcn_wave_barrier();
+            const uint4 m = mk4[lane];
+            const uint32_t a0 = m.x, a1 = max(a0, m.y), a2 = max(a1, m.z), a3 = max(a2, m.w);
+            const uint32_t S = wave_incl_max(a3);
+            // the lanes below: S of lane - 1 (DPP wave shift right by one; lane 0 reads 0)
+            const uint32_t prev = max(carry, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)S, 0x138, 0xf, 0xf, true));
+            carry = max(carry, (uint32_t)__builtin_amdgcn_readlane((int)S, 63));
+            const uint32_t q = ws + 4 * lane;  // this lane's first slot
+            const uint4 v = make_uint4(hk | (max(prev, a0) - 1), hk | (max(prev, a1) - 1),
+                                       hk | (max(prev, a2) - 1), hk | (max(prev, a3) - 1));
+            if (q < tot && q + 4 <= tot && q + 4 > q) {
+                *reinterpret_cast<uint4 *>(d + q) = v;  // 16-B aligned
+            } else {
+                if (q < tot) d[q] = v.x;
+                if (q + 1 < tot) d[q + 1] = v.y;
+                if (q + 2 < tot) d[q + 2] = v.z;
+                if (q + 3 < tot) d[q + 3] = v.w;
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+}
+
 // list 0 of the receive side, {h, len} -> {bstart[h], len} (segments of out for the MSD levels).
 __global__ __launch_bounds__(256) void k_list_to_segments(unsigned long long *__restrict__ list,
                                                           uint32_t n,
@@ -3242,6 +3482,26 @@ hipError_t launch_hist_expand(const void *recv, bool packed16, const uint64_t *p
     else
         launch_k(k_hist_expand<int32_t>, nlist, 1024, 0, s, reinterpret_cast<const int32_t *>(recv), ps, ro, P,
                                              bs, l, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_count_expand(const void *recv, bool packed16, const uint64_t *pos,
+                               const uint64_t *roff, int P, const uint64_t *bstart,
+                               const uint64_t *list, uint32_t nlist, uint32_t *out,
+                               hipStream_t s) {
+    using ull = unsigned long long;
+    if (nlist == 0) return hipSuccess;
+    if (P < 1 || P > 64) return hipErrorInvalidValue;
+    auto *ps = reinterpret_cast<const ull *>(pos);
+    auto *ro = reinterpret_cast<const ull *>(roff);
+    auto *bs = reinterpret_cast<const ull *>(bstart);
+    auto *l = reinterpret_cast<const ull *>(list);
+    if (packed16)
+        launch_k(k_count_expand<uint16_t>, nlist, 1024, 0, s, reinterpret_cast<const uint16_t *>(recv), ps, ro, P,
+                 bs, l, out);
+    else
+        launch_k(k_count_expand<int32_t>, nlist, 1024, 0, s, reinterpret_cast<const int32_t *>(recv), ps, ro, P,
+                 bs, l, out);
     return hipGetLastError();
 }
 

@@ -80,6 +80,9 @@ struct gsort_ctx {
     bool plan_est = true;   // GSORT_EST (default 1)
     bool plan_giant = true; // GSORT_GIANT (default 1): the one-dominant-child path
     double est_slack = 1.0; // GSORT_EST_SLACK (test hook: the sampling-error margin's scale)
+    // GSORT_RECV_CX: receive buckets of K11g class >= recv_cx (1..4) and list 0 are counted by
+    // K18c; 5 = list 0 only; -1 = the round-2 kernels (K11g classes, two-read K18)
+    int recv_cx = 5;
     int ncu = 256;
     int last_plan = 0;      // gsort_last_plan: 0 exact, 1 sampled, 2 sampled then exact
     DevBuf m_ex, m_ey, m_epart, m_eplan, m_edesc, m_edump;
@@ -976,6 +979,9 @@ gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
     // handed back
     constexpr size_t kPlanWords = (size_t)4 * kBuckets16 + 4 * kH16Shards * kRadix + kRadix + 1;
     {
+        // busy while they are made: a refused Y must not reclaim the X just ensured (that left
+        // X null and K3r wrote through it -- found by test_region_buffers_reclaimed_for_a_later_call)
+        c->est_busy = true;
         gsort_status st = GSORT_OK;
         for (DevBuf *b : {&c->m_ex, &c->m_ey})
             if (st == GSORT_OK) st = ensure(c, *b, (b == &c->m_ex ? capx : capy) * 4);
@@ -989,6 +995,9 @@ gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
         if (st == GSORT_OK) st = ensure(c, c->m_edump, (size_t)kSweepTile * 4);
         for (int k = 0; k < kLocalClasses && st == GSORT_OK; ++k)
             st = ensure_list(c, c->m_local[k], kBuckets16);
+        c->est_busy = false;
+        if (st == GSORT_OK && (!c->m_ex.p || !c->m_ey.p))
+            return set_err(c, GSORT_EINVAL, "sampled plan: region buffers missing");
         if (st == GSORT_ENOMEM) {
             (void)reclaim_regions(c, DevBuf{});
             c->err.clear();
@@ -1392,6 +1401,38 @@ constexpr size_t kBsizeBytes = ((size_t)2 * kBuckets16 + 1 + 64 * 64) * 8;
 // self (int32 runs only): run `self_rank` was not received -- it lies at self_src (the
 // sender's sorted block), and the kernels read it there through a run offset taken relative to
 // recv (mod 2^64); the MSD fallback, which needs the runs back to back, copies it in first.
+// Every receive bucket of the lists wl (counts h, read_counters layout) sorted from its P
+// pieces into out: K11g by size class, K18c (or, GSORT_RECV_CX=-1, the two-read K18) past
+// kLocalMax; classes >= c->recv_cx go to K18c as well.  With list0, list 0 is sorted too (it
+// must then hold no bucket past kHxMax).
+gsort_status sort_recv_lists(gsort_ctx *c, const void *recv, bool packed16, const uint64_t *pos,
+                             const uint64_t *roff, int P, const uint64_t *bstart,
+                             const WorkLists &wl, const uint64_t *h, uint32_t *out,
+                             gsort_stats *stats, bool list0 = true) {
+    for (int k = 0; k < kLocalClasses; ++k) {
+        const uint64_t *hk = h + 3 * (k + 1);
+        if (!hk[0]) continue;
+        if (c->recv_cx > 0 && k + 1 >= c->recv_cx)
+            HIP_TRY(c, launch_count_expand(recv, packed16, pos, roff, P, bstart, wl.list[k + 1],
+                                           (uint32_t)hk[0], out, c->stream));
+        else
+            HIP_TRY(c, launch_gather_sort(recv, packed16, pos, roff, P, bstart, wl.list[k + 1],
+                                          (uint32_t)hk[0], k + 1, c->atomic_rank, out,
+                                          c->stream));
+        if (stats) { stats->buckets_local += hk[0]; stats->keys_bucket_sort += hk[1]; }
+    }
+    if (h[0] && list0) {
+        if (c->recv_cx > 0)
+            HIP_TRY(c, launch_count_expand(recv, packed16, pos, roff, P, bstart, wl.list[0],
+                                           (uint32_t)h[0], out, c->stream));
+        else
+            HIP_TRY(c, launch_hist_expand(recv, packed16, pos, roff, P, bstart, wl.list[0],
+                                          (uint32_t)h[0], out, c->stream));
+        if (stats) { stats->buckets_local += h[0]; stats->keys_bucket_sort += h[1]; }
+    }
+    return GSORT_OK;
+}
+
 gsort_status recv_sort(gsort_ctx *c, const void *recv, bool packed16,
                        const std::vector<uint64_t> &rlen, uint64_t n, uint32_t *out,
                        uint32_t *tmp, gsort_stats *stats, int self_rank = -1,
@@ -1445,24 +1486,12 @@ gsort_status recv_sort(gsort_ctx *c, const void *recv, bool packed16,
                                                 std::to_string(c->rank) + ")");
         ST_TRY(check_bounds(c, bstart, kBuckets16 + 1, n, "receive bucket starts"));
     }
-    for (int k = 0; k < kLocalClasses; ++k) {
-        const uint64_t *hk = h + 3 * (k + 1);
-        if (!hk[0]) continue;
-        t = tic(c);
-        HIP_TRY(c, launch_gather_sort(recv, packed16, pos, d_r, P, bstart,
-                                      reinterpret_cast<uint64_t *>(c->m_local[k].p),
-                                      (uint32_t)hk[0], k + 1, c->atomic_rank, out, c->stream));
-        toc(c, PH_BUCKET, t);
-        if (stats) { stats->buckets_local += hk[0]; stats->keys_bucket_sort += hk[1]; }
-    }
-    if (h[0] && h[2] <= kHxMax) {  // buckets past LDS size: K18 counting sort
-        t = tic(c);
-        HIP_TRY(c, launch_hist_expand(recv, packed16, pos, d_r, P, bstart,
-                                      reinterpret_cast<uint64_t *>(c->m_next[0].p),
-                                      (uint32_t)h[0], out, c->stream));
-        toc(c, PH_BUCKET, t);
-        if (stats) { stats->buckets_local += h[0]; stats->keys_bucket_sort += h[1]; }
-    } else if (h[0]) {  // a bucket past kHxMax: all of list 0 into place, then levels 1 and 0
+    const bool list0 = h[0] && h[2] <= kHxMax;  // else: a bucket past kHxMax (below)
+    t = tic(c);
+    ST_TRY(sort_recv_lists(c, recv, packed16, pos, d_r, P, bstart, work_lists(c, 0), h, out, stats,
+                           list0));
+    toc(c, PH_BUCKET, t);
+    if (h[0] && !list0) {  // all of list 0 into place, then MSD levels 1 and 0
         HIP_TRY(c, launch_list_to_segments(reinterpret_cast<uint64_t *>(c->m_next[0].p),
                                            (uint32_t)h[0], bstart, c->stream));
         HIP_TRY(c, launch_gather_copy(recv, packed16, pos, d_r, P, bsize, bstart, out, c->stream));
@@ -1779,9 +1808,12 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
     // send buffer (its run offset below is taken relative to rbuf, mod 2^64) -- at P = 1 that is
     // the whole 512 MiB of a 2^28-key block, at P = 8 an eighth of it
     uint16_t *rbuf = slot_ptr<uint16_t>(c, S_RECV);
+    // test hook GSORT_RCCL_SELF=1: the self piece does go through the transport (RcclComm then
+    // sends it through ncclSend / ncclRecv: tests/test_gpu_rccl.py pins RCCL's message limit)
+    static const bool self_moved = getenv("GSORT_RCCL_SELF") && getenv("GSORT_RCCL_SELF")[0] == '1';
     t = tic_rec(c);
     for (int q = 0; q < P; ++q) {
-        const bool self = q == me;
+        const bool self = q == me && !self_moved;
         sc[q] = self ? 0 : send[q] * 2;
         sd[q] = cut[q] * 2;
         rc[q] = self ? 0 : recv[q] * 2;
@@ -1804,7 +1836,7 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
     uint64_t *d_r = reinterpret_cast<uint64_t *>(c->d_small + OFF_PLAN);
     HIP_TRY(c, hipStreamSynchronize(c->stream));  // h_r may still feed an earlier copy
     for (int p = 0; p < P; ++p) { h_r[p] = roffs[p]; h_r[P + p] = recv[p]; }
-    h_r[me] = (uint64_t)((pack + cut[me]) - rbuf);  // the self piece, in place (see above)
+    if (!self_moved) h_r[me] = (uint64_t)((pack + cut[me]) - rbuf);  // the self piece, in place
     HIP_TRY(c, hipMemcpyAsync(d_r, h_r, (size_t)2 * P * 8, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(c, launch_pos_from_meta(meta_r, d_moff, (uint32_t)hlo[me], (uint32_t)nh[me], P, pos,
                                     bstart + kBuckets16 + 1, c->stream));
@@ -1833,24 +1865,12 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
     t = tic(c);
     uint32_t *out = slot_ptr<uint32_t>(c, S_OUT);
     if (h[0] && h[2] > kHxMax) {  // recv_sort wants the P runs back to back in rbuf
-        if (recv[me])
+        if (recv[me] && !self_moved)
             HIP_TRY(c, hipMemcpyAsync(rbuf + roffs[me], pack + cut[me], recv[me] * 2,
                                       hipMemcpyDeviceToDevice, c->stream));
         ST_TRY(recv_sort(c, rbuf, true, recv, mine, out, slot_ptr<uint32_t>(c, S_TMP), stats));
     } else {
-        for (int cl = 0; cl < kLocalClasses; ++cl) {
-            const uint64_t *hk = h + 3 * (cl + 1);
-            if (!hk[0]) continue;
-            HIP_TRY(c, launch_gather_sort(rbuf, true, pos, d_r, P, bstart, wl.list[cl + 1],
-                                          (uint32_t)hk[0], cl + 1, c->atomic_rank, out,
-                                          c->stream));
-            if (stats) { stats->buckets_local += hk[0]; stats->keys_bucket_sort += hk[1]; }
-        }
-        if (h[0]) {
-            HIP_TRY(c, launch_hist_expand(rbuf, true, pos, d_r, P, bstart, wl.list[0],
-                                          (uint32_t)h[0], out, c->stream));
-            if (stats) { stats->buckets_local += h[0]; stats->keys_bucket_sort += h[1]; }
-        }
+        ST_TRY(sort_recv_lists(c, rbuf, true, pos, d_r, P, bstart, wl, h, out, stats));
     }
     toc(c, PH_MERGE, t);
     if (stats) stats->passes_run = pr;
@@ -2297,6 +2317,7 @@ gsort_status create_common(gsort_ctx *c, int hip_device) {
     if (const char *e = getenv("GSORT_PLAN16")) c->plan16 = atoi(e) != 0;
     if (const char *e = getenv("GSORT_EST")) c->plan_est = atoi(e) != 0;
     if (const char *e = getenv("GSORT_GIANT")) c->plan_giant = atoi(e) != 0;
+    if (const char *e = getenv("GSORT_RECV_CX")) c->recv_cx = atoi(e);
     if (const char *e = getenv("GSORT_EST_SLACK")) c->est_slack = atof(e);
     HIP_TRY(c, hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, hip_device));
     {

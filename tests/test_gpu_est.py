@@ -323,10 +323,13 @@ def test_giant_then_sampled_reuses_scratch(ctx, orc):
 
 
 def test_region_buffers_reclaimed_for_a_later_call():
-    """the sampled plan's region buffers (~2.9x the block) outlive its call.  Under
-    GSORT_ALLOC_TOTAL (a cap on the context's scratch bytes) a sampled-plan sort of 2^23 keys
-    fits (~145 MB), and a following LSD sort of 2^24 keys needs ~145 MB of its own: only with the
-    regions dropped on demand (reclaim_regions) does it fit under 190 MB."""
+    """the sampled plan's region buffers outlive its call.  At 2^23 keys they take
+    ~534 MB (X 64 MB + Y 470 MB: every one of the 65 536 child regions carries >= 2 sample
+    blocks of slack, est_region_keys); with the block, the plan arrays and the lists a sampled
+    sort fits under GSORT_ALLOC_TOTAL = 640 MB.  A following LSD sort of 2^24 keys needs a
+    64 MB S_OUT and a 64 MB S_TMP on top: it fits only with the regions dropped on demand
+    (reclaim_regions).  The third call (2^23 again) finds S_TMP held, so its regions may no
+    longer fit and the exact plan may sort: either way the result must be exact."""
     code = f"""
 import sys, numpy as np
 sys.path[:0] = {[os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
@@ -348,7 +351,7 @@ with gsort.Context() as c:
         c.free(p)
 print("ok")
 """
-    env = dict(os.environ, GSORT_EST="1", GSORT_ALLOC_TOTAL=str(190 << 20))
+    env = dict(os.environ, GSORT_EST="1", GSORT_ALLOC_TOTAL=str(640 << 20))
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
                        timeout=240)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr

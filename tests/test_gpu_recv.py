@@ -1,0 +1,82 @@
+"""Receive side of the distributed sorts: K18c (one-read counting sort of a 16-bit bucket's low
+16 bits) against np.sort, through in-process rank groups on one GPU.
+
+GSORT_RECV_CX routes the receive buckets: 1 = every bucket through K18c (the K11g classes
+too), 5 = only buckets past kLocalMax (the default), -1 = the round-2 kernels (K11g and the
+two-read K18).  The cases reach what K18c must get right: pieces of P ranks starting at any
+2-B / 4-B alignment, empty pieces, buckets of one value, and bins of >= 65 536 copies of one
+value in buckets past 65 535 keys, whose u16 halves wrap (low half: the carry into the
+neighbour bin; high half; both).  The reference's own final order is the sorted multiset
+(mpi_radix_sort.c:185-192, mpi_sample_sort.c:174), so np.sort is the oracle (bit-exact).
+"""
+import numpy as np
+import pytest
+
+from test_gpu_sort import run_group
+
+pytestmark = pytest.mark.gpu
+
+
+def _check(res, keys, P, algo):
+    ref = np.sort(keys)
+    got = np.concatenate([res[r][0] for r in range(P)])
+    assert np.array_equal(got, ref)
+    if algo == "radix":  # exact splitters: rank q holds [qB, (q+1)B)
+        B = -(-keys.size // P)
+        for q in range(P):
+            assert np.array_equal(res[q][0], ref[q * B:(q + 1) * B]), q
+
+
+def _wraps(rng, n):
+    """Three 16-bit buckets: one with 150 000 copies of an even low half (two low-half wraps,
+    carries into the odd neighbour) and 140 000 of that neighbour (high-half wraps, some
+    carries landing on a full high half), one with 200 000 copies of an odd low half, one
+    uniform; all under kHxMax = 2^20 keys per bucket and rank."""
+    hot = np.concatenate([
+        np.full(150000, 0x00070010, np.int64), np.full(140000, 0x00070011, np.int64),
+        np.full(200000, -0x0003FFFF, np.int64),
+        0x00090000 + rng.integers(0, 1 << 16, 120000)])
+    rest = rng.integers(-2**31, 2**31, max(n - hot.size, 0))
+    return np.concatenate([hot, rest]).astype(np.int32)
+
+
+CASES = {
+    # P = 8 weak-scaling shape: 65 536-key buckets (2^22 keys of 22 bits over 8 ranks)
+    "bits22": lambda rng: rng.integers(0, 1 << 22, 1 << 22),
+    # buckets of every K11g class and past kLocalMax (16-bit buckets of ~4K .. ~260K keys)
+    "classes": lambda rng: rng.integers(-(1 << 22), 1 << 22, 3 << 20) >> rng.integers(0, 6, 3 << 20),
+    "wraps": lambda rng: _wraps(rng, 1 << 20),
+    "one_value": lambda rng: np.full(700001, -12345),
+    "few_values": lambda rng: rng.choice(np.array([3, 4, 65539, -7]), 500000),
+}
+
+
+@pytest.mark.parametrize("cx", [1, 5, -1])
+@pytest.mark.parametrize("algo", ["radix", "sample"])
+@pytest.mark.parametrize("case", list(CASES))
+@pytest.mark.parametrize("P", [2, 3, 8])
+def test_receive_buckets(gsort, monkeypatch, case, algo, cx, P):
+    monkeypatch.setenv("GSORT_RECV_CX", str(cx))
+    rng = np.random.default_rng(hash((case, P)) % 2**32)
+    keys = np.asarray(CASES[case](rng)).astype(np.int32)
+    rng.shuffle(keys)
+    if algo == "radix":  # uneven blocks: pieces at any alignment
+        cuts = np.sort(rng.integers(0, keys.size + 1, P - 1))
+    else:  # regular sampling wants the reference's equal blocks (mpi_sample_sort.c:82)
+        B = -(-keys.size // P)
+        cuts = np.arange(1, P) * B
+    blocks = np.split(keys, cuts)
+    res = run_group(gsort, blocks, algo)
+    _check(res, keys, P, algo)
+
+
+@pytest.mark.parametrize("cx", [1, 5])
+def test_receive_one_rank_forced(gsort, monkeypatch, cx):
+    """A one-rank group on the distributed path (GSORT_FORCE_DIST, bench.py's dist_p1): one
+    piece per bucket, 8192-key buckets (K11g class 2, or K18c with cx = 1)."""
+    monkeypatch.setenv("GSORT_FORCE_DIST", "1")
+    monkeypatch.setenv("GSORT_RECV_CX", str(cx))
+    rng = np.random.default_rng(cx)
+    keys = rng.integers(-2**31, 2**31, (1 << 22) + 77).astype(np.int32)
+    res = run_group(gsort, [keys], "radix")
+    _check(res, keys, 1, "radix")

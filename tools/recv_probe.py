@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
 """recv_probe.py [log2 n] -- the distributed radix's per-GPU path on one GPU (development tool):
 a one-rank group with GSORT_FORCE_DIST=1 runs sender grouping, radix select, the packed
-self-exchange and the receive sort.  Key widths pick the receive kernel: 31-bit keys give
-8192-key 16-bit buckets (K11g), 28-bit keys 65536-key buckets (K18: the P = 8 weak-scaling
-case at 2^28 keys per GPU), 27-bit keys 131072-key buckets.  Prints ms per sort and phases;
+self-exchange and the receive sort.  Key widths set the receive bucket size, i.e. the
+weak-scaling shape at 2^28 keys per GPU: 31-bit keys give 8192-key 16-bit buckets (P = 1),
+30-bit 16384 (P = 2), 29-bit 32768 (P = 4), 28-bit 65536 (P = 8), 27-bit 131072.
+GSORT_RECV_CX picks the kernels (K11g classes vs K18c).  Prints ms per sort and phases;
 run it under rocprofv3 --kernel-trace for the per-kernel split."""
 import os
 import sys
@@ -23,8 +24,9 @@ rng = np.random.default_rng(9)
 grp = gsort.Group(1)
 ctx = gsort.Context(group=grp)
 p = ctx.alloc(n * 4)
-for name, bits in [("uniform31 (K11g)", 31), ("bits28 (K18, 65536-key buckets)", 28),
-                   ("bits27 (K18, 131072-key buckets)", 27)]:
+for name, bits in [("uniform31 (8192-key buckets)", 31), ("bits30 (16384-key buckets)", 30),
+                   ("bits29 (32768-key buckets)", 29), ("bits28 (65536-key buckets)", 28),
+                   ("bits27 (131072-key buckets)", 27)]:
     if bits == 31:
         ctx.generate(gsort.UNIFORM, 42, 0, n, p)
     else:
