@@ -183,10 +183,11 @@ hipError_t launch_hist_expand(const void *recv, bool packed16, const uint64_t *p
                               const uint64_t *list, uint32_t nlist, uint32_t *out,
                               hipStream_t s);
 // K18c: the same buckets (any list of {h, len} entries with len <= kHxMax) in one read: packed
-// u16 bin counters, wave-wise expansion by marked slots + max-scan, coalesced stores.
+// u16 bin counters, wave-wise expansion by marked slots + max-scan, coalesced stores; one
+// persistent workgroup per CU (ncu), the next bucket's keys loaded during this one's stores.
 hipError_t launch_count_expand(const void *recv, bool packed16, const uint64_t *pos,
                                const uint64_t *roff, int P, const uint64_t *bstart,
-                               const uint64_t *list, uint32_t nlist, uint32_t *out,
+                               const uint64_t *list, uint32_t nlist, int ncu, uint32_t *out,
                                hipStream_t s);
 // {h, len} list entries -> {bstart[h], len}.
 hipError_t launch_list_to_segments(uint64_t *list, uint32_t n, const uint64_t *bstart,

@@ -25,15 +25,6 @@ namespace {
 
 constexpr uint32_t kFlip = 0x80000000u;
 
-// GSORT_SWZ (A/B builds only): XOR-swizzle the LDS key arrays of K3r / K3a and
-// K11 / K11e -- word i at i ^ ((i >> 6) & 63), a permutation inside every 64-word row, so the
-// sequential reads stay conflict-free while the random scatter writes land on other banks.
-#ifndef GSORT_SWZ
-#define GSORT_SWZ 0
-#endif
-__device__ __forceinline__ uint32_t swz(uint32_t i) {
-    return GSORT_SWZ ? i ^ ((i >> 6) & 63u) : i;
-}
 constexpr uint64_t kGolden = 0x9E3779B97F4A7C15ULL;
 
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
@@ -1654,7 +1645,7 @@ __global__ __launch_bounds__(BLOCK) void k_partition_res(
 #pragma unroll
         for (int i = 0; i < ITEMS; ++i)
             if ((uint32_t)(i * BLOCK) + tid < len[h])
-                s_keys[h][swz(s_cur[h][(k[h][i] >> shift) & 255u] + r[h][i])] = k[h][i];
+                s_keys[h][s_cur[h][(k[h][i] >> shift) & 255u] + r[h][i]] = k[h][i];
     if (tid < kRadix) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -1675,7 +1666,7 @@ __global__ __launch_bounds__(BLOCK) void k_partition_res(
         for (int i = 0; i < ITEMS; ++i) {
             const uint32_t j = (uint32_t)(i * BLOCK) + tid;
             if (j < len[h]) {
-                const uint32_t key = s_keys[h][swz(j)];
+                const uint32_t key = s_keys[h][j];
                 const uint32_t at = to_dump ? j : s_off[h][(key >> shift) & 255u] + j;
                 o[at] = (OT)key;
             }
@@ -1767,7 +1758,7 @@ __device__ __forceinline__ void sort_bucket(uint32_t (&k)[ITEMS], uint32_t len, 
         __syncthreads();
 #pragma unroll
         for (int i = 0; i < ITEMS; ++i)
-            if ((uint32_t)tid < lim(i)) s_a[swz(cnt[k[i] & 255u] + r[i])] = k[i];
+            if ((uint32_t)tid < lim(i)) s_a[cnt[k[i] & 255u] + r[i]] = k[i];
         __syncthreads();
     }
 
@@ -1783,7 +1774,7 @@ __device__ __forceinline__ void sort_bucket(uint32_t (&k)[ITEMS], uint32_t len, 
 #pragma unroll
         for (int i = 0; i < ITEMS; ++i)
             if ((uint32_t)i < R && (uint32_t)(i * 64 + lane) < wlen)
-                k[i] = s_a[swz(base + i * 64 + lane)];
+                k[i] = s_a[base + i * 64 + lane];
         __syncthreads();
         uint32_t rk[ITEMS];
 #pragma unroll
@@ -1812,14 +1803,14 @@ __device__ __forceinline__ void sort_bucket(uint32_t (&k)[ITEMS], uint32_t len, 
 #pragma unroll
         for (int i = 0; i < ITEMS; ++i)
             if ((uint32_t)i < R && (uint32_t)(i * 64 + lane) < wlen)
-                s_a[swz(wc[(k[i] >> shift) & 255u] + rk[i])] = k[i];
+                s_a[wc[(k[i] >> shift) & 255u] + rk[i]] = k[i];
         __syncthreads();
     }
     const __amdgpu_buffer_rsrc_t rs = bucket_rsrc(dst, len * 4u);  // stores past len dropped
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
         const uint32_t j = (uint32_t)(i * BLOCK + tid);
-        __builtin_amdgcn_raw_buffer_store_b32((s_a[swz(j)] + koff) ^ kFlip, rs, (int)(j * 4u), 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32((s_a[j] + koff) ^ kFlip, rs, (int)(j * 4u), 0, 0);
     }
 }
 
@@ -1854,6 +1845,10 @@ __global__ __launch_bounds__(BLOCK) void k_local_sort(const uint32_t *__restrict
 __device__ __forceinline__ uint32_t recv_key(int32_t x, uint32_t) { return (uint32_t)x ^ kFlip; }
 __device__ __forceinline__ uint32_t recv_key(uint16_t x, uint32_t h) { return (h << 16) | x; }
 
+// pieces up to which K11g loads every key straight into registers (a piece lookup of P - 1
+// scalar compares per key); more pieces go through an LDS gather first
+constexpr int kGatherDirectP = 8;
+
 template <int BLOCK, int ITEMS, bool ATOMIC, typename T>
 __global__ __launch_bounds__(BLOCK) void k_gather_sort(const T *__restrict__ recv,
                                                        const unsigned long long *__restrict__ pos,
@@ -1868,6 +1863,7 @@ __global__ __launch_bounds__(BLOCK) void k_gather_sort(const T *__restrict__ rec
     __shared__ uint32_t s_a[TILE];
     __shared__ uint32_t s_wc[WAVES * kRadix];
     __shared__ uint64_t s_src[MAXP];  // piece p: first key in recv
+    __shared__ uint64_t s_delta[MAXP];
     __shared__ uint32_t s_cum[MAXP + 1];
     const int tid = threadIdx.x;
     const uint64_t h = list[2 * blockIdx.x];
@@ -1892,34 +1888,56 @@ __global__ __launch_bounds__(BLOCK) void k_gather_sort(const T *__restrict__ rec
         }
         if (tid == P - 1) s_cum[P] = v;
     }
-    __syncthreads();
-    // gather the pieces into s_a (coalesced per piece, 8 loads in flight per thread), then
-    // take the keys block-strided
-#pragma unroll 1
-    for (int p = 0; p < P; ++p) {
-        const T *src = recv + s_src[p];
-        const uint32_t c0 = s_cum[p], c1 = s_cum[p + 1];
-#pragma unroll 1
-        for (uint32_t b = c0; b < c1; b += 8 * BLOCK) {
-            T v[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const uint32_t j = b + u * BLOCK + tid;
-                v[u] = j < c1 ? src[j - c0] : T(0);
-            }
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const uint32_t j = b + u * BLOCK + tid;
-                if (j < c1) s_a[j] = recv_key(v[u], (uint32_t)h);
-            }
-        }
-    }
+    if (tid < P) s_delta[tid] = s_src[tid] - s_cum[tid];  // key j of piece p: recv[delta + j]
     __syncthreads();
     uint32_t k[ITEMS];
+    if (P <= kGatherDirectP) {
+        // every key straight into registers, all loads in flight: key j lies in piece
+        // p(j) = #{q >= 1 : j >= cum[q]} (the boundaries are wave-uniform scalars)
+        uint32_t cum[kGatherDirectP];
 #pragma unroll
-    for (int i = 0; i < ITEMS; ++i) {
-        const uint32_t j = (uint32_t)(i * BLOCK + tid);
-        k[i] = j < len ? s_a[j] : 0u;
+        for (int q = 1; q < kGatherDirectP; ++q)
+            cum[q] = q < P ? (uint32_t)__builtin_amdgcn_readfirstlane((int)s_cum[q]) : 0xFFFFFFFFu;
+        const uint32_t last = len ? len - 1 : 0u;
+        T v[ITEMS];
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i) {
+            const uint32_t j = min((uint32_t)(i * BLOCK + tid), last);
+            uint32_t q = 0;
+#pragma unroll
+            for (int b = 1; b < kGatherDirectP; ++b) q += j >= cum[b] ? 1u : 0u;
+            v[i] = recv[s_delta[q] + j];
+        }
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i) k[i] = recv_key(v[i], (uint32_t)h);
+    } else {
+        // gather the pieces into s_a (coalesced per piece, 8 loads in flight per thread), then
+        // take the keys block-strided
+#pragma unroll 1
+        for (int p = 0; p < P; ++p) {
+            const T *src = recv + s_src[p];
+            const uint32_t c0 = s_cum[p], c1 = s_cum[p + 1];
+#pragma unroll 1
+            for (uint32_t b = c0; b < c1; b += 8 * BLOCK) {
+                T v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const uint32_t j = b + u * BLOCK + tid;
+                    v[u] = j < c1 ? src[j - c0] : T(0);
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const uint32_t j = b + u * BLOCK + tid;
+                    if (j < c1) s_a[j] = recv_key(v[u], (uint32_t)h);
+                }
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i) {
+            const uint32_t j = (uint32_t)(i * BLOCK + tid);
+            k[i] = j < len ? s_a[j] : 0u;
+        }
     }
     __syncthreads();
     sort_bucket<BLOCK, ITEMS, ATOMIC>(k, len, 2, out + bstart[h], s_a, s_wc);
@@ -2091,12 +2109,15 @@ static_assert(3 * (kHxMax >> 16) <= kCxWrapMax, "K18c wrap list too small for kH
 template <bool WRAP>
 __device__ __forceinline__ void cx_count(uint32_t *s_h, uint32_t v, uint32_t *s_nw,
                                          uint32_t *s_wb, int32_t *s_wd) {
-    const uint32_t sh = (v & 1u) << 4;
+    // word v >> 1 (byte address (v << 1) & ~3), half v & 1: add 1 or 0x10000
+    uint32_t *a = reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(s_h) + ((v << 1) & 0x1FFFCu));
+    const uint32_t inc = (v & 1u) * 0xFFFFu + 1u;  // one v_mad_u32_u24
     if (!WRAP) {
-        atomicAdd(&s_h[v >> 1], 1u << sh);
+        atomicAdd(a, inc);
         return;
     }
-    const uint32_t o = atomicAdd(&s_h[v >> 1], 1u << sh);
+    const uint32_t o = atomicAdd(a, inc);
+    const uint32_t sh = (v & 1u) << 4;
     if (((o >> sh) & 0xFFFFu) == 0xFFFFu) {
         const bool lo = sh == 0, both = lo && (o >> 16) == 0xFFFFu;
         const uint32_t e = atomicAdd(s_nw, lo ? (both ? 3u : 2u) : 1u);
@@ -2141,21 +2162,132 @@ __device__ __forceinline__ void cx_count_piece(const T *src, uint32_t np, uint32
     }
 }
 
-// K18c (receive side; list {h, len}, one 1024-thread workgroup per bucket): the bucket's keys
-// are the P pieces recv[roff[p] + pos[p][h] .. roff[p] + pos[p][h + 1]); keys carry no
-// payload, so sorting them is counting them.
-// 1) One read of the pieces (16-B loads) into the 65 536 packed u16 bin counters (one LDS
-//    atomic per key).
-// 2) Wave w owns bins [4096 w, +4096) as 16 chunks of 256 bins, lane L the 4 bins of words
-//    128 j + 2 L, +1 (one ds_read_b64); the chunk totals are scanned block-wide into output
-//    bases.
-// 3) Each wave writes its chunks' keys in windows of 256 output slots aligned to 16 B in out:
-//    every non-empty bin starting in the window marks its first slot (LDS), lane L reads slots
-//    4 L .. 4 L + 3 (ds_read_b128), a running max inside the lane + a wave max-scan (DPP) hand
-//    every slot its bin (the marks grow with the slot), and the lane stores the 4 keys with ONE
-//    16-B store: a window is 1 KiB written by one instruction.  A frequent value is windows
-//    without marks (the bin carried over).
+// K18c (receive side; list {h, len}): the bucket's keys are the P pieces
+// recv[roff[p] + pos[p][h] .. roff[p] + pos[p][h + 1]); keys carry no payload, so sorting them
+// is counting them.  Persistent: one 1024-thread workgroup per CU walks buckets
+// blockIdx.x, + gridDim.x, ... (the 128 KiB of bin counters allow one per CU), and the next
+// bucket's first 8 x 16 B per thread are loaded while this one is expanded -- so its reads
+// overlap this one's stores and VALU work instead of following them.  Per bucket:
+// 1) the 65 536 packed u16 bin counters count the prefetched vectors, any vectors past them and
+//    the pieces' unaligned heads / tails (one LDS atomic per key);
+// 2) wave w owns bins [4096 w, +4096) (16 chunks of 256 bins, lane L the 4 bins of words
+//    128 j + 2 L, +1); the waves' totals are scanned into their output runs;
+// 3) each wave writes its run in windows of 256 slots aligned to 16 B in out: the bins of every
+//    chunk starting in the window mark their first slot with their key (LDS; chunks streamed
+//    through registers), lane L reads slots 4 L .. 4 L + 3 (ds_read_b128), a running max inside
+//    the lane + a wave max-scan (DPP) give every slot its key (keys grow with the slot; 0 is
+//    both "no mark" and the smallest key), and the lane stores 4 keys with ONE 16-B store.  A
+//    frequent value is windows without marks (the key carried over).
 // 2 B read (16-bit packed pieces; 4 B for int32 pieces) + 4 B written per key.
+template <typename T>
+struct CxTable {  // one bucket's pieces (LDS, double-buffered)
+    uint64_t src[64];    // piece p's first element in recv (elements, mod 2^64)
+    uint32_t len[64];    // its elements
+    uint32_t head[64];   // elements before its first 16-B boundary
+    uint32_t cumv[65];   // 16-B vectors of the pieces before p (vector space)
+    uint64_t dst;        // bstart[h]
+    uint32_t h, keys;    // bucket, keys (0: no bucket)
+};
+
+template <typename T>
+__device__ __forceinline__ void cx_fill_table(CxTable<T> &t, const T *recv,
+                                              const unsigned long long *pos,
+                                              const unsigned long long *roff, int P,
+                                              const unsigned long long *bstart,
+                                              const unsigned long long *list, uint32_t i,
+                                              uint32_t nlist) {  // wave 0 only
+    constexpr uint32_t E = 16 / sizeof(T);
+    const uint32_t lane = threadIdx.x & 63;
+    if (i >= nlist) {
+        if (lane == 0) t.keys = 0;
+        return;
+    }
+    const uint32_t h = (uint32_t)list[2 * i];
+    uint64_t a = 0, b = 0, src = 0;
+    if ((int)lane < P) {
+        a = pos[(uint64_t)lane * (kBuckets16 + 1) + h];
+        b = pos[(uint64_t)lane * (kBuckets16 + 1) + h + 1];
+        src = roff[lane] + a;
+    }
+    const uint32_t n = (uint32_t)(b - a);
+    const uint32_t mis = (uint32_t)((reinterpret_cast<uintptr_t>(recv + src) / sizeof(T)) & (E - 1));
+    const uint32_t hd = min(mis ? E - mis : 0u, n);
+    const uint32_t nv = (n - hd) / E;
+    const uint32_t x = wave_incl_add(nv);
+    if ((int)lane < P) {
+        t.src[lane] = src;
+        t.len[lane] = n;
+        t.head[lane] = hd;
+        t.cumv[lane] = x - nv;
+    }
+    if ((int)lane == P - 1) t.cumv[P] = x;
+    if (lane == 0) {
+        t.h = h;
+        t.keys = (uint32_t)list[2 * i + 1];
+        t.dst = bstart[h];
+    }
+}
+
+// piece of vector g: the last p with cumv[p] <= g (binary search, P <= 64)
+template <typename T>
+__device__ __forceinline__ uint32_t cx_piece(const CxTable<T> &t, int P, uint32_t g) {
+    uint32_t lo = 0, hi = (uint32_t)P;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (t.cumv[mid] <= g) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+template <typename T>
+__device__ __forceinline__ const uint4 *cx_vec(const T *recv, const CxTable<T> &t, int P,
+                                               uint32_t g) {
+    const uint32_t p = cx_piece(t, P, g);
+    return reinterpret_cast<const uint4 *>(recv + t.src[p] + t.head[p]) + (g - t.cumv[p]);
+}
+
+template <bool WRAP, typename T>
+__device__ __forceinline__ void cx_count_vec(uint32_t *s_h, const uint4 &x, uint32_t *s_nw,
+                                             uint32_t *s_wb, int32_t *s_wd) {
+    const uint32_t w4[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        cx_count<WRAP>(s_h, w4[q] & 0xFFFFu, s_nw, s_wb, s_wd);
+        if (sizeof(T) == 2) cx_count<WRAP>(s_h, w4[q] >> 16, s_nw, s_wb, s_wd);
+    }
+}
+
+template <bool WRAP, typename T, uint32_t PF>
+__device__ __forceinline__ void cx_count_bucket(const T *recv, const CxTable<T> &t, int P,
+                                                const uint4 (&x)[PF], uint32_t *s_h,
+                                                uint32_t *s_nw, uint32_t *s_wb, int32_t *s_wd) {
+    constexpr uint32_t NT = 1024, E = 16 / sizeof(T), U = 8;
+    const uint32_t tid = threadIdx.x, nv = t.cumv[P];
+#pragma unroll
+    for (uint32_t u = 0; u < PF; ++u)
+        if (u * NT + tid < nv) cx_count_vec<WRAP, T>(s_h, x[u], s_nw, s_wb, s_wd);
+    // vectors past the prefetch (buckets of more than PF * NT * E keys), U in flight
+#pragma unroll 1
+    for (uint32_t g0 = PF * NT; g0 < nv; g0 += U * NT) {
+        uint4 y[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) y[u] = *cx_vec(recv, t, P, min(g0 + u * NT + tid, nv - 1));
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u)
+            if (g0 + u * NT + tid < nv) cx_count_vec<WRAP, T>(s_h, y[u], s_nw, s_wb, s_wd);
+    }
+    // the pieces' unaligned heads and tails: < E elements each, one per thread
+    for (uint32_t e = tid; e < (uint32_t)P * 2 * E; e += NT) {
+        const uint32_t p = e / (2 * E), k = e % (2 * E);
+        const uint32_t hd = t.head[p], n = t.len[p];
+        const uint32_t body = hd + (t.cumv[p + 1] - t.cumv[p]) * E;
+        uint32_t j = ~0u;
+        if (k < E) { if (k < hd) j = k; }
+        else if (body + (k - E) < n) j = body + (k - E);
+        if (j != ~0u) cx_count<WRAP>(s_h, (uint32_t)recv[t.src[p] + j] & 0xFFFFu, s_nw, s_wb, s_wd);
+    }
+}
+
 template <typename T>
 __global__ __launch_bounds__(1024) void k_count_expand(const T *__restrict__ recv,
                                                        const unsigned long long *__restrict__ pos,
@@ -2163,134 +2295,186 @@ __global__ __launch_bounds__(1024) void k_count_expand(const T *__restrict__ rec
                                                        int P,
                                                        const unsigned long long *__restrict__ bstart,
                                                        const unsigned long long *__restrict__ list,
-                                                       uint32_t *__restrict__ out) {
+                                                       uint32_t nlist, uint32_t *__restrict__ out) {
     constexpr uint32_t NT = 1024, NW = NT / 64, WORDS = 32768, CW = 128;  // words per chunk
     constexpr uint32_t CH = WORDS / NW / CW;                               // 16 chunks per wave
+    constexpr uint32_t PF = 8;  // prefetched 16-B vectors per thread
     __shared__ uint32_t s_h[WORDS];
-    __shared__ uint4 s_mark[NW * 64];  // 256 slots per wave
-    __shared__ uint32_t s_base[NW * CH];
+    // per wave: 256 window slots + 64 dummy words (a lane's marks outside the window)
+    __shared__ uint4 s_mark[NW * 80];
+    __shared__ uint32_t s_base[2 * NW];  // waves' output offsets, totals
     __shared__ uint32_t s_wsum[NW];
-    __shared__ uint64_t s_src[64];
-    __shared__ uint32_t s_len[64];
+    __shared__ CxTable<T> s_t[2];
     __shared__ uint32_t s_wb[kCxWrapMax];
     __shared__ int32_t s_wd[kCxWrapMax];
     __shared__ uint32_t s_nw;
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const uint32_t h = (uint32_t)list[2 * blockIdx.x];
-    const uint32_t len = (uint32_t)list[2 * blockIdx.x + 1];
-    if ((int)tid < P) {
-        const uint64_t a = pos[(uint64_t)tid * (kBuckets16 + 1) + h];
-        const uint64_t b = pos[(uint64_t)tid * (kBuckets16 + 1) + h + 1];
-        s_src[tid] = roff[tid] + a;
-        s_len[tid] = (uint32_t)(b - a);
-    }
-    if (tid == 0) s_nw = 0;
+    uint32_t cur = 0;
+    if (tid < 64) cx_fill_table(s_t[0], recv, pos, roff, P, bstart, list, blockIdx.x, nlist);
+    __syncthreads();
+    uint4 x[PF];
     {
-        uint4 *z = reinterpret_cast<uint4 *>(s_h);
+        const uint32_t nv = s_t[0].cumv[P];
 #pragma unroll
-        for (uint32_t i = 0; i < WORDS / 4 / NT; ++i) z[i * NT + tid] = make_uint4(0, 0, 0, 0);
+        for (uint32_t u = 0; u < PF; ++u)
+            if (u * NT + tid < nv) x[u] = *cx_vec(recv, s_t[0], P, u * NT + tid);
     }
-    __syncthreads();
-    const bool wrap = len >= 65536u;  // below that no half can wrap
 #pragma unroll 1
-    for (int p = 0; p < P; ++p) {
-        if (wrap) cx_count_piece<true>(recv + s_src[p], s_len[p], s_h, &s_nw, s_wb, s_wd);
-        else cx_count_piece<false>(recv + s_src[p], s_len[p], s_h, &s_nw, s_wb, s_wd);
-    }
-    __syncthreads();
-    const uint32_t nw = min(s_nw, kCxWrapMax);  // uniform; 0 unless a half wrapped
-    const uint32_t w0 = w * (WORDS / NW);
-    // lane's 4 bins of chunk j: counts (wrap corrections applied)
-    auto counts = [&](uint32_t j, uint32_t (&c)[4]) {
-        const uint32_t wd = w0 + CW * j + 2 * lane;
-        const uint2 x = *reinterpret_cast<const uint2 *>(s_h + wd);
-        c[0] = x.x & 0xFFFFu;
-        c[1] = x.x >> 16;
-        c[2] = x.y & 0xFFFFu;
-        c[3] = x.y >> 16;
-        for (uint32_t e = 0; e < nw; ++e) {
-            const uint32_t b = s_wb[e] - 2 * wd;  // bin relative to the lane's first
-            if (b < 4u) {
-                const uint32_t d = (uint32_t)s_wd[e];
-                c[0] += b == 0 ? d : 0u;
-                c[1] += b == 1 ? d : 0u;
-                c[2] += b == 2 ? d : 0u;
-                c[3] += b == 3 ? d : 0u;
+    for (uint32_t i = blockIdx.x; i < nlist; i += gridDim.x) {
+        const uint32_t nxt = cur ^ 1u;
+        CxTable<T> &t = s_t[cur];
+        // zero the bins; wave 0 also reads the next bucket's pieces (in flight meanwhile)
+        if (tid < 64) cx_fill_table(s_t[nxt], recv, pos, roff, P, bstart, list, i + gridDim.x, nlist);
+        if (tid == 0) s_nw = 0;
+        {
+            uint4 *z = reinterpret_cast<uint4 *>(s_h);
+#pragma unroll
+            for (uint32_t q = 0; q < WORDS / 4 / NT; ++q) z[q * NT + tid] = make_uint4(0, 0, 0, 0);
+        }
+        __syncthreads();
+        const uint32_t h = (uint32_t)__builtin_amdgcn_readfirstlane((int)t.h);
+        const uint32_t len = (uint32_t)__builtin_amdgcn_readfirstlane((int)t.keys);
+        const uint64_t tdst = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(t.dst >> 32)) << 32) |
+                              (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)t.dst);
+        // count with non-returning atomics; a u16 half that wrapped (>= 65 536 copies of one
+        // value) shows as a total below len, and only then is the bucket counted again with the
+        // wraps tracked (returning atomics)
+        uint32_t nw = 0;
+        const uint32_t w0 = w * (WORDS / NW);
+        // lane's 4 bins of chunk j: counts (wrap corrections applied)
+        auto counts = [&](uint32_t j, uint32_t (&c)[4]) {
+            const uint32_t wd = w0 + CW * j + 2 * lane;
+            const uint2 y = *reinterpret_cast<const uint2 *>(s_h + wd);
+            c[0] = y.x & 0xFFFFu;
+            c[1] = y.x >> 16;
+            c[2] = y.y & 0xFFFFu;
+            c[3] = y.y >> 16;
+            for (uint32_t e = 0; e < nw; ++e) {
+                const uint32_t b = s_wb[e] - 2 * wd;  // bin relative to the lane's first
+                if (b < 4u) {
+                    const uint32_t dd = (uint32_t)s_wd[e];
+                    c[0] += b == 0 ? dd : 0u;
+                    c[1] += b == 1 ? dd : 0u;
+                    c[2] += b == 2 ? dd : 0u;
+                    c[3] += b == 3 ? dd : 0u;
+                }
             }
-        }
-    };
-    // chunk totals
-#pragma unroll 1
-    for (uint32_t j = 0; j < CH; ++j) {
-        uint32_t c[4];
-        counts(j, c);
-        const uint32_t x = wave_incl_add(c[0] + c[1] + c[2] + c[3]);
-        if (lane == 63) s_base[w * CH + j] = x;
-    }
-    __syncthreads();
-    // exclusive scan of the 256 chunk totals in (wave, chunk) = bin order
-    {
-        uint32_t v = 0, x = 0;
-        if (tid < NW * CH) { v = s_base[tid]; x = wave_incl_add(v); }
-        if (tid < NW * CH && lane == 63) s_wsum[w] = x;
+        };
+        auto wave_totals = [&]() -> uint32_t {  // the waves' totals into s_wsum; the bucket's
+            uint32_t tw = 0;
+#pragma unroll 4
+            for (uint32_t j = 0; j < CH; ++j) {
+                uint32_t c[4];
+                counts(j, c);
+                tw += c[0] + c[1] + c[2] + c[3];
+            }
+            const uint32_t y = wave_incl_add(tw);
+            if (lane == 63) s_wsum[w] = y;
+            __syncthreads();
+            uint32_t tot = 0;
+#pragma unroll
+            for (uint32_t ww = 0; ww < NW; ++ww) tot += s_wsum[ww];
+            return tot;
+        };
+        cx_count_bucket<false, T, PF>(recv, t, P, x, s_h, &s_nw, s_wb, s_wd);
         __syncthreads();
-        if (tid < NW * CH) {
-            uint32_t off = 0;
-            for (uint32_t ww = 0; ww < w; ++ww) off += s_wsum[ww];
-            s_base[tid] = off + x - v;
+        if (wave_totals() != len) {  // a half wrapped: count again, tracking the wraps
+            uint4 *z = reinterpret_cast<uint4 *>(s_h);
+#pragma unroll
+            for (uint32_t q = 0; q < WORDS / 4 / NT; ++q) z[q * NT + tid] = make_uint4(0, 0, 0, 0);
+            __syncthreads();
+            cx_count_bucket<true, T, PF>(recv, t, P, x, s_h, &s_nw, s_wb, s_wd);
+            __syncthreads();
+            nw = min(s_nw, kCxWrapMax);  // uniform
+            (void)wave_totals();
+        }
+        // the waves' output offsets (block scan of 16)
+        if (tid < NW) {
+            uint32_t e = 0;
+            for (uint32_t ww = 0; ww < tid; ++ww) e += s_wsum[ww];
+            s_base[tid] = e;
+            s_base[NW + tid] = s_wsum[tid];
         }
         __syncthreads();
-    }
-    uint4 *mk4 = s_mark + 64 * w;
-    uint32_t *mk = reinterpret_cast<uint32_t *>(mk4);
-    uint32_t *dst = out + bstart[h];
-    const uint32_t hk = (h << 16) ^ kFlip;
-#pragma unroll 1
-    for (uint32_t j = 0; j < CH; ++j) {
-        uint32_t c[4];
-        counts(j, c);
-        const uint32_t t = c[0] + c[1] + c[2] + c[3];
-        const uint32_t x = wave_incl_add(t);
-        const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
-        if (tot == 0) continue;
-        uint32_t st[4];  // first slot of each of the lane's bins
-        st[0] = x - t;
-        st[1] = st[0] + c[0];
-        st[2] = st[1] + c[1];
-        st[3] = st[2] + c[2];
-        const uint32_t b0 = 2 * (w0 + CW * j + 2 * lane) + 1;  // mark = bin + 1
-        uint32_t *d = dst + s_base[w * CH + j];
-        // windows aligned to 16 B in out: window r covers slots [256 r - off, +256)
-        const uint32_t off = (uint32_t)(reinterpret_cast<uintptr_t>(d) >> 2) & 3u;
-        uint32_t carry = 0;
-#pragma unroll 1
-        for (uint32_t r0 = 0; r0 < tot + off; r0 += 256) {
-            const uint32_t ws = r0 - off;  // window start slot (mod 2^32)
+        // the next bucket's first vectors: in flight during the expansion below
+        {
+            const uint32_t nv = s_t[nxt].keys ? s_t[nxt].cumv[P] : 0u;
+#pragma unroll
+            for (uint32_t u = 0; u < PF; ++u)
+                if (u * NT + tid < nv) x[u] = *cx_vec(recv, s_t[nxt], P, u * NT + tid);
+        }
+        // expansion: the wave's keys are ONE run of out, walked in windows of 256 slots
+        // aligned to 16 B; the chunks are streamed through registers (a window marks the bins
+        // of every chunk starting in it; the last chunk it touched carries over)
+        // (wave-uniform values read from LDS made scalar: the window loop below then stays a
+        // scalar loop -- with them in VGPRs the compiler ran it as a divergent one)
+        const uint32_t nkw = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_base[NW + w]);
+        if (nkw) {
+            uint4 *mk4 = s_mark + 80 * w;
+            uint32_t *mk = reinterpret_cast<uint32_t *>(mk4);
+            const uint64_t dst0 = tdst + (uint32_t)__builtin_amdgcn_readfirstlane((int)s_base[w]);
+            uint32_t *d = out + dst0;
+            const uint32_t hk = (h << 16) ^ kFlip;
+            const uint32_t off = (uint32_t)(reinterpret_cast<uintptr_t>(d) >> 2) & 3u;
+            // windows [ws, ws + 256) of the wave's run; chunk j's bins mark the windows they
+            // start in (an empty bin is parked at 2^31, past every window), and a window is
+            // finished once the chunk being marked reaches past it
+            uint32_t ws = 0u - off, lo = 0, carry = 0;
+            auto finish = [&]() {  // window ws: keys from the marks, stored; next window cleared
+                __builtin_amdgcn_wave_barrier();
+                const uint4 m = mk4[lane];
+                const uint32_t a0 = m.x, a1 = max(a0, m.y), a2 = max(a1, m.z), a3 = max(a2, m.w);
+                const uint32_t S = wave_incl_max(a3);
+                // the lanes below: S of lane - 1 (DPP wave shift right by one; lane 0 reads 0)
+                const uint32_t prev = max(carry, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)S, 0x138, 0xf, 0xf, true));
+                carry = max(carry, (uint32_t)__builtin_amdgcn_readlane((int)S, 63));
+                const uint32_t q = ws + 4 * lane;  // this lane's first slot
+                const uint4 v = make_uint4(max(prev, a0), max(prev, a1), max(prev, a2), max(prev, a3));
+                if (q + 4 <= nkw && q < nkw) {
+                    *reinterpret_cast<uint4 *>(d + q) = v;  // 16-B aligned
+                } else {
+                    if (q < nkw) d[q] = v.x;
+                    if (q + 1 < nkw) d[q + 1] = v.y;
+                    if (q + 2 < nkw) d[q + 2] = v.z;
+                    if (q + 3 < nkw) d[q + 3] = v.w;
+                }
+                __builtin_amdgcn_wave_barrier();
+                mk4[lane] = make_uint4(0, 0, 0, 0);
+                ws += 256;
+            };
             mk4[lane] = make_uint4(0, 0, 0, 0);
-            __builtin_amdgcn_wave_barrier();
+#pragma unroll 1
+            for (uint32_t j = 0; j < CH; ++j) {
+                uint32_t c[4];
+                counts(j, c);
+                const uint32_t tc = c[0] + c[1] + c[2] + c[3];
+                const uint32_t y = wave_incl_add(tc);
+                uint32_t sm[4], st = lo + y - tc;
+                const uint32_t k0 = hk | (2 * (w0 + CW * j + 2 * lane));
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
-                if (c[i] && st[i] - ws < 256u) mk[st[i] - ws] = b0 + i;
-            __builtin_amdgcn_wave_barrier();
-            const uint4 m = mk4[lane];
-            const uint32_t a0 = m.x, a1 = max(a0, m.y), a2 = max(a1, m.z), a3 = max(a2, m.w);
-            const uint32_t S = wave_incl_max(a3);
-            // the lanes below: S of lane - 1 (DPP wave shift right by one; lane 0 reads 0)
-            const uint32_t prev = max(carry, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)S, 0x138, 0xf, 0xf, true));
-            carry = max(carry, (uint32_t)__builtin_amdgcn_readlane((int)S, 63));
-            const uint32_t q = ws + 4 * lane;  // this lane's first slot
-            const uint4 v = make_uint4(hk | (max(prev, a0) - 1), hk | (max(prev, a1) - 1),
-                                       hk | (max(prev, a2) - 1), hk | (max(prev, a3) - 1));
-            if (q < tot && q + 4 <= tot && q + 4 > q) {
-                *reinterpret_cast<uint4 *>(d + q) = v;  // 16-B aligned
-            } else {
-                if (q < tot) d[q] = v.x;
-                if (q + 1 < tot) d[q + 1] = v.y;
-                if (q + 2 < tot) d[q + 2] = v.z;
-                if (q + 3 < tot) d[q + 3] = v.w;
+                for (int q = 0; q < 4; ++q) {
+                    sm[q] = c[q] ? st : 0x80000000u;
+                    st += c[q];
+                }
+                const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane(
+                    (int)(lo + (uint32_t)__builtin_amdgcn_readlane((int)y, 63)));
+#pragma unroll 1
+                while (true) {
+                    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {  // no branch: a bin off the window marks the dummy
+                        const uint32_t r = sm[q] - ws;
+                        mk[r < 256u ? r : 256u + lane] = k0 + q;
+                    }
+                    if (hi - ws <= 256u) break;  // every bin of chunk j starts before ws + 256
+                    finish();
+                }
+                lo = hi;
             }
-            __builtin_amdgcn_wave_barrier();
+            while (ws + off < nkw + off) finish();
         }
+        __syncthreads();  // the bins, the marks and table cur are reused
+        cur = nxt;
     }
 }
 
@@ -3487,21 +3671,22 @@ hipError_t launch_hist_expand(const void *recv, bool packed16, const uint64_t *p
 
 hipError_t launch_count_expand(const void *recv, bool packed16, const uint64_t *pos,
                                const uint64_t *roff, int P, const uint64_t *bstart,
-                               const uint64_t *list, uint32_t nlist, uint32_t *out,
+                               const uint64_t *list, uint32_t nlist, int ncu, uint32_t *out,
                                hipStream_t s) {
     using ull = unsigned long long;
     if (nlist == 0) return hipSuccess;
-    if (P < 1 || P > 64) return hipErrorInvalidValue;
+    if (P < 1 || P > 64 || ncu < 1) return hipErrorInvalidValue;
     auto *ps = reinterpret_cast<const ull *>(pos);
     auto *ro = reinterpret_cast<const ull *>(roff);
     auto *bs = reinterpret_cast<const ull *>(bstart);
     auto *l = reinterpret_cast<const ull *>(list);
+    const uint32_t grid = std::min<uint32_t>(nlist, (uint32_t)ncu);  // one workgroup per CU
     if (packed16)
-        launch_k(k_count_expand<uint16_t>, nlist, 1024, 0, s, reinterpret_cast<const uint16_t *>(recv), ps, ro, P,
-                 bs, l, out);
+        launch_k(k_count_expand<uint16_t>, grid, 1024, 0, s, reinterpret_cast<const uint16_t *>(recv), ps, ro, P,
+                 bs, l, nlist, out);
     else
-        launch_k(k_count_expand<int32_t>, nlist, 1024, 0, s, reinterpret_cast<const int32_t *>(recv), ps, ro, P,
-                 bs, l, out);
+        launch_k(k_count_expand<int32_t>, grid, 1024, 0, s, reinterpret_cast<const int32_t *>(recv), ps, ro, P,
+                 bs, l, nlist, out);
     return hipGetLastError();
 }
 

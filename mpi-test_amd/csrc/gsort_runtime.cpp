@@ -81,8 +81,10 @@ struct gsort_ctx {
     bool plan_giant = true; // GSORT_GIANT (default 1): the one-dominant-child path
     double est_slack = 1.0; // GSORT_EST_SLACK (test hook: the sampling-error margin's scale)
     // GSORT_RECV_CX: receive buckets of K11g class >= recv_cx (1..4) and list 0 are counted by
-    // K18c; 5 = list 0 only; -1 = the round-2 kernels (K11g classes, two-read K18)
-    int recv_cx = 5;
+    // K18c (default 3: buckets past 9216 keys -- K11g's 512 x 32 and 1024 x 32 classes ran at
+    // 1.6 / 2.0 TB/s, K18c at 1.9 / 2.8, tools/recv_probe.py); 5 = list 0 only; -1 = the
+    // round-2 kernels (K11g classes, two-read K18)
+    int recv_cx = 3;
     int ncu = 256;
     int last_plan = 0;      // gsort_last_plan: 0 exact, 1 sampled, 2 sampled then exact
     DevBuf m_ex, m_ey, m_epart, m_eplan, m_edesc, m_edump;
@@ -1236,6 +1238,46 @@ gsort_status msd_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *ou
         ST_TRY(msd_sort_est(c, in, n, out, stats, &ok, 0, 0, &r));
         c->last_plan = ok ? 1 : 2;
         if (ok) return GSORT_OK;
+        // the block's exact min / max (one read pass + a host round trip), once
+        bool have_mm = false;
+        uint32_t mlo = 0, mhi = 0;
+        auto minmax = [&]() -> gsort_status {
+            if (have_mm) return GSORT_OK;
+            int *mm = reinterpret_cast<int *>(c->d_small + OFF_MINMAX);
+            int *hmm = reinterpret_cast<int *>(c->h_small + OFF_MINMAX);
+            HIP_TRY(c, hipStreamSynchronize(c->stream));  // hmm may feed an earlier copy
+            hmm[0] = 2147483647;
+            hmm[1] = -2147483647 - 1;
+            HIP_TRY(c, hipMemcpyAsync(mm, hmm, 8, hipMemcpyHostToDevice, c->stream));
+            HIP_TRY(c, launch_minmax(reinterpret_cast<const int32_t *>(in), n, mm, c->stream));
+            HIP_TRY(c, hipMemcpyAsync(hmm, mm, 8, hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(c, hipStreamSynchronize(c->stream));
+            mlo = (uint32_t)hmm[0] ^ 0x80000000u;
+            mhi = (uint32_t)hmm[1] ^ 0x80000000u;
+            have_mm = true;
+            return GSORT_OK;
+        };
+        // one value: the sorted block is the block (copied)
+        auto one_value = [&]() -> gsort_status {
+            HIP_TRY(c, hipMemcpyAsync(out, in, n * 4, hipMemcpyDeviceToDevice, c->stream));
+            ok = true;
+            if (stats) {  // one bucket, finished without a partition level
+                stats->passes_run = 0;
+                stats->buckets_local += 1;
+                stats->keys_bucket_sort += n;
+            }
+            return GSORT_OK;
+        };
+        // every sample one value: most likely the whole block is (all-equal 2^28 keys: the
+        // copy 0.60 ms, the counted child below 1.11 ms)
+        if (r.valid && span_lead(r.lo, r.hi) == 32) {
+            ST_TRY(minmax());
+            if (mlo == mhi) {
+                ST_TRY(one_value());
+                c->last_plan = 3;
+                return GSORT_OK;
+            }
+        }
         // one 16-bit child holding at least half of the keys (Zipf, 8- / 16-bit keys, one
         // frequent value): counted, not partitioned (K1m decides from 16384 strided samples)
         if (allow_giant && c->plan_giant && r.valid) {
@@ -1279,25 +1321,11 @@ gsort_status msd_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *ou
                 ST_TRY(msd_sort_est(c, in, n, out, stats, &ok, std::min(lead, 16)));
             } else if (slead == 32 || (known && slead >= 4 && fits(slead - 1))) {
                 // (the samples' span, one bit of margin: the block's may be wider)
-                int *mm = reinterpret_cast<int *>(c->d_small + OFF_MINMAX);
-                int *hmm = reinterpret_cast<int *>(c->h_small + OFF_MINMAX);
-                HIP_TRY(c, hipStreamSynchronize(c->stream));  // hmm may feed an earlier copy
-                hmm[0] = 2147483647;
-                hmm[1] = -2147483647 - 1;
-                HIP_TRY(c, hipMemcpyAsync(mm, hmm, 8, hipMemcpyHostToDevice, c->stream));
-                HIP_TRY(c, launch_minmax(reinterpret_cast<const int32_t *>(in), n, mm, c->stream));
-                HIP_TRY(c, hipMemcpyAsync(hmm, mm, 8, hipMemcpyDeviceToHost, c->stream));
-                HIP_TRY(c, hipStreamSynchronize(c->stream));
-                const uint32_t lo = (uint32_t)hmm[0] ^ 0x80000000u, hi = (uint32_t)hmm[1] ^ 0x80000000u;
+                ST_TRY(minmax());
+                const uint32_t lo = mlo, hi = mhi;
                 const int lead = span_lead(lo, hi);
-                if (lead == 32) {  // one value: the sorted block is the block
-                    HIP_TRY(c, hipMemcpyAsync(out, in, n * 4, hipMemcpyDeviceToDevice, c->stream));
-                    ok = true;
-                    if (stats) {  // one bucket, finished without a partition level
-                        stats->passes_run = 0;
-                        stats->buckets_local += 1;
-                        stats->keys_bucket_sort += n;
-                    }
+                if (lead == 32) {
+                    ST_TRY(one_value());
                 } else if (lead >= 3 && fits(lead)) {
                     ST_TRY(msd_sort_est(c, in, n, out, stats, &ok, std::min(lead, 16), lo));
                 }
@@ -1414,7 +1442,7 @@ gsort_status sort_recv_lists(gsort_ctx *c, const void *recv, bool packed16, cons
         if (!hk[0]) continue;
         if (c->recv_cx > 0 && k + 1 >= c->recv_cx)
             HIP_TRY(c, launch_count_expand(recv, packed16, pos, roff, P, bstart, wl.list[k + 1],
-                                           (uint32_t)hk[0], out, c->stream));
+                                           (uint32_t)hk[0], c->ncu, out, c->stream));
         else
             HIP_TRY(c, launch_gather_sort(recv, packed16, pos, roff, P, bstart, wl.list[k + 1],
                                           (uint32_t)hk[0], k + 1, c->atomic_rank, out,
@@ -1424,7 +1452,7 @@ gsort_status sort_recv_lists(gsort_ctx *c, const void *recv, bool packed16, cons
     if (h[0] && list0) {
         if (c->recv_cx > 0)
             HIP_TRY(c, launch_count_expand(recv, packed16, pos, roff, P, bstart, wl.list[0],
-                                           (uint32_t)h[0], out, c->stream));
+                                           (uint32_t)h[0], c->ncu, out, c->stream));
         else
             HIP_TRY(c, launch_hist_expand(recv, packed16, pos, roff, P, bstart, wl.list[0],
                                           (uint32_t)h[0], out, c->stream));

@@ -256,3 +256,34 @@ def test_kernels_isa_scc_hazard():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "isa_scc_check.py")],
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
+
+
+def test_hot_kernels_use_no_scratch():
+    """No hot-path kernel may spill VGPRs to scratch: a K18c restructure that ran into the
+    128-VGPR limit of 1024-thread workgroups spilled 1480 B per lane and ran 4x slower.  Reads
+    the built code object's notes (private_segment_fixed_size) for every kernel of the sort."""
+    import subprocess
+    import tempfile
+    llvm = "/opt/rocm/lib/llvm/bin"
+    lib = os.path.join(ROOT, "mpi-test_amd", "lib", "libgsort.so")
+    with tempfile.TemporaryDirectory() as d:
+        fat, co = os.path.join(d, "fat.bin"), os.path.join(d, "g.co")
+        subprocess.run([f"{llvm}/llvm-objcopy", f"--dump-section=.hip_fatbin={fat}", lib],
+                       check=True)
+        subprocess.run([f"{llvm}/clang-offload-bundler", "--unbundle", "--type=o",
+                        f"--input={fat}", f"--output={co}",
+                        "--targets=hipv4-amdgcn-amd-amdhsa--gfx950"], check=True)
+        notes = subprocess.run([f"{llvm}/llvm-readelf", "--notes", co], check=True,
+                               capture_output=True, text=True).stdout
+    name, spills = None, []
+    for line in notes.splitlines():
+        line = line.strip()
+        if line.startswith(".name:"):
+            name = line.split(":", 1)[1].strip()
+        elif line.startswith(".private_segment_fixed_size:") and name:
+            if int(line.split(":", 1)[1]) > 0:
+                spills.append(name)
+    hot = ("k_partition_res", "k_local_sort_e", "k_local_sort", "k_est_sample", "k_hist16",
+           "k_count_expand", "k_gather_sort", "k_giant_hist", "k_giant_expand")
+    bad = [n for n in spills if any(h in n for h in hot)]
+    assert not bad, bad

@@ -111,8 +111,10 @@ def test_sampled_plan_distributions(ctx, orc, name):
     assert plan in (SAMPLED, FALLBACK, SHIFTED, GIANT), plan
     if name in ("sorted", "reversed", "sorted_blocks"):  # uniform keys, position-correlated
         assert plan == SAMPLED, name
-    if name in ("zipf", "bits16", "all_equal"):  # one 16-bit child holds (nearly) every key:
+    if name in ("zipf", "bits16"):  # one 16-bit child holds (nearly) every key:
         assert plan == GIANT, name  # counted, not partitioned
+    if name == "all_equal":  # every sample one value, min == max: the block is copied
+        assert plan == SHIFTED, name
     if name == "half_one_value":  # the child holds about half: either way is right
         assert plan in (FALLBACK, GIANT), name
     if name == "bits24":  # a narrow key range: the digits below its shared bits
@@ -277,7 +279,7 @@ def _giant_inputs(orc, n):
 
 
 @pytest.mark.parametrize("name", ["zipf", "bits8", "bits16_negative", "child_in_middle",
-                                  "one_hot_value", "all_equal_min"])
+                                  "one_hot_value"])
 @pytest.mark.parametrize("n", [1 << 22, (1 << 24) + 777])
 def test_giant_child_counted(ctx, orc, name, n):
     keys = _giant_inputs(orc, n)[name]
@@ -286,6 +288,22 @@ def test_giant_child_counted(ctx, orc, name, n):
         assert ctx.last_plan() == GIANT, (name, algo, ctx.last_plan())
         assert np.array_equal(got, np.sort(keys)), (name, algo)
         assert st["passes_run"] == 1 and st["buckets_local"] >= 1
+
+
+@pytest.mark.parametrize("value", [-2**31, -77, 0, 2**31 - 1])
+def test_one_value_block_copied(ctx, value):
+    """All samples one value and min == max (checked by K20 before any counted child): the
+    sorted block is the block, copied; the stats say one bucket and no partition level
+    (the shortcut's stats)."""
+    n = (1 << 22) + 9
+    keys = np.full(n, value, dtype=np.int32)
+    for algo in ("radix", "sample"):
+        got, st = _sort(ctx, keys, algo)
+        assert ctx.last_plan() == SHIFTED, (value, algo, ctx.last_plan())
+        assert np.array_equal(got, keys)
+        if algo == "radix":
+            assert st["passes_run"] == 0 and st["buckets_local"] == 1
+            assert st["keys_bucket_sort"] == n
 
 
 def test_giant_child_sample_misjudged(ctx):
