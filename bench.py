@@ -296,7 +296,7 @@ def dist_p1(gsort, n_local, dist_id, seed, steps=5):
                                                if merge else None),
                              "frac": (round(n_local * 6 / (merge * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
                                       if merge else None),
-                             "note": "K11g + K18: read the 2-B packed key, write the 4-B key"},
+                             "note": "K11g (<= 9216-key buckets) + K18c (larger): read the 2-B packed key, write the 4-B key"},
             "note": "GSORT_FORCE_DIST=1, one-rank RCCL communicator (self-exchange = HBM copy); "
                     "untimed steps, then 3 timed for phases"}
 

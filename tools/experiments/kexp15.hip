@@ -74,8 +74,8 @@ int main(int argc, char **argv) {
                 for (int k = 0; k < 4; ++k) ph[k] += (double)(prof[6 * b + k + 1] - prof[6 * b + k]) * 10.0 / nb;  // ns
         }
         const double ms = t[t.size() / 2];
-        printf("mode %2d bucket %7llu: %.4f ms = %.0f GB/s at 6 B/key; per block us (wave 0 for expand): zero %.2f hist %.2f scan %.2f expand %.2f\n",
-               mode, (unsigned long long)bsize, ms, n * 6.0 / (ms * 1e6), ph[0] / 1e3, ph[1] / 1e3, ph[2] / 1e3, ph[3] / 1e3);
+        printf("bucket %7llu: %.4f ms = %.0f GB/s at 6 B/key (2^%d keys)\n",
+               (unsigned long long)bsize, ms, n * 6.0 / (ms * 1e6), (int)__builtin_ctzll(n));
         if (mode > 0) continue;
         std::vector<uint32_t> out(n);
         CK(hipMemcpy(out.data(), d_out, n * 4, hipMemcpyDeviceToHost));
