@@ -272,7 +272,7 @@ hipError_t launch_compat_keys(const int32_t *a, uint64_t n, int P, int loop, con
 // then the 2048-entry level-3 piece table), dump kSweepTile keys;
 // wl.list[1..4] 65536 entries each, wl.ctr the 15 counters (zeroed by the front).
 #ifndef GSORT_EST_WGS
-#define GSORT_EST_WGS 128
+#define GSORT_EST_WGS 256
 #endif
 constexpr uint32_t kEstWGs = GSORT_EST_WGS;
 constexpr uint32_t kEstBlockKeysHost = 512;  // one 8-key sample segment per block

@@ -1900,13 +1900,21 @@ __global__ __launch_bounds__(BLOCK) void k_gather_sort(const T *__restrict__ rec
             cum[q] = q < P ? (uint32_t)__builtin_amdgcn_readfirstlane((int)s_cum[q]) : 0xFFFFFFFFu;
         const uint32_t last = len ? len - 1 : 0u;
         T v[ITEMS];
+        if (P == 1) {  // one piece: a scalar base (no per-key piece lookup)
+            const uint64_t d0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(s_delta[0] >> 32)) << 32) |
+                                (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)s_delta[0]);
+            const T *src = recv + d0;
 #pragma unroll
-        for (int i = 0; i < ITEMS; ++i) {
-            const uint32_t j = min((uint32_t)(i * BLOCK + tid), last);
-            uint32_t q = 0;
+            for (int i = 0; i < ITEMS; ++i) v[i] = src[min((uint32_t)(i * BLOCK + tid), last)];
+        } else {
 #pragma unroll
-            for (int b = 1; b < kGatherDirectP; ++b) q += j >= cum[b] ? 1u : 0u;
-            v[i] = recv[s_delta[q] + j];
+            for (int i = 0; i < ITEMS; ++i) {
+                const uint32_t j = min((uint32_t)(i * BLOCK + tid), last);
+                uint32_t q = 0;
+#pragma unroll
+                for (int b = 1; b < kGatherDirectP; ++b) q += j >= cum[b] ? 1u : 0u;
+                v[i] = recv[s_delta[q] + j];
+            }
         }
 #pragma unroll
         for (int i = 0; i < ITEMS; ++i) k[i] = recv_key(v[i], (uint32_t)h);

@@ -1702,7 +1702,7 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
     uint64_t *d_cnt = d_xs + (size_t)nb * M;
     const uint64_t *d_all = reinterpret_cast<const uint64_t *>(c->slot[S_STAGE].p);
     t = tic_rec(c);
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < 4 && nb > 0; ++k) {  // (one rank: no boundary, nothing to select)
         const int shift = 24 - 8 * k;
         if (k % 2 == 0) {  // thresholds from the host's prefix
             for (int q = 0; q < nb; ++q) { hx[q] = prefix[q]; hx[nb + q] = g[q]; }
@@ -1862,7 +1862,8 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
     uint64_t *bsize = reinterpret_cast<uint64_t *>(c->m_bsize.p), *bstart = bsize + kBuckets16;
     uint64_t *h_r = reinterpret_cast<uint64_t *>(c->h_small + OFF_PLAN);
     uint64_t *d_r = reinterpret_cast<uint64_t *>(c->d_small + OFF_PLAN);
-    HIP_TRY(c, hipStreamSynchronize(c->stream));  // h_r may still feed an earlier copy
+    // (no stream sync for h_r: nothing has copied from OFF_PLAN since allgather_u64's sync --
+    // the select stages through host vectors -- and a sync here idled the GPU ~40 us)
     for (int p = 0; p < P; ++p) { h_r[p] = roffs[p]; h_r[P + p] = recv[p]; }
     if (!self_moved) h_r[me] = (uint64_t)((pack + cut[me]) - rbuf);  // the self piece, in place
     HIP_TRY(c, hipMemcpyAsync(d_r, h_r, (size_t)2 * P * 8, hipMemcpyHostToDevice, c->stream));
