@@ -2320,6 +2320,12 @@ __global__ __launch_bounds__(1024) void k_count_expand(const T *__restrict__ rec
     uint32_t cur = 0;
     if (tid < 64) cx_fill_table(s_t[0], recv, pos, roff, P, bstart, list, blockIdx.x, nlist);
     __syncthreads();
+    {
+        uint4 *z = reinterpret_cast<uint4 *>(s_h);
+#pragma unroll
+        for (uint32_t q = 0; q < WORDS / 4 / NT; ++q) z[q * NT + tid] = make_uint4(0, 0, 0, 0);
+    }
+    __syncthreads();
     uint4 x[PF];
     {
         const uint32_t nv = s_t[0].cumv[P];
@@ -2331,15 +2337,10 @@ __global__ __launch_bounds__(1024) void k_count_expand(const T *__restrict__ rec
     for (uint32_t i = blockIdx.x; i < nlist; i += gridDim.x) {
         const uint32_t nxt = cur ^ 1u;
         CxTable<T> &t = s_t[cur];
-        // zero the bins; wave 0 also reads the next bucket's pieces (in flight meanwhile)
+        // (the bins are zero: before the first bucket, and the expansion zeroes every word
+        // after its last read); wave 0 reads the next bucket's pieces, in flight meanwhile
         if (tid < 64) cx_fill_table(s_t[nxt], recv, pos, roff, P, bstart, list, i + gridDim.x, nlist);
         if (tid == 0) s_nw = 0;
-        {
-            uint4 *z = reinterpret_cast<uint4 *>(s_h);
-#pragma unroll
-            for (uint32_t q = 0; q < WORDS / 4 / NT; ++q) z[q * NT + tid] = make_uint4(0, 0, 0, 0);
-        }
-        __syncthreads();
         const uint32_t h = (uint32_t)__builtin_amdgcn_readfirstlane((int)t.h);
         const uint32_t len = (uint32_t)__builtin_amdgcn_readfirstlane((int)t.keys);
         const uint64_t tdst = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(t.dst >> 32)) << 32) |
@@ -2455,6 +2456,8 @@ __global__ __launch_bounds__(1024) void k_count_expand(const T *__restrict__ rec
             for (uint32_t j = 0; j < CH; ++j) {
                 uint32_t c[4];
                 counts(j, c);
+                // the chunk's last read: its words are zeroed for the next bucket here
+                *reinterpret_cast<uint2 *>(s_h + w0 + CW * j + 2 * lane) = make_uint2(0, 0);
                 const uint32_t tc = c[0] + c[1] + c[2] + c[3];
                 const uint32_t y = wave_incl_add(tc);
                 uint32_t sm[4], st = lo + y - tc;

@@ -81,10 +81,10 @@ struct gsort_ctx {
     bool plan_giant = true; // GSORT_GIANT (default 1): the one-dominant-child path
     double est_slack = 1.0; // GSORT_EST_SLACK (test hook: the sampling-error margin's scale)
     // GSORT_RECV_CX: receive buckets of K11g class >= recv_cx (1..4) and list 0 are counted by
-    // K18c (default 3: buckets past 9216 keys -- K11g's 512 x 32 and 1024 x 32 classes ran at
-    // 1.6 / 2.0 TB/s, K18c at 1.9 / 2.8, tools/recv_probe.py); 5 = list 0 only; -1 = the
-    // round-2 kernels (K11g classes, two-read K18)
-    int recv_cx = 3;
+    // K18c (default 4: buckets past 16 384 keys -- per 2^28 keys, 16 384-key buckets K11g
+    // 0.72 / K18c 0.85 ms, 32 768-key K11g 1.01 / K18c 0.58 ms, tools/recv_probe.py); 5 = list
+    // 0 only; -1 = the round-2 kernels (K11g classes, two-read K18)
+    int recv_cx = 4;
     int ncu = 256;
     int last_plan = 0;      // gsort_last_plan: 0 exact, 1 sampled, 2 sampled then exact
     DevBuf m_ex, m_ey, m_epart, m_eplan, m_edesc, m_edump;
@@ -1805,8 +1805,14 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
             if (recv[p]) moff[p] = (k++) * nh[me];
     }
     tab.insert(tab.end(), moff.begin(), moff.end());
-    HIP_TRY(c, hipMemcpyAsync(d_tab, tab.data(), tab.size() * 8, hipMemcpyHostToDevice,
-                              c->stream));
+    // staged through pinned memory (a pageable copy blocks the host in the runtime's staging):
+    // OFF_PLAN + 8 KiB is free here -- step (5) below uses OFF_PLAN's first 2P words, and
+    // nothing copies from this range after the stream syncs of the previous call
+    uint64_t *h_tab = reinterpret_cast<uint64_t *>(c->h_small + OFF_PLAN + 8192);
+    if (OFF_PLAN + 8192 + tab.size() * 8 > kSmallBytes)
+        return set_err(c, GSORT_EINVAL, "exchange table too large");
+    std::copy(tab.begin(), tab.end(), h_tab);
+    HIP_TRY(c, hipMemcpyAsync(d_tab, h_tab, tab.size() * 8, hipMemcpyHostToDevice, c->stream));
     const uint64_t *d_rng = d_tab, *d_moff = d_tab + rng.size();
     t = tic(c);
     HIP_TRY(c, launch_meta_counts(gb, d_rng, (int)(rng.size() / 5), meta_s, c->stream));
