@@ -51,7 +51,7 @@ CASES = {
 }
 
 
-@pytest.mark.parametrize("cx", [1, 3, 5, -1])
+@pytest.mark.parametrize("cx", [1, 3, 4, 5, -1])
 @pytest.mark.parametrize("algo", ["radix", "sample"])
 @pytest.mark.parametrize("case", list(CASES))
 @pytest.mark.parametrize("P", [2, 3, 8])
