@@ -218,6 +218,12 @@ hipError_t launch_run_bounds(const int32_t *recv, const uint64_t *roff, const ui
 // pos[p][h] from source p's counts of buckets [h_lo, h_lo + nh) at meta + moff[p]
 // (moff[p] = ~0: nothing received from p) -- the packed exchange.
 // scratch: 64 x P u64.
+// pos (as launch_pos_from_meta) and bstart[0 .. 65536] (exclusive scan of every bucket's total
+// over the sources) in one two-kernel row scan of P + 1 rows; classify then takes bsize =
+// nullptr (sizes from bstart).  scratch: (P + 1) x 64 u64.
+hipError_t launch_recv_plan_from_meta(const uint32_t *meta, const uint64_t *moff, uint32_t h_lo,
+                                     uint32_t nh, int P, uint64_t *pos, uint64_t *bstart,
+                                     uint64_t *scratch, hipStream_t s);
 hipError_t launch_pos_from_meta(const uint32_t *meta, const uint64_t *moff, uint32_t h_lo,
                                 uint32_t nh, int P, uint64_t *pos, uint64_t *scratch,
                                 hipStream_t s);

@@ -1988,7 +1988,7 @@ __global__ __launch_bounds__(kRadix) void k_classify_gather(
     const unsigned long long *__restrict__ bsize, const unsigned long long *__restrict__ bstart,
     WorkLists wl, uint32_t h0, uint32_t h1) {
     const uint32_t h = blockIdx.x * kRadix + threadIdx.x;
-    const uint64_t len = h >= h0 && h < h1 ? bsize[h] : 0ull;
+    const uint64_t len = h >= h0 && h < h1 ? (bsize ? bsize[h] : bstart[h + 1] - bstart[h]) : 0ull;
     // {bucket id, len}: K11g classes, and list 0 (K18 or, past kHxMax, the MSD levels)
     classify_block(h, len, wl);
 }
@@ -2610,6 +2610,16 @@ struct MetaCounts {  // source p's count of bucket h (0 outside [h_lo, h_lo + nh
         return (mo != ~0ull && h >= h_lo && h - h_lo < nh) ? meta[mo + (h - h_lo)] : 0ull;
     }
 };
+struct MetaCountsSum {  // rows 0 .. P-1: MetaCounts; row P: the bucket's total over the sources
+    MetaCounts m;
+    uint32_t P;
+    __device__ unsigned long long operator()(uint32_t row, uint32_t h) const {
+        if (row < P) return m(row, h);
+        unsigned long long t = 0;
+        for (uint32_t p = 0; p < P; ++p) t += m(p, h);
+        return t;
+    }
+};
 struct RowValues {  // v[h] (one row)
     const unsigned long long *v;
     __device__ unsigned long long operator()(uint32_t, uint32_t h) const { return v[h]; }
@@ -2638,7 +2648,8 @@ template <typename Gen>
 __global__ __launch_bounds__(1024) void k_rowscan_apply(Gen gen,
                                                         const unsigned long long *__restrict__ part,
                                                         unsigned long long *__restrict__ out,
-                                                        uint64_t row_stride) {
+                                                        uint64_t row_stride,
+                                                        unsigned long long *out_last) {
     __shared__ unsigned long long s_w[16];
     __shared__ unsigned long long s_pre;
     const uint32_t row = blockIdx.y, b = blockIdx.x, tid = threadIdx.x, lane = tid & 63,
@@ -2660,7 +2671,8 @@ __global__ __launch_bounds__(1024) void k_rowscan_apply(Gen gen,
     __syncthreads();
     unsigned long long run = s_pre + x - c;
     for (uint32_t ww = 0; ww < w; ++ww) run += s_w[ww];
-    unsigned long long *o = out + row * row_stride;
+    // (out_last: the last row goes there instead)
+    unsigned long long *o = out_last && row == gridDim.y - 1 ? out_last : out + row * row_stride;
     o[b * 1024 + tid] = run;
     if (b == kScanBlocks - 1 && tid == 1023) o[kBuckets16] = run + c;
 }
@@ -3583,7 +3595,21 @@ hipError_t launch_pos_from_meta(const uint32_t *meta, const uint64_t *moff, uint
     ull *part = reinterpret_cast<ull *>(scratch);
     launch_k(k_rowscan_reduce<decltype(gen)>, dim3(kScanBlocks, P), 1024, 0, s, gen, part);
     launch_k(k_rowscan_apply<decltype(gen)>, dim3(kScanBlocks, P), 1024, 0, s, gen, part, reinterpret_cast<ull *>(pos),
-                                                          kBuckets16 + 1);
+                                                          kBuckets16 + 1, (ull *)nullptr);
+    return hipGetLastError();
+}
+
+hipError_t launch_recv_plan_from_meta(const uint32_t *meta, const uint64_t *moff, uint32_t h_lo,
+                                     uint32_t nh, int P, uint64_t *pos, uint64_t *bstart,
+                                     uint64_t *scratch, hipStream_t s) {
+    using ull = unsigned long long;
+    if (P < 1 || P > 64) return hipErrorInvalidValue;
+    const MetaCountsSum gen{MetaCounts{meta, reinterpret_cast<const ull *>(moff), h_lo, nh},
+                            (uint32_t)P};
+    ull *part = reinterpret_cast<ull *>(scratch);
+    launch_k(k_rowscan_reduce<decltype(gen)>, dim3(kScanBlocks, P + 1), 1024, 0, s, gen, part);
+    launch_k(k_rowscan_apply<decltype(gen)>, dim3(kScanBlocks, P + 1), 1024, 0, s, gen, part,
+             reinterpret_cast<ull *>(pos), kBuckets16 + 1, reinterpret_cast<ull *>(bstart));
     return hipGetLastError();
 }
 
@@ -3596,7 +3622,7 @@ hipError_t launch_recv_bounds(const uint64_t *pos, int P, uint64_t *bsize, uint6
     ull *part = reinterpret_cast<ull *>(scratch);
     launch_k(k_rowscan_reduce<decltype(gen)>, dim3(kScanBlocks, 1), 1024, 0, s, gen, part);
     launch_k(k_rowscan_apply<decltype(gen)>, dim3(kScanBlocks, 1), 1024, 0, s, gen, part, reinterpret_cast<ull *>(bstart),
-                                                          kBuckets16 + 1);
+                                                          kBuckets16 + 1, (ull *)nullptr);
     return hipGetLastError();
 }
 

@@ -1424,7 +1424,7 @@ gsort_status local_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *
 // (ordered u32): int32 keys, or with packed16 only their low 16 bits, in which case the caller
 // has already filled c->m_rpos (pos[p][h], launch_pos_from_meta).
 // bucket sizes (65536) + starts (65537) + row-scan partials (64 x 64), u64
-constexpr size_t kBsizeBytes = ((size_t)2 * kBuckets16 + 1 + 64 * 64) * 8;
+constexpr size_t kBsizeBytes = ((size_t)2 * kBuckets16 + 1 + 65 * 64) * 8;
 
 // self (int32 runs only): run `self_rank` was not received -- it lies at self_src (the
 // sender's sorted block), and the kernels read it there through a run offset taken relative to
@@ -1781,11 +1781,15 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
         nh[q] = (hi >> 16) - hlo[q] + 1;
         cut[q + 1] = cut[q] + send[q];
     }
-    uint64_t meta_n = 0;
+    // test hook GSORT_RCCL_SELF=1: the self pieces do go through the transport (RcclComm then
+    // sends them through ncclSend / ncclRecv: tests/test_gpu_rccl.py pins RCCL's message limit)
+    static const bool self_moved = getenv("GSORT_RCCL_SELF") && getenv("GSORT_RCCL_SELF")[0] == '1';
+    uint64_t meta_n = 0, meta_self = ~0ull;  // meta_self: this rank's own count section
     std::vector<uint64_t> rng;
     for (int q = 0; q < P; ++q)
         if (send[q]) {
             rng.insert(rng.end(), {cut[q], cut[q + 1], hlo[q], nh[q], meta_n});
+            if (q == me) meta_self = meta_n;
             meta_n += nh[q];
         }
     uint64_t nsrc = 0;
@@ -1793,7 +1797,9 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
     ST_TRY(ensure(c, c->m_meta, (std::max<uint64_t>(meta_n, 1) + nsrc * nh[me] + 1) * 4 +
                                     (rng.size() + P + 2) * 8));
     uint32_t *meta_s = reinterpret_cast<uint32_t *>(c->m_meta.p);
-    uint32_t *meta_r = meta_s + std::max<uint64_t>(meta_n, 1);
+    // (one word of gap: an in-place self offset below, meta_self - (meta_r - meta_s), is then
+    // at most -2 and never the "no source" mark ~0)
+    uint32_t *meta_r = meta_s + std::max<uint64_t>(meta_n, 1) + 1;
     uint64_t *d_tab = reinterpret_cast<uint64_t *>(
         reinterpret_cast<char *>(c->m_meta.p) +
         (((std::max<uint64_t>(meta_n, 1) + nsrc * nh[me] + 1) * 4 + 7) & ~size_t(7)));
@@ -1804,6 +1810,10 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
         for (int p = 0; p < P; ++p)
             if (recv[p]) moff[p] = (k++) * nh[me];
     }
+    // the rank's own counts are read where K15 writes them (an offset relative to meta_r, mod
+    // 2^64), like its own keys below: no self copy in the count exchange either
+    const bool meta_in_place = !self_moved && recv[me] && meta_self != ~0ull;
+    if (meta_in_place) moff[me] = meta_self - (uint64_t)(meta_r - meta_s);
     tab.insert(tab.end(), moff.begin(), moff.end());
     // staged through pinned memory (a pageable copy blocks the host in the runtime's staging):
     // OFF_PLAN + 8 KiB is free here -- step (5) below uses OFF_PLAN's first 2P words, and
@@ -1824,6 +1834,7 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
             if (send[q]) { sc[q] = nh[q] * 4; sd[q] = mo * 4; mo += nh[q]; }
             if (recv[q]) { rc[q] = nh[me] * 4; rd[q] = ro * 4; ro += nh[me]; }
         }
+        if (meta_in_place) sc[me] = rc[me] = 0;
     }
     std::vector<uint64_t> roffs(P + 1, 0);
     for (int p = 0; p < P; ++p) roffs[p + 1] = roffs[p] + recv[p];
@@ -1842,9 +1853,6 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
     // send buffer (its run offset below is taken relative to rbuf, mod 2^64) -- at P = 1 that is
     // the whole 512 MiB of a 2^28-key block, at P = 8 an eighth of it
     uint16_t *rbuf = slot_ptr<uint16_t>(c, S_RECV);
-    // test hook GSORT_RCCL_SELF=1: the self piece does go through the transport (RcclComm then
-    // sends it through ncclSend / ncclRecv: tests/test_gpu_rccl.py pins RCCL's message limit)
-    static const bool self_moved = getenv("GSORT_RCCL_SELF") && getenv("GSORT_RCCL_SELF")[0] == '1';
     t = tic_rec(c);
     for (int q = 0; q < P; ++q) {
         const bool self = q == me && !self_moved;
@@ -1873,12 +1881,13 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
     for (int p = 0; p < P; ++p) { h_r[p] = roffs[p]; h_r[P + p] = recv[p]; }
     if (!self_moved) h_r[me] = (uint64_t)((pack + cut[me]) - rbuf);  // the self piece, in place
     HIP_TRY(c, hipMemcpyAsync(d_r, h_r, (size_t)2 * P * 8, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(c, launch_pos_from_meta(meta_r, d_moff, (uint32_t)hlo[me], (uint32_t)nh[me], P, pos,
-                                    bstart + kBuckets16 + 1, c->stream));
     HIP_TRY(c, hipMemsetAsync(c->d_small + OFF_CTR, 0, kCtrBytes, c->stream));
-    HIP_TRY(c, launch_recv_bounds(pos, P, bsize, bstart, bstart + kBuckets16 + 1, c->stream));
+    // the runs' bucket bounds and the bucket starts in one row scan of P + 1 rows (the last
+    // row is every bucket's total over the sources); classify reads the sizes off bstart
+    HIP_TRY(c, launch_recv_plan_from_meta(meta_r, d_moff, (uint32_t)hlo[me], (uint32_t)nh[me], P,
+                                          pos, bstart, bstart + kBuckets16 + 1, c->stream));
     const WorkLists wl = work_lists(c, 0);
-    HIP_TRY(c, launch_classify_range(bsize, bstart, wl, (uint32_t)hlo[me],
+    HIP_TRY(c, launch_classify_range(nullptr, bstart, wl, (uint32_t)hlo[me],
                                      (uint32_t)(hlo[me] + nh[me]), c->stream));
     toc(c, PH_COUNT, t);
     uint64_t h[3 * (kLocalClasses + 1)];
