@@ -289,7 +289,8 @@ struct EstPlan {
     const uint32_t *in;
     uint64_t n;
     bool flip_in;
-    uint32_t *x, *y, *out;
+    uint32_t *x, *out;
+    uint16_t *y;          // level 2's regions: the low 16 bits of every key
     uint64_t capx, capy;  // keys of x and y
     uint32_t *part8, *part3, *msamp;
     uint32_t *capc, *cap3;

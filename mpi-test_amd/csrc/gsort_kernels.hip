@@ -2719,7 +2719,10 @@ __global__ __launch_bounds__(512) void k_lds_order_check(const uint32_t *__restr
 // per key of the 28).  Here a 1/64 sample sizes them instead: every region gets its estimate
 // plus 6 sigma of sampling error, so the partitions write into gapped regions (level 3 into X,
 // level 2 into Y) whose true fill is only known afterwards, and K11 sorts each child from Y
-// into its exact place in the output.  24 B/key.  A run that would overflow its region is
+// into its exact place in the output.  A level-2 child's keys share their top 16 bits (its
+// level-3 bucket and level-2 digit, below the constant prefix of a shifted plan), so Y holds
+// only the low 16 bits of every key (u16) and K11e puts the child's top half back: 4 + 4 (K3r)
+// + 4 + 2 (K3a) + 2 + 4 (K11e) = 20 B/key.  A run that would overflow its region is
 // diverted to a scratch tile and flagged (the runtime then re-sorts on the exact plan), so the
 // estimate decides speed, never the result.
 //   K1e k_est_sample: sample histograms (8 consecutive keys at a hashed offset of every
@@ -2730,7 +2733,7 @@ __global__ __launch_bounds__(512) void k_lds_order_check(const uint32_t *__restr
 //   K3r / K3a (EST): the reservation partitions with region limits
 //   K12f k_est_tiles: K3a tile descriptors over the level-3 pieces (bucket x shard)
 //   K12g k_est_classify: exact child sizes from the cursors, output offsets, K11 lists
-//   K11e k_local_sort_e: persistent K11 over {src in Y, dst in out, len} entries
+//   K11e k_local_sort_e: K11 over {src in Y | top 16 bits, dst in out | len} entries
 // The eflag word: bit 2 = ineligible (a child estimate above kLocalMax, a u8 counter wrap,
 // every sample in one level-3 bucket, or a region total past its buffer): every later kernel
 // returns at once and the runtime takes the exact plan.  ovf: a region overflowed.
@@ -3063,11 +3066,15 @@ __global__ __launch_bounds__(256) void k_est_tiles(const uint32_t *__restrict__ 
 // lists as {src = bases2[s] + init2, dst | len << 40}.  A child past its limit raises ovf and
 // is not listed (K3a has flagged it already).  The list counters and the status words reach
 // the host through publish_lists, run by block 0 of the K11e launch queued behind K12g.
+// The entry's src carries the child's top 16 bits above bit 40 (Y holds only the low 16 bits):
+// the ordered-u32 key (minus koff) of child (s, e) is pfx . s . e . rest, the digits sb bits
+// below the constant prefix pfx of the shifted plan (K3r's check, from in[0]).
 __global__ __launch_bounds__(kRadix) void k_est_classify(
     const uint32_t *__restrict__ cur2, const uint32_t *__restrict__ init2,
     const uint32_t *__restrict__ lim2, const uint32_t *__restrict__ cur3,
     const uint32_t *__restrict__ init3, const unsigned long long *__restrict__ bases2,
-    WorkLists wl, uint32_t *__restrict__ eflag) {
+    WorkLists wl, uint32_t *__restrict__ eflag, const uint32_t *__restrict__ in, int sb,
+    uint32_t koff) {
     constexpr int NL = kLocalClasses + 1;
     __shared__ unsigned long long s_w[kRadix / 64];
     __shared__ unsigned long long s_fb;
@@ -3109,7 +3116,12 @@ __global__ __launch_bounds__(kRadix) void k_est_classify(
         if (which > 0) {
             unsigned long long *list = reinterpret_cast<unsigned long long *>(wl.list[which]);
             const unsigned long long j = s_base[which] + idx;
-            list[2 * j] = bases2[s] + c0;
+            const uint32_t pfx = sb ? ((in[0] ^ kFlip) - koff) >> (32 - sb) : 0u;
+            const unsigned long long full = ((unsigned long long)pfx << (32 - sb)) |
+                                            ((unsigned long long)s << (24 - sb)) |
+                                            ((unsigned long long)e << (16 - sb));
+            const unsigned long long top = (full >> 16) & 0xffffull;
+            list[2 * j] = (bases2[s] + c0) | (top << 40);
             list[2 * j + 1] = dst | ((unsigned long long)len << 40);
         }
     }
@@ -3145,8 +3157,9 @@ __global__ __launch_bounds__(64) void k_publish_lists(unsigned long long *mail,
 // (no host round trip in between), and the rest once it has read the counts.  With mail set,
 // block 0 first hands K12g's counters and status to the host (publish_lists), off the kernels'
 // critical path.
+// The child's keys come from Y as their low 16 bits; the entry's src word carries the top 16.
 template <int BLOCK, int ITEMS, bool ATOMIC, bool COPY = false>
-__global__ __launch_bounds__(BLOCK) void k_local_sort_e(const uint32_t *__restrict__ in,
+__global__ __launch_bounds__(BLOCK) void k_local_sort_e(const uint16_t *__restrict__ in,
                                                         uint32_t *__restrict__ out,
                                                         const unsigned long long *__restrict__ list,
                                                         const unsigned long long *__restrict__ ctr,
@@ -3162,12 +3175,19 @@ __global__ __launch_bounds__(BLOCK) void k_local_sort_e(const uint32_t *__restri
     if (mail && blockIdx.x == 0) publish_lists(mail, ctr_all, eflag, seq);  // K12g is done
     const uint32_t i = first + blockIdx.x;
     if (i >= (uint32_t)*ctr) return;
-    const uint64_t src = list[2 * i];
+    const uint64_t sw = list[2 * i];
     const uint64_t e = list[2 * i + 1];
-    const uint32_t len = (uint32_t)(e >> 40);
+    const uint32_t len = (uint32_t)(e >> 40), top = (uint32_t)(sw >> 40) << 16;
     if (threadIdx.x < kRadix) s_wc[threadIdx.x] = 0;
     uint32_t k[ITEMS];
-    load_bucket<BLOCK, ITEMS, false>(in + src, len, k);
+    {
+        const __amdgpu_buffer_rsrc_t rs = bucket_rsrc(in + (sw & ((1ull << 40) - 1)), len * 2u);
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j)
+            k[j] = __builtin_amdgcn_raw_buffer_load_b16(rs, (j * BLOCK + (int)threadIdx.x) * 2, 0, 0);
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) k[j] |= top;
+    }
     uint32_t *dst = out + (e & ((1ull << 40) - 1));
     if (COPY) {  // every key of the child is one value (digits below a constant prefix)
         const __amdgpu_buffer_rsrc_t rs = bucket_rsrc(dst, len * 4u);
@@ -3841,10 +3861,11 @@ hipError_t launch_est_level2(const EstPlan &p, hipStream_t s) {
              (const uint32_t *)p.init3, (const uint32_t *)p.lim3,
              reinterpret_cast<const ull *>(p.bases3), max_tiles, (const uint32_t *)p.eflag, p.tp,
              desc, pieces);
-    launch_k(k_partition_res<B, I, false, false, uint32_t, true>, (max_tiles + 1) / 2, B, 0, s,
+    launch_k(k_partition_res<B, I, false, false, uint16_t, true>, (max_tiles + 1) / 2, B, 0, s,
              (const uint32_t *)p.x, p.y, p.n, (const uint32_t *)p.tp, (const TileDesc *)desc,
              reinterpret_cast<const ull *>(p.bases2), p.cur2, (const uint32_t *)p.eflag,
-             (const uint32_t *)nullptr, (const uint32_t *)p.lim2, p.eflag + 1, p.dump,
+             (const uint32_t *)nullptr, (const uint32_t *)p.lim2, p.eflag + 1,
+             reinterpret_cast<uint16_t *>(p.dump),
              (const TileDesc *)pieces, (ull *)nullptr, (ull)0, p.sb, 0u);
     return hipGetLastError();
 }
@@ -3853,7 +3874,8 @@ hipError_t launch_est_classify(const EstPlan &p, hipStream_t s) {
     using ull = unsigned long long;
     launch_k(k_est_classify, kRadix, kRadix, 0, s, (const uint32_t *)p.cur2,
              (const uint32_t *)p.init2, (const uint32_t *)p.lim2, (const uint32_t *)p.cur3,
-             (const uint32_t *)p.init3, reinterpret_cast<const ull *>(p.bases2), p.wl, p.eflag);
+             (const uint32_t *)p.init3, reinterpret_cast<const ull *>(p.bases2), p.wl, p.eflag,
+             p.in, p.sb, p.koff);
     return hipGetLastError();
 }
 
@@ -3871,7 +3893,8 @@ hipError_t launch_local_sort_e(const EstPlan &p, int cls, uint32_t first, uint32
     if (cls < 1 || cls > kLocalClasses) return hipErrorInvalidValue;
     const ull *l = reinterpret_cast<const ull *>(p.wl.list[cls]);
     const ull *call = reinterpret_cast<const ull *>(p.wl.ctr), *ctr = call + 3 * cls;
-    const uint32_t *y = p.y, *ef = p.eflag;
+    const uint16_t *y = p.y;
+    const uint32_t *ef = p.eflag;
     const uint32_t ko = p.koff;
     const int nd = (16 - p.sb + 7) / 8;  // digits for the bits below the plan's two levels
                                          // (sb = 16: a child is one value, K11e copies it)

@@ -986,7 +986,7 @@ gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
         c->est_busy = true;
         gsort_status st = GSORT_OK;
         for (DevBuf *b : {&c->m_ex, &c->m_ey})
-            if (st == GSORT_OK) st = ensure(c, *b, (b == &c->m_ex ? capx : capy) * 4);
+            if (st == GSORT_OK) st = ensure(c, *b, b == &c->m_ex ? capx * 4 : capy * 2);  // Y: u16
         if (st == GSORT_OK)
             st = ensure(c, c->m_epart,
                         (size_t)kEstWGs * (kBuckets16 / 4 + kH16Shards * kRadix + 4) * 4);
@@ -1017,7 +1017,7 @@ gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
     p.n = n;
     p.flip_in = true;
     p.x = static_cast<uint32_t *>(c->m_ex.p);
-    p.y = static_cast<uint32_t *>(c->m_ey.p);
+    p.y = static_cast<uint16_t *>(c->m_ey.p);
     p.out = out;
     p.capx = capx;
     p.capy = capy;
