@@ -115,6 +115,13 @@ class RcclComm : public Comm {
                 return GSORT_EHIP;
             }
         }
+        // nothing for RCCL (one rank; a rank that neither sends nor receives): no group at all
+        // -- an empty ncclGroupStart / End still left ~20 us of idle on the stream
+        // (forced-distributed P = 1 trace, round 3)
+        bool any = false;
+        for (int q = 0; q < size_ && !any; ++q)
+            if (q != rank_ || self_rccl) any = scount[q] || rcount[q];
+        if (!any) return GSORT_OK;
         gsort_status st = check(ncclGroupStart(), "ncclGroupStart");
         if (st != GSORT_OK) return st;
         // messages go in pieces of at most max_msg_ = 2^30 bytes (matched in order on both
