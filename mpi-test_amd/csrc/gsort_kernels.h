@@ -152,15 +152,6 @@ hipError_t launch_plan16(const uint32_t *part, uint32_t nblk, uint64_t *fix, uin
                          uint32_t *cur3, uint32_t *tpfx, const WorkLists &wl2,
                          const WorkLists &wl3, uint64_t *zero, uint32_t nzero, uint32_t *flags,
                          hipStream_t s);
-// K12t: dst0[0 .. n0) = w[0 .. n0), dst1[0 .. n1) = w[n0 .. n0 + n1), zero[0 .. nzero) = 0
-// (words passed by value: n0 + n1 <= kStageWords).
-constexpr uint32_t kStageWords = 128;
-struct StageWords {
-    unsigned long long *dst0, *dst1, *zero;
-    uint32_t n0, n1, nzero;
-    unsigned long long w[kStageWords];
-};
-hipError_t launch_stage_words(const StageWords &a, hipStream_t s);
 // K12p: dst[0 .. n) = src[0 .. n) in pinned host memory, then *flag = seq (system release).
 hipError_t launch_publish(const uint64_t *src, uint32_t n, uint64_t *dst, uint64_t *flag,
                           uint64_t seq, hipStream_t s);

@@ -494,17 +494,6 @@ __global__ __launch_bounds__(64) void k_publish(const unsigned long long *__rest
         __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// K12t: a few host-computed u64 words into device memory through the kernel arguments (the
-// distributed radix's exchange table and run offsets), and a zeroed range: one dispatch where
-// two pinned-memory copies and a memset took three (plus the blit engine's launch gaps).
-__global__ __launch_bounds__(128) void k_stage_words(StageWords a) {
-    for (uint32_t i = threadIdx.x; i < a.n0 + a.n1 || i < a.nzero; i += 128) {
-        if (i < a.n0) a.dst0[i] = a.w[i];
-        else if (i < a.n0 + a.n1) a.dst1[i - a.n0] = a.w[i];
-        if (i < a.nzero) a.zero[i] = 0;
-    }
-}
-
 // ---------------------------------------------------------------------------------------
 // K8: receive-side placement of a distributed pass.  segs[3*i] = {src_off, dst_off, len},
 // sorted by src_off and covering the receive buffer.  Each block copies one contiguous tile
@@ -3822,12 +3811,6 @@ hipError_t launch_compat_keys(const int32_t *a, uint64_t n, int P, int loop, con
     }
     launch_k(k_compat_keys, grid_for(n, 256, 2048), 256, 0, s,
         a, n, cd, key, reinterpret_cast<unsigned long long *>(bad));
-    return hipGetLastError();
-}
-
-hipError_t launch_stage_words(const StageWords &a, hipStream_t s) {
-    if (a.n0 + a.n1 > kStageWords) return hipErrorInvalidValue;
-    launch_k(k_stage_words, 1, 128, 0, s, a);
     return hipGetLastError();
 }
 

@@ -816,19 +816,6 @@ gsort_status wait_mail(gsort_ctx *c, uint64_t seq) {
     return GSORT_OK;
 }
 
-// The work-list counters through the mailbox (K12p + a host spin) instead of a copy and a
-// stream synchronisation: the receive plans' one host round trip before the K11g / K18c
-// launches (the copy's blit dispatch and the synchronisation's wake-up cost ~20-30 us there).
-gsort_status read_counters_mail(gsort_ctx *c, uint64_t *h) {
-    const uint64_t seq = ++c->mail_seq;
-    HIP_TRY(c, launch_publish(reinterpret_cast<const uint64_t *>(c->d_small + OFF_CTR),
-                              (uint32_t)(kCtrBytes / 8), c->d_mail + 8, c->d_mail, seq,
-                              c->stream));
-    ST_TRY(wait_mail(c, seq));
-    memcpy(h, reinterpret_cast<const char *>(c->h_mail + 8), kCtrBytes);
-    return GSORT_OK;
-}
-
 // Levels 3 and 2 through the two-level plan (gsort_kernels.hip, "Two-level plan"): K1h (the
 // 16-bit histogram) + K12a/K12b (counts, bases, bucket bounds, cursors, work lists), then K3r
 // (level 3, in -> tmp, runs reserved on per-shard bucket cursors) and K3a (level 2, tmp -> out,
@@ -1516,7 +1503,7 @@ gsort_status recv_sort(gsort_ctx *c, const void *recv, bool packed16,
                                     bstart + kBuckets16 + 1, c->stream));
     toc(c, PH_COUNT, t);
     uint64_t h[3 * (kLocalClasses + 1)];
-    ST_TRY(read_counters_mail(c, h));
+    ST_TRY(read_counters(c, h));
     if (check_mode()) {
         uint64_t keys = h[1];
         for (int k = 0; k < kLocalClasses; ++k) keys += h[3 * (k + 1) + 1];
@@ -1831,36 +1818,11 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
     // staged through pinned memory (a pageable copy blocks the host in the runtime's staging):
     // OFF_PLAN + 8 KiB is free here -- step (5) below uses OFF_PLAN's first 2P words, and
     // nothing copies from this range after the stream syncs of the previous call
-    std::vector<uint64_t> roffs(P + 1, 0);
-    for (int p = 0; p < P; ++p) roffs[p + 1] = roffs[p] + recv[p];
-    uint16_t *rbuf = slot_ptr<uint16_t>(c, S_RECV);
-    // the receive plan's run offsets (step 5): source p's run at rbuf + h_r[p], h_r[P + p] keys;
-    // the rank's own piece is read in place (its offset relative to rbuf, mod 2^64)
-    std::vector<uint64_t> hr(2 * (size_t)P);
-    for (int p = 0; p < P; ++p) { hr[p] = roffs[p]; hr[P + p] = recv[p]; }
-    if (!self_moved) hr[me] = (uint64_t)((pack + cut[me]) - rbuf);
-    uint64_t *d_r = reinterpret_cast<uint64_t *>(c->d_small + OFF_PLAN);
-    // the table, the run offsets and the zeroed work-list counters in ONE small kernel (K12t,
-    // the words as its arguments) when they fit, else staged through pinned memory
-    const bool staged = tab.size() + hr.size() <= kStageWords;
-    if (staged) {
-        StageWords sw{};
-        sw.dst0 = reinterpret_cast<unsigned long long *>(d_tab);
-        sw.n0 = (uint32_t)tab.size();
-        sw.dst1 = reinterpret_cast<unsigned long long *>(d_r);
-        sw.n1 = (uint32_t)hr.size();
-        sw.zero = reinterpret_cast<unsigned long long *>(c->d_small + OFF_CTR);
-        sw.nzero = (uint32_t)(kCtrBytes / 8);
-        std::copy(tab.begin(), tab.end(), sw.w);
-        std::copy(hr.begin(), hr.end(), sw.w + tab.size());
-        HIP_TRY(c, launch_stage_words(sw, c->stream));
-    } else {
-        uint64_t *h_tab = reinterpret_cast<uint64_t *>(c->h_small + OFF_PLAN + 8192);
-        if (OFF_PLAN + 8192 + tab.size() * 8 > kSmallBytes)
-            return set_err(c, GSORT_EINVAL, "exchange table too large");
-        std::copy(tab.begin(), tab.end(), h_tab);
-        HIP_TRY(c, hipMemcpyAsync(d_tab, h_tab, tab.size() * 8, hipMemcpyHostToDevice, c->stream));
-    }
+    uint64_t *h_tab = reinterpret_cast<uint64_t *>(c->h_small + OFF_PLAN + 8192);
+    if (OFF_PLAN + 8192 + tab.size() * 8 > kSmallBytes)
+        return set_err(c, GSORT_EINVAL, "exchange table too large");
+    std::copy(tab.begin(), tab.end(), h_tab);
+    HIP_TRY(c, hipMemcpyAsync(d_tab, h_tab, tab.size() * 8, hipMemcpyHostToDevice, c->stream));
     const uint64_t *d_rng = d_tab, *d_moff = d_tab + rng.size();
     t = tic(c);
     HIP_TRY(c, launch_meta_counts(gb, d_rng, (int)(rng.size() / 5), meta_s, c->stream));
@@ -1874,6 +1836,8 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
         }
         if (meta_in_place) sc[me] = rc[me] = 0;
     }
+    std::vector<uint64_t> roffs(P + 1, 0);
+    for (int p = 0; p < P; ++p) roffs[p + 1] = roffs[p] + recv[p];
     t = tic_rec(c);
     ST_TRY(comm_try(c, c->comm->alltoallv(meta_s, sc.data(), sd.data(), meta_r, rc.data(),
                                           rd.data(), c->stream)));
@@ -1888,6 +1852,7 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
     // rank's own piece is not moved at all: the receive kernels read it where it lies in the
     // send buffer (its run offset below is taken relative to rbuf, mod 2^64) -- at P = 1 that is
     // the whole 512 MiB of a 2^28-key block, at P = 8 an eighth of it
+    uint16_t *rbuf = slot_ptr<uint16_t>(c, S_RECV);
     t = tic_rec(c);
     for (int q = 0; q < P; ++q) {
         const bool self = q == me && !self_moved;
@@ -1909,14 +1874,14 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
     for (auto &b : c->m_local) ST_TRY(ensure_list(c, b, kBuckets16));
     uint64_t *pos = reinterpret_cast<uint64_t *>(c->m_rpos.p);
     uint64_t *bsize = reinterpret_cast<uint64_t *>(c->m_bsize.p), *bstart = bsize + kBuckets16;
-    if (!staged) {
-        // (no stream sync for h_r: nothing has copied from OFF_PLAN since allgather_u64's sync
-        // -- the select stages through host vectors -- and a sync here idled the GPU ~40 us)
-        uint64_t *h_r = reinterpret_cast<uint64_t *>(c->h_small + OFF_PLAN);
-        std::copy(hr.begin(), hr.end(), h_r);
-        HIP_TRY(c, hipMemcpyAsync(d_r, h_r, hr.size() * 8, hipMemcpyHostToDevice, c->stream));
-        HIP_TRY(c, hipMemsetAsync(c->d_small + OFF_CTR, 0, kCtrBytes, c->stream));
-    }
+    uint64_t *h_r = reinterpret_cast<uint64_t *>(c->h_small + OFF_PLAN);
+    uint64_t *d_r = reinterpret_cast<uint64_t *>(c->d_small + OFF_PLAN);
+    // (no stream sync for h_r: nothing has copied from OFF_PLAN since allgather_u64's sync --
+    // the select stages through host vectors -- and a sync here idled the GPU ~40 us)
+    for (int p = 0; p < P; ++p) { h_r[p] = roffs[p]; h_r[P + p] = recv[p]; }
+    if (!self_moved) h_r[me] = (uint64_t)((pack + cut[me]) - rbuf);  // the self piece, in place
+    HIP_TRY(c, hipMemcpyAsync(d_r, h_r, (size_t)2 * P * 8, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemsetAsync(c->d_small + OFF_CTR, 0, kCtrBytes, c->stream));
     // the runs' bucket bounds and the bucket starts in one row scan of P + 1 rows (the last
     // row is every bucket's total over the sources); classify reads the sizes off bstart
     HIP_TRY(c, launch_recv_plan_from_meta(meta_r, d_moff, (uint32_t)hlo[me], (uint32_t)nh[me], P,
@@ -1926,7 +1891,7 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
                                      (uint32_t)(hlo[me] + nh[me]), c->stream));
     toc(c, PH_COUNT, t);
     uint64_t h[3 * (kLocalClasses + 1)];
-    ST_TRY(read_counters_mail(c, h));
+    ST_TRY(read_counters(c, h));
     if (check_mode()) {
         for (int p = 0; p < P; ++p)
             ST_TRY(check_bounds(c, pos + (size_t)p * (kBuckets16 + 1), kBuckets16 + 1, recv[p],

@@ -282,6 +282,20 @@ def test_radix_multirank_balanced_blocks(gsort, orc, P, local):
             assert all(r[1]["exchanges"] == 1 for r in res)
 
 
+def test_radix_multirank_many_ranks(gsort, orc):
+    """20 ranks (the packed exchange takes up to 64): 20 x 20 pieces, most destination ranges
+    a few 16-bit buckets wide, exact at every rank."""
+    P = 20
+    for dist, n in ((orc.UNIFORM, 200003), (orc.ZIPF, 150001)):
+        keys = orc.gen(dist, P, n)
+        B = -(-n // P)
+        blocks = [keys[r * B:(r + 1) * B] for r in range(P)]
+        res = run_group(gsort, blocks, "radix")
+        ref = np.sort(keys)
+        for q in range(P):
+            assert np.array_equal(res[q][0], ref[q * B:(q + 1) * B]), (dist, q)
+
+
 @pytest.mark.parametrize("P", [1, 2, 4, 8])
 def test_radix_multirank_mixed_inputs(gsort, orc, monkeypatch, P):
     """The packed exchange on uniform and Zipf keys, a few distinct values (destination ranges
