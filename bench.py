@@ -305,7 +305,8 @@ def kernel_rooflines(stats, n_local, plan=0):
     """Per kernel class: total device time over the timed steps (HIP events recorded on
     libgsort's stream around every launch), launches, algorithmic bytes:
     K3 / K3u read + write every key of the launch (8 B/key), K11 reads and writes every key of
-    its buckets once (8 B/key)."""
+    its buckets once (8 B/key); in the sampled plan K3a writes and K11e reads only the low 16
+    bits of every key (6 B/key each)."""
     out = []
 
     def add(kernel, prefixes, ms_list, keys_list, bpk):
