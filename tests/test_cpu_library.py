@@ -287,3 +287,24 @@ def test_hot_kernels_use_no_scratch():
            "k_count_expand", "k_gather_sort", "k_giant_hist", "k_giant_expand")
     bad = [n for n in spills if any(h in n for h in hot)]
     assert not bad, bad
+
+
+def test_bench_roofline_traffic_takes_the_dominant_instantiation():
+    """bench.py prices the dominant kernel's HBM traffic from the newest committed PMC summary:
+    of K11e's size classes it must take the one holding the time (the 2^28 launches), not an
+    average with the small class the bench's 2^24 reference check runs."""
+    import importlib.util
+    import json
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(root, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    got = bench.pmc_traffic("radix", 1 << 28, 1, ("k_local_sort_e",))
+    assert got is not None
+    d = json.load(open(os.path.join(root, got["source"])))["kernels"]
+    k11e = [v for k, v in d.items() if k.startswith("k_local_sort_e")]
+    top = max(k11e, key=lambda v: v["avg_us"] * v["calls"])
+    assert got["hbm_bytes_per_launch"] == round(top["hbm_bytes"])
+    # 2 B read + 4 B written per key at 2^28 keys, within the PMC's few % of overhead
+    assert 0.95 < got["hbm_bytes_per_launch"] / (6 * (1 << 28)) < 1.15
