@@ -258,45 +258,54 @@ def median_check(ctx, fn, dist_id, seed, cpu):
     return res
 
 
-def dist_p1(gsort, n_local, dist_id, seed, steps=5):
-    """The distributed radix path at N = 1 (one-rank RCCL communicator, GSORT_FORCE_DIST):
-    sender grouping, radix select, packed self-exchange through RCCL, receive sort -- the
-    per-GPU cost the weak-scaling points pay before any xGMI time."""
+def dist_p1(gsort, n_local, dist_id, seed, steps=5, algo="radix"):
+    """The distributed path at N = 1 (one-rank RCCL communicator, GSORT_FORCE_DIST) -- the
+    per-GPU cost the multi-GPU points pay before any xGMI time:
+      radix:  sender grouping, radix select, packed self-exchange through RCCL, receive sort;
+      sample: local sort, regular samples + device splitter selection + broadcast, bucket
+              bounds, exchange of exact sizes, receive sort of the received sorted runs
+              (mpi_sample_sort.c:85, 89-128, 148-174)."""
     os.environ["GSORT_FORCE_DIST"] = "1"
     try:
         ctx = gsort.Context(rank=0, nranks=1, device=0, uid=gsort.get_uid())
     finally:
         del os.environ["GSORT_FORCE_DIST"]
+    fn = ctx.radix if algo == "radix" else ctx.sample
     try:
         d = ctx.alloc(n_local * 4)
         ctx.generate(dist_id, seed, 0, n_local, d)
         ctx.reserve(n_local)
         for _ in range(2):
-            ctx.radix(d, n_local, stats=False)
+            fn(d, n_local, stats=False)
         t0 = time.perf_counter()
         for _ in range(steps):
-            ctx.radix(d, n_local, stats=False)
+            fn(d, n_local, stats=False)
         ms = (time.perf_counter() - t0) * 1e3 / steps
-        st = [ctx.radix(d, n_local)[2] for _ in range(3)]
-        out, m, _ = ctx.radix(d, n_local, stats=False)
+        st = [fn(d, n_local)[2] for _ in range(3)]
+        out, m, _ = fn(d, n_local, stats=False)
         fp, fin = ctx.fingerprint(out, m), ctx.fingerprint(d, n_local)
-        ok = fp["sorted"] and fp["sum"] == fin["sum"] and fp["xor"] == fin["xor"]
+        ok = fp["sorted"] and fp["sum"] == fin["sum"] and fp["xor"] == fin["xor"] and m == n_local
         ctx.free(d)
     finally:
         ctx.close()
     avg = {k: round(sum(s[k] for s in st) / len(st), 4)
-           for k in ("ms_total", "ms_hist", "ms_sample", "ms_exchange", "ms_place", "ms_merge",
-                     "ms_bucket_sort")}
+           for k in ("ms_total", "ms_hist", "ms_local_sort", "ms_sample", "ms_exchange",
+                     "ms_place", "ms_merge", "ms_bucket_sort")}
     avg["ms_level"] = [round(sum(s["ms_level"][i] for s in st) / len(st), 4) for i in range(2)]
     merge = avg["ms_merge"]
-    return {"ms_per_step": round(ms, 4), "GKeys_s": round(n_local / (ms * 1e-3) / 1e9, 2),
+    # the radix receive side reads the 2-B packed key; the sample sort exchanges int32 keys
+    bpk = 6 if algo == "radix" else 8
+    return {"algo": algo, "ms_per_step": round(ms, 4),
+            "GKeys_s": round(n_local / (ms * 1e-3) / 1e9, 2),
             "phases_ms_avg": avg, "verified": bool(ok),
-            "receive_sort": {"ms": merge, "bytes_per_key": 6,
-                             "achieved_GBps": (round(n_local * 6 / (merge * 1e-3) / 1e9, 1)
+            "receive_sort": {"ms": merge, "bytes_per_key": bpk,
+                             "achieved_GBps": (round(n_local * bpk / (merge * 1e-3) / 1e9, 1)
                                                if merge else None),
-                             "frac": (round(n_local * 6 / (merge * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
+                             "frac": (round(n_local * bpk / (merge * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
                                       if merge else None),
-                             "note": "K11g (<= 9216-key buckets) + K18c (larger): read the 2-B packed key, write the 4-B key"},
+                             "note": ("K11g (<= 9216-key buckets) + K18c (larger): read the "
+                                      "received key (2-B packed for radix, int32 for sample), "
+                                      "write the 4-B key")},
             "note": "GSORT_FORCE_DIST=1, one-rank RCCL communicator (self-exchange = HBM copy); "
                     "untimed steps, then 3 timed for phases"}
 
@@ -510,12 +519,31 @@ def main():
     fin = ctx.fingerprint(d_in, n_local)
     ok = fp["sorted"]
     if world > 1:
-        v = torch.tensor([fin["sum"] % (1 << 40), fp["sum"] % (1 << 40), 0 if ok else 1],
-                         dtype=torch.int64)
-        dist.all_reduce(v)
-        ok = ok and int(v[2]) == 0 and int(v[0]) % (1 << 40) == int(v[1]) % (1 << 40)
+        # every rank's figures to every rank: the multiset (sum and xor of mix64(key), 64-bit)
+        # of all outputs == of all inputs, every output sorted, rank q's last key <= rank
+        # q+1's first (a misrouted exchange that keeps the multiset fails here), and the sizes
+        # (radix: rank q holds exactly its n_local global positions)
+        def s64(x):  # u64 -> the int64 with the same bits
+            return x - (1 << 64) if x >= 1 << 63 else x
+        mine = torch.tensor([s64(fin["sum"]), s64(fp["sum"]), s64(fin["xor"]), s64(fp["xor"]),
+                             int(fp["sorted"]), n_out, fp["first"], fp["last"]], dtype=torch.int64)
+        rows = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(rows, mine)
+        rows = [[int(x) for x in r.tolist()] for r in rows]
+        m64 = (1 << 64) - 1
+        sum_in = sum(r[0] for r in rows) & m64
+        sum_out = sum(r[1] for r in rows) & m64
+        x_in = x_out = 0
+        for r in rows:
+            x_in ^= r[2] & m64
+            x_out ^= r[3] & m64
+        full = [r for r in rows if r[5]]
+        ok = (all(r[4] for r in rows) and sum_in == sum_out and x_in == x_out
+              and sum(r[5] for r in rows) == n_local * world
+              and all(x[7] <= y[6] for x, y in zip(full, full[1:]))
+              and (a.algo != "radix" or all(r[5] == n_local for r in rows)))
     else:
-        ok = ok and fp["sum"] == fin["sum"] and fp["xor"] == fin["xor"]
+        ok = ok and fp["sum"] == fin["sum"] and fp["xor"] == fin["xor"] and n_out == n_local
 
     n_total = n_local * world
     ms_step = elapsed * 1e3 / a.steps
@@ -598,10 +626,11 @@ def main():
     ctx.close()
     if world == 1 and a.algo == "radix" and not a.no_dist_p1 and \
             os.environ.get("GSORT_FORCE_DIST") != "1":
-        try:
-            line["dist_p1"] = dist_p1(gsort, n_local, dist_id, a.seed)
-        except Exception as e:  # reported, never fatal
-            line["dist_p1"] = {"error": repr(e)}
+        for key, algo in (("dist_p1", "radix"), ("dist_p1_sample", "sample")):
+            try:
+                line[key] = dist_p1(gsort, n_local, dist_id, a.seed, algo=algo)
+            except Exception as e:  # reported, never fatal
+                line[key] = {"error": repr(e)}
     if rank == 0:
         os.write(json_fd, (json.dumps(line) + "\n").encode())
     if world > 1:

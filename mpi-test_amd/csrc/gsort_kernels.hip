@@ -1674,6 +1674,31 @@ __global__ __launch_bounds__(BLOCK) void k_partition_res(
     }
 }
 
+// Wave-wide inclusive scans through DPP (row shifts 1/2/4/8, then the row-15 and row-31
+// broadcasts): VALU only, where __shfl_up costs an LDS-crossbar op per step.
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ uint32_t dpp0(uint32_t x) {  // lanes outside the pattern read 0
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWS, 0xf, true);
+}
+__device__ __forceinline__ uint32_t wave_incl_add(uint32_t x) {
+    x += dpp0<0x111>(x);
+    x += dpp0<0x112>(x);
+    x += dpp0<0x114>(x);
+    x += dpp0<0x118>(x);
+    x += dpp0<0x142, 0xa>(x);
+    x += dpp0<0x143, 0xc>(x);
+    return x;
+}
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
+    x = max(x, dpp0<0x111>(x));
+    x = max(x, dpp0<0x112>(x));
+    x = max(x, dpp0<0x114>(x));
+    x = max(x, dpp0<0x118>(x));
+    x = max(x, dpp0<0x142, 0xa>(x));
+    x = max(x, dpp0<0x143, 0xc>(x));
+    return x;
+}
+
 // Stable wave-level rank of one round (64 keys, lane order = key order) against the wave's
 // running digit counters wc[256] (u32): returns #earlier keys of the wave with this digit.
 //   ATOMIC: one ds_add_rtn_u32 per lane.  The MI355X LDS serializes lanes of one instruction
@@ -1806,6 +1831,124 @@ __device__ __forceinline__ void sort_bucket(uint32_t (&k)[ITEMS], uint32_t len, 
                 s_a[wc[(k[i] >> shift) & 255u] + rk[i]] = k[i];
         __syncthreads();
     }
+    const __amdgpu_buffer_rsrc_t rs = bucket_rsrc(dst, len * 4u);  // stores past len dropped
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+        const uint32_t j = (uint32_t)(i * BLOCK + tid);
+        __builtin_amdgcn_raw_buffer_store_b32((s_a[j] + koff) ^ kFlip, rs, (int)(j * 4u), 0, 0);
+    }
+}
+
+// Body of K11e for two digits (the low 16 bits), split 10 + 6 instead of 8 + 8 so that the
+// second, stable pass needs no LDS atomic and no random offset read ("K11e two
+// passes as 10 + 6 bits"):
+//   pass A (bits 0 .. ABITS-1, unstable): one returning LDS atomic per key on 2^ABITS block
+//     counters, a block scan, one offset read + scatter into s_a -- as the 8-bit first pass.
+//   pass B (bits ABITS .. 15, stable, NB = 2^(16-ABITS) <= 64 digits): wave w takes the
+//     contiguous chunk [w*64*R, (w+1)*64*R) of s_a.  Per round of 64 keys the wave ballots the
+//     digit's bits: a lane's peers (lanes with its digit) give its rank (mbcnt), lane L's own
+//     index taken as a digit gives digit L's count in the round -- so lane L holds the wave's
+//     running count of digit L in a register.  The per-wave totals go through LDS once; every
+//     wave scans them itself (no second barrier), and each key fetches its digit's running
+//     offset from lane e with one ds_bpermute (crossbar, no bank conflicts).  Stable by
+//     construction (lane order = key order), whatever the LDS atomics' lane order.
+// LDS ops per key: pass A 3 random (atomic, offset, scatter); pass B 1 random (scatter) + 1
+// linear read + 1 bpermute; 1 linear read on the way out -- against 6 random + 2 linear for
+// 8 + 8 (SQ_LDS_BANK_CONFLICT: ~3.3 extra cycles per random wave-op).
+// s_c: 2^ABITS words (>= WAVES * 64), zeroed by the caller before its barrier.  The pass-A scan's
+// wave sums borrow the tail of s_a (every key is in registers then).
+template <int BLOCK, int ITEMS, int ABITS>
+__device__ __forceinline__ void sort_bucket16(uint32_t (&k)[ITEMS], uint32_t len,
+                                              uint32_t *__restrict__ dst, uint32_t *s_a,
+                                              uint32_t *s_c, uint32_t koff) {
+    constexpr int WAVES = BLOCK / 64;
+    constexpr int TILE = BLOCK * ITEMS;
+    constexpr uint32_t NA = 1u << ABITS, BB = 16 - ABITS, NB = 1u << BB;
+    constexpr int CPT = (int)NA / BLOCK;  // pass-A counters per thread in the scan
+    static_assert(NB <= 64 && CPT >= 1 && (int)NA >= WAVES * 64, "pass geometry");
+    static_assert(TILE <= 65536, "ranks fit 16 bits");
+    uint32_t *s_wsum = s_a + TILE - WAVES;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    auto lim = [&](int i) -> uint32_t {
+        return len > (uint32_t)(i * BLOCK) ? len - (uint32_t)(i * BLOCK) : 0u;
+    };
+
+    // pass A: unstable counting scatter on the low ABITS bits
+    uint32_t r[ITEMS];
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i)
+        if ((uint32_t)tid < lim(i)) r[i] = atomicAdd(&s_c[k[i] & (NA - 1)], 1u);
+    __syncthreads();
+    {
+        uint32_t c[CPT], sum = 0;
+#pragma unroll
+        for (int j = 0; j < CPT; ++j) { c[j] = s_c[tid * CPT + j]; sum += c[j]; }
+        const uint32_t incl = wave_incl_add(sum);
+        if (lane == 63) s_wsum[w] = incl;
+        __syncthreads();
+        uint32_t run = incl - sum;
+        for (int ww = 0; ww < w; ++ww) run += s_wsum[ww];
+#pragma unroll
+        for (int j = 0; j < CPT; ++j) { s_c[tid * CPT + j] = run; run += c[j]; }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i)
+        if ((uint32_t)tid < lim(i)) s_a[s_c[k[i] & (NA - 1)] + r[i]] = k[i];
+    __syncthreads();
+
+    // pass B: stable on bits ABITS .. 15, wave-chunked
+    const uint32_t R = (len + 64 * WAVES - 1) / (64 * WAVES);
+    const uint32_t base = (uint32_t)w * 64 * R;                   // wave-uniform
+    const uint32_t wlen = len > base ? min(len - base, 64 * R) : 0u;  // keys of this chunk
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i)
+        if ((uint32_t)i < R && (uint32_t)(i * 64 + lane) < wlen) k[i] = s_a[base + i * 64 + lane];
+    uint32_t tot = 0;  // lane L: keys of digit L in this wave's chunk so far
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+        if ((uint32_t)i >= R) continue;  // wave-uniform
+        const uint32_t nv = wlen > (uint32_t)(i * 64) ? wlen - (uint32_t)(i * 64) : 0u;
+        const uint64_t vm = nv >= 64 ? ~0ull : (1ull << nv) - 1;
+        const uint32_t e = (k[i] >> ABITS) & (NB - 1);
+        uint32_t plo = (uint32_t)vm, phi = (uint32_t)(vm >> 32), qlo = plo, qhi = phi;
+#pragma unroll
+        for (int b = 0; b < (int)BB; ++b) {
+            const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int32_t)e, b, 1);
+            const uint32_t lm = (uint32_t)__builtin_amdgcn_sbfe(lane, b, 1);
+            uint64_t bal;
+            asm("v_cmp_ne_u32_e64 %0, 0, %1" : "=s"(bal) : "v"(m));
+            plo = __builtin_amdgcn_bitop3_b32(plo, (uint32_t)bal, m, 0x90);
+            phi = __builtin_amdgcn_bitop3_b32(phi, (uint32_t)(bal >> 32), m, 0x90);
+            qlo = __builtin_amdgcn_bitop3_b32(qlo, (uint32_t)bal, lm, 0x90);
+            qhi = __builtin_amdgcn_bitop3_b32(qhi, (uint32_t)(bal >> 32), lm, 0x90);
+        }
+        const uint32_t c = (uint32_t)(__popc(qlo) + __popc(qhi));  // digit `lane` in this round
+        r[i] = __builtin_amdgcn_mbcnt_hi(phi, __builtin_amdgcn_mbcnt_lo(plo, 0u)) | (c << 16);
+        tot += c;
+    }
+    s_c[w * 64 + lane] = tot;
+    __syncthreads();  // every chunk read of s_a is done, the wave totals are visible
+    uint32_t cur;
+    {
+        uint32_t all = 0, before = 0;
+#pragma unroll
+        for (int ww = 0; ww < WAVES; ++ww) {
+            const uint32_t v = s_c[ww * 64 + lane];
+            all += v;
+            before += ww < w ? v : 0u;
+        }
+        cur = wave_incl_add(all) - all + before;  // digit `lane`'s first slot for this wave
+    }
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+        if ((uint32_t)i >= R) continue;
+        const uint32_t e = (k[i] >> ABITS) & (NB - 1);
+        const uint32_t off = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(e << 2), (int)cur);
+        if ((uint32_t)(i * 64 + lane) < wlen) s_a[off + (r[i] & 0xffffu)] = k[i];
+        cur += r[i] >> 16;
+    }
+    __syncthreads();
     const __amdgpu_buffer_rsrc_t rs = bucket_rsrc(dst, len * 4u);  // stores past len dropped
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
@@ -2081,31 +2224,6 @@ __global__ __launch_bounds__(1024) void k_hist_expand(const T *__restrict__ recv
 }
 
 // ---- K18c: one-read counting sort of a receive bucket's low 16 bits -----------------------
-// Wave-wide inclusive scans through DPP (row shifts 1/2/4/8, then the row-15 and row-31
-// broadcasts): VALU only, where __shfl_up costs an LDS-crossbar op per step.
-template <int CTRL, int ROWS = 0xf>
-__device__ __forceinline__ uint32_t dpp0(uint32_t x) {  // lanes outside the pattern read 0
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWS, 0xf, true);
-}
-__device__ __forceinline__ uint32_t wave_incl_add(uint32_t x) {
-    x += dpp0<0x111>(x);
-    x += dpp0<0x112>(x);
-    x += dpp0<0x114>(x);
-    x += dpp0<0x118>(x);
-    x += dpp0<0x142, 0xa>(x);
-    x += dpp0<0x143, 0xc>(x);
-    return x;
-}
-__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
-    x = max(x, dpp0<0x111>(x));
-    x = max(x, dpp0<0x112>(x));
-    x = max(x, dpp0<0x114>(x));
-    x = max(x, dpp0<0x118>(x));
-    x = max(x, dpp0<0x142, 0xa>(x));
-    x = max(x, dpp0<0x143, 0xc>(x));
-    return x;
-}
-
 // Bin counters: 65 536 u16 halves in 32 768 words (128 KiB).  A half that wraps (>= 65 536
 // copies of one value: buckets past 65 535 keys only) is seen by the one lane whose returning
 // atomic read 0xffff; it records the correction (bin, delta): +65 536 for the wrapped bin,
@@ -3158,7 +3276,7 @@ __global__ __launch_bounds__(64) void k_publish_lists(unsigned long long *mail,
 // block 0 first hands K12g's counters and status to the host (publish_lists), off the kernels'
 // critical path.
 // The child's keys come from Y as their low 16 bits; the entry's src word carries the top 16.
-template <int BLOCK, int ITEMS, bool ATOMIC, bool COPY = false>
+template <int BLOCK, int ITEMS, bool ATOMIC, bool COPY = false, int ABITS = 0>
 __global__ __launch_bounds__(BLOCK) void k_local_sort_e(const uint16_t *__restrict__ in,
                                                         uint32_t *__restrict__ out,
                                                         const unsigned long long *__restrict__ list,
@@ -3170,15 +3288,23 @@ __global__ __launch_bounds__(BLOCK) void k_local_sort_e(const uint16_t *__restri
                                                         unsigned long long seq, uint32_t koff) {
     constexpr int WAVES = BLOCK / 64;
     constexpr int TILE = BLOCK * ITEMS;
+    // ABITS != 0: the 16-bit body (sort_bucket16, ndigits == 2) and its 2^ABITS counters
+    constexpr int NC = ABITS ? (1 << ABITS) : WAVES * kRadix;
     __shared__ uint32_t s_a[TILE];
-    __shared__ uint32_t s_wc[WAVES * kRadix];
+    __shared__ uint32_t s_wc[NC];
     if (mail && blockIdx.x == 0) publish_lists(mail, ctr_all, eflag, seq);  // K12g is done
     const uint32_t i = first + blockIdx.x;
     if (i >= (uint32_t)*ctr) return;
     const uint64_t sw = list[2 * i];
     const uint64_t e = list[2 * i + 1];
     const uint32_t len = (uint32_t)(e >> 40), top = (uint32_t)(sw >> 40) << 16;
-    if (threadIdx.x < kRadix) s_wc[threadIdx.x] = 0;
+    if constexpr (ABITS != 0) {
+#pragma unroll
+        for (int j = 0; j < (NC + BLOCK - 1) / BLOCK; ++j)
+            if (j * BLOCK + (int)threadIdx.x < NC) s_wc[j * BLOCK + threadIdx.x] = 0;
+    } else if (threadIdx.x < kRadix) {
+        s_wc[threadIdx.x] = 0;
+    }
     uint32_t k[ITEMS];
     {
         const __amdgpu_buffer_rsrc_t rs = bucket_rsrc(in + (sw & ((1ull << 40) - 1)), len * 2u);
@@ -3197,7 +3323,8 @@ __global__ __launch_bounds__(BLOCK) void k_local_sort_e(const uint16_t *__restri
         return;
     }
     __syncthreads();
-    sort_bucket<BLOCK, ITEMS, ATOMIC>(k, len, ndigits, dst, s_a, s_wc, koff);
+    if constexpr (ABITS != 0) sort_bucket16<BLOCK, ITEMS, ABITS>(k, len, dst, s_a, s_wc, koff);
+    else sort_bucket<BLOCK, ITEMS, ATOMIC>(k, len, ndigits, dst, s_a, s_wc, koff);
 }
 
 constexpr int cls_of(int block, int items) {
@@ -3886,6 +4013,11 @@ hipError_t launch_est_publish(const EstPlan &p, hipStream_t s) {
     return hipGetLastError();
 }
 
+#ifndef GSORT_K11E_ABITS
+#define GSORT_K11E_ABITS 0
+#endif
+constexpr int kK11eAbits = GSORT_K11E_ABITS;  // sort_bucket16's pass-A bits (0: 8 + 8 body)
+
 hipError_t launch_local_sort_e(const EstPlan &p, int cls, uint32_t first, uint32_t nlist,
                                bool publish, hipStream_t s) {
     using ull = unsigned long long;
@@ -3905,6 +4037,9 @@ hipError_t launch_local_sort_e(const EstPlan &p, int cls, uint32_t first, uint32
         if (nd == 0)                                                                           \
             launch_k(k_local_sort_e<B, I, true, true>, nlist, B, 0, s, y, p.out, l, ctr, first, \
                      nd, mail, call, ef, seq, ko);                                             \
+        else if (kK11eAbits && nd == 2)                                                        \
+            launch_k(k_local_sort_e<B, I, true, false, kK11eAbits>, nlist, B, 0, s, y, p.out, l, \
+                     ctr, first, nd, mail, call, ef, seq, ko);                                 \
         else if (p.atomic_rank)                                                                \
             launch_k(k_local_sort_e<B, I, true>, nlist, B, 0, s, y, p.out, l, ctr, first, nd,  \
                      mail, call, ef, seq, ko);                                                 \

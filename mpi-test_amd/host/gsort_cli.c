@@ -118,9 +118,22 @@ int gsort_cli_main(int argc, char **argv, int algo)
     gsort_uid uid;
     memset(&uid, 0, sizeof uid);
     if (size > 1) {
+        /* the IPC group (POSIX shm + HIP IPC handles) only spans one node: decide from the
+         * node-local rank counts, not from rank 0's GPUs against the world size -- 2 nodes x 8
+         * GPUs at -np 16 is RCCL */
+        MPI_Comm node;
+        int node_size = 1, max_node = 1;
+        MPI_Comm_split_type(MPI_COMM_WORLD, MPI_COMM_TYPE_SHARED, rank, MPI_INFO_NULL, &node);
+        MPI_Comm_size(node, &node_size);
+        MPI_Comm_free(&node);
+        MPI_Allreduce(&node_size, &max_node, 1, MPI_INT, MPI_MAX, MPI_COMM_WORLD);
+        const int one_node = max_node == size;
         if (rank == 0) {
             const char *tr = getenv("GSORT_TRANSPORT");
-            const int ipc = tr && *tr ? strcmp(tr, "ipc") == 0 : gsort_visible_devices() < size;
+            const int ipc = tr && *tr ? strcmp(tr, "ipc") == 0
+                                      : one_node && gsort_visible_devices() < size;
+            if (ipc && !one_node)
+                die("GSORT_TRANSPORT=ipc: the IPC process group needs every rank on one node");
             if (ipc) check(gsort_get_uid_ipc(size, &uid), NULL, "gsort_get_uid_ipc");
             else check(gsort_get_uid(&uid), NULL, "gsort_get_uid");
         }

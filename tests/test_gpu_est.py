@@ -318,6 +318,26 @@ def test_giant_child_sample_misjudged(ctx):
     assert np.array_equal(got, np.sort(keys))
 
 
+@pytest.mark.parametrize("extra", [0, 1], ids=["child_(n-1)/2", "child_(n+1)/2"])
+def test_giant_child_half_of_odd_n(ctx, orc, extra):
+    """odd n and a child of exactly (n - 1) / 2 keys would leave n_cold = n_child + 1
+    cold keys, overlapping the cold-key sort's source and destination.  That child is not
+    dominant (the block goes to another plan); one key more and it is (n_cold = n_child - 1)."""
+    n = (1 << 22) + 1
+    n_child = (n - 1) // 2 + extra
+    rng = np.random.default_rng(43)
+    u = orc.gen(orc.UNIFORM, 44, n)
+    keys = (u | (1 << 30)).astype(np.int32)  # cold keys: top bits far from the child's
+    pos = np.zeros(n, dtype=bool)
+    pos[:: n // 16384] = True  # every K1m sample position in the child
+    rest = np.flatnonzero(~pos)
+    pos[rng.choice(rest, n_child - int(pos.sum()), replace=False)] = True
+    keys[pos] = ((u[pos] & 0xFFFF) + (7 << 16)).astype(np.int32)
+    got, _ = _sort(ctx, keys)
+    assert np.array_equal(got, np.sort(keys))
+    assert (ctx.last_plan() == GIANT) == bool(extra), ctx.last_plan()
+
+
 def test_giant_child_off(gsort, orc):
     c = _ctx(gsort, GSORT_GIANT=0)
     try:

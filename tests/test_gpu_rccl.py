@@ -157,74 +157,6 @@ def test_rccl_self_piece_copied_by_the_product():
     assert lines and json.loads(lines[0][len("RCCL_BIG "):]) == "ok", r.stderr[-3000:]
 
 
-def _child_peer(rank, piece):
-    """Rank `rank` of a 2-process, 2-GPU RCCL group sorting 5 * 2^28 uniform keys per rank
-    (5 GiB): about half of each block, 1.25 GiB packed, goes to the peer in pieces of
-    GSORT_RCCL_MAX_MSG bytes; prints its output's fingerprint."""
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    for p in (root, os.path.join(root, "mpi-test_amd")):
-        sys.path.insert(0, p)
-    import torch
-    import gsort
-    torch.cuda.set_device(rank)
-    uid_path = os.environ["GSORT_PEER_UID"]
-    if rank == 0:
-        with open(uid_path + ".tmp", "wb") as f:
-            f.write(gsort.get_uid())
-        os.rename(uid_path + ".tmp", uid_path)
-    else:
-        import time
-        for _ in range(600):
-            if os.path.exists(uid_path):
-                break
-            time.sleep(0.1)
-    uid = open(uid_path, "rb").read()
-    ctx = gsort.Context(rank=rank, nranks=2, device=rank, uid=uid)
-    nkeys = 5 << 28
-    p = ctx.alloc(nkeys * 4)
-    ctx.generate(gsort.UNIFORM, 100 + rank, 0, nkeys, p)
-    ok = "error"
-    try:
-        # a peer message through the product's exchange: the distributed radix moves half of
-        # each block to the other rank (2 B per key packed); the output is fingerprinted
-        fin = ctx.fingerprint(p, nkeys)
-        out, m, _ = ctx.radix(p, nkeys)
-        fo = ctx.fingerprint(out, m)
-        ok = "ok" if fo["sorted"] else "unsorted"
-        print("PEER " + json.dumps({"rank": rank, "res": ok, "in_sum": fin["sum"],
-                                    "out_sum": fo["sum"], "n_out": m}), flush=True)
-    finally:
-        ctx.free(p)
-        ctx.close()
-
-
-@pytest.mark.skipif(int(os.environ.get("GSORT_TEST_GPUS", "1")) < 2,
-                    reason="needs 2 GPUs (set GSORT_TEST_GPUS=2 on a multi-GPU node)")
-@pytest.mark.parametrize("piece", [1 << 30, (1 << 30) + 256], ids=["2^30", "2^30+256"])
-def test_rccl_peer_message_piece_limit(tmp_path, piece):
-    """the 2^30-byte piece limit was measured on self-messages only.  Two ranks on
-    two GPUs exchange 2.5 GiB-key blocks (each rank sends > 2^30 bytes to its peer through the
-    product's packed exchange): with the product's 2^30-byte pieces the global output must be
-    exact; with 2^30 + 256-byte pieces this records whether peer messages share the limit (the
-    result is printed, not asserted: the multi-GPU run that first executes it decides).  On a
-    one-GPU box it is skipped; the driver's 8-GPU node can set GSORT_TEST_GPUS."""
-    env = dict(os.environ, GSORT_PEER_UID=str(tmp_path / "uid"), GSORT_RCCL_MAX_MSG=str(piece))
-    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--child-peer",
-                               str(r)], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
-                              text=True) for r in range(2)]
-    res = []
-    for pr in procs:
-        out, err = pr.communicate(timeout=600)
-        res += [json.loads(ln[5:]) for ln in out.splitlines() if ln.startswith("PEER ")]
-        assert pr.returncode == 0, err[-3000:]
-    assert len(res) == 2
-    exact = all(r["res"] == "ok" for r in res) and \
-        sum(r["in_sum"] for r in res) % (1 << 64) == sum(r["out_sum"] for r in res) % (1 << 64)
-    print(f"peer pieces of {piece} bytes: {'exact' if exact else 'WRONG'}", res)
-    if piece == 1 << 30:
-        assert exact
-
-
 def _child():
     """Every case in this process; one JSON line of {case id: "ok" | error text}."""
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -277,6 +209,3 @@ if __name__ == "__main__" and "--child" in sys.argv:
     _child()
 if __name__ == "__main__" and "--child-big" in sys.argv:
     _child_big()
-if __name__ == "__main__" and "--child-peer" in sys.argv:
-    _child_peer(int(sys.argv[sys.argv.index("--child-peer") + 1]),
-                int(os.environ.get("GSORT_RCCL_MAX_MSG", str(1 << 30))))
