@@ -1480,7 +1480,8 @@ __global__ __launch_bounds__(256) void k_tile_desc(const uint32_t *__restrict__ 
 // lim[same index as cur] (the run's region, sized from a sample); a run that would not fits
 // raises *ovf and goes to the TILE-key scratch `dump` instead (the caller then re-sorts on the
 // exact plan).  flags bit 2 (the sample found the input ineligible): do nothing.
-template <int BLOCK, int ITEMS, bool L3, bool FIN, typename OT = uint32_t, bool EST = false>
+template <int BLOCK, int ITEMS, bool L3, bool FIN, typename OT = uint32_t, bool EST = false,
+          int TILES = 2>
 __global__ __launch_bounds__(BLOCK) void k_partition_res(
     const uint32_t *__restrict__ in, OT *__restrict__ out, uint64_t n,
     const uint32_t *__restrict__ tpfx, const TileDesc *__restrict__ desc,
@@ -1501,14 +1502,15 @@ __global__ __launch_bounds__(BLOCK) void k_partition_res(
         if (EST && !L3 && ovf && *ovf) return;  // level 3 overflowed: the exact plan sorts again
         if (!L3 && (f & 1u)) { in = raw; flip = kFlip; }
     }
-    __shared__ uint32_t s_keys[2][TILE];
-    __shared__ uint32_t s_cur[2][kRadix];
+    static_assert(TILES == 1 || TILES == 2, "a tile or a pair per workgroup");
+    __shared__ uint32_t s_keys[TILES][TILE];
+    __shared__ uint32_t s_cur[TILES][kRadix];
     // each digit's run as a u32 index into out minus its LDS start (out holds < 2^32 keys): one
     // 4-B random LDS read per key on the way out instead of an 8-B pointer
-    __shared__ uint32_t s_off[2][kRadix];
-    __shared__ uint32_t s_wsum[2][kRadix / 64];
+    __shared__ uint32_t s_off[TILES][kRadix];
+    __shared__ uint32_t s_wsum[TILES][kRadix / 64];
     __shared__ uint32_t s_spare[kAggSpare];
-    __shared__ uint32_t s_ovf[2];  // EST: a run of this tile overflowed its region
+    __shared__ uint32_t s_ovf[TILES];  // EST: a run of this tile overflowed its region
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     uint32_t pr, ntile, last_len = 0;
     if (L3) {
@@ -1519,14 +1521,14 @@ __global__ __launch_bounds__(BLOCK) void k_partition_res(
         pr = xcd_tile(blockIdx.x, gridDim.x);
         ntile = tpfx[kRadix];
     }
-    if (2 * pr >= ntile) return;
-    uint32_t seg[2], len[2];
-    uint64_t t0[2];
-    bool straddle[2] = {false, false};
+    if (TILES * pr >= ntile) return;
+    uint32_t seg[TILES], len[TILES];
+    uint64_t t0[TILES];
+    bool straddle[TILES];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const uint32_t t = 2 * pr + h;
-        seg[h] = 0; len[h] = 0; t0[h] = 0;
+    for (int h = 0; h < TILES; ++h) {
+        const uint32_t t = TILES * pr + h;
+        seg[h] = 0; len[h] = 0; t0[h] = 0; straddle[h] = false;
         if (t < ntile) {
             if (L3) {
                 t0[h] = (uint64_t)t * TILE;
@@ -1540,19 +1542,22 @@ __global__ __launch_bounds__(BLOCK) void k_partition_res(
             }
         }
     }
-    if (tid < kRadix) { s_cur[0][tid] = 0; s_cur[1][tid] = 0; }
-    if (EST && tid < 2) s_ovf[tid] = 0;
-    uint32_t *cursor[2];
-    uint32_t limv[2] = {0, 0};  // EST: the region limits, loaded now (off the reservation path)
+    if (tid < kRadix)
+        for (int h = 0; h < TILES; ++h) s_cur[h][tid] = 0;
+    if (EST && tid < TILES) s_ovf[tid] = 0;
+    uint32_t *cursor[TILES];
+    uint32_t limv[TILES];  // EST: the region limits, loaded now (off the reservation path)
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const uint32_t row = (L3 ? (pr % kShards) : seg[h]) * kRadix;
+    for (int h = 0; h < TILES; ++h) {
+        limv[h] = 0;
+        // the shard of tile t is (t / 2) % 8, as K1h / K1e count it
+        const uint32_t row = (L3 ? ((TILES * pr + h) / 2 % kShards) : seg[h]) * kRadix;
         cursor[h] = cur + row;
         if (EST && tid < kRadix) limv[h] = lim ? lim[row + tid] : ~0u;
     }
-    uint32_t k[2][ITEMS], r[2][ITEMS];
+    uint32_t k[TILES][ITEMS], r[TILES][ITEMS];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < TILES; ++h) {
         if (EST && !L3 && straddle[h]) {  // a tile across pieces of bucket seg[h] (K12f)
             const TileDesc *pc = pieces + seg[h] * kShards;
             uint64_t pa[kShards];
@@ -1577,7 +1582,7 @@ __global__ __launch_bounds__(BLOCK) void k_partition_res(
     }
     if (EST && L3 && koff) {  // the offset retry: keys relative to the block's minimum
 #pragma unroll
-        for (int h = 0; h < 2; ++h)
+        for (int h = 0; h < TILES; ++h)
 #pragma unroll
             for (int i = 0; i < ITEMS; ++i) k[h][i] -= koff;
     }
@@ -1585,7 +1590,7 @@ __global__ __launch_bounds__(BLOCK) void k_partition_res(
         const uint32_t pfx = ((in[0] ^ kFlip) - koff) >> (32 - sb);
         bool bad = false;
 #pragma unroll
-        for (int h = 0; h < 2; ++h)
+        for (int h = 0; h < TILES; ++h)
 #pragma unroll
             for (int i = 0; i < ITEMS; ++i)
                 bad |= (uint32_t)(i * BLOCK) + tid < len[h] && (k[h][i] >> (32 - sb)) != pfx;
@@ -1593,33 +1598,35 @@ __global__ __launch_bounds__(BLOCK) void k_partition_res(
     }
     __syncthreads();  // s_cur zeroed
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+    for (int h = 0; h < TILES; ++h)
 #pragma unroll
         for (int i = 0; i < ITEMS; ++i)
             if ((uint32_t)(i * BLOCK) + tid < len[h])
                 r[h][i] = agg_rank(s_cur[h], (k[h][i] >> shift) & 255u, s_spare);
     __syncthreads();
-    uint32_t excl[2] = {0, 0}, pos[2] = {0, 0}, cnt[2] = {0, 0};
+    uint32_t excl[TILES], pos[TILES], cnt[TILES];
+#pragma unroll
+    for (int h = 0; h < TILES; ++h) excl[h] = pos[h] = cnt[h] = 0;
     // both tiles on one cursor row (always for K3r: one shard; for K3a when both tiles are in
     // one bucket): ONE reservation of both counts, tile 1's run right behind tile 0's, so the
     // pair writes one run of twice the length -- half the run boundaries, whose lines are
     // otherwise written partly by two workgroups (often on two XCDs)
-    const bool merge = 2 * pr + 1 < ntile && cursor[0] == cursor[1];
+    const bool merge = TILES == 2 && 2 * pr + 1 < ntile && cursor[0] == cursor[TILES - 1];
     if (tid < kRadix) {
         cnt[0] = s_cur[0][tid];
-        cnt[1] = s_cur[1][tid];
+        cnt[TILES - 1] = s_cur[TILES - 1][tid];
         if (merge) {
-            if (cnt[0] + cnt[1]) {
-                pos[0] = atomicAdd(&cursor[0][tid], cnt[0] + cnt[1]);
-                pos[1] = pos[0] + cnt[0];
+            if (cnt[0] + cnt[TILES - 1]) {
+                pos[0] = atomicAdd(&cursor[0][tid], cnt[0] + cnt[TILES - 1]);
+                pos[TILES - 1] = pos[0] + cnt[0];
             }
         } else {
 #pragma unroll
-            for (int h = 0; h < 2; ++h)
+            for (int h = 0; h < TILES; ++h)
                 if (cnt[h]) pos[h] = atomicAdd(&cursor[h][tid], cnt[h]);
         }
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
+        for (int h = 0; h < TILES; ++h) {
             const uint32_t c = cnt[h];
             uint32_t v = c;
 #pragma unroll
@@ -1634,21 +1641,21 @@ __global__ __launch_bounds__(BLOCK) void k_partition_res(
     __syncthreads();
     if (tid < kRadix) {
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
+        for (int h = 0; h < TILES; ++h) {
             for (uint32_t ww = 0; ww < w; ++ww) excl[h] += s_wsum[h][ww];
             s_cur[h][tid] = excl[h];
         }
     }
     __syncthreads();
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+    for (int h = 0; h < TILES; ++h)
 #pragma unroll
         for (int i = 0; i < ITEMS; ++i)
             if ((uint32_t)(i * BLOCK) + tid < len[h])
                 s_keys[h][s_cur[h][(k[h][i] >> shift) & 255u] + r[h][i]] = k[h][i];
     if (tid < kRadix) {
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
+        for (int h = 0; h < TILES; ++h) {
             s_off[h][tid] = (uint32_t)((L3 ? bases[tid] : bases[seg[h]]) + pos[h]) - excl[h];
             if (EST && cnt[h] && (uint64_t)pos[h] + cnt[h] > limv[h]) {
                 atomicOr(ovf, 1u);
@@ -1658,7 +1665,7 @@ __global__ __launch_bounds__(BLOCK) void k_partition_res(
     }
     __syncthreads();
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < TILES; ++h) {
         OT *o = out;
         bool to_dump = false;
         if (EST && s_ovf[h]) { o = dump; to_dump = true; }
@@ -1831,124 +1838,6 @@ __device__ __forceinline__ void sort_bucket(uint32_t (&k)[ITEMS], uint32_t len, 
                 s_a[wc[(k[i] >> shift) & 255u] + rk[i]] = k[i];
         __syncthreads();
     }
-    const __amdgpu_buffer_rsrc_t rs = bucket_rsrc(dst, len * 4u);  // stores past len dropped
-#pragma unroll
-    for (int i = 0; i < ITEMS; ++i) {
-        const uint32_t j = (uint32_t)(i * BLOCK + tid);
-        __builtin_amdgcn_raw_buffer_store_b32((s_a[j] + koff) ^ kFlip, rs, (int)(j * 4u), 0, 0);
-    }
-}
-
-// Body of K11e for two digits (the low 16 bits), split 10 + 6 instead of 8 + 8 so that the
-// second, stable pass needs no LDS atomic and no random offset read ("K11e two
-// passes as 10 + 6 bits"):
-//   pass A (bits 0 .. ABITS-1, unstable): one returning LDS atomic per key on 2^ABITS block
-//     counters, a block scan, one offset read + scatter into s_a -- as the 8-bit first pass.
-//   pass B (bits ABITS .. 15, stable, NB = 2^(16-ABITS) <= 64 digits): wave w takes the
-//     contiguous chunk [w*64*R, (w+1)*64*R) of s_a.  Per round of 64 keys the wave ballots the
-//     digit's bits: a lane's peers (lanes with its digit) give its rank (mbcnt), lane L's own
-//     index taken as a digit gives digit L's count in the round -- so lane L holds the wave's
-//     running count of digit L in a register.  The per-wave totals go through LDS once; every
-//     wave scans them itself (no second barrier), and each key fetches its digit's running
-//     offset from lane e with one ds_bpermute (crossbar, no bank conflicts).  Stable by
-//     construction (lane order = key order), whatever the LDS atomics' lane order.
-// LDS ops per key: pass A 3 random (atomic, offset, scatter); pass B 1 random (scatter) + 1
-// linear read + 1 bpermute; 1 linear read on the way out -- against 6 random + 2 linear for
-// 8 + 8 (SQ_LDS_BANK_CONFLICT: ~3.3 extra cycles per random wave-op).
-// s_c: 2^ABITS words (>= WAVES * 64), zeroed by the caller before its barrier.  The pass-A scan's
-// wave sums borrow the tail of s_a (every key is in registers then).
-template <int BLOCK, int ITEMS, int ABITS>
-__device__ __forceinline__ void sort_bucket16(uint32_t (&k)[ITEMS], uint32_t len,
-                                              uint32_t *__restrict__ dst, uint32_t *s_a,
-                                              uint32_t *s_c, uint32_t koff) {
-    constexpr int WAVES = BLOCK / 64;
-    constexpr int TILE = BLOCK * ITEMS;
-    constexpr uint32_t NA = 1u << ABITS, BB = 16 - ABITS, NB = 1u << BB;
-    constexpr int CPT = (int)NA / BLOCK;  // pass-A counters per thread in the scan
-    static_assert(NB <= 64 && CPT >= 1 && (int)NA >= WAVES * 64, "pass geometry");
-    static_assert(TILE <= 65536, "ranks fit 16 bits");
-    uint32_t *s_wsum = s_a + TILE - WAVES;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    auto lim = [&](int i) -> uint32_t {
-        return len > (uint32_t)(i * BLOCK) ? len - (uint32_t)(i * BLOCK) : 0u;
-    };
-
-    // pass A: unstable counting scatter on the low ABITS bits
-    uint32_t r[ITEMS];
-#pragma unroll
-    for (int i = 0; i < ITEMS; ++i)
-        if ((uint32_t)tid < lim(i)) r[i] = atomicAdd(&s_c[k[i] & (NA - 1)], 1u);
-    __syncthreads();
-    {
-        uint32_t c[CPT], sum = 0;
-#pragma unroll
-        for (int j = 0; j < CPT; ++j) { c[j] = s_c[tid * CPT + j]; sum += c[j]; }
-        const uint32_t incl = wave_incl_add(sum);
-        if (lane == 63) s_wsum[w] = incl;
-        __syncthreads();
-        uint32_t run = incl - sum;
-        for (int ww = 0; ww < w; ++ww) run += s_wsum[ww];
-#pragma unroll
-        for (int j = 0; j < CPT; ++j) { s_c[tid * CPT + j] = run; run += c[j]; }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < ITEMS; ++i)
-        if ((uint32_t)tid < lim(i)) s_a[s_c[k[i] & (NA - 1)] + r[i]] = k[i];
-    __syncthreads();
-
-    // pass B: stable on bits ABITS .. 15, wave-chunked
-    const uint32_t R = (len + 64 * WAVES - 1) / (64 * WAVES);
-    const uint32_t base = (uint32_t)w * 64 * R;                   // wave-uniform
-    const uint32_t wlen = len > base ? min(len - base, 64 * R) : 0u;  // keys of this chunk
-#pragma unroll
-    for (int i = 0; i < ITEMS; ++i)
-        if ((uint32_t)i < R && (uint32_t)(i * 64 + lane) < wlen) k[i] = s_a[base + i * 64 + lane];
-    uint32_t tot = 0;  // lane L: keys of digit L in this wave's chunk so far
-#pragma unroll
-    for (int i = 0; i < ITEMS; ++i) {
-        if ((uint32_t)i >= R) continue;  // wave-uniform
-        const uint32_t nv = wlen > (uint32_t)(i * 64) ? wlen - (uint32_t)(i * 64) : 0u;
-        const uint64_t vm = nv >= 64 ? ~0ull : (1ull << nv) - 1;
-        const uint32_t e = (k[i] >> ABITS) & (NB - 1);
-        uint32_t plo = (uint32_t)vm, phi = (uint32_t)(vm >> 32), qlo = plo, qhi = phi;
-#pragma unroll
-        for (int b = 0; b < (int)BB; ++b) {
-            const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int32_t)e, b, 1);
-            const uint32_t lm = (uint32_t)__builtin_amdgcn_sbfe(lane, b, 1);
-            uint64_t bal;
-            asm("v_cmp_ne_u32_e64 %0, 0, %1" : "=s"(bal) : "v"(m));
-            plo = __builtin_amdgcn_bitop3_b32(plo, (uint32_t)bal, m, 0x90);
-            phi = __builtin_amdgcn_bitop3_b32(phi, (uint32_t)(bal >> 32), m, 0x90);
-            qlo = __builtin_amdgcn_bitop3_b32(qlo, (uint32_t)bal, lm, 0x90);
-            qhi = __builtin_amdgcn_bitop3_b32(qhi, (uint32_t)(bal >> 32), lm, 0x90);
-        }
-        const uint32_t c = (uint32_t)(__popc(qlo) + __popc(qhi));  // digit `lane` in this round
-        r[i] = __builtin_amdgcn_mbcnt_hi(phi, __builtin_amdgcn_mbcnt_lo(plo, 0u)) | (c << 16);
-        tot += c;
-    }
-    s_c[w * 64 + lane] = tot;
-    __syncthreads();  // every chunk read of s_a is done, the wave totals are visible
-    uint32_t cur;
-    {
-        uint32_t all = 0, before = 0;
-#pragma unroll
-        for (int ww = 0; ww < WAVES; ++ww) {
-            const uint32_t v = s_c[ww * 64 + lane];
-            all += v;
-            before += ww < w ? v : 0u;
-        }
-        cur = wave_incl_add(all) - all + before;  // digit `lane`'s first slot for this wave
-    }
-#pragma unroll
-    for (int i = 0; i < ITEMS; ++i) {
-        if ((uint32_t)i >= R) continue;
-        const uint32_t e = (k[i] >> ABITS) & (NB - 1);
-        const uint32_t off = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(e << 2), (int)cur);
-        if ((uint32_t)(i * 64 + lane) < wlen) s_a[off + (r[i] & 0xffffu)] = k[i];
-        cur += r[i] >> 16;
-    }
-    __syncthreads();
     const __amdgpu_buffer_rsrc_t rs = bucket_rsrc(dst, len * 4u);  // stores past len dropped
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
@@ -3276,7 +3165,7 @@ __global__ __launch_bounds__(64) void k_publish_lists(unsigned long long *mail,
 // block 0 first hands K12g's counters and status to the host (publish_lists), off the kernels'
 // critical path.
 // The child's keys come from Y as their low 16 bits; the entry's src word carries the top 16.
-template <int BLOCK, int ITEMS, bool ATOMIC, bool COPY = false, int ABITS = 0>
+template <int BLOCK, int ITEMS, bool ATOMIC, bool COPY = false>
 __global__ __launch_bounds__(BLOCK) void k_local_sort_e(const uint16_t *__restrict__ in,
                                                         uint32_t *__restrict__ out,
                                                         const unsigned long long *__restrict__ list,
@@ -3288,23 +3177,15 @@ __global__ __launch_bounds__(BLOCK) void k_local_sort_e(const uint16_t *__restri
                                                         unsigned long long seq, uint32_t koff) {
     constexpr int WAVES = BLOCK / 64;
     constexpr int TILE = BLOCK * ITEMS;
-    // ABITS != 0: the 16-bit body (sort_bucket16, ndigits == 2) and its 2^ABITS counters
-    constexpr int NC = ABITS ? (1 << ABITS) : WAVES * kRadix;
     __shared__ uint32_t s_a[TILE];
-    __shared__ uint32_t s_wc[NC];
+    __shared__ uint32_t s_wc[WAVES * kRadix];
     if (mail && blockIdx.x == 0) publish_lists(mail, ctr_all, eflag, seq);  // K12g is done
     const uint32_t i = first + blockIdx.x;
     if (i >= (uint32_t)*ctr) return;
     const uint64_t sw = list[2 * i];
     const uint64_t e = list[2 * i + 1];
     const uint32_t len = (uint32_t)(e >> 40), top = (uint32_t)(sw >> 40) << 16;
-    if constexpr (ABITS != 0) {
-#pragma unroll
-        for (int j = 0; j < (NC + BLOCK - 1) / BLOCK; ++j)
-            if (j * BLOCK + (int)threadIdx.x < NC) s_wc[j * BLOCK + threadIdx.x] = 0;
-    } else if (threadIdx.x < kRadix) {
-        s_wc[threadIdx.x] = 0;
-    }
+    if (threadIdx.x < kRadix) s_wc[threadIdx.x] = 0;
     uint32_t k[ITEMS];
     {
         const __amdgpu_buffer_rsrc_t rs = bucket_rsrc(in + (sw & ((1ull << 40) - 1)), len * 2u);
@@ -3323,8 +3204,7 @@ __global__ __launch_bounds__(BLOCK) void k_local_sort_e(const uint16_t *__restri
         return;
     }
     __syncthreads();
-    if constexpr (ABITS != 0) sort_bucket16<BLOCK, ITEMS, ABITS>(k, len, dst, s_a, s_wc, koff);
-    else sort_bucket<BLOCK, ITEMS, ATOMIC>(k, len, ndigits, dst, s_a, s_wc, koff);
+    sort_bucket<BLOCK, ITEMS, ATOMIC>(k, len, ndigits, dst, s_a, s_wc, koff);
 }
 
 constexpr int cls_of(int block, int items) {
@@ -3964,12 +3844,19 @@ hipError_t launch_est_front(const EstPlan &p, hipStream_t s) {
     return hipGetLastError();
 }
 
+#ifndef GSORT_K3_TILES
+#define GSORT_K3_TILES 2
+#endif
+// the sampled plan's K3r / K3a: a tile pair per 1024-thread workgroup, or one tile per 512
+constexpr int kEstTiles = GSORT_K3_TILES;
+constexpr int kEstPartBlock = kEstTiles == 2 ? kPartBlock : kPartBlock / 2;
+
 hipError_t launch_est_level3(const EstPlan &p, hipStream_t s) {
     using ull = unsigned long long;
-    constexpr int B = kPartBlock, I = kSweepTile / kPartBlock;
-    const uint64_t pairs = (sweep_tiles(p.n) + 1) / 2;
+    constexpr int B = kEstPartBlock, I = kSweepTile / B;
+    const uint64_t pairs = (sweep_tiles(p.n) + kEstTiles - 1) / kEstTiles;
     if (!p.flip_in) return hipErrorInvalidValue;  // K3r loads the int32 input
-    launch_k(k_partition_res<B, I, true, true, uint32_t, true>, (unsigned)pairs, B, 0, s,
+    launch_k(k_partition_res<B, I, true, true, uint32_t, true, kEstTiles>, (unsigned)pairs, B, 0, s,
              p.in, p.x, p.n, (const uint32_t *)nullptr, (const TileDesc *)nullptr,
              reinterpret_cast<const ull *>(p.bases3), p.cur3, (const uint32_t *)p.eflag,
              (const uint32_t *)nullptr, (const uint32_t *)p.lim3, p.eflag + 1, p.dump,
@@ -3980,7 +3867,7 @@ hipError_t launch_est_level3(const EstPlan &p, hipStream_t s) {
 
 hipError_t launch_est_level2(const EstPlan &p, hipStream_t s) {
     using ull = unsigned long long;
-    constexpr int B = kPartBlock, I = kSweepTile / kPartBlock;
+    constexpr int B = kEstPartBlock, I = kSweepTile / B;
     const uint32_t max_tiles = (uint32_t)est_max_tiles(p.n);
     TileDesc *desc = static_cast<TileDesc *>(p.tdesc);
     TileDesc *pieces = desc + max_tiles;
@@ -3988,7 +3875,8 @@ hipError_t launch_est_level2(const EstPlan &p, hipStream_t s) {
              (const uint32_t *)p.init3, (const uint32_t *)p.lim3,
              reinterpret_cast<const ull *>(p.bases3), max_tiles, (const uint32_t *)p.eflag, p.tp,
              desc, pieces);
-    launch_k(k_partition_res<B, I, false, false, uint16_t, true>, (max_tiles + 1) / 2, B, 0, s,
+    launch_k(k_partition_res<B, I, false, false, uint16_t, true, kEstTiles>,
+             (max_tiles + kEstTiles - 1) / kEstTiles, B, 0, s,
              (const uint32_t *)p.x, p.y, p.n, (const uint32_t *)p.tp, (const TileDesc *)desc,
              reinterpret_cast<const ull *>(p.bases2), p.cur2, (const uint32_t *)p.eflag,
              (const uint32_t *)nullptr, (const uint32_t *)p.lim2, p.eflag + 1,
@@ -4013,11 +3901,6 @@ hipError_t launch_est_publish(const EstPlan &p, hipStream_t s) {
     return hipGetLastError();
 }
 
-#ifndef GSORT_K11E_ABITS
-#define GSORT_K11E_ABITS 0
-#endif
-constexpr int kK11eAbits = GSORT_K11E_ABITS;  // sort_bucket16's pass-A bits (0: 8 + 8 body)
-
 hipError_t launch_local_sort_e(const EstPlan &p, int cls, uint32_t first, uint32_t nlist,
                                bool publish, hipStream_t s) {
     using ull = unsigned long long;
@@ -4037,9 +3920,6 @@ hipError_t launch_local_sort_e(const EstPlan &p, int cls, uint32_t first, uint32
         if (nd == 0)                                                                           \
             launch_k(k_local_sort_e<B, I, true, true>, nlist, B, 0, s, y, p.out, l, ctr, first, \
                      nd, mail, call, ef, seq, ko);                                             \
-        else if (kK11eAbits && nd == 2)                                                        \
-            launch_k(k_local_sort_e<B, I, true, false, kK11eAbits>, nlist, B, 0, s, y, p.out, l, \
-                     ctr, first, nd, mail, call, ef, seq, ko);                                 \
         else if (p.atomic_rank)                                                                \
             launch_k(k_local_sort_e<B, I, true>, nlist, B, 0, s, y, p.out, l, ctr, first, nd,  \
                      mail, call, ef, seq, ko);                                                 \
