@@ -324,7 +324,15 @@ Comm *make_group_comm(GroupState *g, int rank) { return new GroupComm(g, rank); 
 // a peer grew its buffer), synchronises and meets them again (so no rank overwrites a staging
 // buffer a peer is still reading) -- GroupComm's protocol across processes.  (Exporting and
 // opening every send buffer per collective instead failed intermittently on MI355X / ROCm 7.2:
-// hipIpcOpenMemHandle "invalid device pointer" on buffers exported many times.)  The uid carries
+// hipIpcOpenMemHandle "invalid device pointer".  The cause, isolated with
+// tools/experiments/ipc_group.hip (profiles/r04_ipc_export_patterns.txt): an exported
+// allocation that is FREED and replaced by a new one (the context's scratch buffers grow by
+// free + malloc) -- importers of the replacement then read wrong bytes (P = 4: 225 of 768
+// reads) or the runtime prints "IPC Attach: Invalid IPC handle!" and the group hangs, while
+// re-exporting / re-opening one live allocation every round (P = 4, 8: 13 600 reads) and
+// growing into new allocations that are never freed (768 reads) are exact.  So a staging
+// buffer, once exported, is never freed while the group lives -- a grown one is kept in stages_
+// until the destructor, whatever it costs in memory.)  The uid carries
 // the control block's name; rank 0 creates it (gsort_get_uid_ipc) and unlinks it once every
 // rank has attached.
 // ---------------------------------------------------------------------------------------
@@ -447,7 +455,9 @@ class IpcComm : public Comm {
                 if (p) (void)hipFree(p);
                 return st;
             }
-            stages_.push_back(p);  // the old one may still be open in a peer
+            // never freed while the group lives: freeing an exported allocation and exporting
+            // its replacement is what broke the peers' imports (see the header comment)
+            stages_.push_back(p);
             stage_ = p;
             cap_ = cap;
             me.gen = ++gen_;

@@ -1868,6 +1868,15 @@ __global__ __launch_bounds__(BLOCK) void k_local_sort(const uint32_t *__restrict
                                       s_wc);
 }
 
+// Received runs are addressed as recv + offset where a rank's own piece, read in place from its
+// send buffer, carries the offset of that buffer from recv (mod 2^64, made on the host from
+// integer addresses): the address is formed as an integer, not by pointer arithmetic
+// across allocations.
+template <typename T>
+__device__ __forceinline__ const T *run_ptr(const T *recv, uint64_t off) {
+    return reinterpret_cast<const T *>(reinterpret_cast<uintptr_t>(recv) + off * sizeof(T));
+}
+
 // K11g (receive side of the distributed sorts): bucket h of the 2^16 top-16-bit buckets of
 // the P received sorted runs.  Its keys are the P pieces recv[roff[p] + pos[p][h] ..
 // roff[p] + pos[p][h+1]) (int32); they are gathered, sorted on the low 16 bits in LDS and
@@ -1935,7 +1944,7 @@ __global__ __launch_bounds__(BLOCK) void k_gather_sort(const T *__restrict__ rec
         if (P == 1) {  // one piece: a scalar base (no per-key piece lookup)
             const uint64_t d0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(s_delta[0] >> 32)) << 32) |
                                 (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)s_delta[0]);
-            const T *src = recv + d0;
+            const T *src = run_ptr(recv, d0);
 #pragma unroll
             for (int i = 0; i < ITEMS; ++i) v[i] = src[min((uint32_t)(i * BLOCK + tid), last)];
         } else {
@@ -1945,7 +1954,7 @@ __global__ __launch_bounds__(BLOCK) void k_gather_sort(const T *__restrict__ rec
                 uint32_t q = 0;
 #pragma unroll
                 for (int b = 1; b < kGatherDirectP; ++b) q += j >= cum[b] ? 1u : 0u;
-                v[i] = recv[s_delta[q] + j];
+                v[i] = *run_ptr(recv, s_delta[q] + j);
             }
         }
 #pragma unroll
@@ -1955,7 +1964,7 @@ __global__ __launch_bounds__(BLOCK) void k_gather_sort(const T *__restrict__ rec
         // take the keys block-strided
 #pragma unroll 1
         for (int p = 0; p < P; ++p) {
-            const T *src = recv + s_src[p];
+            const T *src = run_ptr(recv, s_src[p]);
             const uint32_t c0 = s_cum[p], c1 = s_cum[p + 1];
 #pragma unroll 1
             for (uint32_t b = c0; b < c1; b += 8 * BLOCK) {
@@ -1992,7 +2001,7 @@ __global__ __launch_bounds__(256) void k_run_bounds(const int32_t *__restrict__ 
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= (uint64_t)P * (kBuckets16 + 1)) return;
     const uint32_t p = (uint32_t)(i / (kBuckets16 + 1)), h = (uint32_t)(i % (kBuckets16 + 1));
-    const int32_t *a = recv + roff[p];
+    const int32_t *a = run_ptr(recv, roff[p]);
     const uint64_t x = (uint64_t)h << 16;
     uint64_t lo = 0, hi = rlen[p];
     while (lo < hi) {
@@ -2060,7 +2069,7 @@ __global__ __launch_bounds__(1024) void k_hist_expand(const T *__restrict__ recv
         __syncthreads();
 #pragma unroll 1
         for (int p = 0; p < P; ++p) {
-            const T *src = recv + s_src[p];
+            const T *src = run_ptr(recv, s_src[p]);
             const uint32_t np = s_len[p];
 #pragma unroll 1
             for (uint32_t j0 = 0; j0 < np; j0 += 8 * NT) {
@@ -2225,7 +2234,7 @@ __device__ __forceinline__ void cx_fill_table(CxTable<T> &t, const T *recv,
         src = roff[lane] + a;
     }
     const uint32_t n = (uint32_t)(b - a);
-    const uint32_t mis = (uint32_t)((reinterpret_cast<uintptr_t>(recv + src) / sizeof(T)) & (E - 1));
+    const uint32_t mis = (uint32_t)((reinterpret_cast<uintptr_t>(run_ptr(recv, src)) / sizeof(T)) & (E - 1));
     const uint32_t hd = min(mis ? E - mis : 0u, n);
     const uint32_t nv = (n - hd) / E;
     const uint32_t x = wave_incl_add(nv);
@@ -2258,7 +2267,7 @@ template <typename T>
 __device__ __forceinline__ const uint4 *cx_vec(const T *recv, const CxTable<T> &t, int P,
                                                uint32_t g) {
     const uint32_t p = cx_piece(t, P, g);
-    return reinterpret_cast<const uint4 *>(recv + t.src[p] + t.head[p]) + (g - t.cumv[p]);
+    return reinterpret_cast<const uint4 *>(run_ptr(recv, t.src[p] + t.head[p])) + (g - t.cumv[p]);
 }
 
 template <bool WRAP, typename T>
@@ -2299,7 +2308,7 @@ __device__ __forceinline__ void cx_count_bucket(const T *recv, const CxTable<T> 
         uint32_t j = ~0u;
         if (k < E) { if (k < hd) j = k; }
         else if (body + (k - E) < n) j = body + (k - E);
-        if (j != ~0u) cx_count<WRAP>(s_h, (uint32_t)recv[t.src[p] + j] & 0xFFFFu, s_nw, s_wb, s_wd);
+        if (j != ~0u) cx_count<WRAP>(s_h, (uint32_t)*run_ptr(recv, t.src[p] + j) & 0xFFFFu, s_nw, s_wb, s_wd);
     }
 }
 
@@ -2520,7 +2529,7 @@ __global__ __launch_bounds__(256) void k_gather_copy(const T *__restrict__ recv,
     for (int p = 0; p < P; ++p) {
         const uint64_t a = pos[(uint64_t)p * (kBuckets16 + 1) + h];
         const uint64_t b = pos[(uint64_t)p * (kBuckets16 + 1) + h + 1];
-        const T *src = recv + roff[p] + a;
+        const T *src = run_ptr(recv, roff[p] + a);
         for (uint64_t j = threadIdx.x; j < b - a; j += 256) dst[j] = recv_key(src[j], h);
         dst += b - a;
     }
@@ -3844,12 +3853,10 @@ hipError_t launch_est_front(const EstPlan &p, hipStream_t s) {
     return hipGetLastError();
 }
 
-#ifndef GSORT_K3_TILES
-#define GSORT_K3_TILES 2
-#endif
-// the sampled plan's K3r / K3a: a tile pair per 1024-thread workgroup, or one tile per 512
-constexpr int kEstTiles = GSORT_K3_TILES;
-constexpr int kEstPartBlock = kEstTiles == 2 ? kPartBlock : kPartBlock / 2;
+// the sampled plan's K3r / K3a: a tile pair per 1024-thread workgroup (one tile per 512-thread
+// workgroup measured slower overall: profiles/r04_ab_k3_pipe_and_tiles.txt)
+constexpr int kEstTiles = 2;
+constexpr int kEstPartBlock = kPartBlock;
 
 hipError_t launch_est_level3(const EstPlan &p, hipStream_t s) {
     using ull = unsigned long long;

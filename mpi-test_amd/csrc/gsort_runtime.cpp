@@ -1428,6 +1428,14 @@ gsort_status local_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *
 // bucket sizes (65536) + starts (65537) + row-scan partials (64 x 64), u64
 constexpr size_t kBsizeBytes = ((size_t)2 * kBuckets16 + 1 + 65 * 64) * 8;
 
+// (a - b) / sizeof(T) for pointers into different allocations, as a u64 (two's complement for
+// a negative offset): integer arithmetic, never a pointer difference across allocations
+template <typename T>
+uint64_t elem_offset(const T *a, const T *b) {
+    const int64_t d = (int64_t)(reinterpret_cast<uintptr_t>(a) - reinterpret_cast<uintptr_t>(b));
+    return (uint64_t)(d / (int64_t)sizeof(T));
+}
+
 // self (int32 runs only): run `self_rank` was not received -- it lies at self_src (the
 // sender's sorted block), and the kernels read it there through a run offset taken relative to
 // recv (mod 2^64); the MSD fallback, which needs the runs back to back, copies it in first.
@@ -1492,7 +1500,7 @@ gsort_status recv_sort(gsort_ctx *c, const void *recv, bool packed16,
     uint64_t off = 0;
     for (int p = 0; p < P; ++p) { h_r[p] = off; h_r[P + p] = rlen[p]; off += rlen[p]; }
     if (self_src)
-        h_r[self_rank] = (uint64_t)(self_src - static_cast<const int32_t *>(recv));
+        h_r[self_rank] = elem_offset(self_src, static_cast<const int32_t *>(recv));
     HIP_TRY(c, hipMemcpyAsync(d_r, h_r, (size_t)2 * P * 8, hipMemcpyHostToDevice, c->stream));
     uint64_t *pos = reinterpret_cast<uint64_t *>(c->m_rpos.p);
     uint64_t *bsize = reinterpret_cast<uint64_t *>(c->m_bsize.p), *bstart = bsize + kBuckets16;
@@ -1881,7 +1889,8 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
     // (no stream sync for h_r: nothing has copied from OFF_PLAN since allgather_u64's sync --
     // the select stages through host vectors -- and a sync here idled the GPU ~40 us)
     for (int p = 0; p < P; ++p) { h_r[p] = roffs[p]; h_r[P + p] = recv[p]; }
-    if (!self_moved) h_r[me] = (uint64_t)((pack + cut[me]) - rbuf);  // the self piece, in place
+    if (!self_moved)  // the self piece, in place: its offset from rbuf in keys, from integer
+        h_r[me] = elem_offset(pack + cut[me], rbuf);  // addresses (mod 2^64, run_ptr)
     HIP_TRY(c, hipMemcpyAsync(d_r, h_r, (size_t)2 * P * 8, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(c, hipMemsetAsync(c->d_small + OFF_CTR, 0, kCtrBytes, c->stream));
     // the runs' bucket bounds and the bucket starts in one row scan of P + 1 rows (the last

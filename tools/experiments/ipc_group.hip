@@ -7,6 +7,9 @@
 //   reexport  one send allocation per rank, re-exported every round (the first IpcComm)
 //   grow      the send allocation is freed and allocated larger every 8th round, then
 //             re-exported (ensure() growing a scratch buffer between collectives)
+//   fresh     freed and allocated again at the same size every 8th round, re-exported
+//   keepgrow  a larger allocation every 8th round, the old one kept (never freed while the
+//             group lives: today's IpcComm staging), re-exported
 //   once      one allocation exported once, every peer opens it once and keeps it (today's)
 // usage: ipc_group.bin P mode [rounds]
 #include <hip/hip_runtime.h>
@@ -54,15 +57,17 @@ static void rank_main(Shared *s, int P, int me, const char *mode, int rounds) {
     size_t cap = size_t(4) << 20;
     char *buf = nullptr;
     hipMalloc((void **)&buf, cap);
-    std::vector<void *> open_peer(P, nullptr);
+    std::vector<void *> open_peer(P, nullptr), kept;
     void *dst = nullptr;
     hipMalloc(&dst, kChunk);
     std::vector<uint32_t> host(kChunk / 4);
     const bool once = !strcmp(mode, "once");
     for (int it = 0; it < rounds; ++it) {
-        if (!strcmp(mode, "grow") && it % 8 == 7) {
-            hipFree(buf);
-            cap += size_t(1) << 20;
+        if (it % 8 == 7 && (!strcmp(mode, "grow") || !strcmp(mode, "fresh") ||
+                            !strcmp(mode, "keepgrow"))) {
+            if (!strcmp(mode, "keepgrow")) kept.push_back(buf);
+            else hipFree(buf);
+            if (strcmp(mode, "fresh")) cap += size_t(1) << 20;
             hipMalloc((void **)&buf, cap);
         }
         const uint64_t off = (uint64_t)((it * 4096 + me * 65536) % (cap - kChunk)) & ~4095ull;
@@ -110,6 +115,7 @@ static void rank_main(Shared *s, int P, int me, const char *mode, int rounds) {
         if (open_peer[q]) hipIpcCloseMemHandle(open_peer[q]);
     barrier(s, P);
     hipFree(buf);
+    for (void *k : kept) hipFree(k);
     hipFree(dst);
 }
 
