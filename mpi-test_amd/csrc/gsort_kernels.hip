@@ -3216,8 +3216,14 @@ __global__ __launch_bounds__(BLOCK) void k_local_sort_e(const uint16_t *__restri
     sort_bucket<BLOCK, ITEMS, ATOMIC>(k, len, ndigits, dst, s_a, s_wc, koff);
 }
 
+#ifndef GSORT_C3_BLOCK
+#define GSORT_C3_BLOCK 512
+#endif
+// class 3 (16 384 keys): 512 threads x 32 keys, or 1024 x 16 (A/B: GSORT_C3_BLOCK=1024)
+constexpr int kC3Block = GSORT_C3_BLOCK, kC3Items = 16384 / kC3Block;
+
 constexpr int cls_of(int block, int items) {
-    return block == 256 ? 1 : block == 1024 ? 4 : items == 18 ? 2 : 3;
+    return block * items == 16384 ? 3 : block == 256 ? 1 : block == 1024 ? 4 : 2;
 }
 
 unsigned grid_for(uint64_t n, unsigned block, unsigned cap) {
@@ -3604,7 +3610,7 @@ hipError_t launch_local_sort(const uint32_t *in, uint32_t *out, const uint64_t *
     switch (cls) {
         case 1: GSORT_K11(256, 18); break;
         case 2: GSORT_K11(512, 18); break;
-        case 3: GSORT_K11(512, 32); break;
+        case 3: GSORT_K11(kC3Block, kC3Items); break;
         default: GSORT_K11(1024, 32); break;
     }
 #undef GSORT_K11
@@ -3698,7 +3704,7 @@ hipError_t launch_gather_sort(const void *recv, bool packed16, const uint64_t *p
     switch (cls) {
         case 1: if (atomic_rank) GSORT_K11G(256, 18, true); else GSORT_K11G(256, 18, false); break;
         case 2: if (atomic_rank) GSORT_K11G(512, 18, true); else GSORT_K11G(512, 18, false); break;
-        case 3: if (atomic_rank) GSORT_K11G(512, 32, true); else GSORT_K11G(512, 32, false); break;
+        case 3: if (atomic_rank) GSORT_K11G(kC3Block, kC3Items, true); else GSORT_K11G(kC3Block, kC3Items, false); break;
         default: if (atomic_rank) GSORT_K11G(1024, 32, true); else GSORT_K11G(1024, 32, false); break;
     }
 #undef GSORT_K11G
@@ -3937,7 +3943,7 @@ hipError_t launch_local_sort_e(const EstPlan &p, int cls, uint32_t first, uint32
     switch (cls) {
         case 1: GSORT_K11E(256, 18); break;
         case 2: GSORT_K11E(512, 18); break;
-        case 3: GSORT_K11E(512, 32); break;
+        case 3: GSORT_K11E(kC3Block, kC3Items); break;
         default: GSORT_K11E(1024, 32); break;
     }
 #undef GSORT_K11E
