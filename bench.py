@@ -439,6 +439,26 @@ def drop_in_e2e(ctx, fn, d_in, n, reps=3):
                     "median of 3; not the headline value"}
 
 
+def verify_rows(rows, n_local, algo):
+    """N > 1 output check from every rank's row [sum_in, sum_out, xor_in, xor_out, sorted, n_out,
+    first, last] (64-bit figures as int64 bit patterns): the multiset of all outputs (sum and
+    xor of mix64(key)) equals that of all inputs, every output is sorted, rank q's last key <=
+    rank q+1's first (a misrouted exchange that keeps the multiset fails here), and the sizes
+    add up (radix: rank q holds exactly its n_local global positions)."""
+    m64 = (1 << 64) - 1
+    sum_in = sum(r[0] for r in rows) & m64
+    sum_out = sum(r[1] for r in rows) & m64
+    x_in = x_out = 0
+    for r in rows:
+        x_in ^= r[2] & m64
+        x_out ^= r[3] & m64
+    full = [r for r in rows if r[5]]
+    return bool(all(r[4] for r in rows) and sum_in == sum_out and x_in == x_out
+                and sum(r[5] for r in rows) == n_local * len(rows)
+                and all(x[7] <= y[6] for x, y in zip(full, full[1:]))
+                and (algo != "radix" or all(r[5] == n_local for r in rows)))
+
+
 def main():
     # stdout carries the one JSON line only: native libraries (RCCL prints a version banner
     # at communicator init) write to fd 1, so point it at stderr and keep the real stdout
@@ -529,19 +549,7 @@ def main():
                              int(fp["sorted"]), n_out, fp["first"], fp["last"]], dtype=torch.int64)
         rows = [torch.zeros_like(mine) for _ in range(world)]
         dist.all_gather(rows, mine)
-        rows = [[int(x) for x in r.tolist()] for r in rows]
-        m64 = (1 << 64) - 1
-        sum_in = sum(r[0] for r in rows) & m64
-        sum_out = sum(r[1] for r in rows) & m64
-        x_in = x_out = 0
-        for r in rows:
-            x_in ^= r[2] & m64
-            x_out ^= r[3] & m64
-        full = [r for r in rows if r[5]]
-        ok = (all(r[4] for r in rows) and sum_in == sum_out and x_in == x_out
-              and sum(r[5] for r in rows) == n_local * world
-              and all(x[7] <= y[6] for x, y in zip(full, full[1:]))
-              and (a.algo != "radix" or all(r[5] == n_local for r in rows)))
+        ok = verify_rows([[int(x) for x in r.tolist()] for r in rows], n_local, a.algo)
     else:
         ok = ok and fp["sum"] == fin["sum"] and fp["xor"] == fin["xor"] and n_out == n_local
 

@@ -1776,9 +1776,24 @@ __device__ __forceinline__ void sort_bucket(uint32_t (&k)[ITEMS], uint32_t len, 
     // digit 0: unstable counting sort into s_a
     {
         uint32_t r[ITEMS];
+        // A wave whose threads each hold keys of ONE digit 0 (runs of consecutive keys: thread t
+        // holds keys i * BLOCK + t, so sorted or reversed input gives every thread a constant low
+        // byte) would issue ITEMS back-to-back atomics on the same 64 addresses, each waiting for
+        // the one before; such a thread adds its count with one atomic instead.
+        bool one = true;
+        const uint32_t d0 = k[0] & 255u;
 #pragma unroll
-        for (int i = 0; i < ITEMS; ++i)
-            if ((uint32_t)tid < lim(i)) r[i] = atomicAdd(&cnt[k[i] & 255u], 1u);
+        for (int i = 1; i < ITEMS; ++i) one &= (uint32_t)tid >= lim(i) || (k[i] & 255u) == d0;
+        if (__ballot(one) == ~0ull) {
+            const uint32_t nv = len > (uint32_t)tid ? min((uint32_t)ITEMS, (len - tid + BLOCK - 1) / BLOCK) : 0u;
+            const uint32_t r0 = nv ? atomicAdd(&cnt[d0], nv) : 0u;
+#pragma unroll
+            for (int i = 0; i < ITEMS; ++i) r[i] = r0 + i;
+        } else {
+#pragma unroll
+            for (int i = 0; i < ITEMS; ++i)
+                if ((uint32_t)tid < lim(i)) r[i] = atomicAdd(&cnt[k[i] & 255u], 1u);
+        }
         __syncthreads();
         uint32_t excl = 0;
         if (tid < kRadix) excl = block_scan(cnt[tid]);
@@ -2868,8 +2883,8 @@ __device__ __forceinline__ uint64_t est_cap(uint32_t cnt, double scale, double s
 // zeroes the nzero work-list counters at zero and sets the last eligibility bit; block 0 of
 // K3r then hands the eligibility word and the number of children with samples to the host
 // (publish_elig).
-// Ineligible (eflag bit 2): a child capacity past kLocalMax (K11 could not take it in one
-// pass), a u8 wrap in K1e, every sample in one level-3 bucket (level 3 would copy; the exact
+// Ineligible (eflag bit 2): a child estimate + 4 sigma past kLocalMax (K11 could not take it
+// in one pass; capacities are clamped to kLocalMax), a u8 wrap in K1e, every sample in one level-3 bucket (level 3 would copy; the exact
 // plan skips that level), or X / Y outgrowing their buffers (capx / capy keys).
 __global__ __launch_bounds__(kRadix) void k_est_plan(
     const uint32_t *__restrict__ part8, const uint32_t *__restrict__ part3,
@@ -2947,7 +2962,12 @@ __global__ __launch_bounds__(kRadix) void k_est_plan(
     const uint32_t m = s_m;
     const double scale = m ? (double)n / (double)m : 0.0;
     const uint64_t cap = est_cap(cnt, scale, slack);
-    if (cap > kLocalMax) s_bad = 1;
+    // eligible while the estimate + 4 sigma fits one K11 pass; the region is the 6-sigma
+    // capacity clamped to kLocalMax (a child that outgrows it overflows and the exact plan
+    // sorts again).  A peaked block (Gaussian keys after the offset retry) has children of
+    // ~27K keys that the 6-sigma rule alone refused.
+    if ((double)cnt * scale + 4.0 * sqrt((double)cnt + 1.0) * scale + 64.0 > (double)kLocalMax)
+        s_bad = 1;
     uint32_t wmax = cnt;  // the largest child's samples (the runtime's retry), per block
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) wmax = max(wmax, (uint32_t)__shfl_xor((int)wmax, o));

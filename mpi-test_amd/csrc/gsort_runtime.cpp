@@ -1306,9 +1306,11 @@ gsort_status msd_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *ou
         // and -- when the first sample's child counts are known (no u8 counter wrapped) -- the
         // largest one now (~64 keys per sample) split 2^shift ways stays below 5/8 of it.  The
         // prefix retry costs a failed sample when wrong; the offset retry also a read pass, so
-        // it needs known counts (no u8 counter wrapped) and a fit after the shift -- e.g.
-        // Gaussian keys pass it (profiles/r02_v18_dist_probe.txt, plan 3), Zipf keys, whose
-        // densest child holds ~29 % of the block, do not.
+        // it needs known counts (no u8 counter wrapped) and a fit after the shift, or -- counts
+        // wrapped, i.e. a peaked block -- a span of at most 24 bits (>= 8 shared): Gaussian keys
+        // (the first sample wraps on their peak; after the offset their children hold <= ~27K
+        // keys at 2^28, sigma 1e6) pass it, Zipf keys, whose densest child holds ~29 % of the
+        // block, do not.
         const bool known = r.maxc != 0xffffffffu;
         auto fits = [&](int lead) {
             const int sb = std::min(lead, 16);
@@ -1321,7 +1323,7 @@ gsort_status msd_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *ou
             const int slead = span_lead(r.lo, r.hi);
             if (lead >= 3 && lead < 32 && fits(lead)) {
                 ST_TRY(msd_sort_est(c, in, n, out, stats, &ok, std::min(lead, 16)));
-            } else if (slead == 32 || (known && slead >= 4 && fits(slead - 1))) {
+            } else if (slead == 32 || ((known || slead >= 8) && slead >= 4 && fits(slead - 1))) {
                 // (the samples' span, one bit of margin: the block's may be wider)
                 ST_TRY(minmax());
                 const uint32_t lo = mlo, hi = mhi;
