@@ -325,6 +325,8 @@ hipError_t launch_est_classify(const EstPlan &p, hipStream_t s);  // K12g
 hipError_t launch_local_sort_e(const EstPlan &p, int cls, uint32_t first, uint32_t nlist,
                                bool publish, hipStream_t s);
 hipError_t launch_est_publish(const EstPlan &p, hipStream_t s);
+// K18c over K12g's list 0: the children past kLocalMax keys (one-read counting sort from Y)
+hipError_t launch_est_oversized(const EstPlan &p, uint32_t nlist, int ncu, hipStream_t s);
 // ---- one dominant 16-bit child (gsort_kernels.hip, "giant child") -----------
 // K1m: res[0] = the most frequent top-16-bit child (ordered u32) of min(n, 16384) evenly
 // strided keys, res[1] = its sample count, res[2] = the samples (u64 each).

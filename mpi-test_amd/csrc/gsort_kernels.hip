@@ -1482,7 +1482,7 @@ __global__ __launch_bounds__(256) void k_tile_desc(const uint32_t *__restrict__ 
 // exact plan).  flags bit 2 (the sample found the input ineligible): do nothing.
 template <int BLOCK, int ITEMS, bool L3, bool FIN, typename OT = uint32_t, bool EST = false,
           int TILES = 2>
-__global__ __launch_bounds__(BLOCK) void k_partition_res(
+__global__ __launch_bounds__(BLOCK, TILES == 1 ? 8 : 1) void k_partition_res(
     const uint32_t *__restrict__ in, OT *__restrict__ out, uint64_t n,
     const uint32_t *__restrict__ tpfx, const TileDesc *__restrict__ desc,
     const unsigned long long *__restrict__ bases, uint32_t *__restrict__ cur,
@@ -2267,6 +2267,35 @@ __device__ __forceinline__ void cx_fill_table(CxTable<T> &t, const T *recv,
     }
 }
 
+// The sampled plan's children past kLocalMax (K12g's list 0, entries {src in Y | the child's top
+// 16 bits << 40, dst | len << 40}, as K11e's): one piece each, read from Y.
+template <typename T>
+__device__ __forceinline__ void cx_fill_table_est(CxTable<T> &t, const T *y,
+                                                  const unsigned long long *list, uint32_t i,
+                                                  uint32_t nlist) {  // wave 0 only
+    constexpr uint32_t E = 16 / sizeof(T);
+    const uint32_t lane = threadIdx.x & 63;
+    if (i >= nlist) {
+        if (lane == 0) t.keys = 0;
+        return;
+    }
+    if (lane == 0) {
+        const uint64_t sw = list[2 * i], e = list[2 * i + 1];
+        const uint64_t src = sw & ((1ull << 40) - 1);
+        const uint32_t n = (uint32_t)(e >> 40);
+        const uint32_t mis = (uint32_t)((reinterpret_cast<uintptr_t>(y + src) / sizeof(T)) & (E - 1));
+        const uint32_t hd = min(mis ? E - mis : 0u, n);
+        t.src[0] = src;
+        t.len[0] = n;
+        t.head[0] = hd;
+        t.cumv[0] = 0;
+        t.cumv[1] = (n - hd) / E;
+        t.h = (uint32_t)(sw >> 40);
+        t.keys = n;
+        t.dst = e & ((1ull << 40) - 1);
+    }
+}
+
 // piece of vector g: the last p with cumv[p] <= g (binary search, P <= 64)
 template <typename T>
 __device__ __forceinline__ uint32_t cx_piece(const CxTable<T> &t, int P, uint32_t g) {
@@ -2327,14 +2356,18 @@ __device__ __forceinline__ void cx_count_bucket(const T *recv, const CxTable<T> 
     }
 }
 
-template <typename T>
+// EST: the sampled plan's oversized children (cx_fill_table_est: recv = Y, P = 1): keys are
+// relative to the block's minimum koff, so the expansion marks relative keys (monotonic in the
+// slot, as the max-scan needs) and the stores add koff and flip.
+template <typename T, bool EST = false>
 __global__ __launch_bounds__(1024) void k_count_expand(const T *__restrict__ recv,
                                                        const unsigned long long *__restrict__ pos,
                                                        const unsigned long long *__restrict__ roff,
                                                        int P,
                                                        const unsigned long long *__restrict__ bstart,
                                                        const unsigned long long *__restrict__ list,
-                                                       uint32_t nlist, uint32_t *__restrict__ out) {
+                                                       uint32_t nlist, uint32_t *__restrict__ out,
+                                                       uint32_t koff = 0) {
     constexpr uint32_t NT = 1024, NW = NT / 64, WORDS = 32768, CW = 128;  // words per chunk
     constexpr uint32_t CH = WORDS / NW / CW;                               // 16 chunks per wave
     constexpr uint32_t PF = 8;  // prefetched 16-B vectors per thread
@@ -2349,7 +2382,11 @@ __global__ __launch_bounds__(1024) void k_count_expand(const T *__restrict__ rec
     __shared__ uint32_t s_nw;
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     uint32_t cur = 0;
-    if (tid < 64) cx_fill_table(s_t[0], recv, pos, roff, P, bstart, list, blockIdx.x, nlist);
+    auto fill = [&](CxTable<T> &t, uint32_t i) {
+        if (EST) cx_fill_table_est(t, recv, list, i, nlist);
+        else cx_fill_table(t, recv, pos, roff, P, bstart, list, i, nlist);
+    };
+    if (tid < 64) fill(s_t[0], blockIdx.x);
     __syncthreads();
     {
         uint4 *z = reinterpret_cast<uint4 *>(s_h);
@@ -2370,7 +2407,7 @@ __global__ __launch_bounds__(1024) void k_count_expand(const T *__restrict__ rec
         CxTable<T> &t = s_t[cur];
         // (the bins are zero: before the first bucket, and the expansion zeroes every word
         // after its last read); wave 0 reads the next bucket's pieces, in flight meanwhile
-        if (tid < 64) cx_fill_table(s_t[nxt], recv, pos, roff, P, bstart, list, i + gridDim.x, nlist);
+        if (tid < 64) fill(s_t[nxt], i + gridDim.x);
         if (tid == 0) s_nw = 0;
         const uint32_t h = (uint32_t)__builtin_amdgcn_readfirstlane((int)t.h);
         const uint32_t len = (uint32_t)__builtin_amdgcn_readfirstlane((int)t.keys);
@@ -2454,7 +2491,7 @@ __global__ __launch_bounds__(1024) void k_count_expand(const T *__restrict__ rec
             uint32_t *mk = reinterpret_cast<uint32_t *>(mk4);
             const uint64_t dst0 = tdst + (uint32_t)__builtin_amdgcn_readfirstlane((int)s_base[w]);
             uint32_t *d = out + dst0;
-            const uint32_t hk = (h << 16) ^ kFlip;
+            const uint32_t hk = EST ? h << 16 : (h << 16) ^ kFlip;
             const uint32_t off = (uint32_t)(reinterpret_cast<uintptr_t>(d) >> 2) & 3u;
             // windows [ws, ws + 256) of the wave's run; chunk j's bins mark the windows they
             // start in (an empty bin is parked at 2^31, past every window), and a window is
@@ -2469,7 +2506,13 @@ __global__ __launch_bounds__(1024) void k_count_expand(const T *__restrict__ rec
                 const uint32_t prev = max(carry, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)S, 0x138, 0xf, 0xf, true));
                 carry = max(carry, (uint32_t)__builtin_amdgcn_readlane((int)S, 63));
                 const uint32_t q = ws + 4 * lane;  // this lane's first slot
-                const uint4 v = make_uint4(max(prev, a0), max(prev, a1), max(prev, a2), max(prev, a3));
+                uint4 v = make_uint4(max(prev, a0), max(prev, a1), max(prev, a2), max(prev, a3));
+                if (EST) {  // relative ordered keys -> int32
+                    v.x = (v.x + koff) ^ kFlip;
+                    v.y = (v.y + koff) ^ kFlip;
+                    v.z = (v.z + koff) ^ kFlip;
+                    v.w = (v.w + koff) ^ kFlip;
+                }
                 if (q + 4 <= nkw && q < nkw) {
                     *reinterpret_cast<uint4 *>(d + q) = v;  // 16-B aligned
                 } else {
@@ -2883,8 +2926,8 @@ __device__ __forceinline__ uint64_t est_cap(uint32_t cnt, double scale, double s
 // zeroes the nzero work-list counters at zero and sets the last eligibility bit; block 0 of
 // K3r then hands the eligibility word and the number of children with samples to the host
 // (publish_elig).
-// Ineligible (eflag bit 2): a child estimate + 4 sigma past kLocalMax (K11 could not take it
-// in one pass; capacities are clamped to kLocalMax), a u8 wrap in K1e, every sample in one level-3 bucket (level 3 would copy; the exact
+// Ineligible (eflag bit 2): a child estimate + 4 sigma past kHxMax (K18c could not take it in
+// one pass; capacities are clamped to kHxMax), a u8 wrap in K1e, every sample in one level-3 bucket (level 3 would copy; the exact
 // plan skips that level), or X / Y outgrowing their buffers (capx / capy keys).
 __global__ __launch_bounds__(kRadix) void k_est_plan(
     const uint32_t *__restrict__ part8, const uint32_t *__restrict__ part3,
@@ -2962,11 +3005,12 @@ __global__ __launch_bounds__(kRadix) void k_est_plan(
     const uint32_t m = s_m;
     const double scale = m ? (double)n / (double)m : 0.0;
     const uint64_t cap = est_cap(cnt, scale, slack);
-    // eligible while the estimate + 4 sigma fits one K11 pass; the region is the 6-sigma
-    // capacity clamped to kLocalMax (a child that outgrows it overflows and the exact plan
-    // sorts again).  A peaked block (Gaussian keys after the offset retry) has children of
-    // ~27K keys that the 6-sigma rule alone refused.
-    if ((double)cnt * scale + 4.0 * sqrt((double)cnt + 1.0) * scale + 64.0 > (double)kLocalMax)
+    // A child is finished by K11e (<= kLocalMax keys) or, past that, by K18c's one-read
+    // counting sort (kLocalMax < len <= kHxMax, K12g's list 0): a peaked block (Gaussian keys
+    // after the offset retry) has children of ~27K keys near its mode, right at kLocalMax.
+    // Eligible while the estimate + 4 sigma fits kHxMax; regions are the 6-sigma capacity
+    // clamped to kHxMax (a child that outgrows it overflows: the exact plan sorts again).
+    if ((double)cnt * scale + 4.0 * sqrt((double)cnt + 1.0) * scale + 64.0 > (double)kHxMax)
         s_bad = 1;
     uint32_t wmax = cnt;  // the largest child's samples (the runtime's retry), per block
 #pragma unroll
@@ -2974,7 +3018,7 @@ __global__ __launch_bounds__(kRadix) void k_est_plan(
     if ((e & 63) == 0) atomicMax(&s_maxc, wmax);
     const uint64_t sampled = __ballot(cnt > 0);  // (outside the branch: all lanes vote)
     if ((e & 63) == 0) atomicAdd(&s_ne, (uint32_t)__popcll(sampled));
-    const uint32_t cc = (uint32_t)min(cap, (uint64_t)kLocalMax);
+    const uint32_t cc = (uint32_t)min(cap, (uint64_t)kHxMax);
     const uint32_t i = s * kRadix + e;
     capc[i] = cc;
     unsigned long long tot;
@@ -3132,12 +3176,14 @@ __global__ __launch_bounds__(kRadix) void k_est_classify(
         unsigned long long tot;
         const unsigned long long ex = block_excl_scan(len, s_w, &tot);  // (syncs: s_fb visible)
         const unsigned long long dst = s_fb + ex;
-        int which = -1;
-        if (len > 0 && !over)
+        int which = -1;  // K11e class, or 0: past kLocalMax, K18c
+        if (len > 0 && !over) {
+            which = 0;
             for (int k = 1; k < NL; ++k)
                 if (len <= kLocalCap[k]) { which = k; break; }
+        }
         unsigned int idx = 0;
-        if (which > 0) {
+        if (which >= 0) {
             idx = atomicAdd(&s_n[which], 1u);
             atomicAdd(&s_keys[which], (unsigned long long)len);
             atomicMax(&s_max[which], (unsigned long long)len);
@@ -3149,7 +3195,7 @@ __global__ __launch_bounds__(kRadix) void k_est_classify(
             atomicMax(&ctr[3 * e + 2], s_max[e]);
         }
         __syncthreads();
-        if (which > 0) {
+        if (which >= 0) {
             unsigned long long *list = reinterpret_cast<unsigned long long *>(wl.list[which]);
             const unsigned long long j = s_base[which] + idx;
             const uint32_t pfx = sb ? ((in[0] ^ kFlip) - koff) >> (32 - sb) : 0u;
@@ -3236,14 +3282,14 @@ __global__ __launch_bounds__(BLOCK) void k_local_sort_e(const uint16_t *__restri
     sort_bucket<BLOCK, ITEMS, ATOMIC>(k, len, ndigits, dst, s_a, s_wc, koff);
 }
 
-#ifndef GSORT_C3_BLOCK
-#define GSORT_C3_BLOCK 512
-#endif
-// class 3 (16 384 keys): 512 threads x 32 keys, or 1024 x 16 (A/B: GSORT_C3_BLOCK=1024)
-constexpr int kC3Block = GSORT_C3_BLOCK, kC3Items = 16384 / kC3Block;
+// class geometries (block x items): class 3 as 1024 x 16 measured slower than 512 x 32 (local
+// 30-bit keys K11e 0.80 -> 0.90 ms, receive 16 384-key buckets 0.73 -> 0.87 ms per 2^28 keys,
+// round 4); class 2 as 256 x 36 needs 133 VGPRs (12 waves per CU)
+constexpr int kC3Block = 512, kC3Items = 32;
+constexpr int kC2Block = 512, kC2Items = 18;
 
 constexpr int cls_of(int block, int items) {
-    return block * items == 16384 ? 3 : block == 256 ? 1 : block == 1024 ? 4 : 2;
+    return block * items == 16384 ? 3 : block * items == 9216 ? 2 : block * items == 4608 ? 1 : 4;
 }
 
 unsigned grid_for(uint64_t n, unsigned block, unsigned cap) {
@@ -3629,7 +3675,7 @@ hipError_t launch_local_sort(const uint32_t *in, uint32_t *out, const uint64_t *
     } while (0)
     switch (cls) {
         case 1: GSORT_K11(256, 18); break;
-        case 2: GSORT_K11(512, 18); break;
+        case 2: GSORT_K11(kC2Block, kC2Items); break;
         case 3: GSORT_K11(kC3Block, kC3Items); break;
         default: GSORT_K11(1024, 32); break;
     }
@@ -3723,7 +3769,7 @@ hipError_t launch_gather_sort(const void *recv, bool packed16, const uint64_t *p
     } while (0)
     switch (cls) {
         case 1: if (atomic_rank) GSORT_K11G(256, 18, true); else GSORT_K11G(256, 18, false); break;
-        case 2: if (atomic_rank) GSORT_K11G(512, 18, true); else GSORT_K11G(512, 18, false); break;
+        case 2: if (atomic_rank) GSORT_K11G(kC2Block, kC2Items, true); else GSORT_K11G(kC2Block, kC2Items, false); break;
         case 3: if (atomic_rank) GSORT_K11G(kC3Block, kC3Items, true); else GSORT_K11G(kC3Block, kC3Items, false); break;
         default: if (atomic_rank) GSORT_K11G(1024, 32, true); else GSORT_K11G(1024, 32, false); break;
     }
@@ -3782,10 +3828,10 @@ hipError_t launch_count_expand(const void *recv, bool packed16, const uint64_t *
     const uint32_t grid = std::min<uint32_t>(nlist, (uint32_t)ncu);  // one workgroup per CU
     if (packed16)
         launch_k(k_count_expand<uint16_t>, grid, 1024, 0, s, reinterpret_cast<const uint16_t *>(recv), ps, ro, P,
-                 bs, l, nlist, out);
+                 bs, l, nlist, out, 0u);
     else
         launch_k(k_count_expand<int32_t>, grid, 1024, 0, s, reinterpret_cast<const int32_t *>(recv), ps, ro, P,
-                 bs, l, nlist, out);
+                 bs, l, nlist, out, 0u);
     return hipGetLastError();
 }
 
@@ -3883,6 +3929,10 @@ hipError_t launch_est_front(const EstPlan &p, hipStream_t s) {
 // workgroup measured slower overall: profiles/r04_ab_k3_pipe_and_tiles.txt)
 constexpr int kEstTiles = 2;
 constexpr int kEstPartBlock = kPartBlock;
+#ifndef GSORT_K3A_TILES
+#define GSORT_K3A_TILES 2
+#endif
+constexpr int kEstTilesL2 = GSORT_K3A_TILES;  // K3a: a pair per 1024 threads, or a tile per 512
 
 hipError_t launch_est_level3(const EstPlan &p, hipStream_t s) {
     using ull = unsigned long long;
@@ -3900,7 +3950,7 @@ hipError_t launch_est_level3(const EstPlan &p, hipStream_t s) {
 
 hipError_t launch_est_level2(const EstPlan &p, hipStream_t s) {
     using ull = unsigned long long;
-    constexpr int B = kEstPartBlock, I = kSweepTile / B;
+    constexpr int T2 = kEstTilesL2, B = kPartBlock * T2 / 2, I = kSweepTile / B;
     const uint32_t max_tiles = (uint32_t)est_max_tiles(p.n);
     TileDesc *desc = static_cast<TileDesc *>(p.tdesc);
     TileDesc *pieces = desc + max_tiles;
@@ -3908,8 +3958,8 @@ hipError_t launch_est_level2(const EstPlan &p, hipStream_t s) {
              (const uint32_t *)p.init3, (const uint32_t *)p.lim3,
              reinterpret_cast<const ull *>(p.bases3), max_tiles, (const uint32_t *)p.eflag, p.tp,
              desc, pieces);
-    launch_k(k_partition_res<B, I, false, false, uint16_t, true, kEstTiles>,
-             (max_tiles + kEstTiles - 1) / kEstTiles, B, 0, s,
+    launch_k(k_partition_res<B, I, false, false, uint16_t, true, T2>,
+             (max_tiles + T2 - 1) / T2, B, 0, s,
              (const uint32_t *)p.x, p.y, p.n, (const uint32_t *)p.tp, (const TileDesc *)desc,
              reinterpret_cast<const ull *>(p.bases2), p.cur2, (const uint32_t *)p.eflag,
              (const uint32_t *)nullptr, (const uint32_t *)p.lim2, p.eflag + 1,
@@ -3924,6 +3974,16 @@ hipError_t launch_est_classify(const EstPlan &p, hipStream_t s) {
              (const uint32_t *)p.init2, (const uint32_t *)p.lim2, (const uint32_t *)p.cur3,
              (const uint32_t *)p.init3, reinterpret_cast<const ull *>(p.bases2), p.wl, p.eflag,
              p.in, p.sb, p.koff);
+    return hipGetLastError();
+}
+
+hipError_t launch_est_oversized(const EstPlan &p, uint32_t nlist, int ncu, hipStream_t s) {
+    using ull = unsigned long long;
+    if (nlist == 0) return hipSuccess;
+    const unsigned grid = (unsigned)std::min<uint32_t>(nlist, (uint32_t)std::max(ncu, 1));
+    launch_k(k_count_expand<uint16_t, true>, grid, 1024, 0, s, (const uint16_t *)p.y,
+             (const ull *)nullptr, (const ull *)nullptr, 1, (const ull *)nullptr,
+             reinterpret_cast<const ull *>(p.wl.list[0]), nlist, p.out, p.koff);
     return hipGetLastError();
 }
 
@@ -3962,7 +4022,7 @@ hipError_t launch_local_sort_e(const EstPlan &p, int cls, uint32_t first, uint32
     } while (0)
     switch (cls) {
         case 1: GSORT_K11E(256, 18); break;
-        case 2: GSORT_K11E(512, 18); break;
+        case 2: GSORT_K11E(kC2Block, kC2Items); break;
         case 3: GSORT_K11E(kC3Block, kC3Items); break;
         default: GSORT_K11E(1024, 32); break;
     }

@@ -997,6 +997,7 @@ gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
         if (st == GSORT_OK) st = ensure(c, c->m_edump, (size_t)kSweepTile * 4);
         for (int k = 0; k < kLocalClasses && st == GSORT_OK; ++k)
             st = ensure_list(c, c->m_local[k], kBuckets16);
+        if (st == GSORT_OK) st = ensure_list(c, c->m_next[0], kBuckets16);  // K18c: > kLocalMax
         c->est_busy = false;
         if (st == GSORT_OK && (!c->m_ex.p || !c->m_ey.p))
             return set_err(c, GSORT_EINVAL, "sampled plan: region buffers missing");
@@ -1107,8 +1108,8 @@ gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
     if (mail[0] != 0) return GSORT_OK;  // a region overflowed: *ok stays false
     uint64_t h[3 * (kLocalClasses + 1)];
     for (int i = 0; i < 3 * (kLocalClasses + 1); ++i) h[i] = mail[8 + i];
-    uint64_t keys = 0, ent = 0;
-    for (int k = 1; k <= kLocalClasses; ++k) { keys += h[3 * k + 1]; ent += h[3 * k]; }
+    uint64_t keys = 0, ent = 0;  // (list 0: the children past kLocalMax, K18c)
+    for (int k = 0; k <= kLocalClasses; ++k) { keys += h[3 * k + 1]; ent += h[3 * k]; }
     if (keys != n || ent > kBuckets16)  // every key in exactly one K11e entry
         return set_err(c, GSORT_EINVAL, "sampled plan: K11e lists hold " + std::to_string(keys) +
                                             " keys in " + std::to_string(ent) + " entries, want " +
@@ -1117,6 +1118,7 @@ gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
         const uint32_t done = k == kspec ? sampled : 0u, cnt = (uint32_t)h[3 * k];
         if (cnt > done) HIP_TRY(c, launch_local_sort_e(p, k, done, cnt - done, false, c->stream));
     }
+    if (h[0]) HIP_TRY(c, launch_est_oversized(p, (uint32_t)h[0], c->ncu, c->stream));
     toc(c, PH_BUCKET, t);
     *ok = true;
     if (stats) stats->buckets_local += ent;

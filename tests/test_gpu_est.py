@@ -117,8 +117,8 @@ def test_sampled_plan_distributions(ctx, orc, name):
         assert plan == SHIFTED, name
     if name == "half_one_value":  # the child holds about half: either way is right
         assert plan in (FALLBACK, GIANT), name
-    if name == "bits24":  # a narrow key range: the digits below its shared bits
-        assert plan == SHIFTED, name
+    if name == "bits24":  # a narrow key range: 256 children of ~32K keys, taken as they are
+        assert plan in (SAMPLED, SHIFTED), name  # (K11e / K18c) or below the shared bits
     assert np.array_equal(got, np.sort(keys)), name
 
 
@@ -157,12 +157,12 @@ def test_sampled_plan_repeated_sorts_reuse_scratch(ctx, orc):
         assert np.array_equal(got, np.sort(keys)), n
 
 
-@pytest.mark.parametrize("bits,plan", [(27, SAMPLED), (26, SAMPLED), (25, SHIFTED)])
+@pytest.mark.parametrize("bits,plan", [(27, SAMPLED), (26, SAMPLED), (25, SAMPLED)])
 def test_sampled_plan_child_classes(ctx, bits, plan):
     """2^24 keys below 2^bits: 16-bit children of 2^(bits-8) keys -- K11e classes 2 and 3
-    (8 192 / 16 384 keys) on the sampled plan; 32 768-key children leave no room for the
-    sampling margin under kLocalMax, so the block is retried with its digits below the 7
-    leading bits every key shares."""
+    (8 192 / 16 384 keys) on the sampled plan; 32 768-key children (bits = 25) straddle
+    kLocalMax: those past it go to K12g's list 0 and K18c's counting sort (round 4; before
+    it the block was retried with its digits below the 7 leading bits every key shares)."""
     rng = np.random.default_rng(bits)
     keys = rng.integers(0, 1 << bits, 1 << 24, dtype=np.int64).astype(np.int32)
     got, _ = _sort(ctx, keys)
@@ -219,14 +219,18 @@ def test_sampled_plan_shifted_prefix_check(ctx, case):
     assert np.array_equal(got, np.sort(keys)), case
 
 
-@pytest.mark.parametrize("lo,hi,n", [(0, 1 << 20, 1 << 23), (-(1 << 27), 0, 1 << 26),
-                                     (5 << 24, (5 << 24) + (1 << 26), 1 << 26),
-                                     (1 << 28, 3 << 27, 1 << 26), (-(1 << 14), 1 << 14, 1 << 23)])
-def test_sampled_plan_shifted_ranges(ctx, lo, hi, n):
-    """Key ranges narrower than int32 at any bit offset (20-, 27-, 26-, 27-bit spans, and one
-    across zero: its ordered keys share no leading bit) with children too large for the first
-    attempt: the retry shifts every digit by the samples' shared leading bits (not only whole
-    bytes)."""
+@pytest.mark.parametrize("lo,hi,n,plans", [
+    (0, 1 << 20, 1 << 23, (SAMPLED, SHIFTED)), (-(1 << 27), 0, 1 << 26, (SAMPLED, SHIFTED)),
+    (5 << 24, (5 << 24) + (1 << 26), 1 << 26, (SAMPLED, SHIFTED)),
+    (1 << 28, 3 << 27, 1 << 26, (SAMPLED, SHIFTED)),
+    (0, 1 << 19, 1 << 24, (SHIFTED,)), (5 << 24, (5 << 24) + (1 << 20), 1 << 24, (SHIFTED,)),
+    (-(1 << 14), 1 << 14, 1 << 23, (SHIFTED,))])
+def test_sampled_plan_shifted_ranges(ctx, lo, hi, n, plans):
+    """Key ranges narrower than int32 at any bit offset (20-, 27-, 26-, 27-, 19-bit spans, and
+    one across zero: its ordered keys share no leading bit).  Children of up to kHxMax keys are
+    taken by the first attempt (those past kLocalMax by K18c, round 4); past kHxMax (the 19- and
+    20-bit spans at 2^24 keys: 8 / 16 children of ~1-2M keys) the retry shifts every digit by
+    the samples' shared leading bits (not only whole bytes)."""
     rng = np.random.default_rng(hi & 0xffff)
     keys = rng.integers(lo, hi, n, dtype=np.int64).astype(np.int32)
     got, _ = _sort(ctx, keys)
@@ -235,7 +239,7 @@ def test_sampled_plan_shifted_ranges(ctx, lo, hi, n):
     # when the first sample's child counts are known, or -- as here, two children wrapped them
     # -- when the samples span at most 24 bits (a peaked block, round 4; before it this case
     # took the one-child count or the exact plan)
-    assert ctx.last_plan() == SHIFTED, (lo, hi, ctx.last_plan())
+    assert ctx.last_plan() in plans, (lo, hi, ctx.last_plan())
 
 
 @pytest.mark.parametrize("case", ["gauss", "gauss_outliers", "two_values_across_zero"])
@@ -254,9 +258,25 @@ def test_sampled_plan_offset_retry(ctx, case):
             keys[[7, n // 3, n - 2]] = [-2**31, 2**31 - 1, 123456789]
     got, _ = _sort(ctx, keys)
     assert np.array_equal(got, np.sort(keys)), case
-    assert ctx.last_plan() in (FALLBACK, SHIFTED, GIANT), ctx.last_plan()
-    if case == "gauss":
-        assert ctx.last_plan() == SHIFTED
+    assert ctx.last_plan() in (SAMPLED, FALLBACK, SHIFTED, GIANT), ctx.last_plan()
+    if case == "gauss":  # ~55 children of ~300K keys: taken at once (K18c), or after the offset
+        assert ctx.last_plan() in (SAMPLED, SHIFTED)
+
+
+@pytest.mark.parametrize("n", [(1 << 24) + 3, 1 << 25])
+def test_sampled_plan_oversized_children(ctx, n):
+    """A peak on a wide span (round 4): 60 % of the keys within +-5 120 of zero, the rest
+    uniform over +-2^23.  The first sample wraps its counters on the peak; the offset retry
+    (samples spanning <= 24 bits) shifts the digits 8 bits down, where the peak's ~40
+    children hold ~250 K keys each -- past kLocalMax, so K12g lists them for K18c's counting
+    sort from Y (list 0) instead of refusing the block."""
+    rng = np.random.default_rng(n & 0xff)
+    keys = np.where(rng.random(n) < 0.6, rng.integers(-5120, 5120, n),
+                    rng.integers(-(1 << 23), 1 << 23, n)).astype(np.int32)
+    keys[[0, n - 1]] = [-(1 << 23), (1 << 23) - 1]  # the span's ends
+    got, st = _sort(ctx, keys)
+    assert np.array_equal(got, np.sort(keys))
+    assert ctx.last_plan() == SHIFTED, ctx.last_plan()
 
 
 # ---- one dominant 16-bit child (DESIGN.md 5.1, "giant child") -------------------------------
