@@ -1744,6 +1744,13 @@ __device__ __forceinline__ uint32_t wave_rank(uint32_t *wc, uint32_t d, bool val
 // Keys past len are neither counted nor placed (a lane-level mask on wave-uniform bounds; a
 // padding key per empty slot would put every such lane on one LDS counter, serialized).
 // The caller zeroes s_wc[0 .. 255] before its barrier.
+#ifndef GSORT_PAD_LDS
+#define GSORT_PAD_LDS 0
+#endif
+constexpr bool kPadLds = GSORT_PAD_LDS != 0;
+// K11's key array: TILE slots (+ one pad word per 32 with kPadLds)
+constexpr int lds_slots(int tile) { return kPadLds ? tile + tile / 32 : tile; }
+
 template <int BLOCK, int ITEMS, bool ATOMIC>
 __device__ __forceinline__ void sort_bucket(uint32_t (&k)[ITEMS], uint32_t len, int ndigits,
                                             uint32_t *__restrict__ dst, uint32_t *s_a,
@@ -1757,6 +1764,10 @@ __device__ __forceinline__ void sort_bucket(uint32_t (&k)[ITEMS], uint32_t len, 
     uint32_t *s_wsum = s_a + TILE - kRadix / 64;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     uint32_t *cnt = s_wc;  // digit 0: block-wide counters, then digit starts
+    // slot j of the key array at word j + j / 32 (kPadLds): a digit's run starts 256 keys
+    // after the previous digit's in a dense block (sorted / reversed input: every key value
+    // once), so without the pad word the 32 lanes of a scatter all land on one bank
+    auto at = [](uint32_t j) -> uint32_t { return kPadLds ? j + (j >> 5) : j; };
     // keys of item i are valid for tid < lim(i) (a wave-uniform bound)
     auto lim = [&](int i) -> uint32_t {
         return len > (uint32_t)(i * BLOCK) ? len - (uint32_t)(i * BLOCK) : 0u;
@@ -1776,24 +1787,9 @@ __device__ __forceinline__ void sort_bucket(uint32_t (&k)[ITEMS], uint32_t len, 
     // digit 0: unstable counting sort into s_a
     {
         uint32_t r[ITEMS];
-        // A wave whose threads each hold keys of ONE digit 0 (runs of consecutive keys: thread t
-        // holds keys i * BLOCK + t, so sorted or reversed input gives every thread a constant low
-        // byte) would issue ITEMS back-to-back atomics on the same 64 addresses, each waiting for
-        // the one before; such a thread adds its count with one atomic instead.
-        bool one = true;
-        const uint32_t d0 = k[0] & 255u;
 #pragma unroll
-        for (int i = 1; i < ITEMS; ++i) one &= (uint32_t)tid >= lim(i) || (k[i] & 255u) == d0;
-        if (__ballot(one) == ~0ull) {
-            const uint32_t nv = len > (uint32_t)tid ? min((uint32_t)ITEMS, (len - tid + BLOCK - 1) / BLOCK) : 0u;
-            const uint32_t r0 = nv ? atomicAdd(&cnt[d0], nv) : 0u;
-#pragma unroll
-            for (int i = 0; i < ITEMS; ++i) r[i] = r0 + i;
-        } else {
-#pragma unroll
-            for (int i = 0; i < ITEMS; ++i)
-                if ((uint32_t)tid < lim(i)) r[i] = atomicAdd(&cnt[k[i] & 255u], 1u);
-        }
+        for (int i = 0; i < ITEMS; ++i)
+            if ((uint32_t)tid < lim(i)) r[i] = atomicAdd(&cnt[k[i] & 255u], 1u);
         __syncthreads();
         uint32_t excl = 0;
         if (tid < kRadix) excl = block_scan(cnt[tid]);
@@ -1805,7 +1801,7 @@ __device__ __forceinline__ void sort_bucket(uint32_t (&k)[ITEMS], uint32_t len, 
         __syncthreads();
 #pragma unroll
         for (int i = 0; i < ITEMS; ++i)
-            if ((uint32_t)tid < lim(i)) s_a[cnt[k[i] & 255u] + r[i]] = k[i];
+            if ((uint32_t)tid < lim(i)) s_a[at(cnt[k[i] & 255u] + r[i])] = k[i];
         __syncthreads();
     }
 
@@ -1821,7 +1817,7 @@ __device__ __forceinline__ void sort_bucket(uint32_t (&k)[ITEMS], uint32_t len, 
 #pragma unroll
         for (int i = 0; i < ITEMS; ++i)
             if ((uint32_t)i < R && (uint32_t)(i * 64 + lane) < wlen)
-                k[i] = s_a[base + i * 64 + lane];
+                k[i] = s_a[at(base + i * 64 + lane)];
         __syncthreads();
         uint32_t rk[ITEMS];
 #pragma unroll
@@ -1850,14 +1846,14 @@ __device__ __forceinline__ void sort_bucket(uint32_t (&k)[ITEMS], uint32_t len, 
 #pragma unroll
         for (int i = 0; i < ITEMS; ++i)
             if ((uint32_t)i < R && (uint32_t)(i * 64 + lane) < wlen)
-                s_a[wc[(k[i] >> shift) & 255u] + rk[i]] = k[i];
+                s_a[at(wc[(k[i] >> shift) & 255u] + rk[i])] = k[i];
         __syncthreads();
     }
     const __amdgpu_buffer_rsrc_t rs = bucket_rsrc(dst, len * 4u);  // stores past len dropped
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
         const uint32_t j = (uint32_t)(i * BLOCK + tid);
-        __builtin_amdgcn_raw_buffer_store_b32((s_a[j] + koff) ^ kFlip, rs, (int)(j * 4u), 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32((s_a[at(j)] + koff) ^ kFlip, rs, (int)(j * 4u), 0, 0);
     }
 }
 
@@ -1870,7 +1866,7 @@ __global__ __launch_bounds__(BLOCK) void k_local_sort(const uint32_t *__restrict
                                                       int ndigits) {
     constexpr int WAVES = BLOCK / 64;
     constexpr int TILE = BLOCK * ITEMS;
-    __shared__ uint32_t s_a[TILE];
+    __shared__ uint32_t s_a[lds_slots(TILE)];
     __shared__ uint32_t s_wc[WAVES * kRadix];  // per-wave digit counts, then offsets
     const uint64_t start = list[2 * blockIdx.x];
     const uint64_t e = list[2 * blockIdx.x + 1];  // len | extra digits << 32 (merged children)
@@ -1916,7 +1912,7 @@ __global__ __launch_bounds__(BLOCK) void k_gather_sort(const T *__restrict__ rec
     constexpr int WAVES = BLOCK / 64;
     constexpr int TILE = BLOCK * ITEMS;
     constexpr int MAXP = 64;
-    __shared__ uint32_t s_a[TILE];
+    __shared__ uint32_t s_a[lds_slots(TILE)];
     __shared__ uint32_t s_wc[WAVES * kRadix];
     __shared__ uint64_t s_src[MAXP];  // piece p: first key in recv
     __shared__ uint64_t s_delta[MAXP];
@@ -3252,7 +3248,7 @@ __global__ __launch_bounds__(BLOCK) void k_local_sort_e(const uint16_t *__restri
                                                         unsigned long long seq, uint32_t koff) {
     constexpr int WAVES = BLOCK / 64;
     constexpr int TILE = BLOCK * ITEMS;
-    __shared__ uint32_t s_a[TILE];
+    __shared__ uint32_t s_a[lds_slots(TILE)];
     __shared__ uint32_t s_wc[WAVES * kRadix];
     if (mail && blockIdx.x == 0) publish_lists(mail, ctr_all, eflag, seq);  // K12g is done
     const uint32_t i = first + blockIdx.x;
