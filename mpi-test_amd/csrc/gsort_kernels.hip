@@ -1767,7 +1767,7 @@ __device__ __forceinline__ void sort_bucket(uint32_t (&k)[ITEMS], uint32_t len, 
     // slot j of the key array at word j + j / 32 (kPadLds): a digit's run starts 256 keys
     // after the previous digit's in a dense block (sorted / reversed input: every key value
     // once), so without the pad word the 32 lanes of a scatter all land on one bank
-    auto at = [](uint32_t j) -> uint32_t { return kPadLds ? j + (j >> 5) : j; };
+    auto at = [](uint32_t j) constexpr -> uint32_t { return kPadLds ? j + (j >> 5) : j; };
     // keys of item i are valid for tid < lim(i) (a wave-uniform bound)
     auto lim = [&](int i) -> uint32_t {
         return len > (uint32_t)(i * BLOCK) ? len - (uint32_t)(i * BLOCK) : 0u;
@@ -1814,10 +1814,12 @@ __device__ __forceinline__ void sort_bucket(uint32_t (&k)[ITEMS], uint32_t len, 
         for (int j = 0; j < kRadix / 64; ++j) wc[j * 64 + lane] = 0;
         const uint32_t base = (uint32_t)w * 64 * R;  // wave-uniform
         const uint32_t wlen = len > base ? len - base : 0u;  // keys of this wave's chunk
+        // base is a multiple of 64: slot base + i * 64 + lane sits at at(base + lane) + i * at(64)
+        const uint32_t p0 = at(base + lane);
 #pragma unroll
         for (int i = 0; i < ITEMS; ++i)
             if ((uint32_t)i < R && (uint32_t)(i * 64 + lane) < wlen)
-                k[i] = s_a[at(base + i * 64 + lane)];
+                k[i] = s_a[p0 + (uint32_t)i * at(64)];
         __syncthreads();
         uint32_t rk[ITEMS];
 #pragma unroll
@@ -1850,10 +1852,13 @@ __device__ __forceinline__ void sort_bucket(uint32_t (&k)[ITEMS], uint32_t len, 
         __syncthreads();
     }
     const __amdgpu_buffer_rsrc_t rs = bucket_rsrc(dst, len * 4u);  // stores past len dropped
+    static_assert(BLOCK % 32 == 0, "slot i * BLOCK + tid at at(tid) + i * at(BLOCK)");
+    const uint32_t f0 = at((uint32_t)tid);
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
         const uint32_t j = (uint32_t)(i * BLOCK + tid);
-        __builtin_amdgcn_raw_buffer_store_b32((s_a[at(j)] + koff) ^ kFlip, rs, (int)(j * 4u), 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32((s_a[f0 + (uint32_t)i * at(BLOCK)] + koff) ^ kFlip, rs,
+                                              (int)(j * 4u), 0, 0);
     }
 }
 
@@ -2887,7 +2892,10 @@ __global__ __launch_bounds__(1024) void k_est_sample(const uint32_t *__restrict_
         hi = max(hi, (uint32_t)__shfl_xor((int)hi, o));
     }
     if ((tid & 63) == 0) {
-        atomicAdd(&s_m, cnt | (wrap << 31));
+        // (the wrap bit by OR: two waves adding it would cancel -- at n = 2^22 only 64
+        // workgroups sample, 1024 keys each, and a 60 % child wraps its u8 counter twice)
+        atomicAdd(&s_m, cnt);
+        if (wrap) atomicOr(&s_m, 1u << 31);
         if (vary) atomicOr(&s_vary, vary);
         if (cnt) { atomicMin(&s_lo, lo); atomicMax(&s_hi, hi); }
     }

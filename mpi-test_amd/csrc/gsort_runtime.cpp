@@ -87,6 +87,7 @@ struct gsort_ctx {
     int recv_cx = 4;
     int ncu = 256;
     int last_plan = 0;      // gsort_last_plan: 0 exact, 1 sampled, 2 sampled then exact
+    bool plan_trace = false; // GSORT_PLAN_TRACE: one stderr line per plan decision
     DevBuf m_ex, m_ey, m_epart, m_eplan, m_edesc, m_edump;
     DevBuf m_gplan;  // one dominant child: counts (65536 u64), starts (65537 u64), chunk bins
     bool est_busy = false;   // msd_sort_est is using m_ex / m_ey (not reclaimable)
@@ -1081,6 +1082,10 @@ gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
     toc(c, PH_LEVEL2, t);
     HIP_TRY(c, launch_est_classify(p, c->stream));
     ST_TRY(wait_word(3, p.seq_elig, "eligibility word"));
+    if (c->plan_trace)
+        fprintf(stderr, "gsort plan: n %llu sb %d koff %u eflag %llx children %llu maxc %llx\n",
+                (unsigned long long)n, sb, koff, (unsigned long long)mail[2],
+                (unsigned long long)mail[4], (unsigned long long)mail[23]);
     if (mail[2] & 4u) {  // ineligible: the exact plan sorts -- unless the samples share leading
         // key bits (a key range narrower than int32: 16-, 20-, 24-, 28-bit keys, dense or
         // sorted ranges) whose removal leaves children K11e can take: then the caller retries
@@ -1105,7 +1110,10 @@ gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
     if (kspec) HIP_TRY(c, launch_local_sort_e(p, kspec, 0, sampled, true, c->stream));
     else HIP_TRY(c, launch_est_publish(p, c->stream));
     ST_TRY(wait_word(1, p.seq_done, "K12g counters"));
-    if (mail[0] != 0) return GSORT_OK;  // a region overflowed: *ok stays false
+    if (mail[0] != 0) {  // a region overflowed: *ok stays false
+        if (c->plan_trace) fprintf(stderr, "gsort plan: overflow %llx\n", (unsigned long long)mail[0]);
+        return GSORT_OK;
+    }
     uint64_t h[3 * (kLocalClasses + 1)];
     for (int i = 0; i < 3 * (kLocalClasses + 1); ++i) h[i] = mail[8 + i];
     uint64_t keys = 0, ent = 0;  // (list 0: the children past kLocalMax, K18c)
@@ -1179,6 +1187,9 @@ gsort_status giant_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *
         n_lo += h_ctr[kH16Shards + x];
     }
     const uint64_t n_child = n - n_cold;
+    if (c->plan_trace)
+        fprintf(stderr, "gsort plan: giant child %x n %llu cold %llu below %llu\n", child,
+                (unsigned long long)n, (unsigned long long)n_cold, (unsigned long long)n_lo);
     if (n_cold > n || n_lo > n_cold)
         return set_err(c, GSORT_EINVAL, "giant child: inconsistent cold counts");
     // the sample misjudged: not worth it.  2 n_child >= n also gives n_cold <= n_child, which
@@ -1290,6 +1301,10 @@ gsort_status msd_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *ou
             HIP_TRY(c, launch_est_mode(in, n, d_res, c->stream));
             HIP_TRY(c, hipMemcpyAsync(h_res, d_res, 24, hipMemcpyDeviceToHost, c->stream));
             HIP_TRY(c, hipStreamSynchronize(c->stream));
+            if (c->plan_trace)
+                fprintf(stderr, "gsort plan: mode child %llx %llu of %llu samples\n",
+                        (unsigned long long)h_res[0], (unsigned long long)h_res[1],
+                        (unsigned long long)h_res[2]);
             if (h_res[2] && 2 * h_res[1] >= h_res[2]) {
                 ST_TRY(giant_sort(c, in, n, out, (uint32_t)h_res[0], stats, &ok));
                 if (ok) {
@@ -2391,6 +2406,7 @@ gsort_status create_common(gsort_ctx *c, int hip_device) {
     if (const char *e = getenv("GSORT_GIANT")) c->plan_giant = atoi(e) != 0;
     if (const char *e = getenv("GSORT_RECV_CX")) c->recv_cx = atoi(e);
     if (const char *e = getenv("GSORT_EST_SLACK")) c->est_slack = atof(e);
+    if (const char *e = getenv("GSORT_PLAN_TRACE")) c->plan_trace = atoi(e) != 0;
     HIP_TRY(c, hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, hip_device));
     {
         std::lock_guard<std::mutex> lk(g_ctx_mu);
