@@ -33,6 +33,31 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     return z ^ (z >> 31);
 }
 
+// Wave-wide inclusive scans through DPP (row shifts 1/2/4/8, then the row-15 and row-31
+// broadcasts): VALU only, where __shfl_up costs an LDS-crossbar op per step.
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ uint32_t dpp0(uint32_t x) {  // lanes outside the pattern read 0
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWS, 0xf, true);
+}
+__device__ __forceinline__ uint32_t wave_incl_add(uint32_t x) {
+    x += dpp0<0x111>(x);
+    x += dpp0<0x112>(x);
+    x += dpp0<0x114>(x);
+    x += dpp0<0x118>(x);
+    x += dpp0<0x142, 0xa>(x);
+    x += dpp0<0x143, 0xc>(x);
+    return x;
+}
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
+    x = max(x, dpp0<0x111>(x));
+    x = max(x, dpp0<0x112>(x));
+    x = max(x, dpp0<0x114>(x));
+    x = max(x, dpp0<0x118>(x));
+    x = max(x, dpp0<0x142, 0xa>(x));
+    x = max(x, dpp0<0x143, 0xc>(x));
+    return x;
+}
+
 // ---------------------------------------------------------------------------------------
 // Duplicate-aggregated LDS counter atomics.  Skewed inputs (sorted runs, many equal keys, the
 // top digits of a Zipf stream) send most lanes of a wave to ONE counter, and same-address LDS
@@ -1482,7 +1507,7 @@ __global__ __launch_bounds__(256) void k_tile_desc(const uint32_t *__restrict__ 
 // exact plan).  flags bit 2 (the sample found the input ineligible): do nothing.
 template <int BLOCK, int ITEMS, bool L3, bool FIN, typename OT = uint32_t, bool EST = false,
           int TILES = 2>
-__global__ __launch_bounds__(BLOCK, TILES == 1 ? 8 : 1) void k_partition_res(
+__global__ __launch_bounds__(BLOCK, TILES == 1 ? 6 : 1) void k_partition_res(
     const uint32_t *__restrict__ in, OT *__restrict__ out, uint64_t n,
     const uint32_t *__restrict__ tpfx, const TileDesc *__restrict__ desc,
     const unsigned long long *__restrict__ bases, uint32_t *__restrict__ cur,
@@ -1628,12 +1653,7 @@ __global__ __launch_bounds__(BLOCK, TILES == 1 ? 8 : 1) void k_partition_res(
 #pragma unroll
         for (int h = 0; h < TILES; ++h) {
             const uint32_t c = cnt[h];
-            uint32_t v = c;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t t = __shfl_up(v, o);
-                if (lane >= o) v += t;
-            }
+            const uint32_t v = wave_incl_add(c);
             if (lane == 63) s_wsum[h][w] = v;
             excl[h] = v - c;
         }
@@ -1681,31 +1701,6 @@ __global__ __launch_bounds__(BLOCK, TILES == 1 ? 8 : 1) void k_partition_res(
     }
 }
 
-// Wave-wide inclusive scans through DPP (row shifts 1/2/4/8, then the row-15 and row-31
-// broadcasts): VALU only, where __shfl_up costs an LDS-crossbar op per step.
-template <int CTRL, int ROWS = 0xf>
-__device__ __forceinline__ uint32_t dpp0(uint32_t x) {  // lanes outside the pattern read 0
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWS, 0xf, true);
-}
-__device__ __forceinline__ uint32_t wave_incl_add(uint32_t x) {
-    x += dpp0<0x111>(x);
-    x += dpp0<0x112>(x);
-    x += dpp0<0x114>(x);
-    x += dpp0<0x118>(x);
-    x += dpp0<0x142, 0xa>(x);
-    x += dpp0<0x143, 0xc>(x);
-    return x;
-}
-__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
-    x = max(x, dpp0<0x111>(x));
-    x = max(x, dpp0<0x112>(x));
-    x = max(x, dpp0<0x114>(x));
-    x = max(x, dpp0<0x118>(x));
-    x = max(x, dpp0<0x142, 0xa>(x));
-    x = max(x, dpp0<0x143, 0xc>(x));
-    return x;
-}
-
 // Stable wave-level rank of one round (64 keys, lane order = key order) against the wave's
 // running digit counters wc[256] (u32): returns #earlier keys of the wave with this digit.
 //   ATOMIC: one ds_add_rtn_u32 per lane.  The MI355X LDS serializes lanes of one instruction
@@ -1744,12 +1739,12 @@ __device__ __forceinline__ uint32_t wave_rank(uint32_t *wc, uint32_t d, bool val
 // Keys past len are neither counted nor placed (a lane-level mask on wave-uniform bounds; a
 // padding key per empty slot would put every such lane on one LDS counter, serialized).
 // The caller zeroes s_wc[0 .. 255] before its barrier.
-#ifndef GSORT_PAD_LDS
-#define GSORT_PAD_LDS 0
-#endif
-constexpr bool kPadLds = GSORT_PAD_LDS != 0;
-// K11's key array: TILE slots (+ one pad word per 32 with kPadLds)
-constexpr int lds_slots(int tile) { return kPadLds ? tile + tile / 32 : tile; }
+// K11's key array: TILE slots, one pad word after every 32 (slot j at word j + j / 32) --
+// except the 32 768-key class, whose 1024 threads hold 32 keys + 32 ranks in 128 VGPRs and
+// spill with the pad's addressing (children that large are rare; dense blocks make 4096-key
+// children at 2^28)
+constexpr bool lds_pad(int tile) { return tile < 32768; }
+constexpr int lds_slots(int tile) { return lds_pad(tile) ? tile + tile / 32 : tile; }
 
 template <int BLOCK, int ITEMS, bool ATOMIC>
 __device__ __forceinline__ void sort_bucket(uint32_t (&k)[ITEMS], uint32_t len, int ndigits,
@@ -1764,22 +1759,19 @@ __device__ __forceinline__ void sort_bucket(uint32_t (&k)[ITEMS], uint32_t len, 
     uint32_t *s_wsum = s_a + TILE - kRadix / 64;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     uint32_t *cnt = s_wc;  // digit 0: block-wide counters, then digit starts
-    // slot j of the key array at word j + j / 32 (kPadLds): a digit's run starts 256 keys
-    // after the previous digit's in a dense block (sorted / reversed input: every key value
-    // once), so without the pad word the 32 lanes of a scatter all land on one bank
-    auto at = [](uint32_t j) constexpr -> uint32_t { return kPadLds ? j + (j >> 5) : j; };
+    // slot j of the key array at word j + j / 32: in a dense block (sorted / reversed input,
+    // keys in steps of 16: every child holds 16 digit-0 values of 256 keys each) a digit's run
+    // starts 256 slots after the previous digit's, so without the pad word the 32 lanes of a
+    // scatter all land on one bank (reversed 2^28 keys: K11e 1.13 -> 0.49 ms, uniform +1 %,
+    // profiles/r04_ab_k11_pad_lds.txt); sequential reads of 32 aligned slots stay on 32 banks
+    auto at = [](uint32_t j) constexpr -> uint32_t { return lds_pad(TILE) ? j + (j >> 5) : j; };
     // keys of item i are valid for tid < lim(i) (a wave-uniform bound)
     auto lim = [&](int i) -> uint32_t {
         return len > (uint32_t)(i * BLOCK) ? len - (uint32_t)(i * BLOCK) : 0u;
     };
 
     auto block_scan = [&](uint32_t c) -> uint32_t {  // tid < 256: exclusive scan over digits
-        uint32_t v = c;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t t = __shfl_up(v, o);
-            if (lane >= o) v += t;
-        }
+        const uint32_t v = wave_incl_add(c);  // DPP: no LDS-crossbar op per step
         if (lane == 63) s_wsum[w] = v;
         return v - c;
     };
@@ -1815,11 +1807,11 @@ __device__ __forceinline__ void sort_bucket(uint32_t (&k)[ITEMS], uint32_t len, 
         const uint32_t base = (uint32_t)w * 64 * R;  // wave-uniform
         const uint32_t wlen = len > base ? len - base : 0u;  // keys of this wave's chunk
         // base is a multiple of 64: slot base + i * 64 + lane sits at at(base + lane) + i * at(64)
-        const uint32_t p0 = at(base + lane);
+        const uint32_t *pa = s_a + at(base + lane);
 #pragma unroll
         for (int i = 0; i < ITEMS; ++i)
             if ((uint32_t)i < R && (uint32_t)(i * 64 + lane) < wlen)
-                k[i] = s_a[p0 + (uint32_t)i * at(64)];
+                k[i] = pa[i * at(64)];
         __syncthreads();
         uint32_t rk[ITEMS];
 #pragma unroll
@@ -1853,12 +1845,12 @@ __device__ __forceinline__ void sort_bucket(uint32_t (&k)[ITEMS], uint32_t len, 
     }
     const __amdgpu_buffer_rsrc_t rs = bucket_rsrc(dst, len * 4u);  // stores past len dropped
     static_assert(BLOCK % 32 == 0, "slot i * BLOCK + tid at at(tid) + i * at(BLOCK)");
-    const uint32_t f0 = at((uint32_t)tid);
+    const uint32_t *fa = s_a + at((uint32_t)tid);
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
         const uint32_t j = (uint32_t)(i * BLOCK + tid);
-        __builtin_amdgcn_raw_buffer_store_b32((s_a[f0 + (uint32_t)i * at(BLOCK)] + koff) ^ kFlip, rs,
-                                              (int)(j * 4u), 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32((fa[i * at(BLOCK)] + koff) ^ kFlip, rs, (int)(j * 4u),
+                                              0, 0);
     }
 }
 
@@ -3936,7 +3928,7 @@ constexpr int kEstPartBlock = kPartBlock;
 #ifndef GSORT_K3A_TILES
 #define GSORT_K3A_TILES 2
 #endif
-constexpr int kEstTilesL2 = GSORT_K3A_TILES;  // K3a: a pair per 1024 threads, or a tile per 512
+constexpr int kEstTilesL2 = GSORT_K3A_TILES;  // K3a: a pair per 1024 threads (one tile per 512: r04_ab_k3a_one_tile_rejected)
 
 hipError_t launch_est_level3(const EstPlan &p, hipStream_t s) {
     using ull = unsigned long long;

@@ -1295,7 +1295,11 @@ gsort_status msd_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *ou
         }
         // one 16-bit child holding at least half of the keys (Zipf, 8- / 16-bit keys, one
         // frequent value): counted, not partitioned (K1m decides from 16384 strided samples)
-        if (allow_giant && c->plan_giant && r.valid) {
+        // (skipped when the first sample's child counts are known -- no u8 counter wrapped --
+        // and its largest child holds well under half of the samples: K1m is a 40 us strided
+        // read; a dominant child always wraps, >= 512 samples in one workgroup's counter)
+        const bool known = r.maxc != 0xffffffffu;
+        if (allow_giant && c->plan_giant && r.valid && !(known && (uint64_t)r.maxc * 160 < n)) {
             uint64_t *d_res = reinterpret_cast<uint64_t *>(c->d_small + OFF_GIANT);
             uint64_t *h_res = reinterpret_cast<uint64_t *>(c->h_small + OFF_GIANT);
             HIP_TRY(c, launch_est_mode(in, n, d_res, c->stream));
@@ -1328,7 +1332,6 @@ gsort_status msd_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *ou
         // (the first sample wraps on their peak; after the offset their children hold <= ~27K
         // keys at 2^28, sigma 1e6) pass it, Zipf keys, whose densest child holds ~29 % of the
         // block, do not.
-        const bool known = r.maxc != 0xffffffffu;
         auto fits = [&](int lead) {
             const int sb = std::min(lead, 16);
             const int fixed = std::max(0, std::min(lead - sb, 16));  // bits fixed below the shift
@@ -1338,10 +1341,29 @@ gsort_status msd_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *ou
         if (r.valid) {
             const int lead = r.vary ? __builtin_clz(r.vary) : 32;
             const int slead = span_lead(r.lo, r.hi);
-            if (lead >= 3 && lead < 32 && fits(lead)) {
+            const bool by_prefix = lead >= 3 && lead < 32 && fits(lead);
+            const bool by_offset =
+                !by_prefix && (slead == 32 || ((known || slead >= 8) && slead >= 4 && fits(slead - 1)));
+            if (by_prefix) {
                 ST_TRY(msd_sort_est(c, in, n, out, stats, &ok, std::min(lead, 16)));
-            } else if (slead == 32 || ((known || slead >= 8) && slead >= 4 && fits(slead - 1))) {
+            } else if (by_offset) {
                 // (the samples' span, one bit of margin: the block's may be wider)
+                // First the samples' range widened by an eighth of its width each way as the
+                // offset (no read pass: K3r checks every key against the constant prefix, so a
+                // key outside the guess fails the attempt); then the exact min / max.
+                if (slead < 32) {
+                    const uint64_t m = ((uint64_t)r.hi - r.lo) / 8 + 1;
+                    const uint32_t glo = r.lo > m ? (uint32_t)(r.lo - m) : 0u;
+                    const uint32_t ghi = (uint32_t)std::min<uint64_t>((uint64_t)r.hi + m, 0xffffffffull);
+                    const int gl = span_lead(glo, ghi);
+                    if (gl >= 3 && fits(gl))
+                        ST_TRY(msd_sort_est(c, in, n, out, stats, &ok, std::min(gl, 16), glo));
+                    if (c->plan_trace)
+                        fprintf(stderr, "gsort plan: offset guess %x..%x lead %d ok %d\n", glo, ghi,
+                                gl, (int)ok);
+                }
+            }
+            if (by_offset && !ok) {
                 ST_TRY(minmax());
                 const uint32_t lo = mlo, hi = mhi;
                 const int lead = span_lead(lo, hi);

@@ -1,5 +1,5 @@
 # round-4 closing batch: every -m gpu test, the driver's bench line, the PMC profile of the
-# bench configuration (tools/profile_pmc.sh), the reversed-input K11e profile, K3a one-tile A/B
+# bench configuration (tools/profile_pmc.sh), reversed / uniform K11e counters, distribution probe
 export TMPDIR=/tmp
 TAG=${1:-r04_v27}
 L=$PWD/mpi-test_amd/lib
