@@ -263,6 +263,29 @@ def test_sampled_plan_offset_retry(ctx, case):
         assert ctx.last_plan() in (SAMPLED, SHIFTED)
 
 
+@pytest.mark.parametrize("case", ["arange", "arange_reversed", "full_span_reversed", "gauss_1e6"])
+def test_dense_and_peaked_2p24(ctx, case):
+    """tools/dist_probe.py's sorted / reverse / gauss shapes at 2^24:
+    dense keys (every value of a range once, ascending or descending; or one key per 256
+    values over the whole int32 range, descending) put a digit's run a fixed stride after the
+    previous one in K11e's key array -- the padded layout -- and a Gaussian block goes through
+    the offset retry guessed from its samples' range.  np.sort parity for both algorithms."""
+    n = 1 << 24
+    if case == "arange":
+        keys = np.arange(n, dtype=np.int32)
+    elif case == "arange_reversed":
+        keys = np.arange(n, 0, -1, dtype=np.int32)
+    elif case == "full_span_reversed":
+        keys = (np.arange(n - 1, -1, -1, dtype=np.int64) * 256 - 2**31).astype(np.int32)
+    else:
+        keys = np.clip(np.random.default_rng(41).normal(0, 1e6, n), -2**31, 2**31 - 1).astype(np.int32)
+    want = np.sort(keys)
+    for algo in ("radix", "sample"):
+        got, _ = _sort(ctx, keys, algo)
+        assert np.array_equal(got, want), (case, algo)
+        assert ctx.last_plan() in (SAMPLED, SHIFTED), (case, algo, ctx.last_plan())
+
+
 @pytest.mark.parametrize("n", [(1 << 24) + 3, 1 << 25])
 def test_sampled_plan_oversized_children(ctx, n):
     """A peak on a wide span (round 4): 60 % of the keys within +-5 120 of zero, the rest
