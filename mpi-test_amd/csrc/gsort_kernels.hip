@@ -3925,10 +3925,7 @@ hipError_t launch_est_front(const EstPlan &p, hipStream_t s) {
 // workgroup measured slower overall: profiles/r04_ab_k3_pipe_and_tiles.txt)
 constexpr int kEstTiles = 2;
 constexpr int kEstPartBlock = kPartBlock;
-#ifndef GSORT_K3A_TILES
-#define GSORT_K3A_TILES 2
-#endif
-constexpr int kEstTilesL2 = GSORT_K3A_TILES;  // K3a: a pair per 1024 threads (one tile per 512: r04_ab_k3a_one_tile_rejected)
+constexpr int kEstTilesL2 = 2;  // K3a: a pair per 1024 threads (one tile per 512: r04_ab_k3a_one_tile_rejected)
 
 hipError_t launch_est_level3(const EstPlan &p, hipStream_t s) {
     using ull = unsigned long long;
