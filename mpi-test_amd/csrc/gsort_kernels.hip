@@ -1844,13 +1844,18 @@ __device__ __forceinline__ void sort_bucket(uint32_t (&k)[ITEMS], uint32_t len, 
         __syncthreads();
     }
     const __amdgpu_buffer_rsrc_t rs = bucket_rsrc(dst, len * 4u);  // stores past len dropped
+    // the bucket is one contiguous run of out: nontemporal stores for the 9216-key classes and
+    // up (K11e class 2: 472 -> 452-462 us; the 4608-key class measured 113 -> 115 us with them,
+    // its runs' partial end lines then miss the neighbours' in L2; K3r / K3a's scattered digit
+    // runs doubled -- profiles/r04_ab_nt_stores.txt)
+    constexpr bool kNtFinal = TILE > 4608;
     static_assert(BLOCK % 32 == 0, "slot i * BLOCK + tid at at(tid) + i * at(BLOCK)");
     const uint32_t *fa = s_a + at((uint32_t)tid);
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
         const uint32_t j = (uint32_t)(i * BLOCK + tid);
         __builtin_amdgcn_raw_buffer_store_b32((fa[i * at(BLOCK)] + koff) ^ kFlip, rs, (int)(j * 4u),
-                                              0, 0);
+                                              0, kNtFinal ? 2 : 0);  // (2: nt)
     }
 }
 
