@@ -332,17 +332,23 @@ hipError_t launch_est_oversized(const EstPlan &p, uint32_t nlist, int ncu, hipSt
 // strided keys, res[1] = its sample count, res[2] = the samples (u64 each).
 hipError_t launch_est_mode(const uint32_t *in, uint64_t n, uint64_t *res, hipStream_t s);
 // K1g: child `child`'s keys (int32 input) into per-workgroup packed histograms of their low 16
-// bits (part: nblk x kH16PartWords u32; fix: kH16Shards x 65536 u64, zero on entry, as K1h),
-// every other key copied to cold + x * shard_cap (x = XCD shard, 8 of them) at a position
-// reserved on ctr[x]; ctr[8 + x] counts the cold keys below the child.  ctr (16 u64) zeroed by
-// the caller; cold holds kH16Shards * giant_shard_cap(n) keys.
-inline uint64_t giant_shard_cap(uint64_t n) {
+// bits (part: g x kH16PartWords u32; fix: kH16Shards x 65536 u64, zero on entry, as K1h), every
+// other key copied into its workgroup's segment cold + b * wg_cap; ctr[1 + b] = segment b's
+// keys, ctr[0] = the cold keys below the child.  ctr (1 + g u64) zeroed by the caller; cold
+// holds g * wg_cap keys (giant_wg_cap: g workgroups, a multiple of 8 up to kH16Blocks, each
+// taking at most wg_cap keys).
+inline uint64_t giant_wg_cap(uint64_t n, uint32_t *g) {
     const uint64_t pairs = (sweep_tiles(n) + 1) / 2;
-    return (pairs + kH16Shards - 1) / kH16Shards * 2 * kSweepTile;
+    const uint64_t g8 = (pairs + kH16Shards - 1) / kH16Shards * kH16Shards;
+    const uint64_t gg = g8 < kH16Blocks ? g8 : kH16Blocks;
+    *g = (uint32_t)gg;
+    return (pairs + gg - 1) / gg * 2 * kSweepTile;
 }
 hipError_t launch_giant_hist(const uint32_t *in, uint64_t n, uint32_t child, uint32_t *part,
-                             uint64_t *fix, uint32_t *cold, uint64_t *ctr, uint32_t *nblk,
-                             uint64_t *shard_cap, hipStream_t s);
+                             uint64_t *fix, uint32_t *cold, uint64_t *ctr, hipStream_t s);
+// K1g's segments gathered into out[0, sum ctr[1..g]) in workgroup order.
+hipError_t launch_giant_gather(const uint32_t *cold, uint64_t n, const uint64_t *ctr,
+                               uint32_t *out, hipStream_t s);
 // K12m + K12s: counts (65536 u64) of the child's low 16 bits (fix zeroed again), starts (65537
 // u64) = their exclusive scan + the cold keys below the child (output positions).
 hipError_t launch_giant_plan(const uint32_t *part, uint32_t nblk, uint64_t *fix,

@@ -105,6 +105,24 @@ __device__ __forceinline__ uint32_t agg_add_pair(uint32_t *words, uint32_t b, ui
               : old;
 }
 
+// agg_add_pair on a given word w0 (wave-uniform): the lanes on w0 add their sum with one atomic
+// from the first of them, every other lane adds its own increment.
+__device__ __forceinline__ uint32_t agg_add_pair_at(uint32_t *words, uint32_t b, uint32_t w0,
+                                                    uint32_t *spare) {
+    const uint32_t w = b >> 1;
+    const bool eq = w == w0;
+    const uint64_t m = __ballot(eq), mhi = __ballot(eq && (b & 1u));
+    const uint64_t mlo = m & ~mhi;
+    const uint32_t lr = lane_rank(m);
+    const uint32_t inc = 1u << ((b & 1u) << 4);
+    uint32_t *a = !eq ? words + w : lr == 0 ? words + w0 : spare + (threadIdx.x & 63);
+    const uint32_t v = !eq ? inc
+                     : lr == 0 ? (uint32_t)__popcll(mlo) + ((uint32_t)__popcll(mhi) << 16) : 0u;
+    const uint32_t old = atomicAdd(a, v);
+    const uint32_t o0 = m ? (uint32_t)__builtin_amdgcn_readlane((int)old, (int)__builtin_ctzll(m)) : 0u;
+    return eq ? o0 + lane_rank(mlo) + (lane_rank(mhi) << 16) : old;
+}
+
 // ---------------------------------------------------------------------------------------
 // K10: canonical splitmix64 stream; identical to oracle.c orc_gen_one.
 // ---------------------------------------------------------------------------------------
@@ -2512,7 +2530,7 @@ __global__ __launch_bounds__(1024) void k_count_expand(const T *__restrict__ rec
                     v.w = (v.w + koff) ^ kFlip;
                 }
                 if (q + 4 <= nkw && q < nkw) {
-                    *reinterpret_cast<uint4 *>(d + q) = v;  // 16-B aligned
+                    *reinterpret_cast<uint4 *>(d + q) = v;  // 16-B aligned (nontemporal: slower, r04_ab_nt_stores)
                 } else {
                     if (q < nkw) d[q] = v.x;
                     if (q + 1 < nkw) d[q + 1] = v.y;
@@ -4097,21 +4115,22 @@ __global__ __launch_bounds__(1024) void k_est_mode(const uint32_t *__restrict__ 
 
 // K1g: K1h's loop (tile pairs b, b + G, .. with the next tile prefetched) over the block; keys of
 // child c go into the workgroup's packed histogram of their LOW 16 bits (part, fix as K1h);
-// every other key is written (as the input int32) to cold + shard * shard_cap at a position
-// reserved per tile on ctr[shard] (8 XCD shards: tile pair p runs on workgroup p % G, shard
-// p % 8); ctr[8 + shard] counts the cold keys below child c.
+// every other key is written (as the input int32) into the workgroup's own segment
+// cold + b * wg_cap, each wave reserving its run there with one LDS atomic -- no barrier and no
+// device atomic per tile (round 4: the per-tile shard reservation behind two workgroup
+// barriers made K1g ~2x K1h's time); ctr[1 + b] = the segment's cold keys, ctr[0] += the cold
+// keys below child c (ctr zeroed by the caller).
 template <int BLOCK, bool FIN>
 __global__ __launch_bounds__(BLOCK) void k_giant_hist(const uint32_t *__restrict__ in, uint64_t n,
                                                       uint32_t child, uint32_t *__restrict__ part,
                                                       unsigned long long *__restrict__ fix,
                                                       uint32_t *__restrict__ cold,
-                                                      unsigned long long shard_cap,
+                                                      unsigned long long wg_cap,
                                                       unsigned long long *__restrict__ ctr) {
     constexpr int ITEMS = kSweepTile / BLOCK;
     constexpr uint32_t kWords = kBuckets16 / 2;
     __shared__ uint32_t s_h[kWords + kAggSpare];
     __shared__ uint32_t s_cnt[2];
-    __shared__ unsigned long long s_base;
     uint32_t *spare = s_h + kWords;
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     for (uint32_t i = tid; i < kWords; i += BLOCK) s_h[i] = 0;
@@ -4126,7 +4145,8 @@ __global__ __launch_bounds__(BLOCK) void k_giant_hist(const uint32_t *__restrict
     };
     const uint32_t shard = blockIdx.x % kShards;
     unsigned long long *fx = fix + (uint64_t)shard * kBuckets16;
-    uint32_t *cs = cold + (uint64_t)shard * shard_cap;
+    uint32_t *cs = cold + (uint64_t)blockIdx.x * wg_cap;
+    uint32_t below = 0;  // lane 0: the wave's cold keys below child c
     uint32_t t = tile_of(0);
     uint32_t k[ITEMS];
     if (t < ntiles) {
@@ -4149,16 +4169,31 @@ __global__ __launch_bounds__(BLOCK) void k_giant_hist(const uint32_t *__restrict
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j)
             g[j] = (uint32_t)(j * BLOCK) + tid < len && (k[j] >> 16) == child;
-        // skewed wave (its first item all child c keys on one packed word): aggregated adds
-        const uint32_t w0 = __builtin_amdgcn_readfirstlane((k[0] & 0xffffu) >> 1);
-        const bool skew = __ballot(g[0] && ((k[0] & 0xffffu) >> 1) == w0) ==
-                          __builtin_amdgcn_read_exec();
+        // a skewed wave (a frequent low half: Zipf keys put ~38 % of the child on one value, whose
+        // plain LDS adds serialize ~24-way): of the words of the first two distinct child keys of
+        // item 0, the one more lanes share is aggregated in every item when at least 8 share it
+        // (~1 % of the keys on one value in uniform children: plain adds)
+        const uint32_t wd = (k[0] & 0xffffu) >> 1;
+        const uint64_t gm = __ballot(g[0]);
+        uint32_t w0 = ~0u, best = 0;
+        if (gm) {
+            const uint32_t wa = (uint32_t)__builtin_amdgcn_readlane((int)wd, (int)__builtin_ctzll(gm));
+            const uint64_t ma = __ballot(g[0] && wd == wa), rest = gm & ~ma;
+            w0 = wa;
+            best = (uint32_t)__popcll(ma);
+            if (rest) {
+                const uint32_t wb = (uint32_t)__builtin_amdgcn_readlane((int)wd, (int)__builtin_ctzll(rest));
+                const uint32_t nb = (uint32_t)__popcll(__ballot(g[0] && wd == wb));
+                if (nb > best) { w0 = wb; best = nb; }
+            }
+        }
+        const bool skew = best >= 8;
         bool wrap = false;
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {
             const uint32_t b = k[j] & 0xffffu;
             old[j] = 0;
-            if (g[j]) old[j] = skew ? agg_add_pair(s_h, b, spare)
+            if (g[j]) old[j] = skew ? agg_add_pair_at(s_h, b, w0, spare)
                                     : atomicAdd(&s_h[b >> 1], 1u << ((b & 1u) << 4));
         }
 #pragma unroll
@@ -4170,7 +4205,7 @@ __global__ __launch_bounds__(BLOCK) void k_giant_hist(const uint32_t *__restrict
                 if (g[j] && ((old[j] >> ((k[j] & 1u) << 4)) & 0xffffu) == 0xffffu)
                     h16_wrap(fx, k[j] & 0xffffu, old[j]);
         }
-        // cold keys: per-wave counts, one reservation per tile on the shard's counter
+        // cold keys: per-wave counts, the wave's run reserved in the workgroup's segment
         uint64_t m[ITEMS];
         uint32_t wc = 0, wl = 0;
 #pragma unroll
@@ -4180,21 +4215,11 @@ __global__ __launch_bounds__(BLOCK) void k_giant_hist(const uint32_t *__restrict
             wc += (uint32_t)__popcll(m[j]);
             wl += (uint32_t)__popcll(__ballot(cj && (k[j] >> 16) < child));
         }
-        uint32_t woff = 0;
-        if (lane == 0 && wc) woff = atomicAdd(&s_cnt[0], wc);
-        if (lane == 0 && wl) atomicAdd(&s_cnt[1], wl);
-        woff = __shfl(woff, 0);
-        lds_barrier();
-        if (tid == 0) {
-            const uint32_t tc = s_cnt[0], tl = s_cnt[1];
-            s_base = tc ? atomicAdd(&ctr[shard], (unsigned long long)tc) : 0ull;
-            if (tl) atomicAdd(&ctr[kShards + shard], (unsigned long long)tl);
-            s_cnt[0] = 0;
-            s_cnt[1] = 0;
-        }
-        lds_barrier();
-        if (wc) {
-            const unsigned long long base = s_base + woff;
+        below += wl;
+        if (wc) {  // (wave-uniform)
+            uint32_t woff = 0;
+            if (lane == 0) woff = atomicAdd(&s_cnt[0], wc);
+            const unsigned long long base = (uint32_t)__shfl((int)woff, 0);
             uint32_t run = 0;
 #pragma unroll
             for (int j = 0; j < ITEMS; ++j) {
@@ -4206,9 +4231,36 @@ __global__ __launch_bounds__(BLOCK) void k_giant_hist(const uint32_t *__restrict
         for (int j = 0; j < ITEMS; ++j) k[j] = kn[j];
         t = tn;
     }
+    if (lane == 0 && below) atomicAdd(&s_cnt[1], below);
     __syncthreads();
     uint32_t *dst = part + (uint64_t)blockIdx.x * kWords;
     for (uint32_t i = tid; i < kWords; i += BLOCK) dst[i] = s_h[i];
+    if (tid == 0) {
+        ctr[1 + blockIdx.x] = s_cnt[0];
+        if (s_cnt[1]) atomicAdd(&ctr[0], (unsigned long long)s_cnt[1]);
+    }
+}
+
+// K1g's cold segments gathered: segment b (ctr[1 + b] keys at cold + b * wg_cap) to
+// out[sum of ctr[1 .. b]), one workgroup per segment.
+__global__ __launch_bounds__(1024) void k_giant_gather(const uint32_t *__restrict__ cold,
+                                                       unsigned long long wg_cap,
+                                                       const unsigned long long *__restrict__ ctr,
+                                                       uint32_t *__restrict__ out) {
+    __shared__ unsigned long long s_off;
+    const uint32_t b = blockIdx.x, tid = threadIdx.x;
+    if (tid < 64) {
+        unsigned long long x = 0;
+        for (uint32_t q = tid; q < b; q += 64) x += ctr[1 + q];
+#pragma unroll
+        for (int o = 32; o; o >>= 1) x += (unsigned long long)__shfl_xor(x, o);
+        if (tid == 0) s_off = x;
+    }
+    __syncthreads();
+    const unsigned long long cnt = ctr[1 + b];
+    const uint32_t *src = cold + (uint64_t)b * wg_cap;
+    uint32_t *dst = out + s_off;
+    for (unsigned long long i = tid; i < cnt; i += 1024) dst[i] = src[i];
 }
 
 // K12m: counts[b] = child c's keys with low 16 bits b: the b-half of word b/2 over the nblk
@@ -4261,9 +4313,7 @@ __global__ __launch_bounds__(1024) void k_giant_scan(const unsigned long long *_
         if (ww < w) run += s_w[ww];
         total += s_w[ww];
     }
-    unsigned long long lo = 0;
-#pragma unroll
-    for (uint32_t x8 = 0; x8 < kShards; ++x8) lo += ctr[kShards + x8];
+    const unsigned long long lo = ctr[0];  // cold keys below the child
     run += lo;
     for (uint32_t b = tid * 64; b < tid * 64 + 64; ++b) {
         starts[b] = run;
@@ -4358,16 +4408,23 @@ hipError_t launch_est_mode(const uint32_t *in, uint64_t n, uint64_t *res, hipStr
 }
 
 hipError_t launch_giant_hist(const uint32_t *in, uint64_t n, uint32_t child, uint32_t *part,
-                             uint64_t *fix, uint32_t *cold, uint64_t *ctr, uint32_t *nblk,
-                             uint64_t *shard_cap, hipStream_t s) {
+                             uint64_t *fix, uint32_t *cold, uint64_t *ctr, hipStream_t s) {
     if (n == 0) return hipErrorInvalidValue;
-    const uint64_t pairs = (sweep_tiles(n) + 1) / 2;
-    const uint64_t g = std::min<uint64_t>((pairs + kShards - 1) / kShards * kShards, kH16Blocks);
-    *nblk = (uint32_t)g;
-    *shard_cap = giant_shard_cap(n);
+    uint32_t g = 0;
+    const uint64_t wg_cap = giant_wg_cap(n, &g);
     using ull = unsigned long long;
-    launch_k(k_giant_hist<1024, true>, (unsigned)g, 1024, 0, s, in, n, child, part,
-             reinterpret_cast<ull *>(fix), cold, (ull)*shard_cap, reinterpret_cast<ull *>(ctr));
+    launch_k(k_giant_hist<1024, true>, g, 1024, 0, s, in, n, child, part,
+             reinterpret_cast<ull *>(fix), cold, (ull)wg_cap, reinterpret_cast<ull *>(ctr));
+    return hipGetLastError();
+}
+
+hipError_t launch_giant_gather(const uint32_t *cold, uint64_t n, const uint64_t *ctr,
+                               uint32_t *out, hipStream_t s) {
+    uint32_t g = 0;
+    const uint64_t wg_cap = giant_wg_cap(n, &g);
+    using ull = unsigned long long;
+    launch_k(k_giant_gather, g, 1024, 0, s, cold, (ull)wg_cap, reinterpret_cast<const ull *>(ctr),
+             out);
     return hipGetLastError();
 }
 

@@ -1152,7 +1152,8 @@ gsort_status msd_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *ou
 gsort_status giant_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *out,
                         uint32_t child, gsort_stats *stats, bool *ok) {
     *ok = false;
-    const uint64_t cap = (uint64_t)kH16Shards * giant_shard_cap(n);
+    uint32_t g = 0;
+    const uint64_t cap = (uint64_t)giant_wg_cap(n, &g) * g;
     ST_TRY(ensure(c, c->slot[S_TMP], cap * 4));
     ST_TRY(ensure(c, c->m_part, (size_t)kH16Blocks * kH16PartWords * 4));
     constexpr size_t kFixBytes = (size_t)kH16Shards * kBuckets16 * 8;
@@ -1161,31 +1162,28 @@ gsort_status giant_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *
     ST_TRY(ensure(c, c->m_gplan, ((size_t)2 * kBuckets16 + 1) * 8 + nchunks_max * 4));
     if (c->fix_clean != c->m_fix.p) HIP_TRY(c, hipMemsetAsync(c->m_fix.p, 0, kFixBytes, c->stream));
     c->fix_clean = nullptr;
+    // ctr: [0] cold keys below the child, [1 + b] workgroup b's cold keys (1 + g <= 257 u64,
+    // inside OFF_GIANT's 4 KiB)
+    static_assert(OFF_GIANT + (4 + 1 + kH16Blocks) * 8 <= OFF_PLAN, "giant counters");
     uint64_t *d_ctr = reinterpret_cast<uint64_t *>(c->d_small + OFF_GIANT) + 4;
     uint64_t *h_ctr = reinterpret_cast<uint64_t *>(c->h_small + OFF_GIANT) + 4;
     uint64_t *counts = static_cast<uint64_t *>(c->m_gplan.p), *starts = counts + kBuckets16;
     uint32_t *chunk_bin = reinterpret_cast<uint32_t *>(starts + kBuckets16 + 1);
     uint32_t *cold = slot_ptr<uint32_t>(c, S_TMP);
-    HIP_TRY(c, hipMemsetAsync(d_ctr, 0, 2 * kH16Shards * 8, c->stream));
-    uint32_t nblk = 0;
-    uint64_t shard_cap = 0;
+    HIP_TRY(c, hipMemsetAsync(d_ctr, 0, (1 + g) * 8, c->stream));
     hipEvent_t t = tic(c);
     HIP_TRY(c, launch_giant_hist(in, n, child, reinterpret_cast<uint32_t *>(c->m_part.p),
-                                 reinterpret_cast<uint64_t *>(c->m_fix.p), cold, d_ctr, &nblk,
-                                 &shard_cap, c->stream));
-    HIP_TRY(c, launch_giant_plan(reinterpret_cast<uint32_t *>(c->m_part.p), nblk,
+                                 reinterpret_cast<uint64_t *>(c->m_fix.p), cold, d_ctr, c->stream));
+    HIP_TRY(c, launch_giant_plan(reinterpret_cast<uint32_t *>(c->m_part.p), g,
                                  reinterpret_cast<uint64_t *>(c->m_fix.p), d_ctr, counts, starts,
                                  c->stream));
     c->fix_clean = c->m_fix.p;  // K12m left it zeroed
     toc(c, PH_COUNT, t);
-    HIP_TRY(c, hipMemcpyAsync(h_ctr, d_ctr, 2 * kH16Shards * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(h_ctr, d_ctr, (1 + g) * 8, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
-    uint64_t shard_cold[kH16Shards], n_cold = 0, n_lo = 0;
-    for (uint32_t x = 0; x < kH16Shards; ++x) {
-        shard_cold[x] = h_ctr[x];
-        n_cold += h_ctr[x];
-        n_lo += h_ctr[kH16Shards + x];
-    }
+    uint64_t n_cold = 0;
+    const uint64_t n_lo = h_ctr[0];
+    for (uint32_t b = 0; b < g; ++b) n_cold += h_ctr[1 + b];
     const uint64_t n_child = n - n_cold;
     if (c->plan_trace)
         fprintf(stderr, "gsort plan: giant child %x n %llu cold %llu below %llu\n", child,
@@ -1195,18 +1193,12 @@ gsort_status giant_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *
     // the sample misjudged: not worth it.  2 n_child >= n also gives n_cold <= n_child, which
     // the cold-key sort below relies on (odd n with n_child = (n - 1) / 2 would overlap)
     if (2 * n_child < n) return GSORT_OK;
-    // the cold keys: gathered from their shard regions into out[0, n_cold), sorted into
+    // the cold keys: gathered from the workgroups' segments into out[0, n_cold), sorted into
     // out[n_child, n) (disjoint: n_cold <= n_child) with S_TMP as scratch, and their part below
     // the child moved to the front (n_lo <= n_cold <= n_child: no overlap either); the child's
     // keys then fill [n_lo, n_lo + n_child)
     if (n_cold) {
-        uint64_t at = 0;
-        for (uint32_t x = 0; x < kH16Shards; ++x) {
-            if (shard_cold[x])
-                HIP_TRY(c, hipMemcpyAsync(out + at, cold + (uint64_t)x * shard_cap,
-                                          shard_cold[x] * 4, hipMemcpyDeviceToDevice, c->stream));
-            at += shard_cold[x];
-        }
+        HIP_TRY(c, launch_giant_gather(cold, n, d_ctr, out, c->stream));
         gsort_stats cst;
         memset(&cst, 0, sizeof(cst));
         const int lp = c->last_plan;
