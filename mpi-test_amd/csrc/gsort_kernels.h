@@ -76,7 +76,7 @@ hipError_t launch_bucket_bounds(const int32_t *sorted, uint64_t n, const int32_t
 // keys): without it each went through a level-1 partition into ~64-key buckets (3.7x slower
 // sort, tools/run_length_probe.py).
 constexpr int kLocalClasses = 4;
-constexpr uint64_t kLocalCap[kLocalClasses + 1] = {0, 256 * 18, 512 * 18, 512 * 32, 1024 * 32};
+constexpr uint64_t kLocalCap[kLocalClasses + 1] = {0, 256 * 18, 512 * 18, 512 * 33, 1024 * 32};
 constexpr uint64_t kLocalMax = kLocalCap[kLocalClasses];
 inline int local_class(uint64_t len) {
     for (int k = 1; k <= kLocalClasses; ++k)

@@ -121,7 +121,7 @@ def _msd_cases(orc):
     rng = lambda s: np.random.default_rng(s)  # noqa: E731
     return {
         # one bucket / first level only
-        # K11 class caps (kLocalCap: 2304, 4608, 6144, 8192, 8704, 9216, 16384), one past each
+        # K11 class caps (kLocalCap: 4608, 9216, 16896, 32768; and older caps), one past each
         "n_cap2304": lambda: orc.gen(orc.UNIFORM, 15, 2304),
         "n_cap2304_plus1": lambda: orc.gen(orc.UNIFORM, 16, 2305),
         "n_cap6144": lambda: orc.gen(orc.UNIFORM, 17, 6144),
@@ -134,8 +134,10 @@ def _msd_cases(orc):
         "n_cap1_plus1": lambda: orc.gen(orc.UNIFORM, 12, 4609),
         "n_cap2": lambda: orc.gen(orc.UNIFORM, 13, 9216),
         "n_cap2_plus1": lambda: orc.gen(orc.UNIFORM, 14, 9217),
-        "n_cap3": lambda: orc.gen(orc.UNIFORM, 1, 16384),
-        "n_cap3_plus1": lambda: orc.gen(orc.UNIFORM, 2, 16385),
+        "n_16384": lambda: orc.gen(orc.UNIFORM, 1, 16384),
+        "n_16385": lambda: orc.gen(orc.UNIFORM, 2, 16385),
+        "n_cap3": lambda: orc.gen(orc.UNIFORM, 25, 16896),
+        "n_cap3_plus1": lambda: orc.gen(orc.UNIFORM, 26, 16897),
         "n_localmax": lambda: orc.gen(orc.UNIFORM, 23, 32768),
         "n_localmax_plus1": lambda: orc.gen(orc.UNIFORM, 24, 32769),
         # level-2 children straddling 16 384 keys (class 3 / class 4 of K11)
