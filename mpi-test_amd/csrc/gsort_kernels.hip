@@ -3159,6 +3159,11 @@ __global__ __launch_bounds__(256) void k_est_tiles(const uint32_t *__restrict__ 
         desc[t] = {v0, len, sb | kStraddle};
 }
 
+#ifndef GSORT_EST_CX
+#define GSORT_EST_CX 5
+#endif
+constexpr int kEstCx = GSORT_EST_CX;  // A/B: sampled children of class >= kEstCx to K18c (list 0)
+
 // K12g: block s, thread e.  Exact sizes: child (s, e) holds cur2 - init2 keys, bucket s' holds
 // sum_x (cur3 - init3) keys, so the child's output offset is the scan of the bucket totals
 // before s plus the scan of its siblings before e.  Non-empty children go to the K11e class
@@ -3198,7 +3203,7 @@ __global__ __launch_bounds__(kRadix) void k_est_classify(
         int which = -1;  // K11e class, or 0: past kLocalMax, K18c
         if (len > 0 && !over) {
             which = 0;
-            for (int k = 1; k < NL; ++k)
+            for (int k = 1; k < NL && k < kEstCx; ++k)
                 if (len <= kLocalCap[k]) { which = k; break; }
         }
         unsigned int idx = 0;
@@ -3303,12 +3308,15 @@ __global__ __launch_bounds__(BLOCK) void k_local_sort_e(const uint16_t *__restri
 
 // class geometries (block x items): class 3 as 1024 x 16 measured slower than 512 x 32 (local
 // 30-bit keys K11e 0.80 -> 0.90 ms, receive 16 384-key buckets 0.73 -> 0.87 ms per 2^28 keys,
-// round 4); class 2 as 256 x 36 needs 133 VGPRs (12 waves per CU)
-constexpr int kC3Block = 512, kC3Items = 32;
+// round 4); class 2 as 256 x 36 needs 133 VGPRs (12 waves per CU).  Class 3 holds 512 x 33 =
+// 16 896 keys (round 4): the P = 2 weak-scaling receive buckets (16 384 +- 128 keys) then all
+// fit it instead of half of them going to K18c's 65 536 counters; 2 workgroups still fit a CU
+// (76 KiB of LDS each)
+constexpr int kC3Block = 512, kC3Items = 33;
 constexpr int kC2Block = 512, kC2Items = 18;
 
 constexpr int cls_of(int block, int items) {
-    return block * items == 16384 ? 3 : block * items == 9216 ? 2 : block * items == 4608 ? 1 : 4;
+    return block * items == 16896 ? 3 : block * items == 9216 ? 2 : block * items == 4608 ? 1 : 4;
 }
 
 unsigned grid_for(uint64_t n, unsigned block, unsigned cap) {
