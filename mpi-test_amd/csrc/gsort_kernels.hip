@@ -3159,10 +3159,10 @@ __global__ __launch_bounds__(256) void k_est_tiles(const uint32_t *__restrict__ 
         desc[t] = {v0, len, sb | kStraddle};
 }
 
-#ifndef GSORT_EST_CX
-#define GSORT_EST_CX 5
-#endif
-constexpr int kEstCx = GSORT_EST_CX;  // A/B: sampled children of class >= kEstCx to K18c (list 0)
+// Sampled children past class 3 (16 897 .. 32 768 keys, e.g. 29-bit keys at 2^28) go to K18c
+// (list 0) with the oversized ones, as the receive side's class 4 does (GSORT_RECV_CX): 2^28
+// 29-bit keys K11 0.67 -> 0.56 ms (profiles/r04_ab_est_class4_k18c.txt)
+constexpr int kEstCx = 4;
 
 // K12g: block s, thread e.  Exact sizes: child (s, e) holds cur2 - init2 keys, bucket s' holds
 // sum_x (cur3 - init3) keys, so the child's output offset is the scan of the bucket totals
