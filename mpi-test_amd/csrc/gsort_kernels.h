@@ -78,6 +78,11 @@ hipError_t launch_bucket_bounds(const int32_t *sorted, uint64_t n, const int32_t
 constexpr int kLocalClasses = 4;
 constexpr uint64_t kLocalCap[kLocalClasses + 1] = {0, 256 * 18, 512 * 18, 512 * 33, 1024 * 32};
 constexpr uint64_t kLocalMax = kLocalCap[kLocalClasses];
+// Sampled-plan children past class 3 (16 897 .. 32 768 keys, e.g. 29-bit keys at 2^28) go to
+// K18c (K12g's list 0) with the oversized ones, as the receive side's class 4 does
+// (GSORT_RECV_CX): 2^28 29-bit keys K11 0.67 -> 0.56 ms (profiles/r04_ab_est_class4_k18c.txt).
+// K11e runs classes 1 .. kEstCx - 1.
+constexpr int kEstCx = 4;
 inline int local_class(uint64_t len) {
     for (int k = 1; k <= kLocalClasses; ++k)
         if (len <= kLocalCap[k]) return k;

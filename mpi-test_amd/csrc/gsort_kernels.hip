@@ -3159,10 +3159,6 @@ __global__ __launch_bounds__(256) void k_est_tiles(const uint32_t *__restrict__ 
         desc[t] = {v0, len, sb | kStraddle};
 }
 
-// Sampled children past class 3 (16 897 .. 32 768 keys, e.g. 29-bit keys at 2^28) go to K18c
-// (list 0) with the oversized ones, as the receive side's class 4 does (GSORT_RECV_CX): 2^28
-// 29-bit keys K11 0.67 -> 0.56 ms (profiles/r04_ab_est_class4_k18c.txt)
-constexpr int kEstCx = 4;
 
 // K12g: block s, thread e.  Exact sizes: child (s, e) holds cur2 - init2 keys, bucket s' holds
 // sum_x (cur3 - init3) keys, so the child's output offset is the scan of the bucket totals
@@ -4022,7 +4018,7 @@ hipError_t launch_local_sort_e(const EstPlan &p, int cls, uint32_t first, uint32
                                bool publish, hipStream_t s) {
     using ull = unsigned long long;
     if (nlist == 0) return hipSuccess;
-    if (cls < 1 || cls > kLocalClasses) return hipErrorInvalidValue;
+    if (cls < 1 || cls >= kEstCx) return hipErrorInvalidValue;
     const ull *l = reinterpret_cast<const ull *>(p.wl.list[cls]);
     const ull *call = reinterpret_cast<const ull *>(p.wl.ctr), *ctr = call + 3 * cls;
     const uint16_t *y = p.y;
@@ -4044,11 +4040,12 @@ hipError_t launch_local_sort_e(const EstPlan &p, int cls, uint32_t first, uint32
             launch_k(k_local_sort_e<B, I, false>, nlist, B, 0, s, y, p.out, l, ctr, first, nd, \
                      mail, call, ef, seq, ko);                                                 \
     } while (0)
+    static_assert(kEstCx == 4, "K11e classes 1..3");
     switch (cls) {
         case 1: GSORT_K11E(256, 18); break;
         case 2: GSORT_K11E(kC2Block, kC2Items); break;
         case 3: GSORT_K11E(kC3Block, kC3Items); break;
-        default: GSORT_K11E(1024, 32); break;
+        default: return hipErrorInvalidValue;  // class 4 children go to K18c (kEstCx)
     }
 #undef GSORT_K11E
     return hipGetLastError();

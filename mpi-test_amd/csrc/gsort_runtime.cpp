@@ -1105,7 +1105,9 @@ gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
     // sampled children: at least its entries, usually exactly), so no host round trip sits
     // between K12g and the largest K11e launch; the other classes follow once the counts are in
     const uint32_t sampled = (uint32_t)std::min<uint64_t>((uint64_t)mail[4], (uint64_t)kBuckets16);
-    const int kspec = sampled ? std::max(local_class(n / sampled), 1) : 0;
+    // (class 4 children go to K18c: the speculative grid then is class 3's, whose blocks past
+    // its count return at once after block 0 has published the counters)
+    const int kspec = sampled ? std::min(std::max(local_class(n / sampled), 1), kEstCx - 1) : 0;
     t = tic(c);
     if (kspec) HIP_TRY(c, launch_local_sort_e(p, kspec, 0, sampled, true, c->stream));
     else HIP_TRY(c, launch_est_publish(p, c->stream));
@@ -1122,7 +1124,7 @@ gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
         return set_err(c, GSORT_EINVAL, "sampled plan: K11e lists hold " + std::to_string(keys) +
                                             " keys in " + std::to_string(ent) + " entries, want " +
                                             std::to_string(n) + " keys");
-    for (int k = 1; k <= kLocalClasses; ++k) {
+    for (int k = 1; k < kEstCx; ++k) {
         const uint32_t done = k == kspec ? sampled : 0u, cnt = (uint32_t)h[3 * k];
         if (cnt > done) HIP_TRY(c, launch_local_sort_e(p, k, done, cnt - done, false, c->stream));
     }

@@ -160,9 +160,10 @@ def test_sampled_plan_repeated_sorts_reuse_scratch(ctx, orc):
 @pytest.mark.parametrize("bits,plan", [(27, SAMPLED), (26, SAMPLED), (25, SAMPLED)])
 def test_sampled_plan_child_classes(ctx, bits, plan):
     """2^24 keys below 2^bits: 16-bit children of 2^(bits-8) keys -- K11e classes 2 and 3
-    (8 192 / 16 384 keys) on the sampled plan; 32 768-key children (bits = 25) straddle
-    kLocalMax: those past it go to K12g's list 0 and K18c's counting sort (round 4; before
-    it the block was retried with its digits below the 7 leading bits every key shares)."""
+    (8 192 / 16 384 keys) on the sampled plan; 32 768-key children (bits = 25) are past class
+    3, so K12g lists them (and those past kLocalMax) for K18c's counting sort from Y (round 4;
+    before it the block was retried with its digits below the 7 leading bits every key
+    shares)."""
     rng = np.random.default_rng(bits)
     keys = rng.integers(0, 1 << bits, 1 << 24, dtype=np.int64).astype(np.int32)
     got, _ = _sort(ctx, keys)
