@@ -81,7 +81,8 @@ constexpr uint64_t kLocalMax = kLocalCap[kLocalClasses];
 // Sampled-plan children past class 3 (16 897 .. 32 768 keys, e.g. 29-bit keys at 2^28) go to
 // K18c (K12g's list 0) with the oversized ones, as the receive side's class 4 does
 // (GSORT_RECV_CX): 2^28 29-bit keys K11 0.67 -> 0.56 ms (profiles/r04_ab_est_class4_k18c.txt).
-// K11e runs classes 1 .. kEstCx - 1.
+// Not on a plan shifted by 8 or more bits (sb >= 8): K11e then sorts one digit in one pass,
+// where K18c still walks 65 536 counters per child (Gaussian 2^28: K11 0.52 -> 1.05 ms).
 constexpr int kEstCx = 4;
 inline int local_class(uint64_t len) {
     for (int k = 1; k <= kLocalClasses; ++k)

@@ -3199,7 +3199,7 @@ __global__ __launch_bounds__(kRadix) void k_est_classify(
         int which = -1;  // K11e class, or 0: past kLocalMax, K18c
         if (len > 0 && !over) {
             which = 0;
-            for (int k = 1; k < NL && k < kEstCx; ++k)
+            for (int k = 1; k < NL && (k < kEstCx || sb >= 8); ++k)  // (kEstCx, gsort_kernels.h)
                 if (len <= kLocalCap[k]) { which = k; break; }
         }
         unsigned int idx = 0;
@@ -4018,7 +4018,7 @@ hipError_t launch_local_sort_e(const EstPlan &p, int cls, uint32_t first, uint32
                                bool publish, hipStream_t s) {
     using ull = unsigned long long;
     if (nlist == 0) return hipSuccess;
-    if (cls < 1 || cls >= kEstCx) return hipErrorInvalidValue;
+    if (cls < 1 || cls > kLocalClasses) return hipErrorInvalidValue;
     const ull *l = reinterpret_cast<const ull *>(p.wl.list[cls]);
     const ull *call = reinterpret_cast<const ull *>(p.wl.ctr), *ctr = call + 3 * cls;
     const uint16_t *y = p.y;
@@ -4040,12 +4040,11 @@ hipError_t launch_local_sort_e(const EstPlan &p, int cls, uint32_t first, uint32
             launch_k(k_local_sort_e<B, I, false>, nlist, B, 0, s, y, p.out, l, ctr, first, nd, \
                      mail, call, ef, seq, ko);                                                 \
     } while (0)
-    static_assert(kEstCx == 4, "K11e classes 1..3");
     switch (cls) {
         case 1: GSORT_K11E(256, 18); break;
         case 2: GSORT_K11E(kC2Block, kC2Items); break;
         case 3: GSORT_K11E(kC3Block, kC3Items); break;
-        default: return hipErrorInvalidValue;  // class 4 children go to K18c (kEstCx)
+        default: GSORT_K11E(1024, 32); break;  // (shifted plans only: kEstCx)
     }
 #undef GSORT_K11E
     return hipGetLastError();

@@ -1105,9 +1105,11 @@ gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
     // sampled children: at least its entries, usually exactly), so no host round trip sits
     // between K12g and the largest K11e launch; the other classes follow once the counts are in
     const uint32_t sampled = (uint32_t)std::min<uint64_t>((uint64_t)mail[4], (uint64_t)kBuckets16);
-    // (class 4 children go to K18c: the speculative grid then is class 3's, whose blocks past
-    // its count return at once after block 0 has published the counters)
-    const int kspec = sampled ? std::min(std::max(local_class(n / sampled), 1), kEstCx - 1) : 0;
+    // (class 4 children go to K18c unless the plan is shifted by 8+ bits: the speculative grid
+    // then is class 3's, whose blocks past its count return at once after block 0 has
+    // published the counters)
+    const int kmax = sb >= 8 ? kLocalClasses : kEstCx - 1;
+    const int kspec = sampled ? std::min(std::max(local_class(n / sampled), 1), kmax) : 0;
     t = tic(c);
     if (kspec) HIP_TRY(c, launch_local_sort_e(p, kspec, 0, sampled, true, c->stream));
     else HIP_TRY(c, launch_est_publish(p, c->stream));
@@ -1124,7 +1126,7 @@ gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
         return set_err(c, GSORT_EINVAL, "sampled plan: K11e lists hold " + std::to_string(keys) +
                                             " keys in " + std::to_string(ent) + " entries, want " +
                                             std::to_string(n) + " keys");
-    for (int k = 1; k < kEstCx; ++k) {
+    for (int k = 1; k <= kmax; ++k) {
         const uint32_t done = k == kspec ? sampled : 0u, cnt = (uint32_t)h[3 * k];
         if (cnt > done) HIP_TRY(c, launch_local_sort_e(p, k, done, cnt - done, false, c->stream));
     }
@@ -2591,6 +2593,31 @@ gsort_status gsort_set_ref_compat(gsort_ctx *c, int radix_p) {
     return GSORT_OK;
 }
 
+// The end of a call: the stream drained.  GSORT_SPIN_DONE (A/B build): the stream writes a
+// sequence word into the pinned mailbox and the host spins on it before the (then immediate)
+// stream synchronisation -- a long final wait otherwise may sleep and wake late.
+#ifndef GSORT_SPIN_DONE
+#define GSORT_SPIN_DONE 0
+#endif
+constexpr size_t kDoneWord = 440;
+static_assert(kDoneWord >= kEstMailWord + kEstMailWords && (kDoneWord + 1) * 8 <= kMailBytes,
+              "done word");
+gsort_status finish_call(gsort_ctx *c) {
+    if (GSORT_SPIN_DONE) {
+        const uint64_t seq = ++c->mail_seq;
+        HIP_TRY(c, hipStreamWriteValue64(c->stream, c->d_mail + kDoneWord, seq, 0));
+        volatile uint64_t *w = c->h_mail + kDoneWord;
+        for (uint64_t spin = 0; *w != seq; ++spin) {
+            if ((spin & 1023) == 1023) {
+                const hipError_t q = hipStreamQuery(c->stream);
+                if (q != hipErrorNotReady && *w != seq) break;  // (the sync below reports it)
+            }
+        }
+    }
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return GSORT_OK;
+}
+
 gsort_status gsort_radix(gsort_ctx *c, const int32_t *d_keys, size_t n_local, int32_t **d_out,
                          size_t *n_out, gsort_stats *stats) {
     ST_TRY(check_ctx(c));
@@ -2620,7 +2647,7 @@ gsort_status gsort_radix(gsort_ctx *c, const int32_t *d_keys, size_t n_local, in
     if (st != GSORT_OK) return st;
     if (c->comm) toc_rec(c, PH_TOTAL, t0);
     else toc(c, PH_TOTAL, t0);
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    ST_TRY(finish_call(c));
     *n_out = nout;
     if (stats) { stats->keys_local_in = n_local; stats->keys_local_out = nout; }
     timing_finish(c, stats);
