@@ -2593,31 +2593,6 @@ gsort_status gsort_set_ref_compat(gsort_ctx *c, int radix_p) {
     return GSORT_OK;
 }
 
-// The end of a call: the stream drained.  GSORT_SPIN_DONE (A/B build): the stream writes a
-// sequence word into the pinned mailbox and the host spins on it before the (then immediate)
-// stream synchronisation -- a long final wait otherwise may sleep and wake late.
-#ifndef GSORT_SPIN_DONE
-#define GSORT_SPIN_DONE 0
-#endif
-constexpr size_t kDoneWord = 440;
-static_assert(kDoneWord >= kEstMailWord + kEstMailWords && (kDoneWord + 1) * 8 <= kMailBytes,
-              "done word");
-gsort_status finish_call(gsort_ctx *c) {
-    if (GSORT_SPIN_DONE) {
-        const uint64_t seq = ++c->mail_seq;
-        HIP_TRY(c, hipStreamWriteValue64(c->stream, c->d_mail + kDoneWord, seq, 0));
-        volatile uint64_t *w = c->h_mail + kDoneWord;
-        for (uint64_t spin = 0; *w != seq; ++spin) {
-            if ((spin & 1023) == 1023) {
-                const hipError_t q = hipStreamQuery(c->stream);
-                if (q != hipErrorNotReady && *w != seq) break;  // (the sync below reports it)
-            }
-        }
-    }
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
-    return GSORT_OK;
-}
-
 gsort_status gsort_radix(gsort_ctx *c, const int32_t *d_keys, size_t n_local, int32_t **d_out,
                          size_t *n_out, gsort_stats *stats) {
     ST_TRY(check_ctx(c));
@@ -2647,7 +2622,7 @@ gsort_status gsort_radix(gsort_ctx *c, const int32_t *d_keys, size_t n_local, in
     if (st != GSORT_OK) return st;
     if (c->comm) toc_rec(c, PH_TOTAL, t0);
     else toc(c, PH_TOTAL, t0);
-    ST_TRY(finish_call(c));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
     *n_out = nout;
     if (stats) { stats->keys_local_in = n_local; stats->keys_local_out = nout; }
     timing_finish(c, stats);
