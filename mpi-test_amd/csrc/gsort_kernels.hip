@@ -2839,7 +2839,7 @@ __device__ __forceinline__ uint32_t est_seg_off(uint32_t j) {  // sample offset 
 // K1e: thread tid samples key tid % 8 of segment tid / 8; workgroup b takes the 512-key
 // blocks j = b * 128 + seg, + kEstWG * 128, ... (so every child's samples spread over all
 // workgroups), sixteen loads in flight per thread.  part8[b][.] = the 65536 u8 child counters
-// (packed 4 per word), part3[b][x * 256 + d] = samples of level-3 bucket d in shard x (tile
+// (packed 4 per word), part3[(d * kEstWG + b) * 8 + x] = samples of level-3 bucket d in shard x (tile
 // pair j / 32, shard pair % 8, as K3r deals them), msamp[b] = samples | wrap << 31,
 // msamp[kEstWG + b] = the key bits that differ from in[0] among its samples, msamp[2 / 3 *
 // kEstWG + b] = their min / max.  koff: keys are taken as ordered u32 minus koff (the
@@ -2917,8 +2917,12 @@ __global__ __launch_bounds__(1024) void k_est_sample(const uint32_t *__restrict_
     __syncthreads();
     uint32_t *dst = part8 + (uint64_t)blockIdx.x * kEstPartWords;
     for (uint32_t i = tid; i < kEstPartWords; i += 1024) dst[i] = s_h[i];
-    uint32_t *d3 = part3 + (uint64_t)blockIdx.x * kEstPart3;
-    for (uint32_t i = tid; i < kEstPart3; i += 1024) d3[i] = s_3[i];
+    // part3 bucket-major, [d][b][x]: K12e's block d then reads its 2048 words contiguously (a
+    // workgroup-major layout made that a 4-B load per 64-B line: 34 MB fetched for 19 MB)
+    for (uint32_t i = tid; i < kEstPart3; i += 1024) {
+        const uint32_t d = i >> 3, x = i & (kShards - 1);
+        part3[((uint64_t)d * kEstWG + blockIdx.x) * kShards + x] = s_3[x * kRadix + d];
+    }
     if (tid == 0) {
         msamp[blockIdx.x] = s_m;
         msamp[kEstWG + blockIdx.x] = s_vary;
@@ -3012,7 +3016,7 @@ __global__ __launch_bounds__(kRadix) void k_est_plan(
         uint32_t pv3[NB3], c3 = 0;
 #pragma unroll
         for (uint32_t b = 0; b < NB3; ++b)
-            pv3[b] = part3[(uint64_t)(b0 + b * (kRadix / 8)) * kEstPart3 + x * kRadix + s];
+            pv3[b] = part3[((uint64_t)s * kEstWG + b0 + b * (kRadix / 8)) * kShards + x];
 #pragma unroll
         for (uint32_t b = 0; b < NB3; ++b) c3 += pv3[b];
         s_3[b0][x] = c3;
