@@ -795,14 +795,31 @@ gsort_status msd_levels(gsort_ctx *c, int L, uint32_t *cur, uint32_t *out, uint3
 }
 
 
+// Mailbox waits poll the stream for errors (a stream that went idle without the word) only
+// every kQueryUs of waiting: each hipStreamQuery puts a marker in the stream, and one every
+// 1024 spins (~1 us) during the sampled plan's eligibility wait queued dozens of them between
+// K12g and K11e -- a ~6 us bubble (profiles/r04_ab_stream_query_rate.txt: 1.376 -> 1.369 ms).
+constexpr int kQueryUs = 200;
+struct QueryTimer {  // (every 1024 spins the waiting thread yields; the query only when due)
+    std::chrono::steady_clock::time_point next = std::chrono::steady_clock::now() +
+                                                 std::chrono::microseconds(kQueryUs);
+    bool due() {
+        const auto now = std::chrono::steady_clock::now();
+        if (now < next) return false;
+        next = now + std::chrono::microseconds(kQueryUs);
+        return true;
+    }
+};
+
 // Wait for K12p's sequence number seq in the mailbox (the counters behind it are then
 // visible).  A stream error, or the stream going idle without the flag, returns GSORT_EHIP
 // instead of spinning forever.
 gsort_status wait_mail(gsort_ctx *c, uint64_t seq) {
     volatile uint64_t *flag = c->h_mail;
+    QueryTimer qt;
     for (uint64_t spin = 0; *flag != seq; ++spin) {
         if ((spin & 1023) == 1023) {
-            const hipError_t q = hipStreamQuery(c->stream);
+            const hipError_t q = qt.due() ? hipStreamQuery(c->stream) : hipErrorNotReady;
             if (q != hipErrorNotReady && *flag != seq) {
                 if (q != hipSuccess)
                     return set_err(c, GSORT_EHIP, std::string("K12p counters: ") +
@@ -1056,9 +1073,10 @@ gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
     volatile uint64_t *mail = c->h_mail + kEstMailWord;
     // poll a sequence word of the mailbox; a stream that goes idle without it is an error
     auto wait_word = [&](size_t w, uint64_t seq, const char *what) -> gsort_status {
+        QueryTimer qt;
         for (uint64_t spin = 0; mail[w] != seq; ++spin) {
             if ((spin & 1023) == 1023) {
-                const hipError_t q = hipStreamQuery(c->stream);
+                const hipError_t q = qt.due() ? hipStreamQuery(c->stream) : hipErrorNotReady;
                 if (q != hipErrorNotReady && mail[w] != seq)
                     return set_err(c, GSORT_EHIP, std::string("sampled plan: ") + what + ": " +
                                                       (q == hipSuccess ? "stream idle without it"
