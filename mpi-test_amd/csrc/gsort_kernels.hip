@@ -1341,12 +1341,22 @@ __global__ __launch_bounds__(kRadix) void k_plan16_count(const uint32_t *__restr
     // par, par + 2, par + 4, par + 6 (b, b + 2, b + 4, b + 6 of every group of eight)
     const uint32_t par = e >> 7, word = s * (kRadix / 2) + (e & 127u);
     uint32_t lo[4] = {0, 0, 0, 0}, hi[4] = {0, 0, 0, 0};
-    for (uint32_t b = par; b < nblk; b += kShards) {
-        uint32_t v[4];
+    // U groups of eight partials per round, all 4 U loads in flight (a round per group left
+    // nblk / 8 dependent HBM round trips: K12a 41 us at 256 partials)
+    constexpr uint32_t U = 8;
+    for (uint32_t b0 = par; b0 < nblk; b0 += kShards * U) {
+        uint32_t v[U][4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = part[(uint64_t)(b + 2 * j) * kWords + word];
+        for (uint32_t u = 0; u < U; ++u) {
+            const uint32_t b = b0 + u * kShards;  // (b < nblk: b + 6 < nblk too, nblk % 8 == 0)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) { lo[j] += v[j] & 0xffffu; hi[j] += v[j] >> 16; }
+            for (int j = 0; j < 4; ++j)
+                v[u][j] = b < nblk ? part[(uint64_t)(b + 2 * j) * kWords + word] : 0u;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) { lo[j] += v[u][j] & 0xffffu; hi[j] += v[u][j] >> 16; }
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
