@@ -356,7 +356,8 @@ hipError_t launch_giant_hist(const uint32_t *in, uint64_t n, uint32_t child, uin
 hipError_t launch_giant_gather(const uint32_t *cold, uint64_t n, const uint64_t *ctr,
                                uint32_t *out, hipStream_t s);
 // K12m + K12s: counts (65536 u64) of the child's low 16 bits (fix zeroed again), starts (65537
-// u64) = their exclusive scan + the cold keys below the child (output positions).
+// u64) = their exclusive scan + the cold keys below the child (output positions); the 64 u64
+// after starts are K12s's scratch.
 hipError_t launch_giant_plan(const uint32_t *part, uint32_t nblk, uint64_t *fix,
                              const uint64_t *ctr, uint64_t *counts, uint64_t *starts,
                              hipStream_t s);

@@ -2900,10 +2900,34 @@ __global__ __launch_bounds__(1024) void k_est_sample(const uint32_t *__restrict_
             lo = min(lo, k);
             hi = max(hi, k);
             const uint32_t b = (k >> (16 - sb)) & 0xffffu, sh = (b & 3u) << 3;
-            const uint32_t old = atomicAdd(&s_h[b >> 2], 1u << sh);
-            wrap |= ((old >> sh) & 255u) == 255u;
             constexpr uint32_t kPairBlocks = 2 * kSweepTile / kEstBlockKeys;
-            atomicAdd(&s_3[((jj[u] / kPairBlocks) % kShards) * kRadix + ((k >> (24 - sb)) & 255u)], 1u);
+            const uint32_t i3 = ((jj[u] / kPairBlocks) % kShards) * kRadix + ((k >> (24 - sb)) & 255u);
+            // a wave whose samples all hit one counter word (8- / 16-bit keys, one frequent
+            // value: same-address LDS adds serialize) adds them with one atomic from its first
+            // lane; a byte wrapped when its old value plus its lanes passed 255
+            const uint64_t ex = __builtin_amdgcn_read_exec();
+            const bool first = lane_rank(ex) == 0;
+            const uint32_t w0 = __builtin_amdgcn_readfirstlane(b >> 2);
+            if (__ballot((b >> 2) == w0) == ex) {
+                uint32_t inc = 0;
+#pragma unroll
+                for (uint32_t q = 0; q < 4; ++q)
+                    inc |= (uint32_t)__popcll(__ballot((b & 3u) == q)) << (8 * q);
+                uint32_t old = 0;
+                if (first) old = atomicAdd(&s_h[w0], inc);
+#pragma unroll
+                for (uint32_t q = 0; q < 4; ++q)
+                    wrap |= ((old >> (8 * q)) & 255u) + ((inc >> (8 * q)) & 255u) > 255u;
+            } else {
+                const uint32_t old = atomicAdd(&s_h[b >> 2], 1u << sh);
+                wrap |= ((old >> sh) & 255u) == 255u;
+            }
+            const uint32_t i30 = __builtin_amdgcn_readfirstlane(i3);
+            if (__ballot(i3 == i30) == ex) {
+                if (first) atomicAdd(&s_3[i30], (uint32_t)__popcll(ex));
+            } else {
+                atomicAdd(&s_3[i3], 1u);
+            }
             ++cnt;
         }
     }
@@ -4309,35 +4333,51 @@ __global__ __launch_bounds__(256) void k_giant_count(const uint32_t *__restrict_
     counts[2 * w + 1] = hi;
 }
 
-// K12s: starts[b] = (cold keys below the child: sum of ctr[8 .. 16)) + the exclusive scan of
-// counts; starts[65536] = the child's end.  One workgroup, 64 bins per thread.
-__global__ __launch_bounds__(1024) void k_giant_scan(const unsigned long long *__restrict__ counts,
-                                                     const unsigned long long *__restrict__ ctr,
-                                                     unsigned long long *__restrict__ starts) {
+// K12s: starts[b] = ctr[0] (the cold keys below the child) + the exclusive scan of counts,
+// starts[65536] = the end; two passes of 64 workgroups over coalesced 1024-bin blocks (one
+// 1024-thread workgroup walking 64 bins per thread took 49 us): K12s-a sums each block into
+// part[64], K12s-b offsets its block by the sums before it.
+__global__ __launch_bounds__(1024) void k_giant_scan_a(const unsigned long long *__restrict__ counts,
+                                                       unsigned long long *__restrict__ part) {
     __shared__ unsigned long long s_w[16];
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    unsigned long long sum = 0;
-    for (uint32_t b = tid * 64; b < tid * 64 + 64; ++b) sum += counts[b];
-    unsigned long long x = sum;
+    unsigned long long x = counts[blockIdx.x * 1024 + tid];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += (unsigned long long)__shfl_xor(x, o);
+    if (lane == 0) s_w[w] = x;
+    __syncthreads();
+    if (tid == 0) {
+        unsigned long long t = 0;
+        for (int i = 0; i < 16; ++i) t += s_w[i];
+        part[blockIdx.x] = t;
+    }
+}
+__global__ __launch_bounds__(1024) void k_giant_scan_b(const unsigned long long *__restrict__ counts,
+                                                       const unsigned long long *__restrict__ part,
+                                                       const unsigned long long *__restrict__ ctr,
+                                                       unsigned long long *__restrict__ starts) {
+    __shared__ unsigned long long s_w[16];
+    __shared__ unsigned long long s_pre;
+    const uint32_t b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (tid < 64) {
+        unsigned long long v = tid < b ? part[tid] : 0ull;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v += (unsigned long long)__shfl_xor(v, o);
+        if (tid == 0) s_pre = v + ctr[0];
+    }
+    const unsigned long long c = counts[b * 1024 + tid];
+    unsigned long long x = c;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-        const unsigned long long v = __shfl_up(x, o);
-        if ((int)lane >= o) x += v;
+        const unsigned long long t = __shfl_up(x, o);
+        if ((int)lane >= o) x += t;
     }
     if (lane == 63) s_w[w] = x;
     __syncthreads();
-    unsigned long long run = x - sum, total = 0;
-    for (uint32_t ww = 0; ww < 16; ++ww) {
-        if (ww < w) run += s_w[ww];
-        total += s_w[ww];
-    }
-    const unsigned long long lo = ctr[0];  // cold keys below the child
-    run += lo;
-    for (uint32_t b = tid * 64; b < tid * 64 + 64; ++b) {
-        starts[b] = run;
-        run += counts[b];
-    }
-    if (tid == 0) starts[kBuckets16] = lo + total;
+    unsigned long long run = s_pre + x - c;
+    for (uint32_t ww = 0; ww < w; ++ww) run += s_w[ww];
+    starts[b * 1024 + tid] = run;
+    if (b == gridDim.x - 1 && tid == 1023) starts[kBuckets16] = run + c;
 }
 
 // K12w: chunk_bin[w] = the bin holding output position starts[0] + w * kExpandChunk (the last
@@ -4452,8 +4492,12 @@ hipError_t launch_giant_plan(const uint32_t *part, uint32_t nblk, uint64_t *fix,
     using ull = unsigned long long;
     launch_k(k_giant_count, kBuckets16 / 2 / 256, 256, 0, s, part, nblk,
              reinterpret_cast<ull *>(fix), reinterpret_cast<ull *>(counts));
-    launch_k(k_giant_scan, 1, 1024, 0, s, reinterpret_cast<const ull *>(counts),
-             reinterpret_cast<const ull *>(ctr), reinterpret_cast<ull *>(starts));
+    static_assert(kBuckets16 == 64 * 1024, "K12s: 64 blocks of 1024 bins");
+    ull *bsum = reinterpret_cast<ull *>(starts + kBuckets16 + 1);  // 64 u64 of scratch
+    launch_k(k_giant_scan_a, 64, 1024, 0, s, reinterpret_cast<const ull *>(counts), bsum);
+    launch_k(k_giant_scan_b, 64, 1024, 0, s, reinterpret_cast<const ull *>(counts),
+             reinterpret_cast<const ull *>(bsum), reinterpret_cast<const ull *>(ctr),
+             reinterpret_cast<ull *>(starts));
     return hipGetLastError();
 }
 

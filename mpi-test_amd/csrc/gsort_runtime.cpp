@@ -1181,7 +1181,7 @@ gsort_status giant_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *
     constexpr size_t kFixBytes = (size_t)kH16Shards * kBuckets16 * 8;
     ST_TRY(ensure(c, c->m_fix, kFixBytes));
     const uint64_t nchunks_max = n / 8192 + 2;
-    ST_TRY(ensure(c, c->m_gplan, ((size_t)2 * kBuckets16 + 1) * 8 + nchunks_max * 4));
+    ST_TRY(ensure(c, c->m_gplan, ((size_t)2 * kBuckets16 + 1 + 64) * 8 + nchunks_max * 4));
     if (c->fix_clean != c->m_fix.p) HIP_TRY(c, hipMemsetAsync(c->m_fix.p, 0, kFixBytes, c->stream));
     c->fix_clean = nullptr;
     // ctr: [0] cold keys below the child, [1 + b] workgroup b's cold keys (1 + g <= 257 u64,
@@ -1190,7 +1190,7 @@ gsort_status giant_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *
     uint64_t *d_ctr = reinterpret_cast<uint64_t *>(c->d_small + OFF_GIANT) + 4;
     uint64_t *h_ctr = reinterpret_cast<uint64_t *>(c->h_small + OFF_GIANT) + 4;
     uint64_t *counts = static_cast<uint64_t *>(c->m_gplan.p), *starts = counts + kBuckets16;
-    uint32_t *chunk_bin = reinterpret_cast<uint32_t *>(starts + kBuckets16 + 1);
+    uint32_t *chunk_bin = reinterpret_cast<uint32_t *>(starts + kBuckets16 + 1 + 64);  // (K12s scratch before it)
     uint32_t *cold = slot_ptr<uint32_t>(c, S_TMP);
     HIP_TRY(c, hipMemsetAsync(d_ctr, 0, (1 + g) * 8, c->stream));
     hipEvent_t t = tic(c);
