@@ -108,13 +108,14 @@ __device__ __forceinline__ uint32_t agg_add_pair(uint32_t *words, uint32_t b, ui
 // agg_add_pair on a given word w0 (wave-uniform): the lanes on w0 add their sum with one atomic
 // from the first of them, every other lane adds its own increment.
 __device__ __forceinline__ uint32_t agg_add_pair_at(uint32_t *words, uint32_t b, uint32_t w0,
-                                                    uint32_t *spare) {
+                                                    uint32_t *spare, bool valid = true) {
+    // (valid false: the lane adds 0 -- every lane issues its atomic, no divergent branch)
     const uint32_t w = b >> 1;
-    const bool eq = w == w0;
+    const bool eq = valid && w == w0;
     const uint64_t m = __ballot(eq), mhi = __ballot(eq && (b & 1u));
     const uint64_t mlo = m & ~mhi;
     const uint32_t lr = lane_rank(m);
-    const uint32_t inc = 1u << ((b & 1u) << 4);
+    const uint32_t inc = valid ? 1u << ((b & 1u) << 4) : 0u;
     uint32_t *a = !eq ? words + w : lr == 0 ? words + w0 : spare + (threadIdx.x & 63);
     const uint32_t v = !eq ? inc
                      : lr == 0 ? (uint32_t)__popcll(mlo) + ((uint32_t)__popcll(mhi) << 16) : 0u;
@@ -4253,11 +4254,11 @@ __global__ __launch_bounds__(BLOCK) void k_giant_hist(const uint32_t *__restrict
         const bool skew = best >= 8;
         bool wrap = false;
 #pragma unroll
-        for (int j = 0; j < ITEMS; ++j) {
+        for (int j = 0; j < ITEMS; ++j) {  // (all lanes issue: a key off the child adds 0 --
+            // an `if` per item left the compiler waiting on each atomic in turn)
             const uint32_t b = k[j] & 0xffffu;
-            old[j] = 0;
-            if (g[j]) old[j] = skew ? agg_add_pair_at(s_h, b, w0, spare)
-                                    : atomicAdd(&s_h[b >> 1], 1u << ((b & 1u) << 4));
+            old[j] = skew ? agg_add_pair_at(s_h, b, w0, spare, g[j])
+                          : atomicAdd(&s_h[b >> 1], g[j] ? 1u << ((b & 1u) << 4) : 0u);
         }
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j)
@@ -4403,7 +4404,20 @@ __global__ __launch_bounds__(1024) void k_giant_scan_b(const unsigned long long 
 
 // K12w: chunk_bin[w] = the bin holding output position starts[0] + w * kExpandChunk (the last
 // bin b with starts[b] <= that position), one thread per chunk.
-constexpr uint32_t kExpandChunk = 8192;
+#ifndef GSORT_EXP_C
+#define GSORT_EXP_C 8192
+#endif
+#ifndef GSORT_EXP_T
+#define GSORT_EXP_T 1024
+#endif
+#ifndef GSORT_EXP_NT
+#define GSORT_EXP_NT 0
+#endif
+constexpr uint32_t kExpandChunk = GSORT_EXP_C, kExpandThreads = GSORT_EXP_T;
+__device__ __forceinline__ void exp_store(uint32_t *p, uint32_t v) {
+    if (GSORT_EXP_NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
 __global__ __launch_bounds__(256) void k_giant_chunks(const unsigned long long *__restrict__ starts,
                                                       uint32_t nchunks, uint32_t *__restrict__ chunk_bin) {
     const uint32_t w = blockIdx.x * 256 + threadIdx.x;
@@ -4422,19 +4436,19 @@ __global__ __launch_bounds__(256) void k_giant_chunks(const unsigned long long *
 // in it marks its first position with b + 1 (the chunk's first bin marks position 0), an
 // inclusive max-scan gives every position its bin, and the keys (c << 16 | bin) go out as int32
 // in coalesced stores.
-__global__ __launch_bounds__(1024) void k_giant_expand(const unsigned long long *__restrict__ starts,
+__global__ __launch_bounds__(kExpandThreads) void k_giant_expand(const unsigned long long *__restrict__ starts,
                                                        const uint32_t *__restrict__ chunk_bin,
                                                        uint32_t nchunks, uint32_t child,
                                                        uint32_t *__restrict__ out) {
-    constexpr uint32_t C = kExpandChunk, PER = C / 1024;
+    constexpr uint32_t C = kExpandChunk, NT = kExpandThreads, PER = C / NT;
     __shared__ uint32_t s_m[C];
-    __shared__ uint32_t s_w[16];
+    __shared__ uint32_t s_w[NT / 64];
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6, ch = blockIdx.x;
     const unsigned long long end = starts[kBuckets16];
     const unsigned long long q0 = starts[0] + (unsigned long long)ch * C;
     const uint32_t len = (uint32_t)min((unsigned long long)C, end - q0);
 #pragma unroll
-    for (uint32_t i = 0; i < PER; ++i) s_m[i * 1024 + tid] = 0;
+    for (uint32_t i = 0; i < PER; ++i) s_m[i * NT + tid] = 0;
     const uint32_t b0 = chunk_bin[ch];
     const uint32_t b1 = ch + 1 < nchunks ? chunk_bin[ch + 1] : kBuckets16 - 1;
     if (starts[b0 + 1] >= q0 + len) {  // one bin covers the chunk (a frequent value)
@@ -4442,11 +4456,11 @@ __global__ __launch_bounds__(1024) void k_giant_expand(const unsigned long long 
         uint32_t *o = out + q0;
 #pragma unroll
         for (uint32_t i = 0; i < PER; ++i)
-            if (i * 1024 + tid < len) o[i * 1024 + tid] = key;
+            if (i * NT + tid < len) exp_store(o + i * NT + tid, key);
         return;
     }
     __syncthreads();
-    for (uint32_t b = b0 + tid; b <= b1; b += 1024) {
+    for (uint32_t b = b0 + tid; b <= b1; b += NT) {
         const unsigned long long st = starts[b], en = starts[b + 1];
         if (en > st && (b == b0 || st < q0 + len))
             atomicMax(&s_m[st > q0 ? (uint32_t)(st - q0) : 0u], b + 1);
@@ -4472,8 +4486,8 @@ __global__ __launch_bounds__(1024) void k_giant_expand(const unsigned long long 
     uint32_t *o = out + q0;
 #pragma unroll
     for (uint32_t i = 0; i < PER; ++i) {
-        const uint32_t j = i * 1024 + tid;
-        if (j < len) o[j] = ((child << 16) | (s_m[j] - 1u)) ^ kFlip;
+        const uint32_t j = i * NT + tid;
+        if (j < len) exp_store(o + j, ((child << 16) | (s_m[j] - 1u)) ^ kFlip);
     }
 }
 
@@ -4530,7 +4544,7 @@ hipError_t launch_giant_expand(const uint64_t *starts, uint64_t n_child, uint32_
     using ull = unsigned long long;
     launch_k(k_giant_chunks, (unsigned)((nch + 255) / 256), 256, 0, s,
              reinterpret_cast<const ull *>(starts), (uint32_t)nch, chunk_bin);
-    launch_k(k_giant_expand, (unsigned)nch, 1024, 0, s, reinterpret_cast<const ull *>(starts),
+    launch_k(k_giant_expand, (unsigned)nch, kExpandThreads, 0, s, reinterpret_cast<const ull *>(starts),
              chunk_bin, (uint32_t)nch, child, out);
     return hipGetLastError();
 }

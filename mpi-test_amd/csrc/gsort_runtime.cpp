@@ -1180,7 +1180,7 @@ gsort_status giant_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *
     ST_TRY(ensure(c, c->m_part, (size_t)kH16Blocks * kH16PartWords * 4));
     constexpr size_t kFixBytes = (size_t)kH16Shards * kBuckets16 * 8;
     ST_TRY(ensure(c, c->m_fix, kFixBytes));
-    const uint64_t nchunks_max = n / 8192 + 2;
+    const uint64_t nchunks_max = n / 2048 + 2;  // K18g chunks of >= 2048 keys
     ST_TRY(ensure(c, c->m_gplan, ((size_t)2 * kBuckets16 + 1 + 64) * 8 + nchunks_max * 4));
     if (c->fix_clean != c->m_fix.p) HIP_TRY(c, hipMemsetAsync(c->m_fix.p, 0, kFixBytes, c->stream));
     c->fix_clean = nullptr;
