@@ -4404,20 +4404,12 @@ __global__ __launch_bounds__(1024) void k_giant_scan_b(const unsigned long long 
 
 // K12w: chunk_bin[w] = the bin holding output position starts[0] + w * kExpandChunk (the last
 // bin b with starts[b] <= that position), one thread per chunk.
-#ifndef GSORT_EXP_C
-#define GSORT_EXP_C 8192
-#endif
-#ifndef GSORT_EXP_T
-#define GSORT_EXP_T 1024
-#endif
-#ifndef GSORT_EXP_NT
-#define GSORT_EXP_NT 0
-#endif
-constexpr uint32_t kExpandChunk = GSORT_EXP_C, kExpandThreads = GSORT_EXP_T;
-__device__ __forceinline__ void exp_store(uint32_t *p, uint32_t v) {
-    if (GSORT_EXP_NT) __builtin_nontemporal_store(v, p);
-    else *p = v;
-}
+// K18g geometry (round 4, profiles/r04_ab_k18g_geometry.txt): 4096-key chunks per 512-thread
+// workgroup (four in flight per CU instead of two 8192 x 1024: each chunk is a chain of
+// dependent loads -- starts, chunk_bin, the bins -- before its stores); the stores of chunks
+// spanning several bins nontemporal (16-bit keys K18g 0.294 -> 0.21 ms), a chunk inside one bin
+// (a frequent value: 8-bit keys, Zipf) stored plainly (nontemporal there measured slower)
+constexpr uint32_t kExpandChunk = 4096, kExpandThreads = 512;
 __global__ __launch_bounds__(256) void k_giant_chunks(const unsigned long long *__restrict__ starts,
                                                       uint32_t nchunks, uint32_t *__restrict__ chunk_bin) {
     const uint32_t w = blockIdx.x * 256 + threadIdx.x;
@@ -4456,7 +4448,7 @@ __global__ __launch_bounds__(kExpandThreads) void k_giant_expand(const unsigned 
         uint32_t *o = out + q0;
 #pragma unroll
         for (uint32_t i = 0; i < PER; ++i)
-            if (i * NT + tid < len) exp_store(o + i * NT + tid, key);
+            if (i * NT + tid < len) o[i * NT + tid] = key;
         return;
     }
     __syncthreads();
@@ -4487,7 +4479,7 @@ __global__ __launch_bounds__(kExpandThreads) void k_giant_expand(const unsigned 
 #pragma unroll
     for (uint32_t i = 0; i < PER; ++i) {
         const uint32_t j = i * NT + tid;
-        if (j < len) exp_store(o + j, ((child << 16) | (s_m[j] - 1u)) ^ kFlip);
+        if (j < len) __builtin_nontemporal_store(((child << 16) | (s_m[j] - 1u)) ^ kFlip, o + j);
     }
 }
 
