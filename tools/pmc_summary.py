@@ -42,7 +42,9 @@ def main(root):
     summary = {"kernels": {}}
     st = stats(os.path.join(root, "stats"))
     pmc = {}
-    for sub in ("fetch", "write", "sq", "clk", "xgmi"):
+    subs = sorted(d for d in os.listdir(root)
+                  if d != "stats" and os.path.isdir(os.path.join(root, d)))
+    for sub in subs:  # every counter pass (profile_pmc.sh, profile_pipes.sh)
         for k, cs in counters(os.path.join(root, sub)).items():
             for c, vals in cs.items():
                 pmc.setdefault(k, {})[c] = sum(vals) / len(vals)
