@@ -21,9 +21,6 @@ struct LaunchTimer {
     void *u = nullptr;
 };
 void set_launch_timer(LaunchTimer *t);  // nullptr: untimed launches
-// The next kernel this thread launches records its end into e (its dispatch carries the event:
-// no marker packet on the stream), e.g. for hipStreamWaitEvent on a second stream.
-void set_next_stop(hipEvent_t e);
 
 inline uint64_t sweep_tiles(uint64_t n) { return (n + kSweepTile - 1) / kSweepTile; }
 inline uint64_t scan_groups(uint64_t n) { return (sweep_tiles(n) + kScanGroup - 1) / kScanGroup; }
@@ -285,7 +282,7 @@ hipError_t launch_compat_keys(const int32_t *a, uint64_t n, int P, int loop, con
 // 4 x kEstWGs, capc / cur2 / lim2 / init2 65536, cap3 / cur3 / lim3 / init3 2048, r2 / r3 / bases3 /
 // bases2 256 u64, tp 257, tdesc (est_max_tiles(n) + 2048) x kTileDescBytes (tile descriptors,
 // then the 2048-entry level-3 piece table), dump kSweepTile keys;
-// wl.list[0..4] 65536 x groups entries each, wl.ctr 15 x groups counters (zeroed by the front).
+// wl.list[1..4] 65536 entries each, wl.ctr the 15 counters (zeroed by the front).
 #ifndef GSORT_EST_WGS
 #define GSORT_EST_WGS 256
 #endif
@@ -322,42 +319,20 @@ struct EstPlan {
     uint64_t seq_elig, seq_done;
     int sb;         // 0 .. 16: the levels' digits start sb bits lower (a constant key prefix)
     uint32_t koff;  // keys taken as ordered u32 minus koff (the offset retry; 0 otherwise)
-    int groups = 1;      // K3a launches (kEstMaxGroups at most; est_groups_for)
-    uint32_t gtiles = 0; // tiles per K3a launch (est_group_tiles)
-    uint32_t persist = 0;  // > 0: K3a launches after the first as persistent grids of that many WGs
 };
-// K3a / K11e overlap: K3a runs as `groups` launches of `gtiles` tiles each
-// (the last takes the rest); K12g launch g lists the level-3 buckets K3a launch g completed into
-// group g's lists (wl.list[k] + g * kBuckets16 entries) and counters (wl.ctr + 15 g), so that
-// group's K11e can run beside the next K3a launch (on a second stream).  groups = 1: one K3a
-// launch, the lists as before.
-constexpr int kEstMaxGroups = 8;
-constexpr uint32_t kEstGroupCtrs = 3 * (kLocalClasses + 1);  // counters per group
-constexpr uint32_t kEstMailCtr = 24;  // mail word of group 0's counters
-constexpr uint32_t kEstMailWords = kEstMailCtr + kEstGroupCtrs * kEstMaxGroups;
-inline uint32_t est_group_tiles(uint64_t n, int groups) {  // even, so launches hold whole pairs
-    const uint64_t t = (est_max_tiles(n) + groups - 1) / groups;
-    return (uint32_t)((t + 1) & ~1ull);
-}
-inline int est_groups_for(uint64_t n, int groups) {  // launches actually needed
-    const uint64_t gt = est_group_tiles(n, groups);
-    return (int)((est_max_tiles(n) + gt - 1) / gt);
-}
+constexpr uint32_t kEstMailWords = 24;
 hipError_t launch_est_front(const EstPlan &p, hipStream_t s);   // K1e + K12e
 hipError_t launch_est_level3(const EstPlan &p, hipStream_t s);  // K3r
-hipError_t launch_est_tiles(const EstPlan &p, hipStream_t s);   // K12f
-hipError_t launch_est_part2(const EstPlan &p, int group, hipStream_t s);  // K3a launch `group`
-hipError_t launch_est_classify(const EstPlan &p, int group, hipStream_t s);  // K12g
-// K11e over entries [first, first + nlist) of group g's class list cls (those at or past the
-// count K12g made return at once); publish: its block 0 first hands every group's counters and
-// the status to the host (mail, seq_done) -- exactly one launch behind the last K12g must, or
-// launch_est_publish
+hipError_t launch_est_level2(const EstPlan &p, hipStream_t s);  // K12f + K3a
+hipError_t launch_est_classify(const EstPlan &p, hipStream_t s);  // K12g
+// K11e over entries [first, first + nlist) of class list cls (those at or past the count K12g
+// made return at once); publish: its block 0 first hands K12g's counters and status to the
+// host (mail, seq_done) -- exactly one launch behind K12g must, or launch_est_publish
 hipError_t launch_local_sort_e(const EstPlan &p, int cls, uint32_t first, uint32_t nlist,
-                               bool publish, hipStream_t s, int group = 0);
+                               bool publish, hipStream_t s);
 hipError_t launch_est_publish(const EstPlan &p, hipStream_t s);
-// K18c over group g's list 0: the children past kLocalMax keys (one-read counting sort from Y)
-hipError_t launch_est_oversized(const EstPlan &p, uint32_t nlist, int ncu, hipStream_t s,
-                                int group = 0);
+// K18c over K12g's list 0: the children past kLocalMax keys (one-read counting sort from Y)
+hipError_t launch_est_oversized(const EstPlan &p, uint32_t nlist, int ncu, hipStream_t s);
 // ---- one dominant 16-bit child (gsort_kernels.hip, "giant child") -----------
 // K1m: res[0] = the most frequent top-16-bit child (ordered u32) of min(n, 16384) evenly
 // strided keys, res[1] = its sample count, res[2] = the samples (u64 each).

@@ -1463,8 +1463,8 @@ __global__ __launch_bounds__(kRadix) void k_plan16_place(
 // runtime passes): the status {eflag, ovf} and its sequence after K12g, the same after K12e
 // (eligibility only), the 15 work-list counters after K12g.
 constexpr uint32_t kMailStatus = 0, kMailSeq = 1, kMailElig = 2, kMailEligSeq = 3,
-                   kMailChildren = 4, kMailVary = 5, kMailLo = 6, kMailHi = 7,
-                   kMailMaxChild = 23, kMailCtr = kEstMailCtr;
+                   kMailChildren = 4, kMailVary = 5, kMailLo = 6, kMailHi = 7, kMailCtr = 8,
+                   kMailMaxChild = 23;
 
 __device__ __forceinline__ void mail_release(unsigned long long *flag, unsigned long long seq) {
     __threadfence_system();
@@ -1512,6 +1512,34 @@ __global__ __launch_bounds__(256) void k_tile_desc(const uint32_t *__restrict__ 
     desc[t] = {t0, (rem >> 13) ? (uint32_t)kSweepTile : (uint32_t)rem, lo};
 }
 
+// Phase stamps (diagnostic build only: make VARIANT=stamps EXTRA=-DGSORT_STAMPS lib; never in
+// the product).  Thread 0 of every K3r / K3a (sampled plan) workgroup writes s_memrealtime
+// (100 MHz) at 7 points -- kernel entry (6), tile known (0), loads landed, ranked, reservations
+// returned, scattered into LDS, stores completed (5) -- each behind a workgroup barrier (and a
+// vmcnt(0) wait where a phase ends in memory traffic), to
+// g_stamps[(L3 ? 0 : 1) * kStampWGs + workgroup][8]
+// (tools/k3_stamps.py).
+#ifdef GSORT_STAMPS
+constexpr uint32_t kStampWGs = 32768;
+__device__ unsigned long long *g_stamps = nullptr;
+// (kept in LDS until the workgroup's last stamp: a global pointer live across the kernel cost
+// it SGPRs past 80 -- 7 waves per SIMD, one workgroup per CU, half the live workgroups)
+#define K3_STAMP(p)                                                                            \
+    do {                                                                                       \
+        __syncthreads();                                                                       \
+        if (EST && threadIdx.x == 0) s_stamp[p] = __builtin_amdgcn_s_memrealtime();            \
+        if (EST && (p) == 5 && threadIdx.x < 8 && g_stamps && blockIdx.x < kStampWGs)          \
+            g_stamps[((L3 ? 0ull : 1ull) * kStampWGs + blockIdx.x) * 8 + threadIdx.x] =        \
+                s_stamp[threadIdx.x]; /* (lanes of wave 0: lane 0's LDS write is visible) */   \
+    } while (0)
+#define K3_STAMP_DECL __shared__ unsigned long long s_stamp[8]
+#define K3_STAMP_WAIT() asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
+#else
+#define K3_STAMP(p) do { } while (0)
+#define K3_STAMP_DECL
+#define K3_STAMP_WAIT() do { } while (0)
+#endif
+
 // K3r / K3a: one workgroup per PAIR of tiles.  Both tiles are ranked (one LDS atomic per key)
 // before either reservation is needed, so the two reservations (one returning device-scope
 // atomicAdd per non-empty digit) are in flight together and their round trip hides behind
@@ -1535,7 +1563,7 @@ __global__ __launch_bounds__(256) void k_tile_desc(const uint32_t *__restrict__ 
 // raises *ovf and goes to the TILE-key scratch `dump` instead (the caller then re-sorts on the
 // exact plan).  flags bit 2 (the sample found the input ineligible): do nothing.
 template <int BLOCK, int ITEMS, bool L3, bool FIN, typename OT = uint32_t, bool EST = false,
-          int TILES = 2, bool LOOP = false>
+          int TILES = 2>
 __global__ __launch_bounds__(BLOCK, TILES == 1 ? 6 : 1) void k_partition_res(
     const uint32_t *__restrict__ in, OT *__restrict__ out, uint64_t n,
     const uint32_t *__restrict__ tpfx, const TileDesc *__restrict__ desc,
@@ -1544,10 +1572,12 @@ __global__ __launch_bounds__(BLOCK, TILES == 1 ? 6 : 1) void k_partition_res(
     const uint32_t *__restrict__ lim = nullptr, uint32_t *__restrict__ ovf = nullptr,
     OT *__restrict__ dump = nullptr, const TileDesc *__restrict__ pieces = nullptr,
     unsigned long long *mail = nullptr, unsigned long long seq = 0, int sb = 0,
-    uint32_t koff = 0, uint32_t tfirst = 0, uint32_t tpairs = 0) {
+    uint32_t koff = 0) {
     constexpr int TILE = BLOCK * ITEMS;
     const int shift = (L3 ? 24 : 16) - (EST ? sb : 0);  // EST: digits sb bits lower
     static_assert(TILE == kSweepTile, "reservation tiles are kSweepTile keys");
+    K3_STAMP_DECL;
+    K3_STAMP(6);
     if (EST && L3 && mail && blockIdx.x == 0) publish_elig(mail, flags, seq);  // K12e is done
     uint32_t flip = 0;
     if (flags) {
@@ -1566,182 +1596,177 @@ __global__ __launch_bounds__(BLOCK, TILES == 1 ? 6 : 1) void k_partition_res(
     __shared__ uint32_t s_spare[kAggSpare];
     __shared__ uint32_t s_ovf[TILES];  // EST: a run of this tile overflowed its region
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    // LOOP (K3a only): a persistent grid walks the launch's tpairs pairs (b, b + gridDim.x, ..
-    // in the XCD-contiguous deal), so the launch holds at most its grid's workgroups per CU
-    // while another stream's kernel runs beside it; otherwise one pair per workgroup
-    for (uint32_t bb = blockIdx.x;; bb += gridDim.x) {
-        uint32_t pr, ntile, last_len = 0;
-        if (L3) {
-            pr = blockIdx.x;
-            ntile = (uint32_t)((n + TILE - 1) / TILE);
-            last_len = (uint32_t)(n - (uint64_t)(ntile - 1) * TILE);
-        } else {
-            // (tfirst: the first tile of this launch -- the sampled plan's K3a runs as G
-            // launches over consecutive tile ranges, so K11e can start on the buckets the
-            // earlier ones completed; a multiple of TILES)
-            if (LOOP && bb >= tpairs) break;
-            pr = tfirst / TILES + xcd_tile(bb, LOOP ? tpairs : gridDim.x);
-            ntile = tpfx[kRadix];
-        }
-        if (TILES * pr >= ntile) {
-            if (LOOP) break;  // (a workgroup's pairs grow with bb: the rest lie past the end too)
-            return;
-        }
-        uint32_t seg[TILES], len[TILES];
-        uint64_t t0[TILES];
-        bool straddle[TILES];
+    uint32_t pr, ntile, last_len = 0;
+    if (L3) {
+        pr = blockIdx.x;
+        ntile = (uint32_t)((n + TILE - 1) / TILE);
+        last_len = (uint32_t)(n - (uint64_t)(ntile - 1) * TILE);
+    } else {
+        pr = xcd_tile(blockIdx.x, gridDim.x);
+        ntile = tpfx[kRadix];
+    }
+    if (TILES * pr >= ntile) return;
+    K3_STAMP(0);
+    uint32_t seg[TILES], len[TILES];
+    uint64_t t0[TILES];
+    bool straddle[TILES];
 #pragma unroll
-        for (int h = 0; h < TILES; ++h) {
-            const uint32_t t = TILES * pr + h;
-            seg[h] = 0; len[h] = 0; t0[h] = 0; straddle[h] = false;
-            if (t < ntile) {
-                if (L3) {
-                    t0[h] = (uint64_t)t * TILE;
-                    len[h] = t == ntile - 1 ? last_len : (uint32_t)TILE;
-                } else {
-                    const TileDesc d = desc[t];
-                    t0[h] = d.t0;
-                    len[h] = d.len;
-                    seg[h] = d.seg;
-                    if (EST && (d.seg & kStraddle)) { straddle[h] = true; seg[h] = d.seg & ~kStraddle; }
-                }
-            }
-        }
-        if (tid < kRadix)
-            for (int h = 0; h < TILES; ++h) s_cur[h][tid] = 0;
-        if (EST && tid < TILES) s_ovf[tid] = 0;
-        uint32_t *cursor[TILES];
-        uint32_t limv[TILES];  // EST: the region limits, loaded now (off the reservation path)
-#pragma unroll
-        for (int h = 0; h < TILES; ++h) {
-            limv[h] = 0;
-            // the shard of tile t is (t / 2) % 8, as K1h / K1e count it
-            const uint32_t row = (L3 ? ((TILES * pr + h) / 2 % kShards) : seg[h]) * kRadix;
-            cursor[h] = cur + row;
-            if (EST && tid < kRadix) limv[h] = lim ? lim[row + tid] : ~0u;
-        }
-        uint32_t k[TILES][ITEMS], r[TILES][ITEMS];
-#pragma unroll
-        for (int h = 0; h < TILES; ++h) {
-            if (EST && !L3 && straddle[h]) {  // a tile across pieces of bucket seg[h] (K12f)
-                const TileDesc *pc = pieces + seg[h] * kShards;
-                uint64_t pa[kShards];
-                uint32_t pv[kShards];
-#pragma unroll
-                for (uint32_t x = 0; x < kShards; ++x) { pa[x] = pc[x].t0; pv[x] = pc[x].len; }
-#pragma unroll
-                for (int i = 0; i < ITEMS; ++i) {
-                    const uint32_t j = (uint32_t)(i * BLOCK) + tid, v = (uint32_t)t0[h] + j;
-                    uint32_t x = 0;
-#pragma unroll
-                    for (uint32_t q = 1; q < kShards; ++q) x += v >= pv[q];
-                    k[h][i] = j < len[h] ? in[pa[x] + (v - pv[x])] : 0u;
-                }
+    for (int h = 0; h < TILES; ++h) {
+        const uint32_t t = TILES * pr + h;
+        seg[h] = 0; len[h] = 0; t0[h] = 0; straddle[h] = false;
+        if (t < ntile) {
+            if (L3) {
+                t0[h] = (uint64_t)t * TILE;
+                len[h] = t == ntile - 1 ? last_len : (uint32_t)TILE;
             } else {
-                load_tile<BLOCK, ITEMS, FIN>(in + t0[h] + tid, len[h] == (uint32_t)TILE, len[h], k[h]);
-            }
-            if (!L3) {
-#pragma unroll
-                for (int i = 0; i < ITEMS; ++i) k[h][i] ^= flip;
-            }
-        }
-        if (EST && L3 && koff) {  // the offset retry: keys relative to the block's minimum
-#pragma unroll
-            for (int h = 0; h < TILES; ++h)
-#pragma unroll
-                for (int i = 0; i < ITEMS; ++i) k[h][i] -= koff;
-        }
-        if (EST && L3 && sb) {  // the prefix the sampled digits skip must hold for every key
-            const uint32_t pfx = ((in[0] ^ kFlip) - koff) >> (32 - sb);
-            bool bad = false;
-#pragma unroll
-            for (int h = 0; h < TILES; ++h)
-#pragma unroll
-                for (int i = 0; i < ITEMS; ++i)
-                    bad |= (uint32_t)(i * BLOCK) + tid < len[h] && (k[h][i] >> (32 - sb)) != pfx;
-            if (__ballot(bad) && (tid & 63) == 0) atomicOr(ovf, 1u);
-        }
-        __syncthreads();  // s_cur zeroed
-#pragma unroll
-        for (int h = 0; h < TILES; ++h)
-#pragma unroll
-            for (int i = 0; i < ITEMS; ++i)
-                if ((uint32_t)(i * BLOCK) + tid < len[h])
-                    r[h][i] = agg_rank(s_cur[h], (k[h][i] >> shift) & 255u, s_spare);
-        __syncthreads();
-        uint32_t excl[TILES], pos[TILES], cnt[TILES];
-#pragma unroll
-        for (int h = 0; h < TILES; ++h) excl[h] = pos[h] = cnt[h] = 0;
-        // both tiles on one cursor row (always for K3r: one shard; for K3a when both tiles are in
-        // one bucket): ONE reservation of both counts, tile 1's run right behind tile 0's, so the
-        // pair writes one run of twice the length -- half the run boundaries, whose lines are
-        // otherwise written partly by two workgroups (often on two XCDs)
-        const bool merge = TILES == 2 && 2 * pr + 1 < ntile && cursor[0] == cursor[TILES - 1];
-        if (tid < kRadix) {
-            cnt[0] = s_cur[0][tid];
-            cnt[TILES - 1] = s_cur[TILES - 1][tid];
-            if (merge) {
-                if (cnt[0] + cnt[TILES - 1]) {
-                    pos[0] = atomicAdd(&cursor[0][tid], cnt[0] + cnt[TILES - 1]);
-                    pos[TILES - 1] = pos[0] + cnt[0];
-                }
-            } else {
-#pragma unroll
-                for (int h = 0; h < TILES; ++h)
-                    if (cnt[h]) pos[h] = atomicAdd(&cursor[h][tid], cnt[h]);
-            }
-#pragma unroll
-            for (int h = 0; h < TILES; ++h) {
-                const uint32_t c = cnt[h];
-                const uint32_t v = wave_incl_add(c);
-                if (lane == 63) s_wsum[h][w] = v;
-                excl[h] = v - c;
+                const TileDesc d = desc[t];
+                t0[h] = d.t0;
+                len[h] = d.len;
+                seg[h] = d.seg;
+                if (EST && (d.seg & kStraddle)) { straddle[h] = true; seg[h] = d.seg & ~kStraddle; }
             }
         }
-        __syncthreads();
-        if (tid < kRadix) {
+    }
+    if (tid < kRadix)
+        for (int h = 0; h < TILES; ++h) s_cur[h][tid] = 0;
+    if (EST && tid < TILES) s_ovf[tid] = 0;
+    uint32_t *cursor[TILES];
+    uint32_t limv[TILES];  // EST: the region limits, loaded now (off the reservation path)
 #pragma unroll
-            for (int h = 0; h < TILES; ++h) {
-                for (uint32_t ww = 0; ww < w; ++ww) excl[h] += s_wsum[h][ww];
-                s_cur[h][tid] = excl[h];
-            }
-        }
-        __syncthreads();
+    for (int h = 0; h < TILES; ++h) {
+        limv[h] = 0;
+        // the shard of tile t is (t / 2) % 8, as K1h / K1e count it
+        const uint32_t row = (L3 ? ((TILES * pr + h) / 2 % kShards) : seg[h]) * kRadix;
+        cursor[h] = cur + row;
+        if (EST && tid < kRadix) limv[h] = lim ? lim[row + tid] : ~0u;
+    }
+    uint32_t k[TILES][ITEMS], r[TILES][ITEMS];
 #pragma unroll
-        for (int h = 0; h < TILES; ++h)
+    for (int h = 0; h < TILES; ++h) {
+        if (EST && !L3 && straddle[h]) {  // a tile across pieces of bucket seg[h] (K12f)
+            const TileDesc *pc = pieces + seg[h] * kShards;
+            uint64_t pa[kShards];
+            uint32_t pv[kShards];
 #pragma unroll
-            for (int i = 0; i < ITEMS; ++i)
-                if ((uint32_t)(i * BLOCK) + tid < len[h])
-                    s_keys[h][s_cur[h][(k[h][i] >> shift) & 255u] + r[h][i]] = k[h][i];
-        if (tid < kRadix) {
-#pragma unroll
-            for (int h = 0; h < TILES; ++h) {
-                s_off[h][tid] = (uint32_t)((L3 ? bases[tid] : bases[seg[h]]) + pos[h]) - excl[h];
-                if (EST && cnt[h] && (uint64_t)pos[h] + cnt[h] > limv[h]) {
-                    atomicOr(ovf, 1u);
-                    s_ovf[h] = 1;  // the block is re-sorted on the exact plan: the tile goes to dump
-                }
-            }
-        }
-        __syncthreads();
-#pragma unroll
-        for (int h = 0; h < TILES; ++h) {
-            OT *o = out;
-            bool to_dump = false;
-            if (EST && s_ovf[h]) { o = dump; to_dump = true; }
+            for (uint32_t x = 0; x < kShards; ++x) { pa[x] = pc[x].t0; pv[x] = pc[x].len; }
 #pragma unroll
             for (int i = 0; i < ITEMS; ++i) {
-                const uint32_t j = (uint32_t)(i * BLOCK) + tid;
-                if (j < len[h]) {
-                    const uint32_t key = s_keys[h][j];
-                    const uint32_t at = to_dump ? j : s_off[h][(key >> shift) & 255u] + j;
-                    o[at] = (OT)key;
-                }
+                const uint32_t j = (uint32_t)(i * BLOCK) + tid, v = (uint32_t)t0[h] + j;
+                uint32_t x = 0;
+#pragma unroll
+                for (uint32_t q = 1; q < kShards; ++q) x += v >= pv[q];
+                k[h][i] = j < len[h] ? in[pa[x] + (v - pv[x])] : 0u;
+            }
+        } else {
+            load_tile<BLOCK, ITEMS, FIN>(in + t0[h] + tid, len[h] == (uint32_t)TILE, len[h], k[h]);
+        }
+        if (!L3) {
+#pragma unroll
+            for (int i = 0; i < ITEMS; ++i) k[h][i] ^= flip;
+        }
+    }
+    if (EST && L3 && koff) {  // the offset retry: keys relative to the block's minimum
+#pragma unroll
+        for (int h = 0; h < TILES; ++h)
+#pragma unroll
+            for (int i = 0; i < ITEMS; ++i) k[h][i] -= koff;
+    }
+    if (EST && L3 && sb) {  // the prefix the sampled digits skip must hold for every key
+        const uint32_t pfx = ((in[0] ^ kFlip) - koff) >> (32 - sb);
+        bool bad = false;
+#pragma unroll
+        for (int h = 0; h < TILES; ++h)
+#pragma unroll
+            for (int i = 0; i < ITEMS; ++i)
+                bad |= (uint32_t)(i * BLOCK) + tid < len[h] && (k[h][i] >> (32 - sb)) != pfx;
+        if (__ballot(bad) && (tid & 63) == 0) atomicOr(ovf, 1u);
+    }
+    K3_STAMP_WAIT();
+    K3_STAMP(1);
+    __syncthreads();  // s_cur zeroed
+#pragma unroll
+    for (int h = 0; h < TILES; ++h)
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i)
+            if ((uint32_t)(i * BLOCK) + tid < len[h])
+                r[h][i] = agg_rank(s_cur[h], (k[h][i] >> shift) & 255u, s_spare);
+    __syncthreads();
+    K3_STAMP(2);
+    uint32_t excl[TILES], pos[TILES], cnt[TILES];
+#pragma unroll
+    for (int h = 0; h < TILES; ++h) excl[h] = pos[h] = cnt[h] = 0;
+    // both tiles on one cursor row (always for K3r: one shard; for K3a when both tiles are in
+    // one bucket): ONE reservation of both counts, tile 1's run right behind tile 0's, so the
+    // pair writes one run of twice the length -- half the run boundaries, whose lines are
+    // otherwise written partly by two workgroups (often on two XCDs)
+    const bool merge = TILES == 2 && 2 * pr + 1 < ntile && cursor[0] == cursor[TILES - 1];
+    if (tid < kRadix) {
+        cnt[0] = s_cur[0][tid];
+        cnt[TILES - 1] = s_cur[TILES - 1][tid];
+        if (merge) {
+            if (cnt[0] + cnt[TILES - 1]) {
+                pos[0] = atomicAdd(&cursor[0][tid], cnt[0] + cnt[TILES - 1]);
+                pos[TILES - 1] = pos[0] + cnt[0];
+            }
+        } else {
+#pragma unroll
+            for (int h = 0; h < TILES; ++h)
+                if (cnt[h]) pos[h] = atomicAdd(&cursor[h][tid], cnt[h]);
+        }
+#pragma unroll
+        for (int h = 0; h < TILES; ++h) {
+            const uint32_t c = cnt[h];
+            const uint32_t v = wave_incl_add(c);
+            if (lane == 63) s_wsum[h][w] = v;
+            excl[h] = v - c;
+        }
+    }
+    K3_STAMP_WAIT();
+    K3_STAMP(3);
+    __syncthreads();
+    if (tid < kRadix) {
+#pragma unroll
+        for (int h = 0; h < TILES; ++h) {
+            for (uint32_t ww = 0; ww < w; ++ww) excl[h] += s_wsum[h][ww];
+            s_cur[h][tid] = excl[h];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < TILES; ++h)
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i)
+            if ((uint32_t)(i * BLOCK) + tid < len[h])
+                s_keys[h][s_cur[h][(k[h][i] >> shift) & 255u] + r[h][i]] = k[h][i];
+    if (tid < kRadix) {
+#pragma unroll
+        for (int h = 0; h < TILES; ++h) {
+            s_off[h][tid] = (uint32_t)((L3 ? bases[tid] : bases[seg[h]]) + pos[h]) - excl[h];
+            if (EST && cnt[h] && (uint64_t)pos[h] + cnt[h] > limv[h]) {
+                atomicOr(ovf, 1u);
+                s_ovf[h] = 1;  // the block is re-sorted on the exact plan: the tile goes to dump
             }
         }
-        if (!LOOP) break;
-        __syncthreads();  // the pair's LDS is read out before the next one is ranked into it
     }
+    __syncthreads();
+    K3_STAMP(4);
+#pragma unroll
+    for (int h = 0; h < TILES; ++h) {
+        OT *o = out;
+        bool to_dump = false;
+        if (EST && s_ovf[h]) { o = dump; to_dump = true; }
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i) {
+            const uint32_t j = (uint32_t)(i * BLOCK) + tid;
+            if (j < len[h]) {
+                const uint32_t key = s_keys[h][j];
+                const uint32_t at = to_dump ? j : s_off[h][(key >> shift) & 255u] + j;
+                o[at] = (OT)key;
+            }
+        }
+    }
+    K3_STAMP_WAIT();
+    K3_STAMP(5);
 }
 
 // Stable wave-level rank of one round (64 keys, lane order = key order) against the wave's
@@ -3185,10 +3210,7 @@ __global__ __launch_bounds__(256) void k_est_tiles(const uint32_t *__restrict__ 
     if (tid == 255) s_tp[kRadix] = run + nt;
     __syncthreads();
     const uint32_t total = s_tp[kRadix];
-    if (blockIdx.x == 0) {  // the tile prefix (K12g assigns buckets to K3a's launches by it)
-        tp[tid] = s_tp[tid];
-        if (tid == 0) tp[kRadix] = total;
-    }
+    if (blockIdx.x == 0 && tid == 0) tp[kRadix] = total;
     const uint32_t t = blockIdx.x * 256 + tid;
     if (t >= total || t >= max_tiles) return;
     uint32_t lo = 0, hi = kRadix;  // s_tp[lo] <= t < s_tp[hi]
@@ -3225,18 +3247,12 @@ __global__ __launch_bounds__(256) void k_est_tiles(const uint32_t *__restrict__ 
 // The entry's src carries the child's top 16 bits above bit 40 (Y holds only the low 16 bits):
 // the ordered-u32 key (minus koff) of child (s, e) is pfx . s . e . rest, the digits sb bits
 // below the constant prefix pfx of the shifted plan (K3r's check, from in[0]).
-// Grouped (ngroups > 1, DESIGN.md 5.1 "K3a / K11e overlap"): K3a runs as ngroups launches of
-// gtiles tiles each; launch `group` of K12g lists only the buckets whose last tile
-// (tp[s + 1] - 1, K12f's prefix) lies in K3a launch `group` -- complete once it has run -- into
-// that group's own lists and counters (wl is the group's), so its K11e can start while the
-// next K3a launch runs.
 __global__ __launch_bounds__(kRadix) void k_est_classify(
     const uint32_t *__restrict__ cur2, const uint32_t *__restrict__ init2,
     const uint32_t *__restrict__ lim2, const uint32_t *__restrict__ cur3,
     const uint32_t *__restrict__ init3, const unsigned long long *__restrict__ bases2,
     WorkLists wl, uint32_t *__restrict__ eflag, const uint32_t *__restrict__ in, int sb,
-    uint32_t koff, const uint32_t *__restrict__ tp, uint32_t group, uint32_t ngroups,
-    uint32_t gtiles) {
+    uint32_t koff) {
     constexpr int NL = kLocalClasses + 1;
     __shared__ unsigned long long s_w[kRadix / 64];
     __shared__ unsigned long long s_fb;
@@ -3244,11 +3260,6 @@ __global__ __launch_bounds__(kRadix) void k_est_classify(
     __shared__ unsigned long long s_keys[NL], s_max[NL], s_base[NL];
     const uint32_t s = blockIdx.x, e = threadIdx.x;
     unsigned long long *ctr = reinterpret_cast<unsigned long long *>(wl.ctr);
-    if (ngroups > 1) {  // (block-uniform) not this launch's bucket, or an empty one
-        if (eflag[1]) return;  // level 3 overflowed: K12f wrote no tile prefix
-        const uint32_t t0 = tp[s], t1 = tp[s + 1];
-        if (t1 <= t0 || min((t1 - 1) / gtiles, ngroups - 1) != group) return;
-    }
     if (!(*eflag & 4u)) {
         if (e < NL) { s_n[e] = 0; s_keys[e] = 0; s_max[e] = 0; }
         unsigned long long te = 0;
@@ -3296,26 +3307,25 @@ __global__ __launch_bounds__(kRadix) void k_est_classify(
     }
 }
 
-// The K12g results for the host: the nctr work-list counters (15 per K3a group) and the status
-// words {eflag, ovf} into the mailbox, then seq (threads 0 .. nctr of one block of at least
-// nctr + 1 threads; every K12g launch has completed).
+// The K12g results for the host: the 15 work-list counters and the status words {eflag, ovf}
+// into the mailbox, then seq (threads 0 .. 15 of one block; K12g has completed).
 __device__ __forceinline__ void publish_lists(unsigned long long *mail,
                                               const unsigned long long *ctr,
-                                              const uint32_t *eflag, unsigned long long seq,
-                                              uint32_t nctr) {
+                                              const uint32_t *eflag, unsigned long long seq) {
+    constexpr uint32_t NC = 3 * (kLocalClasses + 1);
     const uint32_t e = threadIdx.x;
-    if (e < nctr) mail[kMailCtr + e] = ctr[e];
-    if (e == nctr) mail[kMailStatus] = *reinterpret_cast<const unsigned long long *>(eflag);
+    if (e < NC) mail[kMailCtr + e] = ctr[e];
+    if (e == NC) mail[kMailStatus] = *reinterpret_cast<const unsigned long long *>(eflag);
     __syncthreads();
     if (e == 0) mail_release(mail + kMailSeq, seq);
 }
 
 // K12p for the sampled plan when no K11e launch follows K12g directly.
-__global__ __launch_bounds__(256) void k_publish_lists(unsigned long long *mail,
-                                                       const unsigned long long *ctr,
-                                                       const uint32_t *eflag,
-                                                       unsigned long long seq, uint32_t nctr) {
-    publish_lists(mail, ctr, eflag, seq, nctr);
+__global__ __launch_bounds__(64) void k_publish_lists(unsigned long long *mail,
+                                                      const unsigned long long *ctr,
+                                                      const uint32_t *eflag,
+                                                      unsigned long long seq) {
+    publish_lists(mail, ctr, eflag, seq);
 }
 
 // K11e: K11 over a class list of the sampled plan: entry blockIdx.x = {src, dst | len << 40} is
@@ -3337,13 +3347,12 @@ __global__ __launch_bounds__(BLOCK) void k_local_sort_e(const uint16_t *__restri
                                                         unsigned long long *mail,
                                                         const unsigned long long *ctr_all,
                                                         const uint32_t *eflag,
-                                                        unsigned long long seq, uint32_t koff,
-                                                        uint32_t nctr) {
+                                                        unsigned long long seq, uint32_t koff) {
     constexpr int WAVES = BLOCK / 64;
     constexpr int TILE = BLOCK * ITEMS;
     __shared__ uint32_t s_a[lds_slots(TILE)];
     __shared__ uint32_t s_wc[WAVES * kRadix];
-    if (mail && blockIdx.x == 0) publish_lists(mail, ctr_all, eflag, seq, nctr);  // K12g is done
+    if (mail && blockIdx.x == 0) publish_lists(mail, ctr_all, eflag, seq);  // K12g is done
     const uint32_t i = first + blockIdx.x;
     if (i >= (uint32_t)*ctr) return;
     const uint64_t sw = list[2 * i];
@@ -3399,18 +3408,21 @@ unsigned grid_for(uint64_t n, unsigned block, unsigned cap) {
 // attached start event ~5 us (tools/experiments/launch_gap.hip).
 namespace {
 thread_local LaunchTimer *tl_timer = nullptr;
-thread_local hipEvent_t tl_stop = nullptr;
 }  // namespace
 
 void set_launch_timer(LaunchTimer *t) { tl_timer = t; }
-void set_next_stop(hipEvent_t e) { tl_stop = e; }
+
+#ifdef GSORT_STAMPS
+extern "C" __attribute__((visibility("default"))) int gsort_diag_stamps(void *d_buf) {
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &d_buf, sizeof(d_buf));
+}
+#endif
 
 template <typename... KA, typename... A>
 inline void launch_k(void (*k)(KA...), dim3 g, dim3 b, uint32_t shm, hipStream_t s, A... a) {
-    hipEvent_t e1 = tl_stop;  // a stop event the caller waits on from another stream
-    tl_stop = nullptr;
+    hipEvent_t e1 = nullptr;
     if (LaunchTimer *t = tl_timer) {
-        if (!e1) e1 = t->make(t->u);
+        e1 = t->make(t->u);
         if (e1) t->last_stop = e1;
     }
     hipExtLaunchKernelGGL(k, g, b, shm, s, nullptr, e1, 0u, static_cast<KA>(a)...);
@@ -3656,7 +3668,7 @@ hipError_t launch_partition3r(const uint32_t *in, uint32_t *out, uint64_t n, uin
     launch_k(k_partition_res<B, I, true, true>, (unsigned)pairs, B, 0, s,
         in, out, n, nullptr, nullptr, reinterpret_cast<const ull *>(bases), cur3, flags,
         (const uint32_t *)nullptr, (const uint32_t *)nullptr, (uint32_t *)nullptr,
-        (uint32_t *)nullptr, (const TileDesc *)nullptr, (unsigned long long *)nullptr, 0ull, 0, 0u, 0u, 0u);
+        (uint32_t *)nullptr, (const TileDesc *)nullptr, (unsigned long long *)nullptr, 0ull, 0, 0u);
     return hipGetLastError();
 }
 
@@ -3678,11 +3690,11 @@ hipError_t launch_partition2r(const uint32_t *in, uint32_t *out, uint16_t *out16
         launch_k(k_partition_res<B, I, false, false, uint16_t>, g2, B, 0, s, in, out16, n, tpfx,
                  desc, bs, cur, flags, raw, (const uint32_t *)nullptr, (uint32_t *)nullptr,
                  (uint16_t *)nullptr, (const TileDesc *)nullptr, (unsigned long long *)nullptr,
-                 0ull, 0, 0u, 0u, 0u);
+                 0ull, 0, 0u);
     else
         launch_k(k_partition_res<B, I, false, false>, g2, B, 0, s, in, out, n, tpfx, desc, bs,
                  cur, flags, raw, (const uint32_t *)nullptr, (uint32_t *)nullptr,
-                 (uint32_t *)nullptr, (const TileDesc *)nullptr, (unsigned long long *)nullptr, 0ull, 0, 0u, 0u, 0u);
+                 (uint32_t *)nullptr, (const TileDesc *)nullptr, (unsigned long long *)nullptr, 0ull, 0, 0u);
     return hipGetLastError();
 }
 
@@ -4016,7 +4028,7 @@ hipError_t launch_est_front(const EstPlan &p, hipStream_t s) {
              p.capx, p.capy, p.capc, p.cap3, reinterpret_cast<ull *>(p.r2),
              reinterpret_cast<ull *>(p.r3), reinterpret_cast<ull *>(p.bases3),
              reinterpret_cast<ull *>(p.bases2), p.cur2, p.lim2, p.init2, p.cur3, p.lim3, p.init3,
-             reinterpret_cast<ull *>(p.wl.ctr), kEstGroupCtrs * (uint32_t)p.groups, p.eflag);
+             reinterpret_cast<ull *>(p.wl.ctr), (uint32_t)(3 * (kLocalClasses + 1)), p.eflag);
     return hipGetLastError();
 }
 
@@ -4036,105 +4048,63 @@ hipError_t launch_est_level3(const EstPlan &p, hipStream_t s) {
              reinterpret_cast<const ull *>(p.bases3), p.cur3, (const uint32_t *)p.eflag,
              (const uint32_t *)nullptr, (const uint32_t *)p.lim3, p.eflag + 1, p.dump,
              (const TileDesc *)nullptr, reinterpret_cast<ull *>(p.mail), (ull)p.seq_elig, p.sb,
-             p.koff, 0u, 0u);
+             p.koff);
     return hipGetLastError();
 }
 
-hipError_t launch_est_tiles(const EstPlan &p, hipStream_t s) {
-    using ull = unsigned long long;
-    const uint32_t max_tiles = (uint32_t)est_max_tiles(p.n);
-    TileDesc *desc = static_cast<TileDesc *>(p.tdesc);
-    launch_k(k_est_tiles, (max_tiles + 255) / 256, 256, 0, s, (const uint32_t *)p.cur3,
-             (const uint32_t *)p.init3, (const uint32_t *)p.lim3,
-             reinterpret_cast<const ull *>(p.bases3), max_tiles, (const uint32_t *)p.eflag, p.tp,
-             desc, desc + max_tiles);
-    return hipGetLastError();
-}
-
-// K3a launch `group`: tiles [group * gtiles, ..) -- gtiles of them, the last launch the rest
-// of est_max_tiles (tiles past K12f's total return at once)
-hipError_t launch_est_part2(const EstPlan &p, int group, hipStream_t s) {
+hipError_t launch_est_level2(const EstPlan &p, hipStream_t s) {
     using ull = unsigned long long;
     constexpr int T2 = kEstTilesL2, B = kPartBlock * T2 / 2, I = kSweepTile / B;
     const uint32_t max_tiles = (uint32_t)est_max_tiles(p.n);
-    const uint32_t gt = p.groups > 1 ? p.gtiles : max_tiles;
-    const uint32_t t0 = (uint32_t)group * gt;
-    if (group < 0 || group >= p.groups || t0 >= max_tiles || (p.groups > 1 && gt % T2))
-        return hipErrorInvalidValue;
-    const uint32_t nt = group == p.groups - 1 ? max_tiles - t0 : gt;
     TileDesc *desc = static_cast<TileDesc *>(p.tdesc);
-    const uint32_t np = (nt + T2 - 1) / T2;
-    // persistent (the launches after the first, with p.persist workgroups): K11e of the earlier
-    // groups gets the rest of every CU (DESIGN.md 5.1, K3a / K11e overlap)
-    const uint32_t pg = (p.persist + 7) & ~7u;  // (a multiple of 8: every workgroup on one XCD)
-    if (group > 0 && pg && pg < np)
-        launch_k(k_partition_res<B, I, false, false, uint16_t, true, T2, true>, pg, B, 0, s,
-                 (const uint32_t *)p.x, p.y, p.n, (const uint32_t *)p.tp, (const TileDesc *)desc,
-                 reinterpret_cast<const ull *>(p.bases2), p.cur2, (const uint32_t *)p.eflag,
-                 (const uint32_t *)nullptr, (const uint32_t *)p.lim2, p.eflag + 1,
-                 reinterpret_cast<uint16_t *>(p.dump), (const TileDesc *)(desc + max_tiles),
-                 (ull *)nullptr, (ull)0, p.sb, 0u, t0, np);
-    else
-        launch_k(k_partition_res<B, I, false, false, uint16_t, true, T2>, np, B, 0, s,
-                 (const uint32_t *)p.x, p.y, p.n, (const uint32_t *)p.tp, (const TileDesc *)desc,
-                 reinterpret_cast<const ull *>(p.bases2), p.cur2, (const uint32_t *)p.eflag,
-                 (const uint32_t *)nullptr, (const uint32_t *)p.lim2, p.eflag + 1,
-                 reinterpret_cast<uint16_t *>(p.dump), (const TileDesc *)(desc + max_tiles),
-                 (ull *)nullptr, (ull)0, p.sb, 0u, t0, 0u);
+    TileDesc *pieces = desc + max_tiles;
+    launch_k(k_est_tiles, (max_tiles + 255) / 256, 256, 0, s, (const uint32_t *)p.cur3,
+             (const uint32_t *)p.init3, (const uint32_t *)p.lim3,
+             reinterpret_cast<const ull *>(p.bases3), max_tiles, (const uint32_t *)p.eflag, p.tp,
+             desc, pieces);
+    launch_k(k_partition_res<B, I, false, false, uint16_t, true, T2>,
+             (max_tiles + T2 - 1) / T2, B, 0, s,
+             (const uint32_t *)p.x, p.y, p.n, (const uint32_t *)p.tp, (const TileDesc *)desc,
+             reinterpret_cast<const ull *>(p.bases2), p.cur2, (const uint32_t *)p.eflag,
+             (const uint32_t *)nullptr, (const uint32_t *)p.lim2, p.eflag + 1,
+             reinterpret_cast<uint16_t *>(p.dump),
+             (const TileDesc *)pieces, (ull *)nullptr, (ull)0, p.sb, 0u);
     return hipGetLastError();
 }
 
-// group g's lists and counters (launch_est_classify, launch_local_sort_e, launch_est_oversized)
-WorkLists est_group_lists(const EstPlan &p, int group) {
-    WorkLists wl = p.wl;
-    for (int k = 0; k <= kLocalClasses; ++k) wl.list[k] += (size_t)2 * kBuckets16 * group;
-    wl.ctr += (size_t)kEstGroupCtrs * group;
-    return wl;
-}
-
-hipError_t launch_est_classify(const EstPlan &p, int group, hipStream_t s) {
+hipError_t launch_est_classify(const EstPlan &p, hipStream_t s) {
     using ull = unsigned long long;
-    if (group < 0 || group >= p.groups) return hipErrorInvalidValue;
     launch_k(k_est_classify, kRadix, kRadix, 0, s, (const uint32_t *)p.cur2,
              (const uint32_t *)p.init2, (const uint32_t *)p.lim2, (const uint32_t *)p.cur3,
-             (const uint32_t *)p.init3, reinterpret_cast<const ull *>(p.bases2),
-             est_group_lists(p, group), p.eflag, p.in, p.sb, p.koff, (const uint32_t *)p.tp,
-             (uint32_t)group, (uint32_t)p.groups, p.gtiles);
+             (const uint32_t *)p.init3, reinterpret_cast<const ull *>(p.bases2), p.wl, p.eflag,
+             p.in, p.sb, p.koff);
     return hipGetLastError();
 }
 
-hipError_t launch_est_oversized(const EstPlan &p, uint32_t nlist, int ncu, hipStream_t s,
-                                int group) {
+hipError_t launch_est_oversized(const EstPlan &p, uint32_t nlist, int ncu, hipStream_t s) {
     using ull = unsigned long long;
     if (nlist == 0) return hipSuccess;
-    if (group < 0 || group >= p.groups) return hipErrorInvalidValue;
     const unsigned grid = (unsigned)std::min<uint32_t>(nlist, (uint32_t)std::max(ncu, 1));
     launch_k(k_count_expand<uint16_t, true>, grid, 1024, 0, s, (const uint16_t *)p.y,
              (const ull *)nullptr, (const ull *)nullptr, 1, (const ull *)nullptr,
-             reinterpret_cast<const ull *>(est_group_lists(p, group).list[0]), nlist, p.out,
-             p.koff);
+             reinterpret_cast<const ull *>(p.wl.list[0]), nlist, p.out, p.koff);
     return hipGetLastError();
 }
 
 hipError_t launch_est_publish(const EstPlan &p, hipStream_t s) {
     using ull = unsigned long long;
-    launch_k(k_publish_lists, 1, 256, 0, s, reinterpret_cast<ull *>(p.mail),
-             reinterpret_cast<const ull *>(p.wl.ctr), (const uint32_t *)p.eflag, (ull)p.seq_done,
-             kEstGroupCtrs * (uint32_t)p.groups);
+    launch_k(k_publish_lists, 1, 64, 0, s, reinterpret_cast<ull *>(p.mail),
+             reinterpret_cast<const ull *>(p.wl.ctr), (const uint32_t *)p.eflag, (ull)p.seq_done);
     return hipGetLastError();
 }
 
 hipError_t launch_local_sort_e(const EstPlan &p, int cls, uint32_t first, uint32_t nlist,
-                               bool publish, hipStream_t s, int group) {
+                               bool publish, hipStream_t s) {
     using ull = unsigned long long;
     if (nlist == 0) return hipSuccess;
-    if (cls < 1 || cls > kLocalClasses || group < 0 || group >= p.groups)
-        return hipErrorInvalidValue;
-    const WorkLists gl = est_group_lists(p, group);
-    const ull *l = reinterpret_cast<const ull *>(gl.list[cls]);
-    const ull *call = reinterpret_cast<const ull *>(p.wl.ctr);
-    const ull *ctr = reinterpret_cast<const ull *>(gl.ctr) + 3 * cls;
-    const uint32_t nctr = kEstGroupCtrs * (uint32_t)p.groups;
+    if (cls < 1 || cls > kLocalClasses) return hipErrorInvalidValue;
+    const ull *l = reinterpret_cast<const ull *>(p.wl.list[cls]);
+    const ull *call = reinterpret_cast<const ull *>(p.wl.ctr), *ctr = call + 3 * cls;
     const uint16_t *y = p.y;
     const uint32_t *ef = p.eflag;
     const uint32_t ko = p.koff;
@@ -4146,13 +4116,13 @@ hipError_t launch_local_sort_e(const EstPlan &p, int cls, uint32_t first, uint32
     do {                                                                                       \
         if (nd == 0)                                                                           \
             launch_k(k_local_sort_e<B, I, true, true>, nlist, B, 0, s, y, p.out, l, ctr, first, \
-                     nd, mail, call, ef, seq, ko, nctr);                                       \
+                     nd, mail, call, ef, seq, ko);                                             \
         else if (p.atomic_rank)                                                                \
             launch_k(k_local_sort_e<B, I, true>, nlist, B, 0, s, y, p.out, l, ctr, first, nd,  \
-                     mail, call, ef, seq, ko, nctr);                                           \
+                     mail, call, ef, seq, ko);                                                 \
         else                                                                                   \
             launch_k(k_local_sort_e<B, I, false>, nlist, B, 0, s, y, p.out, l, ctr, first, nd, \
-                     mail, call, ef, seq, ko, nctr);                                           \
+                     mail, call, ef, seq, ko);                                                 \
     } while (0)
     switch (cls) {
         case 1: GSORT_K11E(256, 18); break;

@@ -88,12 +88,6 @@ struct gsort_ctx {
     int ncu = 256;
     int last_plan = 0;      // gsort_last_plan: 0 exact, 1 sampled, 2 sampled then exact
     bool plan_trace = false; // GSORT_PLAN_TRACE: one stderr line per plan decision
-    // GSORT_EST_GROUPS: K3a of the sampled plan as that many launches, each group's K12g + K11e
-    // on stream2 behind its launch's stop event (DESIGN.md 5.1, K3a / K11e overlap)
-    int est_groups = 1;
-    int est_persist = 0;  // GSORT_EST_PERSIST: K3a launches 2.. as persistent grids (WGs per CU)
-    hipStream_t stream2 = nullptr;
-    hipEvent_t ev_grp[kEstMaxGroups + 1] = {};
     DevBuf m_ex, m_ey, m_epart, m_eplan, m_edesc, m_edump;
     DevBuf m_gplan;  // one dominant child: counts (65536 u64), starts (65537 u64), chunk bins
     bool est_busy = false;   // msd_sort_est is using m_ex / m_ey (not reclaimable)
@@ -137,9 +131,7 @@ constexpr size_t OFF_HIST = 0, OFF_TOT = 8192, OFF_BASES = 10240, OFF_CTR = 1228
                  OFF_ONE = 12416, OFF_CTR3 = 12544, OFF_PLAN = 20480;
 constexpr size_t OFF_FLAGS = 12408;  // K12b's trivial-level word, inside the published range
 constexpr size_t OFF_MINMAX = 12480;  // the offset retry's exact min / max (2 int32)
-constexpr size_t OFF_GIANT = 16384;   // K1m result (3 u64) + K1g counters (ctr[0] + one per workgroup)
-constexpr size_t OFF_ECTR = 18560;    // the sampled plan's K11e list counters, 15 per K3a group
-static_assert(OFF_ECTR + (size_t)kEstGroupCtrs * kEstMaxGroups * 8 <= OFF_PLAN, "counters");
+constexpr size_t OFF_GIANT = 16384;   // K1m result (3 u64) + K1g counters (16 u64)
 
 gsort_status set_err(gsort_ctx *c, gsort_status st, const std::string &msg) {
     if (c) c->err = msg;
@@ -970,7 +962,7 @@ gsort_status msd_sort_h16(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
 // and the K11e list counts K12g leaves in the mailbox (one wait, after level 2), then launches
 // K11e; *ok = false means nothing was written to out and the caller sorts on the exact plan.
 // the sampled plan's mailbox words start here (EstPlan::mail: kEstMailWords of them)
-constexpr size_t kEstMailWord = 256;
+constexpr size_t kEstMailWord = 400;
 static_assert((kEstMailWord + kEstMailWords) * 8 <= kMailBytes, "mailbox");
 
 // Keys of the region buffers the caps of `nreg` regions can add up to (k_est_plan's est_cap:
@@ -999,9 +991,6 @@ gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
     *ok = false;
     if (retry) *retry = EstRetry{};
     const double slack = std::max(c->est_slack, 0.0);
-    // K3a launches (GSORT_EST_GROUPS; 1: one launch, everything on c->stream)
-    const int groups = std::max(1, std::min(est_groups_for(n, std::min(c->est_groups, kEstMaxGroups)),
-                                            kEstMaxGroups));
     const uint64_t capx = est_region_keys(n, (uint64_t)kH16Shards * kRadix, slack);
     const uint64_t capy = std::min<uint64_t>(est_region_keys(n, kBuckets16, slack),
                                              (uint64_t)kBuckets16 * kLocalMax);
@@ -1025,9 +1014,8 @@ gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
                         ((size_t)est_max_tiles(n) + kH16Shards * kRadix) * kTileDescBytes);
         if (st == GSORT_OK) st = ensure(c, c->m_edump, (size_t)kSweepTile * 4);
         for (int k = 0; k < kLocalClasses && st == GSORT_OK; ++k)
-            st = ensure_list(c, c->m_local[k], (uint64_t)kBuckets16 * groups);
-        if (st == GSORT_OK)  // K18c: > kLocalMax
-            st = ensure_list(c, c->m_next[0], (uint64_t)kBuckets16 * groups);
+            st = ensure_list(c, c->m_local[k], kBuckets16);
+        if (st == GSORT_OK) st = ensure_list(c, c->m_next[0], kBuckets16);  // K18c: > kLocalMax
         c->est_busy = false;
         if (st == GSORT_OK && (!c->m_ex.p || !c->m_ey.p))
             return set_err(c, GSORT_EINVAL, "sampled plan: region buffers missing");
@@ -1075,10 +1063,6 @@ gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
     p.tdesc = c->m_edesc.p;
     p.dump = static_cast<uint32_t *>(c->m_edump.p);
     p.wl = work_lists(c, 0);
-    p.wl.ctr = reinterpret_cast<uint64_t *>(c->d_small + OFF_ECTR);
-    p.groups = groups;
-    p.gtiles = groups > 1 ? est_group_tiles(n, groups) : 0u;
-    p.persist = (uint32_t)std::max(0, c->est_persist * c->ncu);
     p.slack = slack;
     p.atomic_rank = c->atomic_rank;
     p.sb = sb;
@@ -1088,12 +1072,11 @@ gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
     p.seq_done = ++c->mail_seq;
     volatile uint64_t *mail = c->h_mail + kEstMailWord;
     // poll a sequence word of the mailbox; a stream that goes idle without it is an error
-    auto wait_word = [&](size_t w, uint64_t seq, const char *what,
-                         hipStream_t qs = nullptr) -> gsort_status {
+    auto wait_word = [&](size_t w, uint64_t seq, const char *what) -> gsort_status {
         QueryTimer qt;
         for (uint64_t spin = 0; mail[w] != seq; ++spin) {
             if ((spin & 1023) == 1023) {
-                const hipError_t q = qt.due() ? hipStreamQuery(qs ? qs : c->stream) : hipErrorNotReady;
+                const hipError_t q = qt.due() ? hipStreamQuery(c->stream) : hipErrorNotReady;
                 if (q != hipErrorNotReady && mail[w] != seq)
                     return set_err(c, GSORT_EHIP, std::string("sampled plan: ") + what + ": " +
                                                       (q == hipSuccess ? "stream idle without it"
@@ -1113,29 +1096,9 @@ gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
     // K12f, K3a and K12g return at once on an ineligible block too, so they are queued before
     // the host looks at the eligibility word (waiting first left a launch gap behind K3r)
     t = tic(c);
-    HIP_TRY(c, launch_est_tiles(p, c->stream));
-    // Grouped: K3a launch g carries the stop event its group's K12g + K11e wait on (stream2),
-    // so that K11e runs beside K3a launch g + 1
-    hipStream_t s2 = c->stream;
-    hipEvent_t ev[kEstMaxGroups];
-    if (groups > 1) {
-        if (!c->stream2) HIP_TRY(c, hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
-        s2 = c->stream2;
-        for (int g = 0; g < groups; ++g) {
-            ev[g] = c->timing ? next_event(c) : nullptr;
-            if (!ev[g]) {
-                if (!c->ev_grp[g])
-                    HIP_TRY(c, hipEventCreateWithFlags(&c->ev_grp[g], hipEventDisableTiming));
-                ev[g] = c->ev_grp[g];
-            }
-        }
-    }
-    for (int g = 0; g < groups; ++g) {
-        if (groups > 1) set_next_stop(ev[g]);
-        HIP_TRY(c, launch_est_part2(p, g, c->stream));
-    }
+    HIP_TRY(c, launch_est_level2(p, c->stream));
     toc(c, PH_LEVEL2, t);
-    if (groups == 1) HIP_TRY(c, launch_est_classify(p, 0, c->stream));
+    HIP_TRY(c, launch_est_classify(p, c->stream));
     ST_TRY(wait_word(3, p.seq_elig, "eligibility word"));
     if (c->plan_trace)
         fprintf(stderr, "gsort plan: n %llu sb %d koff %u eflag %llx children %llu maxc %llx\n",
@@ -1146,7 +1109,7 @@ gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
         // sorted ranges) whose removal leaves children K11e can take: then the caller retries
         // with every digit that many bits lower (at most 16, the plan's two levels).  One or
         // two shared bits (Zipf, any non-negative keys) rarely turn an ineligible block
-        // eligible and are not worth a second sample.  (Nothing was queued on stream2.)
+        // eligible and are not worth a second sample.
         if (retry) {
             retry->vary = (uint32_t)mail[5];
             retry->lo = (uint32_t)mail[6];
@@ -1156,21 +1119,6 @@ gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
         }
         return GSORT_OK;
     }
-    // From here on stream2 may hold work: c->stream waits for all of it before the call goes on
-    // (an overflowed plan's exact re-sort writes out too), on every path.
-    struct Join {
-        gsort_ctx *c;
-        hipStream_t s2;
-        hipEvent_t e;
-        ~Join() {
-            if (s2 == c->stream) return;
-            if (hipEventRecord(e, s2) != hipSuccess || hipStreamWaitEvent(c->stream, e, 0) != hipSuccess)
-                (void)hipStreamSynchronize(s2);  // (cannot fail silently: order by blocking)
-        }
-    };
-    if (groups > 1 && !c->ev_grp[kEstMaxGroups])
-        HIP_TRY(c, hipEventCreateWithFlags(&c->ev_grp[kEstMaxGroups], hipEventDisableTiming));
-    Join join{c, s2, c->ev_grp[kEstMaxGroups]};
     // K11e of the class the average child falls in, queued right behind K12g (a grid of the
     // sampled children: at least its entries, usually exactly), so no host round trip sits
     // between K12g and the largest K11e launch; the other classes follow once the counts are in
@@ -1180,50 +1128,27 @@ gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t
     // published the counters)
     const int kmax = sb >= 8 ? kLocalClasses : kEstCx - 1;
     const int kspec = sampled ? std::min(std::max(local_class(n / sampled), 1), kmax) : 0;
-    // each group's speculative grid: its share of the sampled children (groups hold equal tile
-    // ranges) with a margin; entries past K12g's count return at once, the rest follow below
-    uint32_t spec[kEstMaxGroups];
-    {
-        const double share = groups > 1 ? (double)p.gtiles / (double)(sweep_tiles(n) + 128) : 1.0;
-        for (int g = 0; g < groups; ++g)
-            spec[g] = groups > 1 ? (uint32_t)std::min<double>(kBuckets16, sampled * share * 1.2 + 64)
-                                 : sampled;
-    }
     t = tic(c);
-    for (int g = 0; g < groups; ++g) {
-        if (groups > 1) {
-            HIP_TRY(c, hipStreamWaitEvent(s2, ev[g], 0));
-            HIP_TRY(c, launch_est_classify(p, g, s2));
-        }
-        if (kspec) HIP_TRY(c, launch_local_sort_e(p, kspec, 0, spec[g], g == groups - 1, s2, g));
-    }
-    if (!kspec) HIP_TRY(c, launch_est_publish(p, s2));
-    ST_TRY(wait_word(1, p.seq_done, "K12g counters", s2));  // (published on s2)
+    if (kspec) HIP_TRY(c, launch_local_sort_e(p, kspec, 0, sampled, true, c->stream));
+    else HIP_TRY(c, launch_est_publish(p, c->stream));
+    ST_TRY(wait_word(1, p.seq_done, "K12g counters"));
     if (mail[0] != 0) {  // a region overflowed: *ok stays false
         if (c->plan_trace) fprintf(stderr, "gsort plan: overflow %llx\n", (unsigned long long)mail[0]);
         return GSORT_OK;
     }
-    constexpr int NC = (int)kEstGroupCtrs;
-    uint64_t h[NC * kEstMaxGroups];
-    for (int i = 0; i < NC * groups; ++i) h[i] = mail[kEstMailCtr + i];
+    uint64_t h[3 * (kLocalClasses + 1)];
+    for (int i = 0; i < 3 * (kLocalClasses + 1); ++i) h[i] = mail[8 + i];
     uint64_t keys = 0, ent = 0;  // (list 0: the children past kLocalMax, K18c)
-    for (int g = 0; g < groups; ++g)
-        for (int k = 0; k <= kLocalClasses; ++k) {
-            keys += h[NC * g + 3 * k + 1];
-            ent += h[NC * g + 3 * k];
-        }
+    for (int k = 0; k <= kLocalClasses; ++k) { keys += h[3 * k + 1]; ent += h[3 * k]; }
     if (keys != n || ent > kBuckets16)  // every key in exactly one K11e entry
         return set_err(c, GSORT_EINVAL, "sampled plan: K11e lists hold " + std::to_string(keys) +
                                             " keys in " + std::to_string(ent) + " entries, want " +
                                             std::to_string(n) + " keys");
-    for (int g = 0; g < groups; ++g) {
-        const uint64_t *hg = h + NC * g;
-        for (int k = 1; k <= kmax; ++k) {
-            const uint32_t done = k == kspec ? spec[g] : 0u, cnt = (uint32_t)hg[3 * k];
-            if (cnt > done) HIP_TRY(c, launch_local_sort_e(p, k, done, cnt - done, false, s2, g));
-        }
-        if (hg[0]) HIP_TRY(c, launch_est_oversized(p, (uint32_t)hg[0], c->ncu, s2, g));
+    for (int k = 1; k <= kmax; ++k) {
+        const uint32_t done = k == kspec ? sampled : 0u, cnt = (uint32_t)h[3 * k];
+        if (cnt > done) HIP_TRY(c, launch_local_sort_e(p, k, done, cnt - done, false, c->stream));
     }
+    if (h[0]) HIP_TRY(c, launch_est_oversized(p, (uint32_t)h[0], c->ncu, c->stream));
     toc(c, PH_BUCKET, t);
     *ok = true;
     if (stats) stats->buckets_local += ent;
@@ -1261,7 +1186,7 @@ gsort_status giant_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *
     c->fix_clean = nullptr;
     // ctr: [0] cold keys below the child, [1 + b] workgroup b's cold keys (1 + g <= 257 u64,
     // inside OFF_GIANT's 4 KiB)
-    static_assert(OFF_GIANT + (4 + 1 + kH16Blocks) * 8 <= OFF_ECTR, "giant counters");
+    static_assert(OFF_GIANT + (4 + 1 + kH16Blocks) * 8 <= OFF_PLAN, "giant counters");
     uint64_t *d_ctr = reinterpret_cast<uint64_t *>(c->d_small + OFF_GIANT) + 4;
     uint64_t *h_ctr = reinterpret_cast<uint64_t *>(c->h_small + OFF_GIANT) + 4;
     uint64_t *counts = static_cast<uint64_t *>(c->m_gplan.p), *starts = counts + kBuckets16;
@@ -2518,9 +2443,6 @@ gsort_status create_common(gsort_ctx *c, int hip_device) {
     if (const char *e = getenv("GSORT_RECV_CX")) c->recv_cx = atoi(e);
     if (const char *e = getenv("GSORT_EST_SLACK")) c->est_slack = atof(e);
     if (const char *e = getenv("GSORT_PLAN_TRACE")) c->plan_trace = atoi(e) != 0;
-    if (const char *e = getenv("GSORT_EST_GROUPS"))
-        c->est_groups = std::max(1, std::min(atoi(e), kEstMaxGroups));
-    if (const char *e = getenv("GSORT_EST_PERSIST")) c->est_persist = std::max(0, std::min(atoi(e), 2));
     HIP_TRY(c, hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, hip_device));
     {
         std::lock_guard<std::mutex> lk(g_ctx_mu);
@@ -2641,7 +2563,6 @@ gsort_status gsort_destroy(gsort_ctx *c) {
     }
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    if (c->stream2) (void)hipStreamSynchronize(c->stream2);
     delete c->comm;
     for_each_buf(c, [](const std::string &, DevBuf &b) { (void)dev_free(b); });
     c->d_small = nullptr;
@@ -2652,9 +2573,6 @@ gsort_status gsort_destroy(gsort_ctx *c) {
     if (c->h_small) (void)hipHostFree(c->h_small);
     if (c->h_mail) (void)hipHostFree(c->h_mail);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
-    for (auto e : c->ev_grp)
-        if (e) (void)hipEventDestroy(e);
-    if (c->stream2) (void)hipStreamDestroy(c->stream2);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return GSORT_OK;
