@@ -192,10 +192,15 @@ Comm *make_rccl_comm(int rank, int nranks, const gsort_uid *uid, std::string *er
 }
 
 // ---------------------------------------------------------------------------------------
-// In-process rank group.  Each collective: every rank synchronises its stream (its send data
-// is complete), publishes pointers, meets the others at a barrier, pulls what it needs with
-// hipMemcpyAsync on its own stream, synchronises, and meets them again (so no sender reuses a
-// buffer a peer is still reading).
+// In-process rank group, stream-ordered like RCCL (no host wait on the GPU inside a
+// collective).  Each collective: every rank records a "ready" event on its stream (its send
+// data is complete once the stream reaches it), publishes pointers and events, meets the others
+// at a host barrier, makes its stream wait for the peers' ready events and pulls what it needs
+// with hipMemcpyAsync, records a "done" event, meets them again, and makes its stream wait for
+// the peers' done events (so no rank reuses a buffer a peer is still reading).  The two
+// barriers order every event's record before the waits on it and before its next record.
+// (Round 4 and before synchronised both streams in every collective: the P-rank emulation then
+// paid host round trips that the RCCL path does not.)
 // ---------------------------------------------------------------------------------------
 struct GroupState {
     int n;
@@ -206,7 +211,15 @@ struct GroupState {
     bool broken = false;
     std::vector<const void *> ptr;
     std::vector<const size_t *> count, displ;
-    explicit GroupState(int n_) : n(n_), ptr(n_), count(n_), displ(n_) {}
+    std::vector<hipEvent_t> ready, done;  // per rank, created by the rank on first use
+    explicit GroupState(int n_)
+        : n(n_), ptr(n_), count(n_), displ(n_), ready(n_, nullptr), done(n_, nullptr) {}
+    ~GroupState() {
+        for (auto e : ready)
+            if (e) (void)hipEventDestroy(e);
+        for (auto e : done)
+            if (e) (void)hipEventDestroy(e);
+    }
 };
 
 GroupState *group_state_create(int nranks) { return new GroupState(nranks); }
@@ -253,30 +266,54 @@ class GroupComm : public Comm {
         return GSORT_EHIP;
     }
 
-    gsort_status allgather(const void *send, void *recv, size_t bytes, hipStream_t s) override {
-        gsort_status st = hip([&] { return hipStreamSynchronize(s); }, "hipStreamSynchronize");
-        if (st != GSORT_OK) return st;
-        g_->ptr[rank_] = send;
+    // the collective's first half: this rank's ready event recorded and published, the
+    // barrier, the stream made to wait for every peer's ready event
+    gsort_status open(hipStream_t s) {
+        gsort_status st = GSORT_OK;
+        for (hipEvent_t *e : {&g_->ready[rank_], &g_->done[rank_]})
+            if (!*e && st == GSORT_OK)
+                st = hip([&] { return hipEventCreateWithFlags(e, hipEventDisableTiming); },
+                         "hipEventCreateWithFlags");
+        if (st == GSORT_OK)
+            st = hip([&] { return hipEventRecord(g_->ready[rank_], s); }, "hipEventRecord");
+        // (a failed rank still meets the barrier: the others must not wait for it in vain)
         if (!barrier()) return fail("barrier timeout");
+        for (int r = 0; r < size_ && st == GSORT_OK; ++r)
+            if (r != rank_)
+                st = hip([&] { return hipStreamWaitEvent(s, g_->ready[r], 0); },
+                         "hipStreamWaitEvent");
+        return st;
+    }
+    // the second half: done event recorded, the barrier, the stream made to wait for the peers'
+    // done events (their reads of this rank's buffers)
+    gsort_status close(hipStream_t s, gsort_status st) {
+        if (st == GSORT_OK)
+            st = hip([&] { return hipEventRecord(g_->done[rank_], s); }, "hipEventRecord");
+        if (!barrier()) return fail("barrier timeout");
+        for (int r = 0; r < size_ && st == GSORT_OK; ++r)
+            if (r != rank_)
+                st = hip([&] { return hipStreamWaitEvent(s, g_->done[r], 0); },
+                         "hipStreamWaitEvent");
+        return st;
+    }
+    gsort_status allgather(const void *send, void *recv, size_t bytes, hipStream_t s) override {
+        g_->ptr[rank_] = send;
+        gsort_status st = open(s);
         for (int r = 0; r < size_ && st == GSORT_OK; ++r)
             if (bytes)
                 st = hip([&] {
                     return hipMemcpyAsync((char *)recv + (size_t)r * bytes, g_->ptr[r], bytes,
                                           hipMemcpyDeviceToDevice, s);
                 }, "hipMemcpyAsync");
-        if (st == GSORT_OK) st = hip([&] { return hipStreamSynchronize(s); }, "hipStreamSynchronize");
-        if (!barrier()) return fail("barrier timeout");
-        return st;
+        return close(s, st);
     }
     gsort_status alltoallv(const void *send, const size_t *scount, const size_t *sdispl,
                            void *recv, const size_t *rcount, const size_t *rdispl,
                            hipStream_t s) override {
-        gsort_status st = hip([&] { return hipStreamSynchronize(s); }, "hipStreamSynchronize");
-        if (st != GSORT_OK) return st;
         g_->ptr[rank_] = send;
         g_->count[rank_] = scount;
         g_->displ[rank_] = sdispl;
-        if (!barrier()) return fail("barrier timeout");
+        gsort_status st = open(s);
         for (int r = 0; r < size_ && st == GSORT_OK; ++r) {
             const size_t c = g_->count[r][rank_];
             if (c != rcount[r]) { st = fail("send/recv count mismatch"); break; }
@@ -287,22 +324,16 @@ class GroupComm : public Comm {
                                           hipMemcpyDeviceToDevice, s);
                 }, "hipMemcpyAsync");
         }
-        gsort_status st2 = hip([&] { return hipStreamSynchronize(s); }, "hipStreamSynchronize");
-        if (!barrier()) return fail("barrier timeout");
-        return st != GSORT_OK ? st : st2;
+        return close(s, st);
     }
     gsort_status bcast(void *buf, size_t bytes, int root, hipStream_t s) override {
-        gsort_status st = hip([&] { return hipStreamSynchronize(s); }, "hipStreamSynchronize");
-        if (st != GSORT_OK) return st;
         g_->ptr[rank_] = buf;
-        if (!barrier()) return fail("barrier timeout");
-        if (rank_ != root && bytes)
+        gsort_status st = open(s);
+        if (st == GSORT_OK && rank_ != root && bytes)
             st = hip([&] {
                 return hipMemcpyAsync(buf, g_->ptr[root], bytes, hipMemcpyDeviceToDevice, s);
             }, "hipMemcpyAsync");
-        gsort_status st2 = hip([&] { return hipStreamSynchronize(s); }, "hipStreamSynchronize");
-        if (!barrier()) return fail("barrier timeout");
-        return st != GSORT_OK ? st : st2;
+        return close(s, st);
     }
 
   private:

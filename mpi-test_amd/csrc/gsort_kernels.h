@@ -210,8 +210,17 @@ hipError_t launch_gb_from_plan(const uint64_t *bases, const uint64_t *totals,
 // K13s: one radix-select round decided on the device (boundary q: prefix[q] += the largest
 // digit d whose all-gathered count of keys below prefix[q] + (d << shift) stays <= g[q]; the
 // next round's M thresholds prefix[q] + (d << (shift - 8)) written to xs).
-hipError_t launch_select_digit(const uint64_t *all, const uint64_t *g, uint64_t N, int P, int nb,
-                               int M, int shift, uint64_t *prefix, uint64_t *xs, hipStream_t s);
+// all: P rows of W u64 (boundary q's M counts at q * M); shift 0 (the last round) writes no xs.
+hipError_t launch_select_digit(const uint64_t *all, int W, const uint64_t *g, uint64_t N, int P,
+                               int nb, int M, int shift, uint64_t *prefix, uint64_t *xs,
+                               hipStream_t s);
+// K13g: block q sorts boundary q's 16-bit group (prefix[q] >> 16, known after the second select
+// round) in place in the packed buffer (u16 low halves; gb = the block's 16-bit bucket bounds);
+// big[q] = 1 if its group holds more than 32 768 keys (left unsorted: the caller's host path),
+// else 0 (nb flags).
+hipError_t launch_boundary_sort16(uint16_t *pack, const uint64_t *gb, const uint64_t *prefix,
+                                  const uint64_t *g, uint64_t N, int nb, bool atomic_rank,
+                                  uint64_t *big, hipStream_t s);
 // K13 on the packed buffer (bucket bounds gb): out[i] = #keys < xs[i] (ordered u32).
 hipError_t launch_count_below16(const uint16_t *a, const uint64_t *gb, const uint64_t *xs,
                                 int m, uint64_t *out, hipStream_t s);

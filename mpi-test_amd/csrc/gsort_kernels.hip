@@ -1814,7 +1814,9 @@ __device__ __forceinline__ uint32_t wave_rank(uint32_t *wc, uint32_t d, bool val
 constexpr bool lds_pad(int tile) { return tile < 32768; }
 constexpr int lds_slots(int tile) { return lds_pad(tile) ? tile + tile / 32 : tile; }
 
-template <int BLOCK, int ITEMS, bool ATOMIC>
+// STORE16: dst holds u16 -- the sorted keys' low 16 bits are stored there (no flip): the
+// distributed sender's boundary groups, sorted in place in the packed send buffer.
+template <int BLOCK, int ITEMS, bool ATOMIC, bool STORE16 = false>
 __device__ __forceinline__ void sort_bucket(uint32_t (&k)[ITEMS], uint32_t len, int ndigits,
                                             uint32_t *__restrict__ dst, uint32_t *s_a,
                                             uint32_t *s_wc, uint32_t koff = 0) {
@@ -1911,7 +1913,7 @@ __device__ __forceinline__ void sort_bucket(uint32_t (&k)[ITEMS], uint32_t len, 
                 s_a[at(wc[(k[i] >> shift) & 255u] + rk[i])] = k[i];
         __syncthreads();
     }
-    const __amdgpu_buffer_rsrc_t rs = bucket_rsrc(dst, len * 4u);  // stores past len dropped
+    const __amdgpu_buffer_rsrc_t rs = bucket_rsrc(dst, len * (STORE16 ? 2u : 4u));  // stores past len dropped
     // the bucket is one contiguous run of out: nontemporal stores for the 9216-key classes and
     // up (K11e class 2: 472 -> 452-462 us; the 4608-key class measured 113 -> 115 us with them,
     // its runs' partial end lines then miss the neighbours' in L2; K3r / K3a's scattered digit
@@ -1922,8 +1924,11 @@ __device__ __forceinline__ void sort_bucket(uint32_t (&k)[ITEMS], uint32_t len, 
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
         const uint32_t j = (uint32_t)(i * BLOCK + tid);
-        __builtin_amdgcn_raw_buffer_store_b32((fa[i * at(BLOCK)] + koff) ^ kFlip, rs, (int)(j * 4u),
-                                              0, kNtFinal ? 2 : 0);  // (2: nt)
+        if (STORE16)
+            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)fa[i * at(BLOCK)], rs, (int)(j * 2u), 0, 0);
+        else
+            __builtin_amdgcn_raw_buffer_store_b32((fa[i * at(BLOCK)] + koff) ^ kFlip, rs,
+                                                  (int)(j * 4u), 0, kNtFinal ? 2 : 0);  // (2: nt)
     }
 }
 
@@ -3732,14 +3737,15 @@ hipError_t launch_count_below16(const uint16_t *a, const uint64_t *gb, const uin
 // <= g[q] (the counts grow with d), prefix[q] gains it, and the next round's M thresholds
 // prefix[q] + (d << (shift - 8)) go to xs.  Boundaries at the end (g[q] >= N) keep their prefix.
 __global__ __launch_bounds__(256) void k_select_digit(const unsigned long long *__restrict__ all,
+                                                      int W,
                                                       const unsigned long long *__restrict__ g,
                                                       unsigned long long N, int P, int nb, int M,
                                                       int shift, unsigned long long *prefix,
                                                       unsigned long long *__restrict__ xs) {
     __shared__ uint32_t s_ok;
     const int q = blockIdx.x, d = threadIdx.x;
-    unsigned long long below = 0;
-    for (int p = 0; p < P; ++p) below += all[((size_t)p * nb + q) * M + d];
+    unsigned long long below = 0;  // (rank p's row: W words, boundary q's M counts at q * M)
+    for (int p = 0; p < P; ++p) below += all[(size_t)p * W + (size_t)q * M + d];
     const unsigned long long gq = g[q], p0 = prefix[q];
     if (d == 0) s_ok = 0;
     __syncthreads();
@@ -3749,15 +3755,72 @@ __global__ __launch_bounds__(256) void k_select_digit(const unsigned long long *
     const uint32_t best = s_ok ? s_ok - 1 : 0;
     const unsigned long long pf = gq >= N ? p0 : p0 + ((unsigned long long)best << shift);
     if (d == 0) prefix[q] = pf;
-    for (int j = d; j < M; j += 256) xs[(size_t)q * M + j] = pf + ((unsigned long long)j << (shift - 8));
+    if (shift >= 8)  // (the last round leaves the boundary keys; no next thresholds)
+        for (int j = d; j < M; j += 256) xs[(size_t)q * M + j] = pf + ((unsigned long long)j << (shift - 8));
 }
 
-hipError_t launch_select_digit(const uint64_t *all, const uint64_t *g, uint64_t N, int P, int nb,
-                               int M, int shift, uint64_t *prefix, uint64_t *xs, hipStream_t s) {
+// K13g: after the second select round every boundary's 16-bit group h_q = prefix[q] >> 16 is
+// known on the device; block q sorts its group in place in the packed send buffer (u16 low
+// halves, gb = the 16-bit bucket bounds) so that rounds 3 and 4 can binary-search it and the
+// cut splits it by value -- with no host round trip.  Boundaries sharing a group
+// (consecutive q: the boundary keys grow with q) leave it to the first of them; a boundary at
+// the block's end (g[q] >= N) has none.  A group past this kernel's 32 768 keys is left as it
+// is and flagged in big[q] (every block writes its flag, 0 or 1; the rounds' all-gathered count
+// rows carry the flags to every rank, and the runtime then sorts such groups on the host path
+// and repeats rounds 3 and 4).
+template <bool ATOMIC>
+__global__ __launch_bounds__(1024) void k_boundary_sort16(uint16_t *__restrict__ pack,
+                                                          const unsigned long long *__restrict__ gb,
+                                                          const unsigned long long *__restrict__ prefix,
+                                                          const unsigned long long *__restrict__ g,
+                                                          unsigned long long N,
+                                                          unsigned long long *__restrict__ big) {
+    constexpr int BLOCK = 1024, ITEMS = 32, TILE = BLOCK * ITEMS;
+    __shared__ uint32_t s_a[lds_slots(TILE)];
+    __shared__ uint32_t s_wc[(BLOCK / 64) * kRadix];
+    const int q = blockIdx.x;
+    const unsigned long long h = prefix[q] >> 16;
+    const bool mine = g[q] < N && h < kBuckets16 &&
+                      !(q > 0 && g[q - 1] < N && (prefix[q - 1] >> 16) == h);
+    const unsigned long long a = mine ? gb[h] : 0ull, b = mine ? gb[h + 1] : 0ull;
+    const bool too_big = b > a && b - a > (unsigned long long)TILE;
+    if (threadIdx.x == 0) big[q] = too_big ? 1ull : 0ull;
+    if (b <= a || too_big) return;
+    const uint32_t len = (uint32_t)(b - a), top = (uint32_t)h << 16;
+    if (threadIdx.x < kRadix) s_wc[threadIdx.x] = 0;
+    uint32_t k[ITEMS];
+    const __amdgpu_buffer_rsrc_t rs = bucket_rsrc(pack + a, len * 2u);
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j)
+        k[j] = top | __builtin_amdgcn_raw_buffer_load_b16(rs, (j * BLOCK + (int)threadIdx.x) * 2, 0, 0);
+    __syncthreads();
+    sort_bucket<BLOCK, ITEMS, ATOMIC, true>(k, len, 2, reinterpret_cast<uint32_t *>(pack + a), s_a,
+                                            s_wc);
+}
+
+hipError_t launch_boundary_sort16(uint16_t *pack, const uint64_t *gb, const uint64_t *prefix,
+                                  const uint64_t *g, uint64_t N, int nb, bool atomic_rank,
+                                  uint64_t *big, hipStream_t s) {
     using ull = unsigned long long;
     if (nb <= 0) return hipSuccess;
-    if (shift < 8 || M < 256) return hipErrorInvalidValue;
-    launch_k(k_select_digit, nb, 256, 0, s, reinterpret_cast<const ull *>(all),
+    if (atomic_rank)
+        launch_k(k_boundary_sort16<true>, nb, 1024, 0, s, pack, reinterpret_cast<const ull *>(gb),
+                 reinterpret_cast<const ull *>(prefix), reinterpret_cast<const ull *>(g), (ull)N,
+                 reinterpret_cast<ull *>(big));
+    else
+        launch_k(k_boundary_sort16<false>, nb, 1024, 0, s, pack, reinterpret_cast<const ull *>(gb),
+                 reinterpret_cast<const ull *>(prefix), reinterpret_cast<const ull *>(g), (ull)N,
+                 reinterpret_cast<ull *>(big));
+    return hipGetLastError();
+}
+
+hipError_t launch_select_digit(const uint64_t *all, int W, const uint64_t *g, uint64_t N, int P,
+                               int nb, int M, int shift, uint64_t *prefix, uint64_t *xs,
+                               hipStream_t s) {
+    using ull = unsigned long long;
+    if (nb <= 0) return hipSuccess;
+    if (shift < 0 || shift > 24 || shift % 8 || M < 256 || W < nb * M) return hipErrorInvalidValue;
+    launch_k(k_select_digit, nb, 256, 0, s, reinterpret_cast<const ull *>(all), W,
              reinterpret_cast<const ull *>(g), (ull)N, P, nb, M, shift,
              reinterpret_cast<ull *>(prefix), reinterpret_cast<ull *>(xs));
     return hipGetLastError();

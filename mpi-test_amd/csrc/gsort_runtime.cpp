@@ -1751,84 +1751,96 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
     int pr = stats ? stats->passes_run : 0;
     if (check_mode()) ST_TRY(check_bounds(c, gb, kBuckets16 + 1, n_in, "sender bucket bounds"));
 
-    // (2) radix select of v_q, the g_q-th smallest key, for the P-1 inner boundaries.  Rounds 0
-    // and 2 are decided on the device (K13s writes the next round's thresholds), rounds 1 and 3
-    // on the host, which needs their counts: two host synchronisations for the four rounds.
-    const int nb = P - 1, M = 257;
+    // (2) radix select of v_q, the g_q-th smallest key, for the P-1 inner boundaries: 4 rounds of
+    // 8 bits, every round decided on the device (K13s sums the all-gathered counts, picks the
+    // digit and writes the next round's thresholds), and after round 1 -- the boundaries'
+    // 16-bit groups known -- K13g sorts each boundary group in place in the packed buffer, so
+    // rounds 2 and 3 binary-search it and the cut splits it by value.  The host waits ONCE, for
+    // the last round's counts (the cut and the exchange sizes RCCL needs on the host).  A
+    // boundary group past K13g's 32 768 keys (skewed input) is flagged in the count rows of
+    // rounds 2 and 3, so every rank sees it: all ranks then sort the groups on the host path and
+    // repeat rounds 2 and 3 with the host between them (select_rounds below).
+    const int nb = P - 1, M = 257, W = nb * M + nb;  // count row: nb x M counts + nb K13g flags
     std::vector<uint64_t> g(nb), prefix(nb, 0), hx((size_t)2 * nb + (size_t)nb * M),
-        all((size_t)P * nb * M);
+        all((size_t)P * W);
     std::vector<int> dsel(nb, 0);
     for (int q = 0; q < nb; ++q) g[q] = std::min<uint64_t>((uint64_t)(q + 1) * B, N);
-    ST_TRY(ensure(c, c->m_split, (size_t)std::max(nb, 1) * (M * 16 + 16)));
-    ST_TRY(ensure(c, c->slot[S_STAGE], (size_t)P * std::max(nb, 1) * M * 8));
-    // m_split: prefix (nb) | g (nb) | thresholds (nb x M) | counts (nb x M), u64
+    ST_TRY(ensure(c, c->m_split, (size_t)std::max(nb, 1) * (M * 16 + 32)));
+    ST_TRY(ensure(c, c->slot[S_STAGE], (size_t)P * std::max(W, 1) * 8));
+    // m_split: prefix (nb) | g (nb) | thresholds (nb x M) | counts (nb x M) + flags (nb), u64
     uint64_t *d_pref = reinterpret_cast<uint64_t *>(c->m_split.p), *d_g = d_pref + nb;
     uint64_t *d_xs = d_g + nb;
     uint64_t *d_cnt = d_xs + (size_t)nb * M;
     const uint64_t *d_all = reinterpret_cast<const uint64_t *>(c->slot[S_STAGE].p);
-    t = tic_rec(c);
-    for (int k = 0; k < 4 && nb > 0; ++k) {  // (one rank: no boundary, nothing to select)
-        const int shift = 24 - 8 * k;
-        if (k % 2 == 0) {  // thresholds from the host's prefix
-            for (int q = 0; q < nb; ++q) { hx[q] = prefix[q]; hx[nb + q] = g[q]; }
-            for (int q = 0; q < nb; ++q)
-                for (int d = 0; d < M; ++d)
-                    hx[2 * nb + (size_t)q * M + d] = prefix[q] + ((uint64_t)d << shift);
-            HIP_TRY(c, hipMemcpyAsync(d_pref, hx.data(), hx.size() * 8, hipMemcpyHostToDevice,
-                                      c->stream));
-        }
-        HIP_TRY(c, launch_count_below16(pack, gb, d_xs, nb * M, d_cnt, c->stream));
-        ST_TRY(comm_try(c, c->comm->allgather(d_cnt, c->slot[S_STAGE].p, (size_t)nb * M * 8,
-                                              c->stream)));
-        if (k % 2 == 0) {
-            HIP_TRY(c, launch_select_digit(d_all, d_g, N, P, nb, M, shift, d_pref, d_xs,
+    // rounds k0 .. 3 from the thresholds in d_xs (K13g after round 1 when k0 == 0), then the last
+    // round's rows and the boundary keys to the host
+    auto select_rounds = [&](int k0) -> gsort_status {
+        for (int k = k0; k < 4; ++k) {
+            HIP_TRY(c, launch_count_below16(pack, gb, d_xs, nb * M, d_cnt, c->stream));
+            ST_TRY(comm_try(c, c->comm->allgather(d_cnt, c->slot[S_STAGE].p, (size_t)W * 8,
+                                                  c->stream)));
+            HIP_TRY(c, launch_select_digit(d_all, W, d_g, N, P, nb, M, 24 - 8 * k, d_pref, d_xs,
                                            c->stream));
-            continue;
+            if (k == 1)
+                HIP_TRY(c, launch_boundary_sort16(pack, gb, d_pref, d_g, N, nb, c->atomic_rank,
+                                                  d_cnt + (size_t)nb * M, c->stream));
         }
         HIP_TRY(c, hipMemcpyAsync(all.data(), d_all, all.size() * 8, hipMemcpyDeviceToHost,
                                   c->stream));
         HIP_TRY(c, hipMemcpyAsync(prefix.data(), d_pref, (size_t)nb * 8, hipMemcpyDeviceToHost,
                                   c->stream));
         HIP_TRY(c, hipStreamSynchronize(c->stream));
-        for (int q = 0; q < nb; ++q) {
-            if (g[q] >= N) continue;  // boundary at the end: every key goes left
-            int best = 0;
-            for (int d = 0; d < 256; ++d) {
-                uint64_t below = 0;
-                for (int p = 0; p < P; ++p) below += all[((size_t)p * nb + q) * M + d];
-                if (below <= g[q]) best = d; else break;
-            }
-            dsel[q] = best;
-            prefix[q] += (uint64_t)best << shift;
-        }
-        if (k == 1) {  // the 16-bit group of every boundary is known: sort it on this rank
+        return GSORT_OK;
+    };
+    // the thresholds of round 0 (prefix 0) and of round 2 after the host path (prefix: the top
+    // 16 bits); prefix and g go along
+    auto put_thresholds = [&](int shift) -> gsort_status {
+        for (int q = 0; q < nb; ++q) { hx[q] = prefix[q]; hx[nb + q] = g[q]; }
+        for (int q = 0; q < nb; ++q)
+            for (int d = 0; d < M; ++d)
+                hx[2 * nb + (size_t)q * M + d] = prefix[q] + ((uint64_t)d << shift);
+        HIP_TRY(c, hipMemcpyAsync(d_pref, hx.data(), hx.size() * 8, hipMemcpyHostToDevice,
+                                  c->stream));
+        return GSORT_OK;
+    };
+    t = tic_rec(c);
+    if (nb > 0) {  // (one rank: no boundary, nothing to select)
+        ST_TRY(put_thresholds(24));
+        ST_TRY(select_rounds(0));
+        bool big = false;
+        for (int p = 0; p < P; ++p)
+            for (int q = 0; q < nb; ++q) big |= all[(size_t)p * W + (size_t)nb * M + q] != 0;
+        if (big) {  // a boundary group past K13g's reach on some rank: every rank takes this
             std::vector<std::pair<uint64_t, uint64_t>> groups;  // {h, first position}
-            std::vector<uint64_t> glen;
-            for (int q = 0; q < nb; ++q) {
-                if (g[q] >= N) continue;
-                const uint64_t *row = &all[((size_t)me * nb + q) * M];
-                if (row[dsel[q] + 1] > row[dsel[q]])
-                    groups.push_back({prefix[q] >> 16, row[dsel[q]]});
-            }
+            for (int q = 0; q < nb; ++q)
+                if (g[q] < N) groups.push_back({prefix[q] >> 16, 0});
             std::sort(groups.begin(), groups.end());
             groups.erase(std::unique(groups.begin(), groups.end()), groups.end());
-            if (!groups.empty()) {
-                // group lengths: the next bucket's start (gb) on the host for these few groups
-                std::vector<uint64_t> h_gb(groups.size());
-                for (size_t i = 0; i < groups.size(); ++i)
-                    HIP_TRY(c, hipMemcpyAsync(&h_gb[i], gb + groups[i].first + 1, 8,
-                                              hipMemcpyDeviceToHost, c->stream));
-                HIP_TRY(c, hipStreamSynchronize(c->stream));
-                ST_TRY(sort_groups16(c, pack, groups, h_gb));
-            }
+            std::vector<uint64_t> h_gb(2 * groups.size());
+            for (size_t i = 0; i < groups.size(); ++i)
+                HIP_TRY(c, hipMemcpyAsync(&h_gb[2 * i], gb + groups[i].first, 16,
+                                          hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(c, hipStreamSynchronize(c->stream));
+            std::vector<std::pair<uint64_t, uint64_t>> nonempty;
+            std::vector<uint64_t> ends;
+            for (size_t i = 0; i < groups.size(); ++i)
+                if (h_gb[2 * i + 1] > h_gb[2 * i]) {
+                    nonempty.push_back({groups[i].first, h_gb[2 * i]});
+                    ends.push_back(h_gb[2 * i + 1]);
+                }
+            if (!nonempty.empty()) ST_TRY(sort_groups16(c, pack, nonempty, ends));
+            for (int q = 0; q < nb; ++q) prefix[q] = prefix[q] >> 16 << 16;
+            ST_TRY(put_thresholds(8));
+            ST_TRY(select_rounds(2));
         }
+        for (int q = 0; q < nb; ++q) dsel[q] = (int)(prefix[q] & 255u);
     }
     toc_rec(c, PH_SAMPLE, t);
     // (3) cut points from the last round: lt = count(< v_q), le = count(< v_q + 1)
     std::vector<uint64_t> lt((size_t)P * nb), le((size_t)P * nb), send(P), recv(P);
     for (int p = 0; p < P; ++p)
         for (int q = 0; q < nb; ++q) {
-            const uint64_t *row = &all[((size_t)p * nb + q) * M];
+            const uint64_t *row = &all[(size_t)p * W + (size_t)q * M];
             lt[(size_t)p * nb + q] = g[q] >= N ? n_all[p] : row[dsel[q]];
             le[(size_t)p * nb + q] = g[q] >= N ? n_all[p] : row[dsel[q] + 1];
         }

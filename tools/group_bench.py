@@ -30,6 +30,7 @@ def main():
     P, n = a.ranks, 1 << a.keys_log2
     grp = gsort.Group(P)
     out = [None] * P
+    out_walls = [None] * P
     barrier = threading.Barrier(P)
 
     def worker(r):
@@ -40,14 +41,16 @@ def main():
             c.reserve(n)
             fn = c.radix if a.algo == "radix" else c.sample
             fn(d, n)
-            sts = []
-            barrier.wait()
-            t0 = time.perf_counter()
-            for _ in range(a.steps):
+            sts, walls = [], []
+            for _ in range(a.steps):  # each step between two barriers of all ranks
+                barrier.wait()
+                t0 = time.perf_counter()
                 _, n_out, st = fn(d, n)
                 sts.append(st)
-            barrier.wait()
-            wall = (time.perf_counter() - t0) / a.steps
+                barrier.wait()
+                walls.append(time.perf_counter() - t0)
+            wall = sum(walls) / a.steps
+            out_walls[r] = walls
             keys = ("ms_total", "ms_local_sort", "ms_sample", "ms_exchange", "ms_merge",
                     "ms_hist", "ms_bucket_sort")
             out[r] = {k: sum(s[k] for s in sts) / len(sts) for k in keys}
@@ -61,9 +64,14 @@ def main():
         t.join()
     grp.close()
     tot = {k: round(sum(o[k] for o in out), 4) for k in out[0]}
+    steps = sorted(max(w[i] for w in out_walls) * 1e3 for i in range(a.steps))
+    med = steps[len(steps) // 2]
     print(json.dumps({"ranks": P, "keys_per_rank": n, "algo": a.algo,
                       "sum_over_ranks_ms": tot,
-                      "wall_ms": round(max(o["wall_ms"] for o in out), 4)}))
+                      "wall_ms": round(max(o["wall_ms"] for o in out), 4),
+                      "step_ms": [round(x, 4) for x in steps],
+                      "median_step_ms": round(med, 4),
+                      "median_ms_per_2p28_keys": round(med / P * (1 << 28) / n, 4)}))
 
 
 if __name__ == "__main__":
