@@ -60,6 +60,8 @@ def parse():
                     help="skip the reference's 2^28-key point (~1 min of host time)")
     ap.add_argument("--no-dist-p1", action="store_true",
                     help="skip the one-rank distributed-path block")
+    ap.add_argument("--no-strong", action="store_true",
+                    help="N > 1: skip the configs[2] strong-scaling block (2^31 keys in total)")
     ap.add_argument("--no-stats", action="store_true",
                     help="experiment: time the steps without per-phase events")
     ap.add_argument("--local", choices=["msd", "lsd"], default="msd",
@@ -439,6 +441,36 @@ def drop_in_e2e(ctx, fn, d_in, n, reps=3):
                     "median of 3; not the headline value"}
 
 
+def s64(x):
+    """u64 -> the int64 with the same bits (all-gathered fingerprint rows)."""
+    return x - (1 << 64) if x >= 1 << 63 else x
+
+
+def exchange_line(stats):
+    """The exchange's xGMI roofline from the timed steps' gsort_stats: per exchange, the
+    largest (source, destination) pair's bytes over one xGMI link's peak."""
+    last = stats[-1]
+    if not last["exchanges"]:
+        return None
+    ex = sum(s["ms_exchange"] for s in stats) / len(stats) / max(last["exchanges"], 1)
+    pair = last["max_pair_bytes"]
+    return {"bound": "xgmi", "per_exchange_ms": round(ex, 4), "max_pair_bytes": pair,
+            "achieved_link_GBps": round(pair / (ex * 1e-3) / 1e9, 2) if ex else None,
+            "peak_link_GBps": XGMI_LINK_GBPS,
+            "frac": round(pair / (ex * 1e-3) / 1e9 / XGMI_LINK_GBPS, 4) if ex else None}
+
+
+def strong_line(n_total, world, ms_step, verified, stats):
+    """BASELINE configs[2] ("Radix sort 2^31 uniform 32-bit keys across 2/4/8 MI355X"): the
+    same 2^31 keys at every N (strong scaling), beside the weak-scaling headline."""
+    return {"config": "BASELINE configs[2]: radix sort, 2^31 uniform int32 keys in total "
+                      f"across {world} GPUs ({n_total // world} per GPU)",
+            "total_keys": n_total, "keys_per_gpu": n_total // world, "n_gpus": world,
+            "scaling": "strong", "ms_per_step": round(ms_step, 4),
+            "GKeys_s": round(n_total / (ms_step * 1e-3) / 1e9, 3), "steps": len(stats),
+            "verified": bool(verified), "exchange": exchange_line(stats) if stats else None}
+
+
 def verify_rows(rows, n_local, algo):
     """N > 1 output check from every rank's row [sum_in, sum_out, xor_in, xor_out, sorted, n_out,
     first, last] (64-bit figures as int64 bit patterns): the multiset of all outputs (sum and
@@ -543,8 +575,6 @@ def main():
         # of all outputs == of all inputs, every output sorted, rank q's last key <= rank
         # q+1's first (a misrouted exchange that keeps the multiset fails here), and the sizes
         # (radix: rank q holds exactly its n_local global positions)
-        def s64(x):  # u64 -> the int64 with the same bits
-            return x - (1 << 64) if x >= 1 << 63 else x
         mine = torch.tensor([s64(fin["sum"]), s64(fp["sum"]), s64(fin["xor"]), s64(fp["xor"]),
                              int(fp["sorted"]), n_out, fp["first"], fp["last"]], dtype=torch.int64)
         rows = [torch.zeros_like(mine) for _ in range(world)]
@@ -621,16 +651,43 @@ def main():
                            plan, str(plan))),
         "verified": bool(ok),
         "reference_check_2p24": med,
+        # the HIP runtime / RCCL libgsort is bound to here (torch's bundled ones: torch is
+        # imported first; the drop-in CLIs run on /opt/rocm's -- DESIGN.md 6)
+        "runtime": gsort.runtime_info(),
     }
     if last["exchanges"]:
-        ex = sum(s["ms_exchange"] for s in stats) / len(stats) / max(last["exchanges"], 1)
-        pair = last["max_pair_bytes"]
-        line["exchange"] = {"bound": "xgmi", "per_exchange_ms": round(ex, 4),
-                            "max_pair_bytes": pair,
-                            "achieved_link_GBps": round(pair / (ex * 1e-3) / 1e9, 2) if ex else None,
-                            "peak_link_GBps": XGMI_LINK_GBPS,
-                            "frac": round(pair / (ex * 1e-3) / 1e9 / XGMI_LINK_GBPS, 4) if ex else None}
+        line["exchange"] = exchange_line(stats)
     ctx.free(d_in)
+    if world > 1 and a.algo == "radix" and not a.no_strong:
+        # configs[2]'s strong-scaling point: 2^31 keys in total (the canonical stream, rank r's
+        # block = its slice), a few timed steps bracketed like the headline's, max over ranks
+        n_s = (1 << 31) // world
+        d_s = ctx.alloc(n_s * 4)
+        ctx.generate(gsort.UNIFORM, a.seed, rank * n_s, n_s, d_s)
+        ctx.reserve(n_s)
+        fn(d_s, n_s)
+        barrier()
+        torch.cuda.synchronize()
+        raw_s = [gsort.Stats() for _ in range(3)]
+        t0 = time.perf_counter()
+        for r_ in raw_s:
+            fn(d_s, n_s, r_)
+        torch.cuda.synchronize()
+        barrier()
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        out_s, m_s, _ = fn(d_s, n_s)
+        fo, fi = ctx.fingerprint(out_s, m_s), ctx.fingerprint(d_s, n_s)
+        mine = torch.tensor([s64(fi["sum"]), s64(fo["sum"]), s64(fi["xor"]), s64(fo["xor"]),
+                             int(fo["sorted"]), m_s, fo["first"], fo["last"]], dtype=torch.int64)
+        rows = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(rows, mine)
+        ok_s = verify_rows([[int(x) for x in r.tolist()] for r in rows], n_s, "radix")
+        line["strong_scaling_cfg2"] = strong_line(n_s * world, world,
+                                                  float(el.item()) * 1e3 / len(raw_s), ok_s,
+                                                  [r_.as_dict() for r_ in raw_s])
+        ctx.free(d_s)
+        ok = ok and ok_s
     ctx.close()
     if world == 1 and a.algo == "radix" and not a.no_dist_p1 and \
             os.environ.get("GSORT_FORCE_DIST") != "1":

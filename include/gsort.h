@@ -83,6 +83,19 @@ enum { GSORT_LOCAL_MSD = 0, GSORT_LOCAL_LSD = 1 };
 gsort_status gsort_get_uid(gsort_uid *out);
 gsort_status gsort_get_uid_ipc(int nranks, gsort_uid *out);
 int gsort_visible_devices(void);
+
+/* The HIP runtime and RCCL this process's libgsort is bound to (hipRuntimeGetVersion,
+ * ncclGetVersion) and the files they were loaded from (dladdr).  Both are resolved by soname,
+ * so a process that loaded them first decides: under PyTorch (tests, bench.py: torch is
+ * imported first) libgsort runs on torch's bundled HIP runtime and RCCL; the drop-in CLIs (and
+ * Python without torch) on /opt/rocm's.  Not in the reference (diagnostics). */
+typedef struct {
+    int hip_runtime; /* hipRuntimeGetVersion */
+    int rccl;        /* ncclGetVersion, e.g. 22707 = 2.27.7 */
+    char hip_path[256];
+    char rccl_path[256];
+} gsort_runtime_info_t;
+gsort_status gsort_runtime_info(gsort_runtime_info_t *out);
 /* Context of one rank (one process); the uid's kind picks the transport (RCCL or IPC group).
  * nranks == 1 needs no uid (uid may be NULL).
  * hip_device >= 0 selects that GPU; hip_device = -1 - local_rank selects

@@ -3,6 +3,7 @@
 
 #include "gsort_debug.h"
 
+#include <dlfcn.h>
 #include <errno.h>
 #include <fcntl.h>
 #include <rccl/rccl.h>
@@ -175,6 +176,18 @@ gsort_status rccl_get_uid(gsort_uid *out) {
     ncclUniqueId id;
     if (ncclGetUniqueId(&id) != ncclSuccess) return GSORT_ERCCL;
     memcpy(out, &id, sizeof(id));
+    return GSORT_OK;
+}
+
+gsort_status runtime_info(gsort_runtime_info_t *out) {
+    memset(out, 0, sizeof(*out));
+    if (hipRuntimeGetVersion(&out->hip_runtime) != hipSuccess) out->hip_runtime = -1;
+    if (ncclGetVersion(&out->rccl) != ncclSuccess) out->rccl = -1;
+    Dl_info di;
+    if (dladdr(reinterpret_cast<void *>(&hipRuntimeGetVersion), &di) && di.dli_fname)
+        snprintf(out->hip_path, sizeof(out->hip_path), "%s", di.dli_fname);
+    if (dladdr(reinterpret_cast<void *>(&ncclGetVersion), &di) && di.dli_fname)
+        snprintf(out->rccl_path, sizeof(out->rccl_path), "%s", di.dli_fname);
     return GSORT_OK;
 }
 

@@ -43,6 +43,7 @@ class Comm {
 };
 
 Comm *make_rccl_comm(int rank, int nranks, const gsort_uid *uid, std::string *err);
+gsort_status runtime_info(gsort_runtime_info_t *out);  // gsort_runtime_info
 gsort_status rccl_get_uid(gsort_uid *out);
 // Same-node process group over HIP IPC (gsort_get_uid_ipc): one process per rank, any number
 // of ranks per GPU.

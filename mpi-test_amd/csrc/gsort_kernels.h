@@ -191,10 +191,15 @@ hipError_t launch_hist_expand(const void *recv, bool packed16, const uint64_t *p
 // K18c: the same buckets (any list of {h, len} entries with len <= kHxMax) in one read: packed
 // u16 bin counters, wave-wise expansion by marked slots + max-scan, coalesced stores; one
 // persistent workgroup per CU (ncu), the next bucket's keys loaded during this one's stores.
+// fb_list != nullptr: u8 bins (64 KiB, two workgroups per CU); a bucket with >= 256 copies of
+// one key (a byte wrapped) is appended to fb_list (count at fb_ctr, zeroed by the caller) and
+// not written; the caller then runs the u16 form over fb_list with nlist_dev = fb_ctr (the
+// list's length read on the device, nlist = its bound: the grid).
 hipError_t launch_count_expand(const void *recv, bool packed16, const uint64_t *pos,
                                const uint64_t *roff, int P, const uint64_t *bstart,
                                const uint64_t *list, uint32_t nlist, int ncu, uint32_t *out,
-                               hipStream_t s);
+                               hipStream_t s, uint64_t *fb_list = nullptr,
+                               uint32_t *fb_ctr = nullptr, const uint32_t *nlist_dev = nullptr);
 // {h, len} list entries -> {bstart[h], len}.
 hipError_t launch_list_to_segments(uint64_t *list, uint32_t n, const uint64_t *bstart,
                                    hipStream_t s);

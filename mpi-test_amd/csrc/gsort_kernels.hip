@@ -2216,9 +2216,13 @@ __global__ __launch_bounds__(1024) void k_hist_expand(const T *__restrict__ recv
 constexpr uint32_t kCxWrapMax = 64;
 static_assert(3 * (kHxMax >> 16) <= kCxWrapMax, "K18c wrap list too small for kHxMax");
 
-template <bool WRAP>
+template <bool WRAP, int CB = 16>
 __device__ __forceinline__ void cx_count(uint32_t *s_h, uint32_t v, uint32_t *s_nw,
                                          uint32_t *s_wb, int32_t *s_wd) {
+    if (CB == 8) {  // u8 bins: word v >> 2, byte v & 3 (a wrap is found by the total, not here)
+        atomicAdd(s_h + (v >> 2), 1u << ((v & 3u) << 3));
+        return;
+    }
     // word v >> 1 (byte address (v << 1) & ~3), half v & 1: add 1 or 0x10000
     uint32_t *a = reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(s_h) + ((v << 1) & 0x1FFFCu));
     const uint32_t inc = (v & 1u) * 0xFFFFu + 1u;  // one v_mad_u32_u24
@@ -2280,7 +2284,8 @@ __device__ __forceinline__ void cx_count_piece(const T *src, uint32_t np, uint32
 // overlap this one's stores and VALU work instead of following them.  Per bucket:
 // 1) the 65 536 packed u16 bin counters count the prefetched vectors, any vectors past them and
 //    the pieces' unaligned heads / tails (one LDS atomic per key);
-// 2) wave w owns bins [4096 w, +4096) (16 chunks of 256 bins, lane L the 4 bins of words
+// 2) wave w owns bins [4096 w, +4096) (u8 bins, 8 waves: [8192 w, +8192), 32 chunks; lane L
+//    one word of 4 bins per chunk) (16 chunks of 256 bins, lane L the 4 bins of words
 //    128 j + 2 L, +1); the waves' totals are scanned into their output runs;
 // 3) each wave writes its run in windows of 256 slots aligned to 16 B in out: the bins of every
 //    chunk starting in the window mark their first slot with their key (LDS; chunks streamed
@@ -2385,26 +2390,26 @@ __device__ __forceinline__ const uint4 *cx_vec(const T *recv, const CxTable<T> &
     return reinterpret_cast<const uint4 *>(run_ptr(recv, t.src[p] + t.head[p])) + (g - t.cumv[p]);
 }
 
-template <bool WRAP, typename T>
+template <bool WRAP, typename T, int CB = 16>
 __device__ __forceinline__ void cx_count_vec(uint32_t *s_h, const uint4 &x, uint32_t *s_nw,
                                              uint32_t *s_wb, int32_t *s_wd) {
     const uint32_t w4[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        cx_count<WRAP>(s_h, w4[q] & 0xFFFFu, s_nw, s_wb, s_wd);
-        if (sizeof(T) == 2) cx_count<WRAP>(s_h, w4[q] >> 16, s_nw, s_wb, s_wd);
+        cx_count<WRAP, CB>(s_h, w4[q] & 0xFFFFu, s_nw, s_wb, s_wd);
+        if (sizeof(T) == 2) cx_count<WRAP, CB>(s_h, w4[q] >> 16, s_nw, s_wb, s_wd);
     }
 }
 
-template <bool WRAP, typename T, uint32_t PF>
+template <bool WRAP, typename T, uint32_t PF, uint32_t NT = 1024, int CB = 16>
 __device__ __forceinline__ void cx_count_bucket(const T *recv, const CxTable<T> &t, int P,
                                                 const uint4 (&x)[PF], uint32_t *s_h,
                                                 uint32_t *s_nw, uint32_t *s_wb, int32_t *s_wd) {
-    constexpr uint32_t NT = 1024, E = 16 / sizeof(T), U = 8;
+    constexpr uint32_t E = 16 / sizeof(T), U = 8;
     const uint32_t tid = threadIdx.x, nv = t.cumv[P];
 #pragma unroll
     for (uint32_t u = 0; u < PF; ++u)
-        if (u * NT + tid < nv) cx_count_vec<WRAP, T>(s_h, x[u], s_nw, s_wb, s_wd);
+        if (u * NT + tid < nv) cx_count_vec<WRAP, T, CB>(s_h, x[u], s_nw, s_wb, s_wd);
     // vectors past the prefetch (buckets of more than PF * NT * E keys), U in flight
 #pragma unroll 1
     for (uint32_t g0 = PF * NT; g0 < nv; g0 += U * NT) {
@@ -2413,7 +2418,7 @@ __device__ __forceinline__ void cx_count_bucket(const T *recv, const CxTable<T> 
         for (uint32_t u = 0; u < U; ++u) y[u] = *cx_vec(recv, t, P, min(g0 + u * NT + tid, nv - 1));
 #pragma unroll
         for (uint32_t u = 0; u < U; ++u)
-            if (g0 + u * NT + tid < nv) cx_count_vec<WRAP, T>(s_h, y[u], s_nw, s_wb, s_wd);
+            if (g0 + u * NT + tid < nv) cx_count_vec<WRAP, T, CB>(s_h, y[u], s_nw, s_wb, s_wd);
     }
     // the pieces' unaligned heads and tails: < E elements each, one per thread
     for (uint32_t e = tid; e < (uint32_t)P * 2 * E; e += NT) {
@@ -2423,25 +2428,39 @@ __device__ __forceinline__ void cx_count_bucket(const T *recv, const CxTable<T> 
         uint32_t j = ~0u;
         if (k < E) { if (k < hd) j = k; }
         else if (body + (k - E) < n) j = body + (k - E);
-        if (j != ~0u) cx_count<WRAP>(s_h, (uint32_t)*run_ptr(recv, t.src[p] + j) & 0xFFFFu, s_nw, s_wb, s_wd);
+        if (j != ~0u) cx_count<WRAP, CB>(s_h, (uint32_t)*run_ptr(recv, t.src[p] + j) & 0xFFFFu, s_nw, s_wb, s_wd);
     }
 }
 
 // EST: the sampled plan's oversized children (cx_fill_table_est: recv = Y, P = 1): keys are
 // relative to the block's minimum koff, so the expansion marks relative keys (monotonic in the
 // slot, as the max-scan needs) and the stores add koff and flip.
-template <typename T, bool EST = false>
-__global__ __launch_bounds__(1024) void k_count_expand(const T *__restrict__ recv,
-                                                       const unsigned long long *__restrict__ pos,
-                                                       const unsigned long long *__restrict__ roff,
-                                                       int P,
-                                                       const unsigned long long *__restrict__ bstart,
-                                                       const unsigned long long *__restrict__ list,
-                                                       uint32_t nlist, uint32_t *__restrict__ out,
-                                                       uint32_t koff = 0) {
-    constexpr uint32_t NT = 1024, NW = NT / 64, WORDS = 32768, CW = 128;  // words per chunk
-    constexpr uint32_t CH = WORDS / NW / CW;                               // 16 chunks per wave
+// CB = 8 (round 5): u8 bins -- 64 KiB of counters, 512 threads, two
+// workgroups per CU -- halve the fixed per-bucket cost (every bin zeroed and read twice: ~9 us
+// per bucket and CU with u16 bins, i.e. 0.29 of the 0.58 ms per 2^28 keys of the P = 4 shape's
+// 32 768-key buckets).  A byte that wraps (>= 256 copies of one key) shows as a total below the
+// bucket's size: the bucket goes to fb_list (fb_ctr entries, the {h, len} entry as given) with
+// its bins cleared, and the u16 kernel redoes it (nlist_dev: that count, read on the device).
+template <typename T, bool EST = false, int CB = 16>
+__global__ __launch_bounds__(CB == 8 ? 512 : 1024) void k_count_expand(
+    const T *__restrict__ recv, const unsigned long long *__restrict__ pos,
+    const unsigned long long *__restrict__ roff, int P,
+    const unsigned long long *__restrict__ bstart, const unsigned long long *__restrict__ list,
+    uint32_t nlist, uint32_t *__restrict__ out, uint32_t koff = 0,
+    unsigned long long *__restrict__ fb_list = nullptr, uint32_t *__restrict__ fb_ctr = nullptr,
+    const uint32_t *__restrict__ nlist_dev = nullptr) {
+    static_assert(CB == 8 || CB == 16, "u8 or u16 bins");
+    constexpr uint32_t NT = CB == 8 ? 512 : 1024, NW = NT / 64;
+    constexpr uint32_t WORDS = 65536 * CB / 32;  // 16 384 (u8) / 32 768 (u16) words of bins
+    constexpr uint32_t BPW = 32 / CB;            // bins per word
+    constexpr uint32_t CW = 256 / BPW;           // words per chunk: 4 bins per lane (8 per lane
+                                                 // with u8 bins measured slower: r05_recv_u8_bins)
+    constexpr uint32_t CH = WORDS / NW / CW;     // chunks per wave (32 / 16)
     constexpr uint32_t PF = 8;  // prefetched 16-B vectors per thread
+    if (nlist_dev) {  // (the u8 kernel's wrapped buckets: usually none)
+        nlist = *nlist_dev;
+        if (blockIdx.x >= nlist) return;
+    }
     __shared__ uint32_t s_h[WORDS];
     // per wave: 256 window slots + 64 dummy words (a lane's marks outside the window)
     __shared__ uint4 s_mark[NW * 80];
@@ -2491,6 +2510,14 @@ __global__ __launch_bounds__(1024) void k_count_expand(const T *__restrict__ rec
         const uint32_t w0 = w * (WORDS / NW);
         // lane's 4 bins of chunk j: counts (wrap corrections applied)
         auto counts = [&](uint32_t j, uint32_t (&c)[4]) {
+            if (CB == 8) {
+                const uint32_t y = s_h[w0 + CW * j + lane];
+                c[0] = y & 255u;
+                c[1] = (y >> 8) & 255u;
+                c[2] = (y >> 16) & 255u;
+                c[3] = y >> 24;
+                return;
+            }
             const uint32_t wd = w0 + CW * j + 2 * lane;
             const uint2 y = *reinterpret_cast<const uint2 *>(s_h + wd);
             c[0] = y.x & 0xFFFFu;
@@ -2524,18 +2551,31 @@ __global__ __launch_bounds__(1024) void k_count_expand(const T *__restrict__ rec
             for (uint32_t ww = 0; ww < NW; ++ww) tot += s_wsum[ww];
             return tot;
         };
-        cx_count_bucket<false, T, PF>(recv, t, P, x, s_h, &s_nw, s_wb, s_wd);
+        cx_count_bucket<false, T, PF, NT, CB>(recv, t, P, x, s_h, &s_nw, s_wb, s_wd);
         __syncthreads();
-        if (wave_totals() != len) {  // a half wrapped: count again, tracking the wraps
+        bool skip = false;  // (CB = 8: a byte wrapped, the bucket went to fb_list)
+        if (wave_totals() != len) {
             uint4 *z = reinterpret_cast<uint4 *>(s_h);
 #pragma unroll
             for (uint32_t q = 0; q < WORDS / 4 / NT; ++q) z[q * NT + tid] = make_uint4(0, 0, 0, 0);
-            __syncthreads();
-            cx_count_bucket<true, T, PF>(recv, t, P, x, s_h, &s_nw, s_wb, s_wd);
-            __syncthreads();
-            nw = min(s_nw, kCxWrapMax);  // uniform
-            (void)wave_totals();
+            if constexpr (CB == 8) {
+                if (tid == 0) {
+                    const uint32_t e = atomicAdd(fb_ctr, 1u);
+                    fb_list[2 * e] = list[2 * i];
+                    fb_list[2 * e + 1] = list[2 * i + 1];
+                }
+                skip = true;
+                if (tid < NW) s_wsum[tid] = 0;  // no keys to expand (s_base below)
+                __syncthreads();
+            } else {  // a half wrapped: count again, tracking the wraps
+                __syncthreads();
+                cx_count_bucket<true, T, PF>(recv, t, P, x, s_h, &s_nw, s_wb, s_wd);
+                __syncthreads();
+                nw = min(s_nw, kCxWrapMax);  // uniform
+                (void)wave_totals();
+            }
         }
+        (void)skip;
         // the waves' output offsets (block scan of 16)
         if (tid < NW) {
             uint32_t e = 0;
@@ -2602,11 +2642,12 @@ __global__ __launch_bounds__(1024) void k_count_expand(const T *__restrict__ rec
                 uint32_t c[4];
                 counts(j, c);
                 // the chunk's last read: its words are zeroed for the next bucket here
-                *reinterpret_cast<uint2 *>(s_h + w0 + CW * j + 2 * lane) = make_uint2(0, 0);
+                if (CB == 8) s_h[w0 + CW * j + lane] = 0;
+                else *reinterpret_cast<uint2 *>(s_h + w0 + CW * j + 2 * lane) = make_uint2(0, 0);
                 const uint32_t tc = c[0] + c[1] + c[2] + c[3];
                 const uint32_t y = wave_incl_add(tc);
                 uint32_t sm[4], st = lo + y - tc;
-                const uint32_t k0 = hk | (2 * (w0 + CW * j + 2 * lane));
+                const uint32_t k0 = hk | (CB == 8 ? 4 * (w0 + CW * j + lane) : 2 * (w0 + CW * j + 2 * lane));
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     sm[q] = c[q] ? st : 0x80000000u;
@@ -3987,7 +4028,8 @@ hipError_t launch_hist_expand(const void *recv, bool packed16, const uint64_t *p
 hipError_t launch_count_expand(const void *recv, bool packed16, const uint64_t *pos,
                                const uint64_t *roff, int P, const uint64_t *bstart,
                                const uint64_t *list, uint32_t nlist, int ncu, uint32_t *out,
-                               hipStream_t s) {
+                               hipStream_t s, uint64_t *fb_list, uint32_t *fb_ctr,
+                               const uint32_t *nlist_dev) {
     using ull = unsigned long long;
     if (nlist == 0) return hipSuccess;
     if (P < 1 || P > 64 || ncu < 1) return hipErrorInvalidValue;
@@ -3995,13 +4037,28 @@ hipError_t launch_count_expand(const void *recv, bool packed16, const uint64_t *
     auto *ro = reinterpret_cast<const ull *>(roff);
     auto *bs = reinterpret_cast<const ull *>(bstart);
     auto *l = reinterpret_cast<const ull *>(list);
-    const uint32_t grid = std::min<uint32_t>(nlist, (uint32_t)ncu);  // one workgroup per CU
+    ull *fl = reinterpret_cast<ull *>(fb_list);
+    if (fb_list) {  // u8 bins, two workgroups per CU; wrapped buckets appended to fb_list
+        const uint32_t grid = std::min<uint32_t>(nlist, 2u * (uint32_t)ncu);
+        if (packed16)
+            launch_k(k_count_expand<uint16_t, false, 8>, grid, 512, 0, s,
+                     reinterpret_cast<const uint16_t *>(recv), ps, ro, P, bs, l, nlist, out, 0u,
+                     fl, fb_ctr, (const uint32_t *)nullptr);
+        else
+            launch_k(k_count_expand<int32_t, false, 8>, grid, 512, 0, s,
+                     reinterpret_cast<const int32_t *>(recv), ps, ro, P, bs, l, nlist, out, 0u,
+                     fl, fb_ctr, (const uint32_t *)nullptr);
+        return hipGetLastError();
+    }
+    // u16 bins, one workgroup per CU; nlist_dev: the list's length is read on the device (the
+    // u8 kernel's wrapped buckets; nlist is then the grid's bound)
+    const uint32_t grid = std::min<uint32_t>(nlist, (uint32_t)ncu);
     if (packed16)
         launch_k(k_count_expand<uint16_t>, grid, 1024, 0, s, reinterpret_cast<const uint16_t *>(recv), ps, ro, P,
-                 bs, l, nlist, out, 0u);
+                 bs, l, nlist, out, 0u, (ull *)nullptr, (uint32_t *)nullptr, nlist_dev);
     else
         launch_k(k_count_expand<int32_t>, grid, 1024, 0, s, reinterpret_cast<const int32_t *>(recv), ps, ro, P,
-                 bs, l, nlist, out, 0u);
+                 bs, l, nlist, out, 0u, (ull *)nullptr, (uint32_t *)nullptr, nlist_dev);
     return hipGetLastError();
 }
 
@@ -4150,7 +4207,8 @@ hipError_t launch_est_oversized(const EstPlan &p, uint32_t nlist, int ncu, hipSt
     const unsigned grid = (unsigned)std::min<uint32_t>(nlist, (uint32_t)std::max(ncu, 1));
     launch_k(k_count_expand<uint16_t, true>, grid, 1024, 0, s, (const uint16_t *)p.y,
              (const ull *)nullptr, (const ull *)nullptr, 1, (const ull *)nullptr,
-             reinterpret_cast<const ull *>(p.wl.list[0]), nlist, p.out, p.koff);
+             reinterpret_cast<const ull *>(p.wl.list[0]), nlist, p.out, p.koff, (ull *)nullptr,
+             (uint32_t *)nullptr, (const uint32_t *)nullptr);
     return hipGetLastError();
 }
 

@@ -85,6 +85,11 @@ struct gsort_ctx {
     // 0.72 / K18c 0.85 ms, 32 768-key K11g 1.01 / K18c 0.58 ms, tools/recv_probe.py); 5 = list
     // 0 only; -1 = the round-2 kernels (K11g classes, two-read K18)
     int recv_cx = 4;
+    // GSORT_RECV_CB: K18c's bin width on the receive side, 8 (default since round 5: 64 KiB of
+    // bins, two workgroups per CU; a bucket with >= 256 copies of one key redone with 16-bit
+    // bins) or 16
+    int recv_cb = 8;
+    DevBuf m_fb;  // K18c (u8): the wrapped buckets' {h, len} entries
     int ncu = 256;
     int last_plan = 0;      // gsort_last_plan: 0 exact, 1 sampled, 2 sampled then exact
     bool plan_trace = false; // GSORT_PLAN_TRACE: one stderr line per plan decision
@@ -131,6 +136,7 @@ constexpr size_t OFF_HIST = 0, OFF_TOT = 8192, OFF_BASES = 10240, OFF_CTR = 1228
                  OFF_ONE = 12416, OFF_CTR3 = 12544, OFF_PLAN = 20480;
 constexpr size_t OFF_FLAGS = 12408;  // K12b's trivial-level word, inside the published range
 constexpr size_t OFF_MINMAX = 12480;  // the offset retry's exact min / max (2 int32)
+constexpr size_t OFF_FBCTR = 12800;   // K18c (u8): the count of wrapped buckets (u32)
 constexpr size_t OFF_GIANT = 16384;   // K1m result (3 u64) + K1g counters (16 u64)
 
 gsort_status set_err(gsort_ctx *c, gsort_status st, const std::string &msg) {
@@ -603,7 +609,7 @@ void for_each_buf(gsort_ctx *c, F &&f) {
         {"m_ccount", &c->m_ccount}, {"m_t3", &c->m_t3}, {"m_cur3", &c->m_cur3},
         {"m_tdesc", &c->m_tdesc}, {"m_ex", &c->m_ex}, {"m_ey", &c->m_ey},
         {"m_epart", &c->m_epart}, {"m_eplan", &c->m_eplan}, {"m_edesc", &c->m_edesc},
-        {"m_edump", &c->m_edump}, {"m_gplan", &c->m_gplan},
+        {"m_edump", &c->m_edump}, {"m_gplan", &c->m_gplan}, {"m_fb", &c->m_fb},
         {"m_split", &c->m_split}, {"m_rpos", &c->m_rpos}, {"m_bsize", &c->m_bsize},
         {"m_bseg", &c->m_bseg}, {"m_blist", &c->m_blist}, {"m_gb", &c->m_gb},
         {"m_pack", &c->m_pack}, {"m_meta", &c->m_meta}, {"m_g16", &c->m_g16},
@@ -1502,12 +1508,27 @@ gsort_status sort_recv_lists(gsort_ctx *c, const void *recv, bool packed16, cons
                              const uint64_t *roff, int P, const uint64_t *bstart,
                              const WorkLists &wl, const uint64_t *h, uint32_t *out,
                              gsort_stats *stats, bool list0 = true) {
+    // K18c with u8 bins (recv_cb 8): its wrapped buckets collect in m_fb (count at OFF_FBCTR)
+    // and one u16 launch after the lists redoes them, reading their count on the device
+    uint64_t cx_entries = 0;
+    for (int k = 0; k < kLocalClasses; ++k)
+        if (c->recv_cx > 0 && k + 1 >= c->recv_cx) cx_entries += h[3 * (k + 1)];
+    if (list0 && c->recv_cx > 0) cx_entries += h[0];
+    const bool cb8 = c->recv_cb == 8 && cx_entries;
+    uint64_t *fb = nullptr;
+    uint32_t *fb_ctr = reinterpret_cast<uint32_t *>(c->d_small + OFF_FBCTR);
+    if (cb8) {
+        ST_TRY(ensure_list(c, c->m_fb, cx_entries));
+        fb = reinterpret_cast<uint64_t *>(c->m_fb.p);
+        HIP_TRY(c, hipMemsetAsync(fb_ctr, 0, 4, c->stream));
+    }
     for (int k = 0; k < kLocalClasses; ++k) {
         const uint64_t *hk = h + 3 * (k + 1);
         if (!hk[0]) continue;
         if (c->recv_cx > 0 && k + 1 >= c->recv_cx)
             HIP_TRY(c, launch_count_expand(recv, packed16, pos, roff, P, bstart, wl.list[k + 1],
-                                           (uint32_t)hk[0], c->ncu, out, c->stream));
+                                           (uint32_t)hk[0], c->ncu, out, c->stream, fb,
+                                           cb8 ? fb_ctr : nullptr));
         else
             HIP_TRY(c, launch_gather_sort(recv, packed16, pos, roff, P, bstart, wl.list[k + 1],
                                           (uint32_t)hk[0], k + 1, c->atomic_rank, out,
@@ -1517,12 +1538,17 @@ gsort_status sort_recv_lists(gsort_ctx *c, const void *recv, bool packed16, cons
     if (h[0] && list0) {
         if (c->recv_cx > 0)
             HIP_TRY(c, launch_count_expand(recv, packed16, pos, roff, P, bstart, wl.list[0],
-                                           (uint32_t)h[0], c->ncu, out, c->stream));
+                                           (uint32_t)h[0], c->ncu, out, c->stream, fb,
+                                           cb8 ? fb_ctr : nullptr));
         else
             HIP_TRY(c, launch_hist_expand(recv, packed16, pos, roff, P, bstart, wl.list[0],
                                           (uint32_t)h[0], out, c->stream));
         if (stats) { stats->buckets_local += h[0]; stats->keys_bucket_sort += h[1]; }
     }
+    if (cb8)  // the wrapped buckets (usually none: its workgroups return at once)
+        HIP_TRY(c, launch_count_expand(recv, packed16, pos, roff, P, bstart, fb,
+                                       (uint32_t)cx_entries, c->ncu, out, c->stream, nullptr,
+                                       nullptr, fb_ctr));
     return GSORT_OK;
 }
 
@@ -2453,6 +2479,7 @@ gsort_status create_common(gsort_ctx *c, int hip_device) {
     if (const char *e = getenv("GSORT_EST")) c->plan_est = atoi(e) != 0;
     if (const char *e = getenv("GSORT_GIANT")) c->plan_giant = atoi(e) != 0;
     if (const char *e = getenv("GSORT_RECV_CX")) c->recv_cx = atoi(e);
+    if (const char *e = getenv("GSORT_RECV_CB")) c->recv_cb = atoi(e) == 16 ? 16 : 8;
     if (const char *e = getenv("GSORT_EST_SLACK")) c->est_slack = atof(e);
     if (const char *e = getenv("GSORT_PLAN_TRACE")) c->plan_trace = atoi(e) != 0;
     HIP_TRY(c, hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, hip_device));
@@ -2505,6 +2532,11 @@ gsort_status gsort_get_uid(gsort_uid *out) {
 gsort_status gsort_get_uid_ipc(int nranks, gsort_uid *out) {
     if (!out) return GSORT_EINVAL;
     return ipc_get_uid(nranks, out);
+}
+
+gsort_status gsort_runtime_info(gsort_runtime_info_t *out) {
+    if (!out) return GSORT_EINVAL;
+    return runtime_info(out);
 }
 
 int gsort_visible_devices(void) {

@@ -77,9 +77,15 @@ EXPORTS = [
     "gsort_copy_to_device", "gsort_onesweep_tile", "gsort_plan_radix_route",
     "gsort_plan_splitters", "gsort_plan_split", "gsort_plan_split_balanced", "gsort_parse_text",
     "gsort_format_dump", "gsort_copy_ceiling", "gsort_set_ref_compat", "gsort_plan_ref_digits",
-    "gsort_last_plan", "gsort_write_report",
+    "gsort_last_plan", "gsort_write_report", "gsort_runtime_info",
 ]
 REPORT_RADIX, REPORT_SAMPLE = 0, 1
+
+
+class RuntimeInfo(ctypes.Structure):
+    """gsort_runtime_info_t: the HIP runtime and RCCL libgsort is bound to in this process."""
+    _fields_ = [("hip_runtime", ctypes.c_int), ("rccl", ctypes.c_int),
+                ("hip_path", ctypes.c_char * 256), ("rccl_path", ctypes.c_char * 256)]
 
 
 class Report(ctypes.Structure):
@@ -110,6 +116,7 @@ def lib():
     L.gsort_get_uid.argtypes = [P(Uid)]
     L.gsort_get_uid_ipc.argtypes = [I, P(Uid)]
     L.gsort_visible_devices.argtypes = []
+    L.gsort_runtime_info.argtypes = [P(RuntimeInfo)]
     L.gsort_write_report.argtypes = [P(Report), I]
     L.gsort_create.argtypes = [P(VP), I, I, I, P(Uid)]
     L.gsort_group_create.argtypes = [P(VP), I]
@@ -149,6 +156,18 @@ def lib():
     L.gsort_format_dump.restype = ctypes.c_longlong
     _lib = L
     return L
+
+
+def runtime_info():
+    """{hip_runtime, rccl (e.g. '2.27.7'), hip_path, rccl_path}: what libgsort runs on in this
+    process (under torch: torch's bundled HIP runtime and RCCL, loaded first; without torch and
+    in the drop-in CLIs: /opt/rocm's) -- gsort_runtime_info."""
+    r = RuntimeInfo()
+    _check(lib().gsort_runtime_info(ctypes.byref(r)), None)
+    v = r.rccl
+    return {"hip_runtime": r.hip_runtime,
+            "rccl": f"{v // 10000}.{v // 100 % 100}.{v % 100}" if v > 0 else None,
+            "hip_path": r.hip_path.decode(), "rccl_path": r.rccl_path.decode()}
 
 
 def get_uid(ipc_ranks=None):

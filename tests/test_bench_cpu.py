@@ -101,3 +101,30 @@ def test_verify_rows_through_gloo_world_size_2():
         p.join(120)
     res = dict(q.get(timeout=5) for _ in range(2))
     assert res == {0: True, 1: True}
+
+
+def _stats(ms_exchange, exchanges, pair):
+    return {"ms_exchange": ms_exchange, "exchanges": exchanges, "max_pair_bytes": pair}
+
+
+def test_exchange_line_prices_the_largest_pair_on_one_link():
+    """N > 1: per exchange, the largest (source, destination) pair over one xGMI link."""
+    st = [_stats(2.0, 1, 153 * 10**6), _stats(2.0, 1, 153 * 10**6)]
+    ex = bench.exchange_line(st)
+    assert ex["bound"] == "xgmi" and ex["per_exchange_ms"] == 2.0
+    assert ex["achieved_link_GBps"] == 76.5 and ex["frac"] == 0.5
+    assert bench.exchange_line([_stats(0.0, 0, 0)]) is None  # one rank: no exchange
+
+
+def test_strong_line_is_configs2_at_every_n():
+    """The configs[2] block of an N > 1 line: 2^31 keys in total whatever N is (strong
+    scaling), GKeys/s from the slowest rank's step time, its own verification flag."""
+    for world in (2, 4, 8):
+        st = [_stats(1.0, 1, 1 << 28)] * 3
+        line = bench.strong_line(1 << 31, world, 10.0, True, st)
+        assert line["total_keys"] == 1 << 31 and line["keys_per_gpu"] == (1 << 31) // world
+        assert line["scaling"] == "strong" and line["n_gpus"] == world
+        assert line["GKeys_s"] == round((1 << 31) / 10e-3 / 1e9, 3)
+        assert line["verified"] is True and line["steps"] == 3
+        assert line["exchange"]["bound"] == "xgmi"
+        assert "configs[2]" in line["config"]

@@ -207,24 +207,16 @@ def test_rccl_mpirun_stdout_equals_reference(orc, ref_large, tmp_path, cid):
 
 # ---- RCCL peer messages -----------------------------------------------------------------------
 @need(2)
-@pytest.mark.parametrize("piece", [1 << 30, (1 << 30) + 256], ids=["2^30", "2^30+256"])
-def test_rccl_peer_message_piece_limit(tmp_path, piece):
-    """The 2^30-byte piece limit was measured on self-messages only (profiles/
-    r02_rccl_piece_sweep.txt).  Two GPUs sort 5 * 2^28 uniform keys each: about half of each
-    block, 1.25 GiB packed, goes to the peer in pieces of GSORT_RCCL_MAX_MSG bytes.  With the
-    product's 2^30-byte pieces the global output must be exact; with 2^30 + 256-byte pieces the
-    result is recorded (printed), not asserted: the first multi-GPU run decides."""
+def test_rccl_peer_message_in_2p30_pieces(tmp_path):
+    """Peer messages past 2^30 bytes in the product's 2^30-byte pieces (the limit measured on
+    self-messages, profiles/r02_rccl_piece_sweep.txt, pinned on both runtime stacks by
+    tests/test_gpu_rccl.py).  Two GPUs sort 5 * 2^28 uniform keys each: about half of each
+    block, 1.25 GiB packed, goes to the peer; the global output must be exact.  (Round 4 also
+    ran 2^30 + 256-byte pieces here and only printed the result -- a test that could not fail:
+    removed)"""
     case = {"algo": "radix", "dist": "uniform", "n": 2 * (5 << 28), "seed": 100}
-    try:
-        res, _ = run_ranks(2, case, tmp_path, env={"GSORT_RCCL_MAX_MSG": str(piece)})
-        check_global_order(res, case["n"])
-        exact = True
-    except AssertionError as e:
-        if piece == 1 << 30:
-            raise
-        exact = False
-        print("peer pieces of", piece, "bytes:", e)
-    print(f"peer pieces of {piece} bytes: {'exact' if exact else 'WRONG'}")
+    res, _ = run_ranks(2, case, tmp_path, env={"GSORT_RCCL_MAX_MSG": str(1 << 30)})
+    check_global_order(res, case["n"])
 
 
 if __name__ == "__main__" and "--child" in sys.argv:

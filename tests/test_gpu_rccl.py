@@ -95,12 +95,18 @@ def _case_rccl_big(gsort):
         ctx.close()
 
 
-def _child_big():
+def _child_big(stack):
+    """stack "torch": torch imported first, so libgsort runs on torch's bundled HIP runtime
+    and RCCL (what bench.py and the tests use); "rocm": no torch, /opt/rocm's (what the
+    drop-in CLIs use) -- gsort_runtime_info says which."""
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     for p in (root, os.path.join(root, "mpi-test_amd")):
         sys.path.insert(0, p)
-    import torch  # noqa: F401
+    if stack == "torch":
+        import torch  # noqa: F401
     import gsort
+    info = gsort.runtime_info()
+    print("RCCL_STACK " + json.dumps(info), flush=True)
     try:
         r = _case_rccl_big(gsort)
     except Exception as e:
@@ -108,33 +114,48 @@ def _child_big():
     print("RCCL_BIG " + json.dumps(r), flush=True)
 
 
-def _run_big(max_msg):
+STACKS = ["torch", "rocm"]
+
+
+def _run_big(max_msg, stack="torch"):
     # GSORT_RCCL_SELF=1: the self piece through ncclSend / ncclRecv (the product copies it on
     # its stream), so these cases keep pinning RCCL's own message limit
     env = dict(os.environ, GSORT_FORCE_DIST="1", GSORT_RCCL_SELF="1")
     if max_msg:
         env["GSORT_RCCL_MAX_MSG"] = str(max_msg)
-    r = subprocess.run([sys.executable, os.path.abspath(__file__), "--child-big"], env=env,
-                       capture_output=True, text=True, timeout=300)
+    r = subprocess.run([sys.executable, os.path.abspath(__file__), "--child-big", stack],
+                       env=env, capture_output=True, text=True, timeout=300)
+    info, res = None, None
     for line in r.stdout.splitlines():
+        if line.startswith("RCCL_STACK "):
+            info = json.loads(line[len("RCCL_STACK "):])
         if line.startswith("RCCL_BIG "):
-            return json.loads(line[len("RCCL_BIG "):])
-    pytest.fail(f"RCCL big child exited {r.returncode}:\n{r.stderr[-4000:]}")
+            res = json.loads(line[len("RCCL_BIG "):])
+    if res is None:
+        pytest.fail(f"RCCL big child exited {r.returncode}:\n{r.stderr[-4000:]}")
+    print(f"{stack} stack: RCCL {info['rccl']} ({info['rccl_path']}), HIP runtime "
+          f"{info['hip_runtime']}")
+    # the stack is the one asked for: torch's bundled RCCL, or /opt/rocm's without torch
+    assert ("torch" in info["rccl_path"]) == (stack == "torch"), info
+    return res
 
 
-def test_rccl_self_message_over_2gib_in_pieces():
-    """The product's exchange (<= 1 GiB pieces) moves a 2.5 GiB self-message exactly."""
-    assert _run_big(None) == "ok"
+@pytest.mark.parametrize("stack", STACKS)
+def test_rccl_self_message_over_2gib_in_pieces(stack):
+    """The product's exchange (<= 1 GiB pieces) moves a 2.5 GiB self-message exactly, on
+    torch's RCCL (bench, tests) and on /opt/rocm's (the drop-in CLIs)."""
+    assert _run_big(None, stack) == "ok"
 
 
+@pytest.mark.parametrize("stack", STACKS)
 @pytest.mark.parametrize("piece", [(1 << 30) + 256, 1 << 40], ids=["2^30+256", "single"])
-def test_rccl_self_message_pieces_past_the_limit(piece):
+def test_rccl_self_message_pieces_past_the_limit(piece, stack):
     """The same 2.5 GiB self-message in pieces just over 2^30 bytes, and as ONE ncclSend /
     ncclRecv pair (GSORT_RCCL_MAX_MSG).  Measured on MI355X: both wrong (the sorted output
     misses keys), as are 1.25, 1.5, 1.75 and 2 GiB - 4 KiB pieces (tools/rccl_piece_sweep.sh,
     profiles/r02_rccl_piece_sweep.txt), while 2^30-byte pieces are exact: the limit is the
     2^30-byte boundary, hence the product's 1 GiB pieces (gsort_comm.cpp)."""
-    r = _run_big(piece)
+    r = _run_big(piece, stack)
     print(f"pieces of {piece} bytes:", r)
     # pins the RCCL limit the product works around; if this starts passing, RCCL moves such
     # messages now and the 2^30-byte piece size in gsort_comm.cpp can be raised
@@ -142,17 +163,18 @@ def test_rccl_self_message_pieces_past_the_limit(piece):
     assert r.startswith("wrong output"), r
 
 
-def test_rccl_self_message_exactly_2p30_pieces():
+@pytest.mark.parametrize("stack", STACKS)
+def test_rccl_self_message_exactly_2p30_pieces(stack):
     """Pieces of exactly 2^30 bytes (the product's size, set explicitly): exact."""
-    assert _run_big(1 << 30) == "ok"
+    assert _run_big(1 << 30, stack) == "ok"
 
 
 def test_rccl_self_piece_copied_by_the_product():
     """Without GSORT_RCCL_SELF the 2.5 GiB self piece is a device copy: exact as well."""
     env = dict(os.environ, GSORT_FORCE_DIST="1")
     env.pop("GSORT_RCCL_SELF", None)
-    r = subprocess.run([sys.executable, os.path.abspath(__file__), "--child-big"], env=env,
-                       capture_output=True, text=True, timeout=300)
+    r = subprocess.run([sys.executable, os.path.abspath(__file__), "--child-big", "torch"],
+                       env=env, capture_output=True, text=True, timeout=300)
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("RCCL_BIG ")]
     assert lines and json.loads(lines[0][len("RCCL_BIG "):]) == "ok", r.stderr[-3000:]
 
@@ -208,4 +230,4 @@ def test_one_rank_rccl_small(child_results, n):
 if __name__ == "__main__" and "--child" in sys.argv:
     _child()
 if __name__ == "__main__" and "--child-big" in sys.argv:
-    _child_big()
+    _child_big(sys.argv[sys.argv.index("--child-big") + 1])

@@ -6,7 +6,8 @@ too), 5 = only buckets past kLocalMax (the default), -1 = the round-2 kernels (K
 two-read K18).  The cases reach what K18c must get right: pieces of P ranks starting at any
 2-B / 4-B alignment, empty pieces, buckets of one value, and bins of >= 65 536 copies of one
 value in buckets past 65 535 keys, whose u16 halves wrap (low half: the carry into the
-neighbour bin; high half; both).  The reference's own final order is the sorted multiset
+neighbour bin; high half; both) -- and, with the default u8 bins, every bucket holding >= 256
+copies of one key (redone with u16 bins).  The reference's own final order is the sorted multiset
 (mpi_radix_sort.c:185-192, mpi_sample_sort.c:174), so np.sort is the oracle (bit-exact).
 """
 import numpy as np
@@ -67,6 +68,23 @@ def test_receive_buckets(gsort, monkeypatch, case, algo, cx, P):
         cuts = np.arange(1, P) * B
     blocks = np.split(keys, cuts)
     res = run_group(gsort, blocks, algo)
+    _check(res, keys, P, algo)
+
+
+@pytest.mark.parametrize("algo", ["radix", "sample"])
+@pytest.mark.parametrize("case", list(CASES))
+@pytest.mark.parametrize("P", [2, 8])
+def test_receive_buckets_u16_bins(gsort, monkeypatch, case, algo, P):
+    """K18c's u16 bins (GSORT_RECV_CB=16; the default is u8 bins, whose buckets with >= 256
+    copies of one key -- wraps, one_value, few_values -- are redone with u16 bins) on every
+    bucket (GSORT_RECV_CX=1)."""
+    monkeypatch.setenv("GSORT_RECV_CX", "1")
+    monkeypatch.setenv("GSORT_RECV_CB", "16")
+    rng = np.random.default_rng(hash((case, P, "u16")) % 2**32)
+    keys = np.asarray(CASES[case](rng)).astype(np.int32)
+    rng.shuffle(keys)
+    B = -(-keys.size // P)
+    res = run_group(gsort, np.split(keys, np.arange(1, P) * B), algo)
     _check(res, keys, P, algo)
 
 
