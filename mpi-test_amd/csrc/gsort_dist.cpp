@@ -1,0 +1,945 @@
+// gsort_dist.cpp -- the distributed sorts of libgsort: the receive side (P
+// sorted runs -> one sorted block), the distributed radix (radix select + one packed exchange;
+// the LSD-pass form; the reference-compat order) and the sample sort.
+// Reference being replaced: mpi_radix_sort.c:133-195 (per-pass all-to-all through rank 0) and
+// mpi_sample_sort.c:89-174 (samples, splitters, buckets, all-to-all, final qsort).
+#include "gsort_ctx.h"
+
+namespace gsort {
+namespace rt {
+
+// ---- receive side: P sorted runs (after an exchange) -> one sorted block ---------------------
+// Replaces the re-sort of the received keys (the reference's final qsort, mpi_sample_sort.c:174;
+// for the radix path the last pass's placement, mpi_radix_sort.c:185-192).  The runs are
+// bucketed by their top 16 bits with binary searches (no pass over the keys), and K11g sorts
+// every bucket's low 16 bits straight from the P pieces: one read + one write per key.  Buckets
+// larger than kLocalMax are gathered into place and finish through the MSD levels 1 and 0.
+// recv holds the P runs back to back (run p has rlen[p] keys), each grouped by the top 16 bits
+// (ordered u32): int32 keys, or with packed16 only their low 16 bits, in which case the caller
+// has already filled c->m_rpos (pos[p][h], launch_pos_from_meta).
+// bucket sizes (65536) + starts (65537) + row-scan partials (64 x 64), u64
+constexpr size_t kBsizeBytes = ((size_t)2 * kBuckets16 + 1 + 65 * 64) * 8;
+
+// (a - b) / sizeof(T) for pointers into different allocations, as a u64 (two's complement for
+// a negative offset): integer arithmetic, never a pointer difference across allocations
+template <typename T>
+uint64_t elem_offset(const T *a, const T *b) {
+    const int64_t d = (int64_t)(reinterpret_cast<uintptr_t>(a) - reinterpret_cast<uintptr_t>(b));
+    return (uint64_t)(d / (int64_t)sizeof(T));
+}
+
+// self (int32 runs only): run `self_rank` was not received -- it lies at self_src (the
+// sender's sorted block), and the kernels read it there through a run offset taken relative to
+// recv (mod 2^64); the MSD fallback, which needs the runs back to back, copies it in first.
+// Every receive bucket of the lists wl (counts h, read_counters layout) sorted from its P
+// pieces into out: K11g by size class, K18c (or, GSORT_RECV_CX=-1, the two-read K18) past
+// kLocalMax; classes >= c->recv_cx go to K18c as well.  With list0, list 0 is sorted too (it
+// must then hold no bucket past kHxMax).
+gsort_status sort_recv_lists(gsort_ctx *c, const void *recv, bool packed16, const uint64_t *pos,
+                             const uint64_t *roff, int P, const uint64_t *bstart,
+                             const WorkLists &wl, const uint64_t *h, uint32_t *out,
+                             gsort_stats *stats, bool list0 = true) {
+    // K18c with u8 bins (recv_cb 8): its wrapped buckets collect in m_fb (count at OFF_FBCTR)
+    // and one u16 launch after the lists redoes them, reading their count on the device
+    uint64_t cx_entries = 0;
+    for (int k = 0; k < kLocalClasses; ++k)
+        if (c->recv_cx > 0 && k + 1 >= c->recv_cx) cx_entries += h[3 * (k + 1)];
+    if (list0 && c->recv_cx > 0) cx_entries += h[0];
+    const bool cb8 = c->recv_cb == 8 && cx_entries;
+    uint64_t *fb = nullptr;
+    uint32_t *fb_ctr = reinterpret_cast<uint32_t *>(c->d_small + OFF_FBCTR);
+    if (cb8) {
+        ST_TRY(ensure_list(c, c->m_fb, cx_entries));
+        fb = reinterpret_cast<uint64_t *>(c->m_fb.p);
+        HIP_TRY(c, hipMemsetAsync(fb_ctr, 0, 4, c->stream));
+    }
+    for (int k = 0; k < kLocalClasses; ++k) {
+        const uint64_t *hk = h + 3 * (k + 1);
+        if (!hk[0]) continue;
+        if (c->recv_cx > 0 && k + 1 >= c->recv_cx)
+            HIP_TRY(c, launch_count_expand(recv, packed16, pos, roff, P, bstart, wl.list[k + 1],
+                                           (uint32_t)hk[0], c->ncu, out, c->stream, fb,
+                                           cb8 ? fb_ctr : nullptr));
+        else
+            HIP_TRY(c, launch_gather_sort(recv, packed16, pos, roff, P, bstart, wl.list[k + 1],
+                                          (uint32_t)hk[0], k + 1, c->atomic_rank, out,
+                                          c->stream));
+        if (stats) { stats->buckets_local += hk[0]; stats->keys_bucket_sort += hk[1]; }
+    }
+    if (h[0] && list0) {
+        if (c->recv_cx > 0)
+            HIP_TRY(c, launch_count_expand(recv, packed16, pos, roff, P, bstart, wl.list[0],
+                                           (uint32_t)h[0], c->ncu, out, c->stream, fb,
+                                           cb8 ? fb_ctr : nullptr));
+        else
+            HIP_TRY(c, launch_hist_expand(recv, packed16, pos, roff, P, bstart, wl.list[0],
+                                          (uint32_t)h[0], out, c->stream));
+        if (stats) { stats->buckets_local += h[0]; stats->keys_bucket_sort += h[1]; }
+    }
+    if (cb8)  // the wrapped buckets (usually none: its workgroups return at once)
+        HIP_TRY(c, launch_count_expand(recv, packed16, pos, roff, P, bstart, fb,
+                                       (uint32_t)cx_entries, c->ncu, out, c->stream, nullptr,
+                                       nullptr, fb_ctr));
+    return GSORT_OK;
+}
+
+gsort_status recv_sort(gsort_ctx *c, const void *recv, bool packed16,
+                       const std::vector<uint64_t> &rlen, uint64_t n, uint32_t *out,
+                       uint32_t *tmp, gsort_stats *stats, int self_rank = -1,
+                       const int32_t *self_src = nullptr) {
+    const int P = (int)rlen.size();
+    if (n == 0) return GSORT_OK;
+    if (!packed16 && (P > 64 || c->local_algo == GSORT_LOCAL_LSD)) {  // K11g: <= 64 pieces
+        if (self_src && rlen[self_rank]) {
+            uint64_t o = 0;
+            for (int p = 0; p < self_rank; ++p) o += rlen[p];
+            HIP_TRY(c, hipMemcpyAsync(static_cast<int32_t *>(const_cast<void *>(recv)) + o,
+                                      self_src, rlen[self_rank] * 4, hipMemcpyDeviceToDevice,
+                                      c->stream));
+        }
+        int pr = 0;
+        return local_sort(c, reinterpret_cast<const uint32_t *>(recv), n, out, tmp, &pr, stats);
+    }
+    if (P > 64) return set_err(c, GSORT_EINVAL, "packed exchange supports at most 64 ranks");
+    hipEvent_t t = tic(c);
+    ST_TRY(ensure(c, c->m_rpos, (size_t)P * (kBuckets16 + 1) * 8));
+    ST_TRY(ensure(c, c->m_bsize, kBsizeBytes));
+    ST_TRY(ensure_list(c, c->m_next[0], kBuckets16));
+    for (auto &b : c->m_local) ST_TRY(ensure_list(c, b, kBuckets16));
+    uint64_t *h_r = reinterpret_cast<uint64_t *>(c->h_small + OFF_PLAN);
+    uint64_t *d_r = reinterpret_cast<uint64_t *>(c->d_small + OFF_PLAN);
+    HIP_TRY(c, hipStreamSynchronize(c->stream));  // h_r may still feed an earlier copy
+    uint64_t off = 0;
+    for (int p = 0; p < P; ++p) { h_r[p] = off; h_r[P + p] = rlen[p]; off += rlen[p]; }
+    if (self_src)
+        h_r[self_rank] = elem_offset(self_src, static_cast<const int32_t *>(recv));
+    HIP_TRY(c, hipMemcpyAsync(d_r, h_r, (size_t)2 * P * 8, hipMemcpyHostToDevice, c->stream));
+    uint64_t *pos = reinterpret_cast<uint64_t *>(c->m_rpos.p);
+    uint64_t *bsize = reinterpret_cast<uint64_t *>(c->m_bsize.p), *bstart = bsize + kBuckets16;
+    uint64_t *ctr = reinterpret_cast<uint64_t *>(c->d_small + OFF_CTR);
+    HIP_TRY(c, hipMemsetAsync(ctr, 0, kCtrBytes, c->stream));
+    if (!packed16)
+        HIP_TRY(c, launch_run_bounds(reinterpret_cast<const int32_t *>(recv), d_r, d_r + P, P, pos,
+                                     c->stream));
+    HIP_TRY(c, launch_recv_classify(pos, P, bsize, bstart, work_lists(c, 0),
+                                    bstart + kBuckets16 + 1, c->stream));
+    toc(c, PH_COUNT, t);
+    uint64_t h[3 * (kLocalClasses + 1)];
+    ST_TRY(read_counters(c, h));
+    if (check_mode()) {
+        uint64_t keys = h[1];
+        for (int k = 0; k < kLocalClasses; ++k) keys += h[3 * (k + 1) + 1];
+        if (keys != n)
+            return set_err(c, GSORT_EINVAL, "GSORT_CHECK receive lists hold " +
+                                                std::to_string(keys) + " keys, want " +
+                                                std::to_string(n) + " (rank " +
+                                                std::to_string(c->rank) + ")");
+        ST_TRY(check_bounds(c, bstart, kBuckets16 + 1, n, "receive bucket starts"));
+    }
+    const bool list0 = h[0] && h[2] <= kHxMax;  // else: a bucket past kHxMax (below)
+    t = tic(c);
+    ST_TRY(sort_recv_lists(c, recv, packed16, pos, d_r, P, bstart, work_lists(c, 0), h, out, stats,
+                           list0));
+    toc(c, PH_BUCKET, t);
+    if (h[0] && !list0) {  // all of list 0 into place, then MSD levels 1 and 0
+        HIP_TRY(c, launch_list_to_segments(reinterpret_cast<uint64_t *>(c->m_next[0].p),
+                                           (uint32_t)h[0], bstart, c->stream));
+        HIP_TRY(c, launch_gather_copy(recv, packed16, pos, d_r, P, bsize, bstart, out, c->stream));
+        for (int k = 3; k < 3 * (kLocalClasses + 1); ++k) h[k] = 0;
+        int levels = 0;
+        ST_TRY(msd_levels(c, 1, out, out, tmp, 0, h, stats, &levels));
+    }
+    return GSORT_OK;
+}
+
+// Allgather one u64 per rank into host memory (counts used to size RCCL messages).
+gsort_status allgather_u64(gsort_ctx *c, uint64_t v, std::vector<uint64_t> &out) {
+    out.assign(c->nranks, 0);
+    if (c->nranks == 1) { out[0] = v; return GSORT_OK; }
+    uint64_t *h = reinterpret_cast<uint64_t *>(c->h_small + OFF_PLAN);
+    uint64_t *d = reinterpret_cast<uint64_t *>(c->d_small + OFF_PLAN);
+    h[0] = v;
+    HIP_TRY(c, hipMemcpyAsync(d, h, 8, hipMemcpyHostToDevice, c->stream));
+    ST_TRY(comm_try(c, c->comm->allgather(d, d + 1, 8, c->stream)));
+    HIP_TRY(c, hipMemcpyAsync(h + 1, d + 1, 8 * c->nranks, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    for (int r = 0; r < c->nranks; ++r) out[r] = h[1 + r];
+    return GSORT_OK;
+}
+
+void block_of(uint64_t N, int P, int r, uint64_t *B, uint64_t *len) {
+    *B = P ? (N + P - 1) / P : 0;
+    const uint64_t lo = (uint64_t)r * *B;
+    *len = lo >= N ? 0 : std::min(*B, N - lo);
+}
+
+// Sort the listed groups {start, len} of an int32 block in place on their low 16 bits (their
+// top 16 bits are equal): K11 for groups of <= kLocalMax keys, the LSD passes otherwise.
+gsort_status sort_groups(gsort_ctx *c, int32_t *a,
+                         const std::vector<std::pair<uint64_t, uint64_t>> &groups) {
+    std::vector<uint64_t> small[kLocalClasses];
+    for (const auto &gr : groups) {
+        const int k = local_class(gr.second);
+        if (k) {
+            small[k - 1].push_back(gr.first);
+            small[k - 1].push_back(gr.second);
+            continue;
+        }
+        ST_TRY(ensure(c, c->m_bseg, gr.second * 8));
+        uint32_t *t0 = reinterpret_cast<uint32_t *>(c->m_bseg.p), *t1 = t0 + gr.second;
+        int pr = 0;  // lsd_sort leaves its result in its `out` (t0)
+        ST_TRY(lsd_sort(c, reinterpret_cast<const uint32_t *>(a + gr.first), gr.second, t0, t1,
+                        &pr));
+        HIP_TRY(c, hipMemcpyAsync(a + gr.first, t0, gr.second * 4, hipMemcpyDeviceToDevice,
+                                  c->stream));
+    }
+    for (int k = 0; k < kLocalClasses; ++k) {
+        if (small[k].empty()) continue;
+        ST_TRY(ensure(c, c->m_blist, small[k].size() * 8));
+        HIP_TRY(c, hipMemcpyAsync(c->m_blist.p, small[k].data(), small[k].size() * 8,
+                                  hipMemcpyHostToDevice, c->stream));
+        uint32_t *ab = reinterpret_cast<uint32_t *>(a);
+        HIP_TRY(c, launch_local_sort(ab, ab, reinterpret_cast<uint64_t *>(c->m_blist.p),
+                                     (uint32_t)(small[k].size() / 2), k + 1, 2, true,
+                                     c->atomic_rank, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));  // small[k] is host memory
+    }
+    return GSORT_OK;
+}
+
+// The same on the packed send buffer: groups = {16-bit bucket h, first position}, ends[i] =
+// the group's end (gb[h + 1]).  Each group is rebuilt as int32 keys in scratch, sorted by
+// sort_groups (K11 or LSD passes by size), and packed back in place.
+gsort_status sort_groups16(gsort_ctx *c, uint16_t *pack,
+                           const std::vector<std::pair<uint64_t, uint64_t>> &groups,
+                           const std::vector<uint64_t> &ends) {
+    uint64_t total = 0;
+    for (size_t i = 0; i < groups.size(); ++i) total += ends[i] - groups[i].second;
+    ST_TRY(ensure(c, c->m_g16, std::max<uint64_t>(total, 1) * 4));
+    int32_t *scr = reinterpret_cast<int32_t *>(c->m_g16.p);
+    std::vector<std::pair<uint64_t, uint64_t>> local;
+    uint64_t off = 0;
+    for (size_t i = 0; i < groups.size(); ++i) {
+        const uint64_t a = groups[i].second, len = ends[i] - a;
+        HIP_TRY(c, launch_unpack16(pack + a, len, (uint32_t)groups[i].first, scr + off,
+                                   c->stream));
+        local.push_back({off, len});
+        off += len;
+    }
+    ST_TRY(sort_groups(c, scr, local));
+    for (size_t i = 0; i < groups.size(); ++i)
+        HIP_TRY(c, launch_pack16(scr + local[i].first, local[i].second, pack + groups[i].second,
+                                 c->stream));
+    return GSORT_OK;
+}
+
+// ---- distributed radix (P > 1): local sort, exact splitters, ONE exchange, local sort ------
+// The reference keeps rank q on global positions [qB, (q+1)B) by routing every key through
+// rank 0 on each of its base-P passes (mpi_radix_sort.c:139 Scatter, :150-173 all-to-all,
+// :180-192 Gatherv).  Here: (1) each rank sorts its block (MSD local sort); (2) radix select of
+// the exact boundary keys: 4 rounds of 8 bits, each counting the keys below 257 thresholds per
+// boundary by binary search on the sorted blocks (K13) and all-gathering the counts; (3) the
+// cut of every block (gsort_plan_split: copies of a boundary key go left in rank order); (4) one
+// grouped send/recv of contiguous runs; (5) the received sorted runs are bucketed by their top
+// 16 bits and every bucket is finished in LDS (recv_sort).
+gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in,
+                              int32_t **d_out, uint64_t *n_out, gsort_stats *stats) {
+    const int P = c->nranks, me = c->rank;
+    std::vector<uint64_t> n_all;
+    ST_TRY(allgather_u64(c, n_in, n_all));
+    uint64_t N = 0;
+    for (uint64_t v : n_all) N += v;
+    uint64_t B, mine;
+    block_of(N, P, me, &B, &mine);
+    // the packed exchange sends one u32 count per (destination, 16-bit bucket): every rank's
+    // block, and so every count, must stay below 2^32 keys (decided identically on all ranks)
+    for (int r = 0; r < P; ++r)
+        if (n_all[r] >= (1ull << 32))
+            return set_err(c, GSORT_EINVAL, "radix: a rank holds >= 2^32 keys (rank " +
+                                                std::to_string(r) + "); split the input further");
+    const uint64_t cap = std::max<uint64_t>(std::max(n_in, mine), 1);
+    ST_TRY(ensure(c, c->slot[S_TMP], cap * 4));
+    ST_TRY(ensure(c, c->slot[S_RECV], std::max<uint64_t>(mine, 1) * 4));
+    ST_TRY(ensure(c, c->slot[S_OUT], std::max<uint64_t>(mine, 1) * 4));
+    ST_TRY(ensure(c, c->m_gb, (size_t)(kBuckets16 + 1) * 8));
+    ST_TRY(ensure(c, c->m_pack, std::max<uint64_t>(n_in, 1) * 2));
+    uint64_t *gb = reinterpret_cast<uint64_t *>(c->m_gb.p);
+    uint16_t *pack = reinterpret_cast<uint16_t *>(c->m_pack.p);
+    // (1) group the block by its top 16 bits (MSD levels 3 and 2 only: the receivers sort the
+    // low 16 bits anyway).  Level 2 stores just the low 16 bits of every key -- the packed send
+    // buffer -- and the 16-bit bucket bounds gb come from the MSD plan (K17), not the keys.  A
+    // block of <= kLocalMax keys is sorted whole in LDS instead, then bounded and packed.
+    if (stats) stats->local_algo = c->local_algo;
+    const bool packed_msd = n_in > kLocalMax;
+    hipEvent_t t;
+    {
+        gsort_stats tmp_st;
+        memset(&tmp_st, 0, sizeof(tmp_st));
+        int32_t *sorted = nullptr;
+        if (!packed_msd) {
+            ST_TRY(ensure(c, c->slot[S_SORTED], std::max<uint64_t>(n_in, 1) * 4));
+            sorted = slot_ptr<int32_t>(c, S_SORTED);
+        }
+        ST_TRY(msd_sort(c, reinterpret_cast<const uint32_t *>(d_keys), n_in,
+                        reinterpret_cast<uint32_t *>(sorted), slot_ptr<uint32_t>(c, S_TMP),
+                        stats ? stats : &tmp_st, true, packed_msd ? pack : nullptr, gb));
+        t = tic(c);
+        if (packed_msd && c->plan16) {
+            // gb written by the two-level plan
+        } else if (packed_msd) {
+            HIP_TRY(c, launch_gb_from_plan(reinterpret_cast<uint64_t *>(c->d_small + OFF_BASES),
+                                           reinterpret_cast<uint64_t *>(c->d_small + OFF_TOT),
+                                           reinterpret_cast<uint64_t *>(c->m_next[0].p),
+                                           (uint32_t)c->group16_nseg,
+                                           reinterpret_cast<uint64_t *>(c->m_cstart.p), n_in,
+                                           gb, c->stream));
+        } else {
+            uint64_t *h_one = reinterpret_cast<uint64_t *>(c->h_small + OFF_ONE);
+            uint64_t *d_one = reinterpret_cast<uint64_t *>(c->d_small + OFF_ONE);
+            HIP_TRY(c, hipStreamSynchronize(c->stream));  // h_one may feed an earlier copy
+            h_one[0] = 0;
+            h_one[1] = n_in;
+            HIP_TRY(c, hipMemcpyAsync(d_one, h_one, 16, hipMemcpyHostToDevice, c->stream));
+            HIP_TRY(c, launch_run_bounds(sorted, d_one, d_one + 1, 1, gb, c->stream));
+            HIP_TRY(c, launch_pack16(sorted, n_in, pack, c->stream));
+        }
+        toc(c, PH_PLACE, t);
+    }
+    int pr = stats ? stats->passes_run : 0;
+    if (check_mode()) ST_TRY(check_bounds(c, gb, kBuckets16 + 1, n_in, "sender bucket bounds"));
+
+    // (2) radix select of v_q, the g_q-th smallest key, for the P-1 inner boundaries: 4 rounds of
+    // 8 bits, every round decided on the device (K13s sums the all-gathered counts, picks the
+    // digit and writes the next round's thresholds), and after round 1 -- the boundaries'
+    // 16-bit groups known -- K13g sorts each boundary group in place in the packed buffer, so
+    // rounds 2 and 3 binary-search it and the cut splits it by value.  The host waits ONCE, for
+    // the last round's counts (the cut and the exchange sizes RCCL needs on the host).  A
+    // boundary group past K13g's 32 768 keys (skewed input) is flagged in the count rows of
+    // rounds 2 and 3, so every rank sees it: all ranks then sort the groups on the host path and
+    // repeat rounds 2 and 3 with the host between them (select_rounds below).
+    const int nb = P - 1, M = 257, W = nb * M + nb;  // count row: nb x M counts + nb K13g flags
+    std::vector<uint64_t> g(nb), prefix(nb, 0), hx((size_t)2 * nb + (size_t)nb * M),
+        all((size_t)P * W);
+    std::vector<int> dsel(nb, 0);
+    for (int q = 0; q < nb; ++q) g[q] = std::min<uint64_t>((uint64_t)(q + 1) * B, N);
+    ST_TRY(ensure(c, c->m_split, (size_t)std::max(nb, 1) * (M * 16 + 32)));
+    ST_TRY(ensure(c, c->slot[S_STAGE], (size_t)P * std::max(W, 1) * 8));
+    // m_split: prefix (nb) | g (nb) | thresholds (nb x M) | counts (nb x M) + flags (nb), u64
+    uint64_t *d_pref = reinterpret_cast<uint64_t *>(c->m_split.p), *d_g = d_pref + nb;
+    uint64_t *d_xs = d_g + nb;
+    uint64_t *d_cnt = d_xs + (size_t)nb * M;
+    const uint64_t *d_all = reinterpret_cast<const uint64_t *>(c->slot[S_STAGE].p);
+    // rounds k0 .. 3 from the thresholds in d_xs (K13g after round 1 when k0 == 0), then the last
+    // round's rows and the boundary keys to the host
+    auto select_rounds = [&](int k0) -> gsort_status {
+        for (int k = k0; k < 4; ++k) {
+            HIP_TRY(c, launch_count_below16(pack, gb, d_xs, nb * M, d_cnt, c->stream));
+            ST_TRY(comm_try(c, c->comm->allgather(d_cnt, c->slot[S_STAGE].p, (size_t)W * 8,
+                                                  c->stream)));
+            HIP_TRY(c, launch_select_digit(d_all, W, d_g, N, P, nb, M, 24 - 8 * k, d_pref, d_xs,
+                                           c->stream));
+            if (k == 1)
+                HIP_TRY(c, launch_boundary_sort16(pack, gb, d_pref, d_g, N, nb, c->atomic_rank,
+                                                  d_cnt + (size_t)nb * M, c->stream));
+        }
+        HIP_TRY(c, hipMemcpyAsync(all.data(), d_all, all.size() * 8, hipMemcpyDeviceToHost,
+                                  c->stream));
+        HIP_TRY(c, hipMemcpyAsync(prefix.data(), d_pref, (size_t)nb * 8, hipMemcpyDeviceToHost,
+                                  c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        return GSORT_OK;
+    };
+    // the thresholds of round 0 (prefix 0) and of round 2 after the host path (prefix: the top
+    // 16 bits); prefix and g go along
+    auto put_thresholds = [&](int shift) -> gsort_status {
+        for (int q = 0; q < nb; ++q) { hx[q] = prefix[q]; hx[nb + q] = g[q]; }
+        for (int q = 0; q < nb; ++q)
+            for (int d = 0; d < M; ++d)
+                hx[2 * nb + (size_t)q * M + d] = prefix[q] + ((uint64_t)d << shift);
+        HIP_TRY(c, hipMemcpyAsync(d_pref, hx.data(), hx.size() * 8, hipMemcpyHostToDevice,
+                                  c->stream));
+        return GSORT_OK;
+    };
+    t = tic_rec(c);
+    if (nb > 0) {  // (one rank: no boundary, nothing to select)
+        ST_TRY(put_thresholds(24));
+        ST_TRY(select_rounds(0));
+        bool big = false;
+        for (int p = 0; p < P; ++p)
+            for (int q = 0; q < nb; ++q) big |= all[(size_t)p * W + (size_t)nb * M + q] != 0;
+        if (big) {  // a boundary group past K13g's reach on some rank: every rank takes this
+            std::vector<std::pair<uint64_t, uint64_t>> groups;  // {h, first position}
+            for (int q = 0; q < nb; ++q)
+                if (g[q] < N) groups.push_back({prefix[q] >> 16, 0});
+            std::sort(groups.begin(), groups.end());
+            groups.erase(std::unique(groups.begin(), groups.end()), groups.end());
+            std::vector<uint64_t> h_gb(2 * groups.size());
+            for (size_t i = 0; i < groups.size(); ++i)
+                HIP_TRY(c, hipMemcpyAsync(&h_gb[2 * i], gb + groups[i].first, 16,
+                                          hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(c, hipStreamSynchronize(c->stream));
+            std::vector<std::pair<uint64_t, uint64_t>> nonempty;
+            std::vector<uint64_t> ends;
+            for (size_t i = 0; i < groups.size(); ++i)
+                if (h_gb[2 * i + 1] > h_gb[2 * i]) {
+                    nonempty.push_back({groups[i].first, h_gb[2 * i]});
+                    ends.push_back(h_gb[2 * i + 1]);
+                }
+            if (!nonempty.empty()) ST_TRY(sort_groups16(c, pack, nonempty, ends));
+            for (int q = 0; q < nb; ++q) prefix[q] = prefix[q] >> 16 << 16;
+            ST_TRY(put_thresholds(8));
+            ST_TRY(select_rounds(2));
+        }
+        for (int q = 0; q < nb; ++q) dsel[q] = (int)(prefix[q] & 255u);
+    }
+    toc_rec(c, PH_SAMPLE, t);
+    // (3) cut points from the last round: lt = count(< v_q), le = count(< v_q + 1)
+    std::vector<uint64_t> lt((size_t)P * nb), le((size_t)P * nb), send(P), recv(P);
+    for (int p = 0; p < P; ++p)
+        for (int q = 0; q < nb; ++q) {
+            const uint64_t *row = &all[(size_t)p * W + (size_t)q * M];
+            lt[(size_t)p * nb + q] = g[q] >= N ? n_all[p] : row[dsel[q]];
+            le[(size_t)p * nb + q] = g[q] >= N ? n_all[p] : row[dsel[q] + 1];
+        }
+    gsort_status ps = gsort_plan_split(P, n_all.data(), lt.data(), le.data(), me, send.data(),
+                                       recv.data());
+    if (ps != GSORT_OK) return set_err(c, ps, "inconsistent splitter counts");
+    // (4) one exchange of the keys' low 16 bits: every destination block's keys lie in a known
+    // range of 16-bit buckets (from the boundary keys), so the top 16 bits travel as one count
+    // per (destination, bucket) instead of 2 bytes per key
+    std::vector<uint64_t> hlo(P), nh(P), cut(P + 1, 0);
+    for (int q = 0; q < P; ++q) {
+        const uint64_t lo = q == 0 ? 0 : (g[q - 1] >= N ? 0xFFFFFFFFull : prefix[q - 1]);
+        const uint64_t hi = q == P - 1 ? 0xFFFFFFFFull : (g[q] >= N ? 0xFFFFFFFFull : prefix[q]);
+        hlo[q] = lo >> 16;
+        nh[q] = (hi >> 16) - hlo[q] + 1;
+        cut[q + 1] = cut[q] + send[q];
+    }
+    // test hook GSORT_RCCL_SELF=1: the self pieces do go through the transport (RcclComm then
+    // sends them through ncclSend / ncclRecv: tests/test_gpu_rccl.py pins RCCL's message limit)
+    static const bool self_moved = getenv("GSORT_RCCL_SELF") && getenv("GSORT_RCCL_SELF")[0] == '1';
+    uint64_t meta_n = 0, meta_self = ~0ull;  // meta_self: this rank's own count section
+    std::vector<uint64_t> rng;
+    for (int q = 0; q < P; ++q)
+        if (send[q]) {
+            rng.insert(rng.end(), {cut[q], cut[q + 1], hlo[q], nh[q], meta_n});
+            if (q == me) meta_self = meta_n;
+            meta_n += nh[q];
+        }
+    uint64_t nsrc = 0;
+    for (int p = 0; p < P; ++p) nsrc += recv[p] ? 1 : 0;
+    ST_TRY(ensure(c, c->m_meta, (std::max<uint64_t>(meta_n, 1) + nsrc * nh[me] + 1) * 4 +
+                                    (rng.size() + P + 2) * 8));
+    uint32_t *meta_s = reinterpret_cast<uint32_t *>(c->m_meta.p);
+    // (one word of gap: an in-place self offset below, meta_self - (meta_r - meta_s), is then
+    // at most -2 and never the "no source" mark ~0)
+    uint32_t *meta_r = meta_s + std::max<uint64_t>(meta_n, 1) + 1;
+    uint64_t *d_tab = reinterpret_cast<uint64_t *>(
+        reinterpret_cast<char *>(c->m_meta.p) +
+        (((std::max<uint64_t>(meta_n, 1) + nsrc * nh[me] + 1) * 4 + 7) & ~size_t(7)));
+    std::vector<uint64_t> tab(rng);
+    std::vector<uint64_t> moff(P, ~0ull);
+    {
+        uint64_t k = 0;
+        for (int p = 0; p < P; ++p)
+            if (recv[p]) moff[p] = (k++) * nh[me];
+    }
+    // the rank's own counts are read where K15 writes them (an offset relative to meta_r, mod
+    // 2^64), like its own keys below: no self copy in the count exchange either
+    const bool meta_in_place = !self_moved && recv[me] && meta_self != ~0ull;
+    if (meta_in_place) moff[me] = meta_self - (uint64_t)(meta_r - meta_s);
+    tab.insert(tab.end(), moff.begin(), moff.end());
+    // staged through pinned memory (a pageable copy blocks the host in the runtime's staging):
+    // OFF_PLAN + 8 KiB is free here -- step (5) below uses OFF_PLAN's first 2P words, and
+    // nothing copies from this range after the stream syncs of the previous call
+    uint64_t *h_tab = reinterpret_cast<uint64_t *>(c->h_small + OFF_PLAN + 8192);
+    if (OFF_PLAN + 8192 + tab.size() * 8 > kSmallBytes)
+        return set_err(c, GSORT_EINVAL, "exchange table too large");
+    std::copy(tab.begin(), tab.end(), h_tab);
+    HIP_TRY(c, hipMemcpyAsync(d_tab, h_tab, tab.size() * 8, hipMemcpyHostToDevice, c->stream));
+    const uint64_t *d_rng = d_tab, *d_moff = d_tab + rng.size();
+    t = tic(c);
+    HIP_TRY(c, launch_meta_counts(gb, d_rng, (int)(rng.size() / 5), meta_s, c->stream));
+    toc(c, PH_PLACE, t);
+    std::vector<size_t> sc(P, 0), sd(P, 0), rc(P, 0), rd(P, 0);
+    {
+        uint64_t mo = 0, ro = 0;
+        for (int q = 0; q < P; ++q) {
+            if (send[q]) { sc[q] = nh[q] * 4; sd[q] = mo * 4; mo += nh[q]; }
+            if (recv[q]) { rc[q] = nh[me] * 4; rd[q] = ro * 4; ro += nh[me]; }
+        }
+        if (meta_in_place) sc[me] = rc[me] = 0;
+    }
+    std::vector<uint64_t> roffs(P + 1, 0);
+    for (int p = 0; p < P; ++p) roffs[p + 1] = roffs[p] + recv[p];
+    t = tic_rec(c);
+    ST_TRY(comm_try(c, c->comm->alltoallv(meta_s, sc.data(), sd.data(), meta_r, rc.data(),
+                                          rd.data(), c->stream)));
+    toc_rec(c, PH_EXCH, t);
+    for (int q = 0; q < P; ++q)
+        if (stats && q != me) {
+            stats->bytes_sent += send[q] * 2;
+            stats->max_pair_bytes = std::max<uint64_t>(stats->max_pair_bytes, send[q] * 2);
+        }
+    if (roffs[P] != mine) return set_err(c, GSORT_EINVAL, "exchange plan does not fill the block");
+    // the payload, queued right behind the counts: the receive plan below overlaps it.  The
+    // rank's own piece is not moved at all: the receive kernels read it where it lies in the
+    // send buffer (its run offset below is taken relative to rbuf, mod 2^64) -- at P = 1 that is
+    // the whole 512 MiB of a 2^28-key block, at P = 8 an eighth of it
+    uint16_t *rbuf = slot_ptr<uint16_t>(c, S_RECV);
+    t = tic_rec(c);
+    for (int q = 0; q < P; ++q) {
+        const bool self = q == me && !self_moved;
+        sc[q] = self ? 0 : send[q] * 2;
+        sd[q] = cut[q] * 2;
+        rc[q] = self ? 0 : recv[q] * 2;
+        rd[q] = roffs[q] * 2;
+    }
+    ST_TRY(comm_try(c, c->comm->alltoallv(pack, sc.data(), sd.data(), rbuf, rc.data(), rd.data(),
+                                          c->stream)));
+    toc_rec(c, PH_EXCH, t);
+    if (stats) stats->exchanges = 1;
+    // (5) the receive plan from the counts alone: run bounds, bucket starts, the K11g / K18
+    // work lists of this rank's bucket range
+    t = tic(c);
+    ST_TRY(ensure(c, c->m_rpos, (size_t)P * (kBuckets16 + 1) * 8));
+    ST_TRY(ensure(c, c->m_bsize, kBsizeBytes));
+    ST_TRY(ensure_list(c, c->m_next[0], kBuckets16));
+    for (auto &b : c->m_local) ST_TRY(ensure_list(c, b, kBuckets16));
+    uint64_t *pos = reinterpret_cast<uint64_t *>(c->m_rpos.p);
+    uint64_t *bsize = reinterpret_cast<uint64_t *>(c->m_bsize.p), *bstart = bsize + kBuckets16;
+    uint64_t *h_r = reinterpret_cast<uint64_t *>(c->h_small + OFF_PLAN);
+    uint64_t *d_r = reinterpret_cast<uint64_t *>(c->d_small + OFF_PLAN);
+    // (no stream sync for h_r: nothing has copied from OFF_PLAN since allgather_u64's sync --
+    // the select stages through host vectors -- and a sync here idled the GPU ~40 us)
+    for (int p = 0; p < P; ++p) { h_r[p] = roffs[p]; h_r[P + p] = recv[p]; }
+    if (!self_moved)  // the self piece, in place: its offset from rbuf in keys, from integer
+        h_r[me] = elem_offset(pack + cut[me], rbuf);  // addresses (mod 2^64, run_ptr)
+    HIP_TRY(c, hipMemcpyAsync(d_r, h_r, (size_t)2 * P * 8, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemsetAsync(c->d_small + OFF_CTR, 0, kCtrBytes, c->stream));
+    // the runs' bucket bounds and the bucket starts in one row scan of P + 1 rows (the last
+    // row is every bucket's total over the sources); classify reads the sizes off bstart
+    HIP_TRY(c, launch_recv_plan_from_meta(meta_r, d_moff, (uint32_t)hlo[me], (uint32_t)nh[me], P,
+                                          pos, bstart, bstart + kBuckets16 + 1, c->stream));
+    const WorkLists wl = work_lists(c, 0);
+    HIP_TRY(c, launch_classify_range(nullptr, bstart, wl, (uint32_t)hlo[me],
+                                     (uint32_t)(hlo[me] + nh[me]), c->stream));
+    toc(c, PH_COUNT, t);
+    uint64_t h[3 * (kLocalClasses + 1)];
+    ST_TRY(read_counters(c, h));
+    if (check_mode()) {
+        for (int p = 0; p < P; ++p)
+            ST_TRY(check_bounds(c, pos + (size_t)p * (kBuckets16 + 1), kBuckets16 + 1, recv[p],
+                                "received run bounds"));
+        uint64_t keys = 0;
+        for (int l = 0; l <= kLocalClasses; ++l) keys += h[3 * l + 1];
+        if (keys != mine)
+            return set_err(c, GSORT_EINVAL, "GSORT_CHECK receive lists hold " +
+                                                std::to_string(keys) + " keys, want " +
+                                                std::to_string(mine) + " (rank " +
+                                                std::to_string(me) + ")");
+    }
+    // (6) every bucket sorted from its P pieces: K11g by size class, K18 past kLocalMax; a
+    // bucket past K18's reach sends the block through recv_sort's MSD levels 1 and 0
+    t = tic(c);
+    uint32_t *out = slot_ptr<uint32_t>(c, S_OUT);
+    if (h[0] && h[2] > kHxMax) {  // recv_sort wants the P runs back to back in rbuf
+        if (recv[me] && !self_moved)
+            HIP_TRY(c, hipMemcpyAsync(rbuf + roffs[me], pack + cut[me], recv[me] * 2,
+                                      hipMemcpyDeviceToDevice, c->stream));
+        ST_TRY(recv_sort(c, rbuf, true, recv, mine, out, slot_ptr<uint32_t>(c, S_TMP), stats));
+    } else {
+        ST_TRY(sort_recv_lists(c, rbuf, true, pos, d_r, P, bstart, wl, h, out, stats));
+    }
+    toc(c, PH_MERGE, t);
+    if (stats) stats->passes_run = pr;
+    *d_out = slot_ptr<int32_t>(c, S_OUT);
+    *n_out = mine;
+    return GSORT_OK;
+}
+
+// ---- distributed LSD radix (P > 1, GSORT_LOCAL_LSD) ----------------------------------------
+// Per non-trivial digit: local K1/K2 (tile counts; the digit totals of this rank), all-gather
+// of the P x 256 per-rank digit counts, local K3 (stable by digit), route contiguous slices to
+// the ranks owning their global positions (one grouped send/recv round), then place the
+// received runs (K8).  Keeps the reference's invariant that rank q holds positions
+// [qB, (q+1)B) after each pass (mpi_radix_sort.c:139,:192) without moving keys through rank 0.
+// sort_keys != nullptr (the reference-compat sort): the passes sort the u32 keys sort_keys[i]
+// (never flipped) stably and d_keys[i] travels with them as the value; the output is the
+// values.  Keys and values go through the same exchange and placement, so the order is
+// (key, source rank, source order), the reference's per-pass order (mpi_radix_sort.c:164-192).
+gsort_status radix_dist(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in, int32_t **d_out,
+                        uint64_t *n_out, gsort_stats *stats, const uint32_t *sort_keys) {
+    const int P = c->nranks, me = c->rank;
+    const bool kv = sort_keys != nullptr, fl = !kv;
+    std::vector<uint64_t> n_all;
+    ST_TRY(allgather_u64(c, n_in, n_all));
+    uint64_t N = 0;
+    for (uint64_t v : n_all) N += v;
+    uint64_t B, mine;
+    block_of(N, P, me, &B, &mine);
+    const uint64_t cap = std::max<uint64_t>(std::max(n_in, B), 1);
+    for (Slot s : {S_CUR, S_SORTED, S_RECV, S_OUT}) ST_TRY(ensure(c, c->slot[s], cap * 4));
+    if (kv)
+        for (DevBuf *b : {&c->slot[S_TMP], &c->m_vtmp[0], &c->m_vtmp[1], &c->m_vtmp[2]})
+            ST_TRY(ensure(c, *b, cap * 4));
+    ST_TRY(ensure_pass_scratch(c, cap));
+    if (N == 0) { *d_out = slot_ptr<int32_t>(c, S_OUT); *n_out = 0; return GSORT_OK; }
+
+    // K1 on the input: tile counts of digit 0 + all four digit histograms; all-gathered they
+    // give the global digit totals (invariant under the exchange), so every rank skips the
+    // same trivial digits.
+    uint64_t *d_hist = reinterpret_cast<uint64_t *>(c->d_small + OFF_HIST);
+    uint64_t *d_tot = reinterpret_cast<uint64_t *>(c->d_small + OFF_TOT);
+    const uint32_t *src = kv ? sort_keys : reinterpret_cast<const uint32_t *>(d_keys);
+    HIP_TRY(c, hipMemsetAsync(d_hist, 0, 4 * kRadix * 8, c->stream));
+    hipEvent_t t = tic(c);
+    HIP_TRY(c, launch_tile_counts(src, n_in, 0, fl, d_tcounts(c), d_hist, c->stream));
+    toc(c, PH_COUNT, t);
+    DevBuf &allh = c->slot[S_STAGE];
+    ST_TRY(ensure(c, allh, (size_t)P * 4 * kRadix * 8));
+    ST_TRY(comm_try(c, c->comm->allgather(d_hist, allh.p, 4 * kRadix * 8, c->stream)));
+    std::vector<uint64_t> H((size_t)P * 4 * kRadix);
+    HIP_TRY(c, hipMemcpyAsync(H.data(), allh.p, H.size() * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    std::vector<int> active;
+    for (int p = 0; p < 4; ++p) {
+        uint64_t mx = 0;
+        for (int d = 0; d < kRadix; ++d) {
+            uint64_t tot = 0;
+            for (int r = 0; r < P; ++r) tot += H[((size_t)r * 4 + p) * kRadix + d];
+            mx = std::max(mx, tot);
+        }
+        if (mx < N) active.push_back(p);
+    }
+    if (active.empty()) active.push_back(0);  // still redistribute to balanced blocks
+
+    std::vector<uint64_t> hp((size_t)P * kRadix), send(P), recv(P), seg((size_t)4 * P * kRadix);
+    std::vector<size_t> sc(P), sd(P), rc(P), rd(P);
+    uint64_t n_src = n_in;
+    uint32_t *placed[2] = {slot_ptr<uint32_t>(c, S_CUR), slot_ptr<uint32_t>(c, kv ? S_TMP : S_OUT)};
+    // kv: the values' source, sorted / received copies and placed blocks (the last into S_OUT)
+    const uint32_t *vsrc = reinterpret_cast<const uint32_t *>(d_keys);
+    uint32_t *vsorted = reinterpret_cast<uint32_t *>(c->m_vtmp[0].p);
+    uint32_t *vrecv = reinterpret_cast<uint32_t *>(c->m_vtmp[1].p);
+    uint32_t *vplaced = reinterpret_cast<uint32_t *>(c->m_vtmp[2].p);
+    const int k = (int)active.size();
+    for (int i = 0; i < k; ++i) {
+        const int p = active[i];
+        const bool first = i == 0, last = i == k - 1;
+        // this rank's tile counts and totals of digit p, then everyone's totals
+        if (!(first && p == 0)) ST_TRY(count_tiles(c, src, n_src, p, first && fl));
+        uint32_t *sorted = slot_ptr<uint32_t>(c, S_SORTED);
+        ST_TRY(scan_and_scatter(c, src, sorted, n_src, p, first && fl, false, kv ? vsrc : nullptr,
+                                kv ? vsorted : nullptr));
+        if (n_src == 0) HIP_TRY(c, hipMemsetAsync(d_tot, 0, kRadix * 8, c->stream));
+        uint64_t *d_allt = reinterpret_cast<uint64_t *>(allh.p);
+        ST_TRY(comm_try(c, c->comm->allgather(d_tot, d_allt, kRadix * 8, c->stream)));
+        HIP_TRY(c, hipMemcpyAsync(hp.data(), d_allt, hp.size() * 8, hipMemcpyDeviceToHost,
+                                  c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+
+        size_t nseg = 0;
+        ST_TRY(gsort_plan_radix_route(P, hp.data(), B, me, send.data(), recv.data(), seg.data(),
+                                      &nseg));
+        size_t so = 0, ro = 0;
+        for (int q = 0; q < P; ++q) {
+            sc[q] = send[q] * 4; sd[q] = so; so += sc[q];
+            rc[q] = recv[q] * 4; rd[q] = ro; ro += rc[q];
+            if (stats && q != me) {
+                stats->bytes_sent += sc[q] * (kv ? 2 : 1);
+                stats->max_pair_bytes = std::max<uint64_t>(stats->max_pair_bytes, sc[q]);
+            }
+        }
+        uint32_t *rbuf = slot_ptr<uint32_t>(c, S_RECV);
+        t = tic_rec(c);
+        ST_TRY(comm_try(c, c->comm->alltoallv(sorted, sc.data(), sd.data(), rbuf, rc.data(),
+                                              rd.data(), c->stream)));
+        if (kv)
+            ST_TRY(comm_try(c, c->comm->alltoallv(vsorted, sc.data(), sd.data(), vrecv,
+                                                  rc.data(), rd.data(), c->stream)));
+        toc_rec(c, PH_EXCH, t);
+        if (stats) stats->exchanges++;
+        // placement table: {offset in recv buffer, dest offset, length}
+        uint64_t *h_seg = reinterpret_cast<uint64_t *>(c->h_small + OFF_PLAN);
+        uint64_t *d_seg = reinterpret_cast<uint64_t *>(c->d_small + OFF_PLAN);
+        if (nseg * 24 > kSmallBytes - OFF_PLAN) return set_err(c, GSORT_EINVAL, "segment table");
+        HIP_TRY(c, hipStreamSynchronize(c->stream));  // h_seg may still feed an earlier copy
+        for (size_t s = 0; s < nseg; ++s) {
+            const uint64_t r = seg[4 * s];
+            h_seg[3 * s + 0] = rd[r] / 4 + seg[4 * s + 1];
+            h_seg[3 * s + 1] = seg[4 * s + 2];
+            h_seg[3 * s + 2] = seg[4 * s + 3];
+        }
+        HIP_TRY(c, hipMemcpyAsync(d_seg, h_seg, nseg * 24, hipMemcpyHostToDevice, c->stream));
+        uint32_t *dst = last && !kv ? slot_ptr<uint32_t>(c, S_OUT) : placed[i & 1];
+        t = tic(c);
+        if (!(kv && last))  // kv: the keys of the last pass are not needed
+            HIP_TRY(c, launch_place(rbuf, dst, d_seg, (int)nseg, mine, nullptr, 0, last && fl,
+                                    c->stream));
+        if (kv) {
+            uint32_t *vdst = last ? slot_ptr<uint32_t>(c, S_OUT) : vplaced;
+            HIP_TRY(c, launch_place(vrecv, vdst, d_seg, (int)nseg, mine, nullptr, 0, false,
+                                    c->stream));
+            vsrc = vdst;
+        }
+        toc(c, PH_PLACE, t);
+        src = dst;
+        n_src = mine;
+    }
+    if (stats) stats->passes_run = k;
+    *d_out = slot_ptr<int32_t>(c, S_OUT);
+    *n_out = mine;
+    return GSORT_OK;
+}
+
+// ---- reference-compat radix (gsort_set_ref_compat) -----------------------
+// The reference's radix sort is a stable sort of the values by the base-P digits of |v| that
+// number_digit_at extracts (mpi_radix_sort.c:54-58), loop = number_digits(max) of them (:100).
+// K20 + an all-gather give the global min / max, gsort_plan_ref_digits the reference's digit
+// plan, K19 the composite key of every value; then stable key-value LSD passes: locally, or
+// through radix_dist's exchange (kv), so rank q ends with positions [qB, (q+1)B).
+gsort_status radix_compat(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in, int32_t **d_out,
+                          uint64_t *n_out, gsort_stats *stats) {
+    const int Pref = c->ref_compat > 0 ? c->ref_compat : c->nranks;
+    std::vector<uint64_t> n_all;
+    ST_TRY(allgather_u64(c, n_in, n_all));
+    uint64_t N = 0;
+    for (uint64_t v : n_all) N += v;
+    const uint64_t Bref = (N + Pref - 1) / Pref;
+    if (N > 0 && (int64_t)N - (int64_t)(Bref * (uint64_t)(Pref - 1)) <= 0)
+        return set_err(c, GSORT_EINVAL, "ref compat: the reference's last block would be empty "
+                                        "(N < (P-1)*ceil(N/P) + 1, quirk Q8)");
+    const size_t cap = std::max<uint64_t>(n_in, 1) * 4;
+    ST_TRY(ensure(c, c->m_cmm, 16));
+    ST_TRY(ensure(c, c->m_ckey[0], cap));
+    // global min / max (K20)
+    int32_t *h_mm = reinterpret_cast<int32_t *>(c->h_small + OFF_PLAN);
+    HIP_TRY(c, hipStreamSynchronize(c->stream));  // h_small may feed an earlier copy
+    h_mm[0] = INT32_MAX;
+    h_mm[1] = INT32_MIN;
+    memset(h_mm + 2, 0, 8);  // K19's bad-key counter
+    HIP_TRY(c, hipMemcpyAsync(c->m_cmm.p, h_mm, 16, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, launch_minmax(d_keys, n_in, reinterpret_cast<int *>(c->m_cmm.p), c->stream));
+    HIP_TRY(c, hipMemcpyAsync(h_mm, c->m_cmm.p, 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    std::vector<uint64_t> mm;
+    ST_TRY(allgather_u64(c, (uint64_t)(uint32_t)h_mm[0] | ((uint64_t)(uint32_t)h_mm[1] << 32), mm));
+    int32_t gmin = INT32_MAX, gmax = -1;  // the reference's max_element starts at -1 (:77)
+    for (int r = 0; r < c->nranks; ++r) {
+        if (!n_all[r]) continue;
+        gmin = std::min(gmin, (int32_t)(uint32_t)mm[r]);
+        gmax = std::max(gmax, (int32_t)(uint32_t)(mm[r] >> 32));
+    }
+    if (N > 0 && gmin == INT32_MIN)
+        return set_err(c, GSORT_EINVAL, "ref compat: an INT_MIN key has no |v|; the reference "
+                                        "indexes a negative bucket there (quirk Q5)");
+    int loop = 0;
+    int32_t mod[64];
+    double scale[64];
+    if (gsort_plan_ref_digits(Pref, gmax, &loop, mod, scale, 64) != GSORT_OK)
+        return set_err(c, GSORT_EINVAL, "ref compat: digit plan");
+    uint32_t *key = reinterpret_cast<uint32_t *>(c->m_ckey[0].p);
+    if (loop < 1) {  // no pass (P = 1, Q1): the input order, only redistributed
+        HIP_TRY(c, hipMemsetAsync(key, 0, cap, c->stream));
+    } else {
+        HIP_TRY(c, launch_compat_keys(d_keys, n_in, Pref, loop, mod, scale, key,
+                                      reinterpret_cast<uint64_t *>(c->m_cmm.p) + 1, c->stream));
+        uint64_t *h_bad = reinterpret_cast<uint64_t *>(c->h_small + OFF_PLAN);
+        HIP_TRY(c, hipMemcpyAsync(h_bad, reinterpret_cast<uint64_t *>(c->m_cmm.p) + 1, 8,
+                                  hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        std::vector<uint64_t> bad;
+        ST_TRY(allgather_u64(c, *h_bad, bad));
+        for (uint64_t b : bad)
+            if (b) return set_err(c, GSORT_EINVAL, "ref compat: a digit outside [0, P) (the "
+                                                   "reference indexes outside its buckets)");
+    }
+    if (c->comm) return radix_dist(c, d_keys, n_in, d_out, n_out, stats, key);
+    // one rank: the stable key-value LSD passes locally (K1 + four histograms, K2, K3 kv)
+    ST_TRY(ensure(c, c->slot[S_OUT], cap));
+    ST_TRY(ensure(c, c->m_ckey[1], cap));
+    ST_TRY(ensure(c, c->m_vtmp[0], cap));
+    ST_TRY(ensure(c, c->m_vtmp[1], cap));
+    ST_TRY(ensure_pass_scratch(c, n_in));
+    *d_out = slot_ptr<int32_t>(c, S_OUT);
+    *n_out = n_in;
+    if (n_in == 0) return GSORT_OK;
+    uint64_t *d_hist = reinterpret_cast<uint64_t *>(c->d_small + OFF_HIST);
+    uint64_t *h_hist = reinterpret_cast<uint64_t *>(c->h_small + OFF_HIST);
+    HIP_TRY(c, hipMemsetAsync(d_hist, 0, 4 * kRadix * 8, c->stream));
+    hipEvent_t t = tic(c);
+    HIP_TRY(c, launch_tile_counts(key, n_in, 0, false, d_tcounts(c), d_hist, c->stream));
+    toc(c, PH_COUNT, t);
+    HIP_TRY(c, hipMemcpyAsync(h_hist, d_hist, 4 * kRadix * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    std::vector<int> active;
+    for (int p = 0; p < 4; ++p) {
+        const uint64_t *h = h_hist + p * kRadix;
+        if (*std::max_element(h, h + kRadix) < n_in) active.push_back(p);
+    }
+    if (active.empty()) {
+        HIP_TRY(c, launch_copy(reinterpret_cast<const uint32_t *>(d_keys),
+                               slot_ptr<uint32_t>(c, S_OUT), n_in, c->stream));
+        return GSORT_OK;
+    }
+    uint32_t *kb[2] = {key, reinterpret_cast<uint32_t *>(c->m_ckey[1].p)};
+    uint32_t *vb[2] = {reinterpret_cast<uint32_t *>(c->m_vtmp[0].p),
+                       reinterpret_cast<uint32_t *>(c->m_vtmp[1].p)};
+    const uint32_t *vsrc = reinterpret_cast<const uint32_t *>(d_keys);
+    const int k = (int)active.size();
+    for (int i = 0; i < k; ++i) {
+        const bool last = i == k - 1;
+        uint32_t *vdst = last ? slot_ptr<uint32_t>(c, S_OUT) : vb[i & 1];
+        if (!(i == 0 && active[0] == 0)) ST_TRY(count_tiles(c, kb[i & 1], n_in, active[i], false));
+        ST_TRY(scan_and_scatter(c, kb[i & 1], kb[(i & 1) ^ 1], n_in, active[i], false, false, vsrc,
+                                vdst));
+        vsrc = vdst;
+    }
+    if (stats) stats->passes_run = k;
+    return GSORT_OK;
+}
+
+// ---- sample sort ------------------------------------------------------------------------
+gsort_status sample_dist(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in, int32_t **d_out,
+                         uint64_t *n_out, gsort_stats *stats) {
+    const int P = c->nranks, me = c->rank;
+    std::vector<uint64_t> n_all;
+    ST_TRY(allgather_u64(c, n_in, n_all));
+    uint64_t N = 0;
+    for (uint64_t v : n_all) N += v;
+    // mpi_sample_sort.c:72 size_bucket = ceil(N/P); :89-90 k = 2P-1, interval = B / k
+    const uint64_t B = (N + P - 1) / P;
+    const int k = 2 * P - 1;
+    const uint64_t interval = B / k;
+    if (P * k > 1024) return set_err(c, GSORT_EINVAL, "too many ranks for sample sort");
+    for (int r = 0; r < P; ++r)  // :94-99, decided identically on every rank
+        if ((uint64_t)(k - 1) * interval >= n_all[r])
+            return set_err(c, GSORT_ENOSAMPLE,
+                           "no enough sample: rank " + std::to_string(r) + " holds " +
+                               std::to_string(n_all[r]) + " keys, needs index " +
+                               std::to_string((uint64_t)(k - 1) * interval));
+    const uint64_t cap = std::max<uint64_t>(n_in, 1);
+    ST_TRY(ensure(c, c->slot[S_SORTED], cap * 4));
+    int32_t *sorted = slot_ptr<int32_t>(c, S_SORTED);
+    int pr = 0;
+    ST_TRY(local_sort(c, reinterpret_cast<const uint32_t *>(d_keys), n_in,
+                      reinterpret_cast<uint32_t *>(sorted), nullptr, &pr, nullptr, true));
+
+    // K4 samples -> root (grouped send/recv), K5 on root, broadcast splitters
+    hipEvent_t t = tic_rec(c);
+    int32_t *d_samp = reinterpret_cast<int32_t *>(c->d_small + OFF_PLAN);
+    int32_t *d_all = d_samp + 64;
+    int32_t *d_spl = d_all + 1024 + 64;
+    uint64_t *d_bounds = reinterpret_cast<uint64_t *>(d_spl + 64);
+    HIP_TRY(c, launch_regular_sample(sorted, interval, k, d_samp, c->stream));
+    std::vector<size_t> sc(P, 0), sd(P, 0), rc(P, 0), rd(P, 0);
+    sc[0] = (size_t)k * 4;
+    if (me == 0)
+        for (int r = 0; r < P; ++r) { rc[r] = (size_t)k * 4; rd[r] = (size_t)r * k * 4; }
+    ST_TRY(comm_try(c, c->comm->alltoallv(d_samp, sc.data(), sd.data(), d_all, rc.data(),
+                                          rd.data(), c->stream)));
+    if (me == 0) HIP_TRY(c, launch_select_splitters(d_all, P * k, k, P - 1, d_spl, c->stream));
+    ST_TRY(comm_try(c, c->comm->bcast(d_spl, (size_t)(P - 1) * 4, 0, c->stream)));
+    HIP_TRY(c, launch_bucket_bounds(sorted, n_in, d_spl, P - 1, d_bounds, c->stream));
+    toc_rec(c, PH_SAMPLE, t);
+    int32_t *h_spl = reinterpret_cast<int32_t *>(c->h_small + OFF_PLAN);
+    uint64_t *h_bounds = reinterpret_cast<uint64_t *>(c->h_small + OFF_PLAN + 1024);
+    HIP_TRY(c, hipMemcpyAsync(h_spl, d_spl, (size_t)(P - 1) * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(h_bounds, d_bounds, (size_t)(P - 1) * 8, hipMemcpyDeviceToHost,
+                              c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    c->splitters.assign(h_spl, h_spl + P - 1);
+    c->bucket_counts.assign(P, 0);
+    uint64_t prev = 0;
+    for (int j = 0; j < P; ++j) {
+        const uint64_t end = j < P - 1 ? h_bounds[j] : n_in;
+        c->bucket_counts[j] = end - prev;
+        prev = end;
+    }
+    // bucket-count matrix: allgather P counts per rank (mpi_sample_sort.c:161,:168 sends the
+    // length in the MPI tag of a fixed-size message; here exact lengths size the messages)
+    uint64_t *d_cnt = reinterpret_cast<uint64_t *>(c->d_small + OFF_PLAN + 16384);
+    uint64_t *d_mat = d_cnt + 64;
+    uint64_t *h_cnt = reinterpret_cast<uint64_t *>(c->h_small + OFF_PLAN + 16384);
+    std::vector<uint64_t> M((size_t)P * P);
+    if (!c->sample_balanced) {
+        memcpy(h_cnt, c->bucket_counts.data(), (size_t)P * 8);
+        HIP_TRY(c, hipMemcpyAsync(d_cnt, h_cnt, (size_t)P * 8, hipMemcpyHostToDevice, c->stream));
+        ST_TRY(comm_try(c, c->comm->allgather(d_cnt, d_mat, (size_t)P * 8, c->stream)));
+        HIP_TRY(c, hipMemcpyAsync(M.data(), d_mat, M.size() * 8, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+    } else {
+        // duplicate-aware buckets: keys < s_j (strict K6) and <= s_j of every rank, then the
+        // same cut rule as the distributed radix with the boundary clamped into s_j's copies
+        const int S = P - 1;
+        uint64_t *d_lt = d_bounds + 64;
+        HIP_TRY(c, launch_bucket_bounds(sorted, n_in, d_spl, S, d_lt, c->stream, true));
+        uint64_t *d_ll = d_cnt;  // this rank: [lt x S | le x S]
+        HIP_TRY(c, hipMemcpyAsync(d_ll, d_lt, (size_t)S * 8, hipMemcpyDeviceToDevice, c->stream));
+        HIP_TRY(c, hipMemcpyAsync(d_ll + S, d_bounds, (size_t)S * 8, hipMemcpyDeviceToDevice,
+                                  c->stream));
+        uint64_t *d_all2 = d_cnt + 64;
+        ST_TRY(comm_try(c, c->comm->allgather(d_ll, d_all2, (size_t)2 * S * 8, c->stream)));
+        std::vector<uint64_t> A((size_t)P * 2 * S), lt((size_t)P * S), le((size_t)P * S);
+        HIP_TRY(c, hipMemcpyAsync(A.data(), d_all2, A.size() * 8, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        for (int p = 0; p < P; ++p)
+            for (int j = 0; j < S; ++j) {
+                lt[(size_t)p * S + j] = A[(size_t)p * 2 * S + j];
+                le[(size_t)p * S + j] = A[(size_t)p * 2 * S + S + j];
+            }
+        // every rank plans every rank's row (host, identical inputs) -> the full matrix
+        std::vector<uint64_t> snd(P), rcv(P);
+        for (int p = 0; p < P; ++p) {
+            const gsort_status st =
+                gsort_plan_split_balanced(P, n_all.data(), lt.data(), le.data(), p, snd.data(),
+                                          rcv.data());
+            if (st != GSORT_OK) return set_err(c, st, "inconsistent sample bucket bounds");
+            for (int q = 0; q < P; ++q) M[(size_t)p * P + q] = snd[q];
+        }
+        for (int q = 0; q < P; ++q) c->bucket_counts[q] = M[(size_t)me * P + q];
+    }
+    uint64_t total = 0;
+    size_t so = 0, ro = 0;
+    for (int q = 0; q < P; ++q) {
+        sc[q] = c->bucket_counts[q] * 4; sd[q] = so; so += sc[q];
+        rc[q] = M[(size_t)q * P + me] * 4; rd[q] = ro; ro += rc[q];
+        total += M[(size_t)q * P + me];
+        if (stats && q != me) {
+            stats->bytes_sent += sc[q];
+            stats->max_pair_bytes = std::max<uint64_t>(stats->max_pair_bytes, sc[q]);
+        }
+    }
+    const uint64_t cap2 = std::max<uint64_t>(total, 1);
+    ST_TRY(ensure(c, c->slot[S_RECV], cap2 * 4));
+    ST_TRY(ensure(c, c->slot[S_OUT], cap2 * 4));
+    ST_TRY(ensure(c, c->slot[S_TMP], cap2 * 4));
+    int32_t *rbuf = slot_ptr<int32_t>(c, S_RECV);
+    // the rank's own bucket stays where it is (recv_sort reads it in place)
+    const size_t self_off = sd[me];
+    sc[me] = 0;
+    rc[me] = 0;
+    t = tic_rec(c);
+    ST_TRY(comm_try(c, c->comm->alltoallv(sorted, sc.data(), sd.data(), rbuf, rc.data(),
+                                          rd.data(), c->stream)));
+    toc_rec(c, PH_EXCH, t);
+    if (stats) stats->exchanges = 1;
+    // final local order of the received bucket (mpi_sample_sort.c:174): the P received runs
+    // are sorted slices of the senders' sorted blocks -> recv_sort
+    std::vector<uint64_t> rlen(P);
+    for (int q = 0; q < P; ++q) rlen[q] = M[(size_t)q * P + me];
+    t = tic(c);
+    ST_TRY(recv_sort(c, rbuf, false, rlen, total, slot_ptr<uint32_t>(c, S_OUT),
+                     slot_ptr<uint32_t>(c, S_TMP), stats, me, sorted + self_off / 4));
+    toc(c, PH_MERGE, t);
+    if (stats) stats->passes_run = pr;
+    *d_out = slot_ptr<int32_t>(c, S_OUT);
+    *n_out = total;
+    return GSORT_OK;
+}
+
+
+// The sort writes its scratch slots; an input living in one of them would be overwritten.
+}  // namespace rt
+}  // namespace gsort

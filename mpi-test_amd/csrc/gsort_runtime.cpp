@@ -1,143 +1,14 @@
-// gsort_runtime.cpp -- the C-ABI of libgsort (include/gsort.h): contexts, the local sort,
-// the distributed radix and sample sort orchestration, and drop-in staging.
+// gsort_runtime.cpp -- the C-ABI of libgsort (include/gsort.h): contexts, device memory,
+// timing, diagnostics and drop-in staging; the sorts themselves are in gsort_local.cpp (one
+// rank) and gsort_dist.cpp (P ranks), sharing the context through gsort_ctx.h.
 //
 // Reference being replaced: sort() of mpi_radix_sort.c:60-205 and mpi_sample_sort.c:28-218.
 // Data stays resident on each rank's GPU for the whole sort; the host only moves per-pass
 // digit counts (a few KB) to size the RCCL messages, which need host-side counts.
-#include <hip/hip_runtime.h>
-#include <stdint.h>
-#include <stdio.h>
-#include <stdlib.h>
-#include <string.h>
+#include "gsort_ctx.h"
 
-#include <algorithm>
-#include <cmath>
-#include <atomic>
-#include <chrono>
-#include <map>
-#include <mutex>
-#include <set>
-#include <string>
-#include <thread>
-#include <vector>
-
-#include "gsort.h"
-#include "gsort_comm.h"
-#include "gsort_debug.h"
-#include "gsort_kernels.h"
-
-using namespace gsort;
-
-struct gsort_group {
-    GroupState *st;
-};
-
-namespace {
-
-enum Slot { S_TMP, S_OUT, S_CUR, S_SORTED, S_RECV, S_IN, S_STAGE, S_NSLOTS };
-enum Phase { PH_COUNT, PH_PASS0, PH_PASS1, PH_PASS2, PH_PASS3, PH_EXCH, PH_PLACE, PH_SAMPLE,
-             PH_MERGE, PH_TOTAL, PH_LEVEL3, PH_LEVEL2, PH_LEVEL1, PH_LEVEL0, PH_BUCKET, PH_N };
-
-constexpr size_t kSmallBytes = 256 * 1024;  // device + pinned scratch for counts, plans
-constexpr size_t kMailBytes = 4096;          // K12p mailbox: flag, then the counters (u64)
-
-struct DevBuf {
-    void *p = nullptr;     // what the kernels use
-    size_t cap = 0;        // usable bytes at p
-    void *base = nullptr;  // the allocation (p - kGuardBytes with GSORT_CANARY)
-    // GSORT_EFENCE: the reserved VA range [base, base + va_bytes) and its physical handle
-    size_t va_bytes = 0, map_bytes = 0;
-    hipMemGenericAllocationHandle_t handle{};
-};
-
-}  // namespace
-
-struct gsort_ctx {
-    int rank = 0, nranks = 1, device = 0;
-    hipStream_t stream = nullptr;
-    Comm *comm = nullptr;
-    std::string err;
-    DevBuf slot[S_NSLOTS];
-    DevBuf tcounts;  // K1/K2: per-tile digit counts -> in-group offsets (u32 [tiles][256])
-    DevBuf gsum;     // K2: per-group digit prefixes (u64 [groups][256])
-    int local_algo = GSORT_LOCAL_MSD;
-    bool sample_balanced = false;  // gsort_set_sample_balanced
-    int ref_compat = 0;            // gsort_set_ref_compat: 0 off, -1 P = nranks, else P
-    // reference-compat radix: composite keys (two), values in flight, min/max + bad counter
-    DevBuf m_ckey[2], m_vtmp[3], m_cmm;
-    bool atomic_rank = false;  // LDS lane-order property verified on this device (create)
-    // MSD scratch: segment plan/maps, child starts, work lists (u64 {start, len} pairs)
-    DevBuf m_tpfx, m_gpfx, m_segmap, m_groupmap, m_cstart, m_next[2], m_local[kLocalClasses];
-    uint64_t group16_nseg = 0;  // msd_sort(group16): level-2 segments (list m_next[0])
-    // two-level plan front end (K1h / K12h / K3a): 16-bit histogram partials, wrap repairs,
-    // level-2 cursors, K11 lists of the level-3 buckets; counters read while levels 3/2 run
-    bool plan16 = true;
-    DevBuf m_part, m_fix, m_cur, m_local3[kLocalClasses];
-    DevBuf m_ccount, m_t3, m_cur3;  // K12a child counts, per-shard level-3 counts + totals, K3r cursors
-    DevBuf m_tdesc;                 // K12c: K3a tile descriptors
-    // sampled plan (K1e .. K11e): level-3 / level-2 region buffers, sample partials, plan
-    // arrays, K3a tile descriptors, overflow scratch tile
-    bool plan_est = true;   // GSORT_EST (default 1)
-    bool plan_giant = true; // GSORT_GIANT (default 1): the one-dominant-child path
-    double est_slack = 1.0; // GSORT_EST_SLACK (test hook: the sampling-error margin's scale)
-    // GSORT_RECV_CX: receive buckets of K11g class >= recv_cx (1..4) and list 0 are counted by
-    // K18c (default 4: buckets past 16 384 keys -- per 2^28 keys, 16 384-key buckets K11g
-    // 0.72 / K18c 0.85 ms, 32 768-key K11g 1.01 / K18c 0.58 ms, tools/recv_probe.py); 5 = list
-    // 0 only; -1 = the round-2 kernels (K11g classes, two-read K18)
-    int recv_cx = 4;
-    // GSORT_RECV_CB: K18c's bin width on the receive side, 8 (default since round 5: 64 KiB of
-    // bins, two workgroups per CU; a bucket with >= 256 copies of one key redone with 16-bit
-    // bins) or 16
-    int recv_cb = 8;
-    DevBuf m_fb;  // K18c (u8): the wrapped buckets' {h, len} entries
-    int ncu = 256;
-    int last_plan = 0;      // gsort_last_plan: 0 exact, 1 sampled, 2 sampled then exact
-    bool plan_trace = false; // GSORT_PLAN_TRACE: one stderr line per plan decision
-    DevBuf m_ex, m_ey, m_epart, m_eplan, m_edesc, m_edump;
-    DevBuf m_gplan;  // one dominant child: counts (65536 u64), starts (65537 u64), chunk bins
-    bool est_busy = false;   // msd_sort_est is using m_ex / m_ey (not reclaimable)
-    size_t scratch_bytes = 0;  // device bytes held by ensure()-managed scratch
-    // K12p mailbox: pinned host memory the GPU writes the work-list counters into, then a
-    // sequence number (polled by the host: no copy or event on the stream)
-    uint64_t *h_mail = nullptr, *d_mail = nullptr;
-    uint64_t mail_seq = 0;
-    void *fix_clean = nullptr;  // m_fix.p when it is known to be zero (K12a clears it after use)
-    DevBuf m_split;  // radix select thresholds + counts of the distributed radix
-    DevBuf m_rpos, m_bsize;  // receive side: run bucket bounds (P x 65537), bucket size/start
-    DevBuf m_bseg, m_blist;  // boundary groups of the distributed radix: scratch, K11 list
-    DevBuf m_gb, m_pack, m_meta, m_g16;  // packed exchange: bucket bounds, low 16 bits, counts
-    // device small area: [0, 8K) hist4 (4x256 u64) | [8K, 10K) pass digit totals (256 u64) |
-    // [10K, 12K) pass digit bases (256 u64) | [20K, 256K) plans / samples / routing tables
-    DevBuf small;               // kSmallBytes; d_small aliases small.p
-    char *d_small = nullptr;
-    char *h_small = nullptr;  // pinned mirror
-    std::map<void *, DevBuf> user_bufs;  // gsort_device_alloc (guarded with GSORT_CANARY)
-    std::vector<int32_t> splitters;
-    std::vector<uint64_t> bucket_counts;
-    // timing
-    bool timing = false;
-    std::vector<hipEvent_t> ev_pool;
-    size_t ev_used = 0;
-    struct Span { int phase; hipEvent_t a, b; };
-    std::vector<Span> spans;
-    LaunchTimer timer;  // kernel-attached timing events (tic / toc)
-    // host staging of the drop-in path (gsort_scatter_from_root / gsort_gather_to_root):
-    // kStageBufs pinned chunks, allocated on first use
-    char *h_stage[4] = {nullptr, nullptr, nullptr, nullptr};
-    hipEvent_t ev_stage[4] = {nullptr, nullptr, nullptr, nullptr};
-};
-
-namespace {
-
-// [12K, 12K+96): MSD work-list counters, {entries, keys, longest} for the next-level list and
-// the K11 class lists; [12K+128, 12K+144): a one-entry list for a single-bucket sort;
-// [12K+256, 12K+352): the counters of the level-3 K11 lists of the two-level plan
-constexpr size_t OFF_HIST = 0, OFF_TOT = 8192, OFF_BASES = 10240, OFF_CTR = 12288,
-                 OFF_ONE = 12416, OFF_CTR3 = 12544, OFF_PLAN = 20480;
-constexpr size_t OFF_FLAGS = 12408;  // K12b's trivial-level word, inside the published range
-constexpr size_t OFF_MINMAX = 12480;  // the offset retry's exact min / max (2 int32)
-constexpr size_t OFF_FBCTR = 12800;   // K18c (u8): the count of wrapped buckets (u32)
-constexpr size_t OFF_GIANT = 16384;   // K1m result (3 u64) + K1g counters (16 u64)
+namespace gsort {
+namespace rt {
 
 gsort_status set_err(gsort_ctx *c, gsort_status st, const std::string &msg) {
     if (c) c->err = msg;
@@ -149,30 +20,6 @@ gsort_status set_err(gsort_ctx *c, gsort_status st, const std::string &msg) {
 std::mutex g_ctx_mu;
 std::set<gsort_ctx *> g_ctxs;
 gsort_status check_all_guards(gsort_ctx *c, const char *where);
-
-// Every HIP call of the runtime goes through hip_op (GSORT_SERIAL: serialized + device-synced,
-// then with GSORT_CANARY the guards of all contexts are checked after the call).
-#define HIP_TRY(ctx, expr)                                                                   \
-    do {                                                                                     \
-        if (trace_mode()) trace_op((ctx)->rank, #expr);                                      \
-        hipError_t e_ = hip_op([&]() -> hipError_t { return (expr); });                      \
-        if (e_ != hipSuccess && trace_mode()) trace_dump(#expr);                             \
-        if (e_ != hipSuccess) fault_info(ctx, #expr);                                        \
-        if (e_ != hipSuccess)                                                                \
-            return set_err(ctx, GSORT_EHIP, std::string(#expr) + ": " +                      \
-                                                hipGetErrorString(e_) + " (rank " +          \
-                                                std::to_string((ctx)->rank) + ")");         \
-        if (serial_mode() && canary_mode()) {                                                \
-            gsort_status g_ = check_all_guards(ctx, #expr);                                  \
-            if (g_ != GSORT_OK) return g_;                                                   \
-        }                                                                                    \
-    } while (0)
-
-#define ST_TRY(expr)                         \
-    do {                                     \
-        gsort_status s_ = (expr);            \
-        if (s_ != GSORT_OK) return s_;       \
-    } while (0)
 
 gsort_status comm_try(gsort_ctx *c, gsort_status st) {
     if (st != GSORT_OK) c->err = c->comm->err + " (rank " + std::to_string(c->rank) + ")";
@@ -427,8 +274,6 @@ gsort_status ensure(gsort_ctx *c, DevBuf &b, size_t bytes) {
     }
 }
 
-template <class T>
-T *slot_ptr(gsort_ctx *c, Slot s) { return reinterpret_cast<T *>(c->slot[s].p); }
 
 // ---- timing ---------------------------------------------------------------------------
 hipEvent_t next_event(gsort_ctx *c) {
@@ -531,7 +376,7 @@ gsort_status count_tiles(gsort_ctx *c, const uint32_t *src, uint64_t n, int digi
 // The pass's 256 digit counts are left in the small area at OFF_TOT (used for routing).
 gsort_status scan_and_scatter(gsort_ctx *c, const uint32_t *src, uint32_t *dst, uint64_t n,
                               int digit, bool flip_in, bool flip_out,
-                              const uint32_t *vin = nullptr, uint32_t *vout = nullptr) {
+                              const uint32_t *vin, uint32_t *vout) {
     uint64_t *totals = reinterpret_cast<uint64_t *>(c->d_small + OFF_TOT);
     uint64_t *bases = reinterpret_cast<uint64_t *>(c->d_small + OFF_BASES);
     hipEvent_t t = tic(c);
@@ -549,50 +394,12 @@ gsort_status reset_call(gsort_ctx *c) {
     return GSORT_OK;
 }
 
-// ---- LSD local sort: K1 (+ all four histograms) then per non-trivial digit K1/K2/K3 -----
-// Reference: the per-key digit loop mpi_radix_sort.c:144-147 (there: base P, all passes
-// through rank 0) and the local qsort mpi_sample_sort.c:85 / :174.
-gsort_status lsd_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *out,
-                      uint32_t *tmp, int *passes_run) {
-    if (passes_run) *passes_run = 0;
-    if (n == 0) return GSORT_OK;
-    ST_TRY(ensure_pass_scratch(c, n));
-    uint64_t *d_hist = reinterpret_cast<uint64_t *>(c->d_small + OFF_HIST);
-    uint64_t *h_hist = reinterpret_cast<uint64_t *>(c->h_small + OFF_HIST);
-    HIP_TRY(c, hipMemsetAsync(d_hist, 0, 4 * kRadix * 8, c->stream));
-    hipEvent_t t = tic(c);
-    HIP_TRY(c, launch_tile_counts(in, n, 0, true, d_tcounts(c), d_hist, c->stream));
-    toc(c, PH_COUNT, t);
-    HIP_TRY(c, hipMemcpyAsync(h_hist, d_hist, 4 * kRadix * 8, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
-    int active[4], k = 0;
-    for (int p = 0; p < 4; ++p) {
-        const uint64_t *h = h_hist + p * kRadix;
-        if (*std::max_element(h, h + kRadix) < n) active[k++] = p;  // skip trivial digits
-    }
-    if (k == 0) {
-        HIP_TRY(c, launch_copy(in, out, n, c->stream));
-        return GSORT_OK;
-    }
-    const uint32_t *src = in;
-    for (int i = 0; i < k; ++i) {
-        uint32_t *dst = ((k - 1 - i) % 2 == 0) ? out : tmp;
-        if (!(i == 0 && active[0] == 0)) ST_TRY(count_tiles(c, src, n, active[i], i == 0));
-        ST_TRY(scan_and_scatter(c, src, dst, n, active[i], i == 0, i == k - 1));
-        src = dst;
-    }
-    if (passes_run) *passes_run = k;
-    return GSORT_OK;
-}
-
 // ---- MSD local sort (gsort_kernels.hip, "MSD partition sort") --------------------------
 // Level 3 partitions the whole input by its top digit (K1 + K2 + K3u, in -> tmp); every later
 // level partitions the buckets still larger than kLocalMax by the next digit (alternating
 // tmp -> out -> tmp -> out, same positions); every bucket of <= kLocalMax keys is finished by
 // K11 in LDS and stored to out as int32.  The host reads two counters per level (a few us) to
 // size the next launches.  Same reference hot loops as lsd_sort.
-constexpr size_t kCtrBytes = 3 * 8 * (kLocalClasses + 1);
-static_assert(OFF_CTR + kCtrBytes <= OFF_FLAGS && OFF_FLAGS + 4 <= OFF_ONE, "counter area");
 
 gsort_status ensure_list(gsort_ctx *c, DevBuf &b, uint64_t entries) {
     return ensure(c, b, (size_t)std::max<uint64_t>(entries, 1) * 16);
@@ -721,1696 +528,8 @@ WorkLists work_lists(gsort_ctx *c, int next) {
     return wl;
 }
 
-// The MSD levels L, L-1, .. 0 (gsort_kernels.hip, "MSD partition sort").  On entry h holds
-// the counters of the work lists filled by level L+1: m_next[cur_list] (buckets still larger
-// than kLocalMax, ordered u32 in `cur`) and m_local[k] (K11 buckets of `cur`, digits L..0
-// left).  Level L partitions cur -> the other buffer (tmp <-> out); level 0 stores int32 into
-// out, as does K11.
-// flip_first: cur is the int32 input itself (the first level flips on load).
-gsort_status msd_levels(gsort_ctx *c, int L, uint32_t *cur, uint32_t *out, uint32_t *tmp,
-                        int cur_list, uint64_t *h, gsort_stats *stats, int *levels,
-                        int last_level = 0, uint16_t *out16 = nullptr, bool flip_first = false) {
-    auto lst = [](DevBuf &b) { return reinterpret_cast<uint64_t *>(b.p); };
-    uint64_t *ctr = reinterpret_cast<uint64_t *>(c->d_small + OFF_CTR);
-    auto lists = [&](int next) { return work_lists(c, next); };
-    hipEvent_t t;
-    for (;; --L) {
-        for (int k = 0; k < kLocalClasses; ++k) {  // buckets finished in LDS: digits L..0 remain
-            const uint64_t *hk = h + 3 * (k + 1);
-            if (!hk[0]) continue;
-            t = tic(c);
-            HIP_TRY(c, launch_local_sort(cur, out, lst(c->m_local[k]), (uint32_t)hk[0], k + 1,
-                                         L + 1, false, c->atomic_rank, c->stream));
-            toc(c, PH_BUCKET, t);
-            if (stats) { stats->buckets_local += hk[0]; stats->keys_bucket_sort += hk[1]; }
-        }
-        const uint64_t nseg = h[0], keys = h[1];
-        if (nseg == 0 || L < 0) break;
-        uint32_t *dst = cur == tmp ? out : tmp;
-        const uint64_t max_tiles = sweep_tiles(keys) + nseg;
-        const uint64_t max_groups = (max_tiles + kScanGroup - 1) / kScanGroup + nseg;
-        ST_TRY(ensure(c, c->m_tpfx, (nseg + 1) * 4));
-        ST_TRY(ensure(c, c->m_gpfx, (nseg + 1) * 4));
-        ST_TRY(ensure(c, c->m_segmap, max_tiles * 4));
-        ST_TRY(ensure(c, c->m_groupmap, max_groups * 4));
-        ST_TRY(ensure(c, c->tcounts, max_tiles * kRadix * 4));
-        ST_TRY(ensure(c, c->gsum, max_groups * kRadix * 8));
-        ST_TRY(ensure(c, c->m_cstart, nseg * kRadix * 8));
-        const uint64_t child_cap = std::min<uint64_t>(nseg * kRadix, keys);
-        ST_TRY(ensure_list(c, c->m_next[cur_list ^ 1], std::min<uint64_t>(child_cap, keys / kLocalMax + 1)));
-        for (int k = 0; k < kLocalClasses; ++k)
-            ST_TRY(ensure_list(c, c->m_local[k],
-                               std::min<uint64_t>(child_cap, keys / (kLocalCap[k] + 1) + 1)));
-        SegPass sp;
-        sp.in = cur;
-        sp.out = dst;
-        sp.flip_in = flip_first;
-        flip_first = false;
-        sp.segs = lst(c->m_next[cur_list]);
-        sp.nseg = (uint32_t)nseg;
-        sp.shift = 8 * L;
-        sp.flip_out = L == last_level;
-        sp.max_tiles = (uint32_t)max_tiles;
-        sp.max_groups = (uint32_t)max_groups;
-        sp.tpfx = reinterpret_cast<uint32_t *>(c->m_tpfx.p);
-        sp.gpfx = reinterpret_cast<uint32_t *>(c->m_gpfx.p);
-        sp.segmap = reinterpret_cast<uint32_t *>(c->m_segmap.p);
-        sp.groupmap = reinterpret_cast<uint32_t *>(c->m_groupmap.p);
-        sp.tcounts = d_tcounts(c);
-        sp.gsum = d_gsum(c);
-        sp.cstart = reinterpret_cast<uint64_t *>(c->m_cstart.p);
-        sp.lists = lists(cur_list ^ 1);
-        // digit 0: every child is a run of equal keys; a partition-only sort stops here too
-        if (L == last_level) sp.lists.ctr = nullptr;
-        if (L == last_level) sp.out16 = out16;
-        t = tic(c);
-        HIP_TRY(c, hipMemsetAsync(ctr, 0, kCtrBytes, c->stream));
-        HIP_TRY(c, launch_seg_count(sp, c->stream));
-        toc(c, PH_COUNT, t);
-        t = tic(c);
-        HIP_TRY(c, launch_seg_partition(sp, c->stream));
-        toc(c, PH_LEVEL3 + (3 - L), t);
-        if (stats) stats->keys_level[3 - L] += keys;
-        ++*levels;
-        if (L == last_level) break;
-        ST_TRY(read_counters(c, h));
-        cur = dst;
-        cur_list ^= 1;
-    }
-    return GSORT_OK;
-}
-
-
-// Mailbox waits poll the stream for errors (a stream that went idle without the word) only
-// every kQueryUs of waiting: each hipStreamQuery puts a marker in the stream, and one every
-// 1024 spins (~1 us) during the sampled plan's eligibility wait queued dozens of them between
-// K12g and K11e -- a ~6 us bubble (profiles/r04_ab_stream_query_rate.txt: 1.376 -> 1.369 ms).
-constexpr int kQueryUs = 200;
-struct QueryTimer {  // (every 1024 spins the waiting thread yields; the query only when due)
-    std::chrono::steady_clock::time_point next = std::chrono::steady_clock::now() +
-                                                 std::chrono::microseconds(kQueryUs);
-    bool due() {
-        const auto now = std::chrono::steady_clock::now();
-        if (now < next) return false;
-        next = now + std::chrono::microseconds(kQueryUs);
-        return true;
-    }
-};
-
-// Wait for K12p's sequence number seq in the mailbox (the counters behind it are then
-// visible).  A stream error, or the stream going idle without the flag, returns GSORT_EHIP
-// instead of spinning forever.
-gsort_status wait_mail(gsort_ctx *c, uint64_t seq) {
-    volatile uint64_t *flag = c->h_mail;
-    QueryTimer qt;
-    for (uint64_t spin = 0; *flag != seq; ++spin) {
-        if ((spin & 1023) == 1023) {
-            const hipError_t q = qt.due() ? hipStreamQuery(c->stream) : hipErrorNotReady;
-            if (q != hipErrorNotReady && *flag != seq) {
-                if (q != hipSuccess)
-                    return set_err(c, GSORT_EHIP, std::string("K12p counters: ") +
-                                                      hipGetErrorString(q) + " (rank " +
-                                                      std::to_string(c->rank) + ")");
-                return set_err(c, GSORT_EHIP, "K12p counters: stream idle without the flag");
-            }
-            std::this_thread::yield();
-        }
-    }
-    std::atomic_thread_fence(std::memory_order_acquire);
-    return GSORT_OK;
-}
-
-// Levels 3 and 2 through the two-level plan (gsort_kernels.hip, "Two-level plan"): K1h (the
-// 16-bit histogram) + K12a/K12b (counts, bases, bucket bounds, cursors, work lists), then K3r
-// (level 3, in -> tmp, runs reserved on per-shard bucket cursors) and K3a (level 2, tmp -> out,
-// or the low 16 bits -> out16 with group16).  The work-list counters are copied to the host
-// right after K12b and read once levels 3 and 2 are queued, so the GPU never waits on the host
-// in the common case.  Then K11 for the small level-3 buckets (three digits, tmp -> out) and
-// for the level-2 children (two digits, in place in out); children still larger than kLocalMax
-// go on through msd_levels from level 1.  cstart (65537 u64) receives the 16-bit bucket bounds.
-gsort_status msd_sort_h16(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *out,
-                          uint32_t *tmp, gsort_stats *stats, bool group16, uint16_t *out16,
-                          uint64_t *cstart) {
-    uint64_t *totals = reinterpret_cast<uint64_t *>(c->d_small + OFF_TOT);
-    uint64_t *bases = reinterpret_cast<uint64_t *>(c->d_small + OFF_BASES);
-    uint64_t *ctr = reinterpret_cast<uint64_t *>(c->d_small + OFF_CTR);
-    uint64_t *ctr3 = reinterpret_cast<uint64_t *>(c->d_small + OFF_CTR3);
-    constexpr size_t kFixBytes = (size_t)kH16Shards * kBuckets16 * 8;
-    ST_TRY(ensure(c, c->m_part, (size_t)kH16Blocks * kH16PartWords * 4));
-    ST_TRY(ensure(c, c->m_fix, kFixBytes));
-    ST_TRY(ensure(c, c->m_cur, (size_t)kBuckets16 * 4));
-    ST_TRY(ensure(c, c->m_tpfx, (kRadix + 1) * 4));
-    ST_TRY(ensure(c, c->m_ccount, (size_t)kBuckets16 * 8));
-    ST_TRY(ensure(c, c->m_t3, (size_t)(kH16Shards + 1) * kRadix * 8));
-    ST_TRY(ensure(c, c->m_cur3, (size_t)kH16Shards * kRadix * 4));
-    ST_TRY(ensure(c, c->m_tdesc, (size_t)(sweep_tiles(n) + kRadix) * kTileDescBytes));
-    if (!cstart) {
-        ST_TRY(ensure(c, c->m_cstart, (size_t)(kBuckets16 + 1) * 8));
-        cstart = reinterpret_cast<uint64_t *>(c->m_cstart.p);
-    }
-    const uint64_t nchild = std::min<uint64_t>(kBuckets16, n);
-    WorkLists wl2 = work_lists(c, 0), wl3 = work_lists(c, 1);
-    if (!group16) {
-        ST_TRY(ensure_list(c, c->m_next[0], std::min<uint64_t>(nchild, n / kLocalMax + 1)));
-        ST_TRY(ensure_list(c, c->m_next[1], 1));
-        for (int k = 0; k < kLocalClasses; ++k) {
-            ST_TRY(ensure_list(c, c->m_local[k],
-                               std::min<uint64_t>(nchild, n / (kLocalCap[k] + 1) + 1)));
-            ST_TRY(ensure_list(c, c->m_local3[k], kRadix));
-        }
-        wl2 = work_lists(c, 0);
-        wl3 = work_lists(c, 1);
-        for (int k = 0; k < kLocalClasses; ++k)
-            wl3.list[k + 1] = reinterpret_cast<uint64_t *>(c->m_local3[k].p);
-        wl3.ctr = ctr3;
-    } else {
-        wl2.ctr = nullptr;
-        wl3.ctr = nullptr;
-    }
-    uint32_t *tpfx = reinterpret_cast<uint32_t *>(c->m_tpfx.p);
-    uint32_t *cur = reinterpret_cast<uint32_t *>(c->m_cur.p);
-    uint32_t *cur3 = reinterpret_cast<uint32_t *>(c->m_cur3.p);
-    uint64_t *t3 = reinterpret_cast<uint64_t *>(c->m_t3.p);
-    uint32_t nblk = 0;
-    constexpr uint32_t kCtrWords = (uint32_t)((OFF_CTR3 + kCtrBytes - OFF_CTR) / 8);
-    // K12b's trivial-level word (zeroed by K12a and published with the counters); the
-    // distributed sender (group16) needs every level's output, so it never skips
-    uint32_t *flags = group16 ? nullptr : reinterpret_cast<uint32_t *>(c->d_small + OFF_FLAGS);
-    static_assert(kCtrWords <= kRadix && kCtrWords * 8 <= kMailBytes - 64, "counter words");
-    if (c->fix_clean != c->m_fix.p)  // new allocation: K12a keeps it zero from here on
-        HIP_TRY(c, hipMemsetAsync(c->m_fix.p, 0, kFixBytes, c->stream));
-    c->fix_clean = nullptr;
-    hipEvent_t t = tic(c);
-    HIP_TRY(c, launch_hist16(in, n, true, reinterpret_cast<uint32_t *>(c->m_part.p),
-                             reinterpret_cast<uint64_t *>(c->m_fix.p), &nblk, c->stream));
-    HIP_TRY(c, launch_plan16(reinterpret_cast<uint32_t *>(c->m_part.p), nblk,
-                             reinterpret_cast<uint64_t *>(c->m_fix.p), n, group16,
-                             reinterpret_cast<uint64_t *>(c->m_ccount.p), t3,
-                             t3 + (size_t)kH16Shards * kRadix, bases, totals, cstart, cur, cur3,
-                             tpfx, wl2, wl3, group16 ? nullptr : ctr, kCtrWords, flags,
-                             c->stream));
-    c->fix_clean = c->m_fix.p;
-    const uint64_t seq = ++c->mail_seq;
-    if (!group16)
-        HIP_TRY(c, launch_publish(ctr, kCtrWords, c->d_mail + 8, c->d_mail, seq, c->stream));
-    toc(c, PH_COUNT, t);
-    t = tic(c);
-    HIP_TRY(c, launch_partition3r(in, tmp, n, cur3, bases, flags, c->stream));
-    toc(c, PH_LEVEL3, t);
-    t = tic(c);
-    HIP_TRY(c, launch_partition2r(tmp, out, group16 ? out16 : nullptr, n, tpfx, c->m_tdesc.p,
-                                  bases, totals, cur, flags, in, c->stream));
-    toc(c, PH_LEVEL2, t);
-    int levels = 2;
-    if (group16 && stats) { stats->keys_level[0] += n; stats->keys_level[1] += n; }
-    if (!group16) {
-        ST_TRY(wait_mail(c, seq));
-        uint64_t h[3 * (kLocalClasses + 1)], h3[3 * (kLocalClasses + 1)];
-        const char *mail = reinterpret_cast<const char *>(c->h_mail + 8);
-        memcpy(h, mail, kCtrBytes);
-        memcpy(h3, mail + (OFF_CTR3 - OFF_CTR), kCtrBytes);
-        uint32_t fl = 0;
-        memcpy(&fl, mail + (OFF_FLAGS - OFF_CTR), 4);
-        const bool triv3 = fl & 1u, triv2 = fl & 2u;
-        levels = 2 - (int)triv3 - (int)triv2;
-        if (stats) {
-            if (!triv3) stats->keys_level[0] += n;
-            if (!triv2) stats->keys_level[1] += n;
-            for (int k = 0; k < kLocalClasses; ++k)  // K11'd whole at level 3
-                stats->keys_level[1] -= std::min<uint64_t>(h3[3 * (k + 1) + 1],
-                                                           stats->keys_level[1]);
-        }
-        if (triv2) {  // levels 3 and 2 moved nothing: level 1 reads the int32 input
-            if (stats) stats->passes_run = levels;
-            ST_TRY(msd_levels(c, 1, const_cast<uint32_t *>(in), out, tmp, 0, h, stats, &levels,
-                              0, nullptr, true));
-            if (stats) stats->passes_run = levels;
-            return GSORT_OK;
-        }
-        for (int k = 0; k < kLocalClasses; ++k) {
-            const uint64_t *hk = h3 + 3 * (k + 1);
-            if (!hk[0]) continue;
-            t = tic(c);
-            HIP_TRY(c, launch_local_sort(tmp, out, reinterpret_cast<uint64_t *>(c->m_local3[k].p),
-                                         (uint32_t)hk[0], k + 1, 3, false, c->atomic_rank,
-                                         c->stream));
-            toc(c, PH_BUCKET, t);
-            if (stats) { stats->buckets_local += hk[0]; stats->keys_bucket_sort += hk[1]; }
-        }
-        ST_TRY(msd_levels(c, 1, out, out, tmp, 0, h, stats, &levels));
-    }
-    if (stats) stats->passes_run = levels;
-    return GSORT_OK;
-}
-
-// The sampled plan (gsort_kernels.hip, "Sampled plan"): levels 3 and 2 into gapped regions
-// sized from a 1/64 sample, K11e into out.  The host reads the eligibility / overflow words
-// and the K11e list counts K12g leaves in the mailbox (one wait, after level 2), then launches
-// K11e; *ok = false means nothing was written to out and the caller sorts on the exact plan.
-// the sampled plan's mailbox words start here (EstPlan::mail: kEstMailWords of them)
-constexpr size_t kEstMailWord = 400;
-static_assert((kEstMailWord + kEstMailWords) * 8 <= kMailBytes, "mailbox");
-
-// Keys of the region buffers the caps of `nreg` regions can add up to (k_est_plan's est_cap:
-// max(a, b) <= a + b, Cauchy-Schwarz on the sigma terms: sum sqrt(cnt + 1) <=
-// sqrt(nreg (m + nreg)); m >= the samples of all full blocks)
-uint64_t est_region_keys(uint64_t n, uint64_t nreg, double slack) {
-    const double m = (double)std::max<uint64_t>((n / kEstBlockKeysHost) * 8, 8);
-    const double sig = 6.0 * ((double)n / m) * std::sqrt((double)nreg * (m + (double)nreg));
-    const double floor2 = 2.0 * kEstBlockKeysHost * (double)nreg;
-    return n + nreg + (uint64_t)std::ceil(slack * (sig + floor2 + 64.0 * (double)nreg)) + 1024;
-}
-
-// What an ineligible first attempt saw: the key bits that vary among the samples (against key
-// 0) and the samples' min / max, all as ordered u32.
-struct EstRetry {
-    bool valid = false;
-    uint32_t vary = 0, lo = 0, hi = 0, maxc = 0;  // maxc: samples of the largest child
-};
-
-// Leading bits shared by every key of a range (clz of its span), 32 for a single value.
-int span_lead(uint32_t lo, uint32_t hi) { return hi > lo ? __builtin_clz(hi - lo) : 32; }
-
-gsort_status msd_sort_est(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *out,
-                          gsort_stats *stats, bool *ok, int sb = 0, uint32_t koff = 0,
-                          EstRetry *retry = nullptr) {
-    *ok = false;
-    if (retry) *retry = EstRetry{};
-    const double slack = std::max(c->est_slack, 0.0);
-    const uint64_t capx = est_region_keys(n, (uint64_t)kH16Shards * kRadix, slack);
-    const uint64_t capy = std::min<uint64_t>(est_region_keys(n, kBuckets16, slack),
-                                             (uint64_t)kBuckets16 * kLocalMax);
-    // the region buffers are the plan's only large allocations: without room for them (or for
-    // its small plan arrays) the exact plan sorts (it needs none of them), and the regions are
-    // handed back
-    constexpr size_t kPlanWords = (size_t)4 * kBuckets16 + 4 * kH16Shards * kRadix + kRadix + 1;
-    {
-        // busy while they are made: a refused Y must not reclaim the X just ensured (that left
-        // X null and K3r wrote through it -- found by test_region_buffers_reclaimed_for_a_later_call)
-        c->est_busy = true;
-        gsort_status st = GSORT_OK;
-        for (DevBuf *b : {&c->m_ex, &c->m_ey})
-            if (st == GSORT_OK) st = ensure(c, *b, b == &c->m_ex ? capx * 4 : capy * 2);  // Y: u16
-        if (st == GSORT_OK)
-            st = ensure(c, c->m_epart,
-                        (size_t)kEstWGs * (kBuckets16 / 4 + kH16Shards * kRadix + 4) * 4);
-        if (st == GSORT_OK) st = ensure(c, c->m_eplan, kPlanWords * 4 + 4 * kRadix * 8 + 64);
-        if (st == GSORT_OK)
-            st = ensure(c, c->m_edesc,
-                        ((size_t)est_max_tiles(n) + kH16Shards * kRadix) * kTileDescBytes);
-        if (st == GSORT_OK) st = ensure(c, c->m_edump, (size_t)kSweepTile * 4);
-        for (int k = 0; k < kLocalClasses && st == GSORT_OK; ++k)
-            st = ensure_list(c, c->m_local[k], kBuckets16);
-        if (st == GSORT_OK) st = ensure_list(c, c->m_next[0], kBuckets16);  // K18c: > kLocalMax
-        c->est_busy = false;
-        if (st == GSORT_OK && (!c->m_ex.p || !c->m_ey.p))
-            return set_err(c, GSORT_EINVAL, "sampled plan: region buffers missing");
-        if (st == GSORT_ENOMEM) {
-            (void)reclaim_regions(c, DevBuf{});
-            c->err.clear();
-            return GSORT_OK;  // *ok stays false
-        }
-        ST_TRY(st);
-    }
-    struct Busy {
-        bool &f;
-        explicit Busy(bool &x) : f(x) { f = true; }
-        ~Busy() { f = false; }
-    } busy(c->est_busy);
-    EstPlan p{};
-    p.in = in;
-    p.n = n;
-    p.flip_in = true;
-    p.x = static_cast<uint32_t *>(c->m_ex.p);
-    p.y = static_cast<uint16_t *>(c->m_ey.p);
-    p.out = out;
-    p.capx = capx;
-    p.capy = capy;
-    p.part8 = static_cast<uint32_t *>(c->m_epart.p);
-    p.part3 = p.part8 + (size_t)kEstWGs * (kBuckets16 / 4);
-    p.msamp = p.part3 + (size_t)kEstWGs * kH16Shards * kRadix;
-    uint64_t *u64 = static_cast<uint64_t *>(c->m_eplan.p);
-    p.r2 = u64;
-    p.r3 = u64 + kRadix;
-    p.bases3 = u64 + 2 * kRadix;
-    p.bases2 = u64 + 3 * kRadix;
-    uint32_t *w = reinterpret_cast<uint32_t *>(u64 + 4 * kRadix);
-    p.capc = w;
-    p.cur2 = w + kBuckets16;
-    p.lim2 = w + 2 * kBuckets16;
-    p.init2 = w + 3 * kBuckets16;
-    w += 4 * kBuckets16;
-    p.cap3 = w;
-    p.cur3 = w + kH16Shards * kRadix;
-    p.lim3 = w + 2 * kH16Shards * kRadix;
-    p.init3 = w + 3 * kH16Shards * kRadix;
-    p.tp = w + 4 * kH16Shards * kRadix;
-    p.eflag = p.tp + kRadix + 2;  // 2 words, 8-B aligned (published as one u64)
-    p.tdesc = c->m_edesc.p;
-    p.dump = static_cast<uint32_t *>(c->m_edump.p);
-    p.wl = work_lists(c, 0);
-    p.slack = slack;
-    p.atomic_rank = c->atomic_rank;
-    p.sb = sb;
-    p.koff = koff;
-    p.mail = c->d_mail + kEstMailWord;
-    p.seq_elig = ++c->mail_seq;
-    p.seq_done = ++c->mail_seq;
-    volatile uint64_t *mail = c->h_mail + kEstMailWord;
-    // poll a sequence word of the mailbox; a stream that goes idle without it is an error
-    auto wait_word = [&](size_t w, uint64_t seq, const char *what) -> gsort_status {
-        QueryTimer qt;
-        for (uint64_t spin = 0; mail[w] != seq; ++spin) {
-            if ((spin & 1023) == 1023) {
-                const hipError_t q = qt.due() ? hipStreamQuery(c->stream) : hipErrorNotReady;
-                if (q != hipErrorNotReady && mail[w] != seq)
-                    return set_err(c, GSORT_EHIP, std::string("sampled plan: ") + what + ": " +
-                                                      (q == hipSuccess ? "stream idle without it"
-                                                                       : hipGetErrorString(q)));
-                std::this_thread::yield();
-            }
-        }
-        std::atomic_thread_fence(std::memory_order_acquire);
-        return GSORT_OK;
-    };
-    hipEvent_t t = tic(c);
-    HIP_TRY(c, launch_est_front(p, c->stream));
-    toc(c, PH_COUNT, t);
-    t = tic(c);
-    HIP_TRY(c, launch_est_level3(p, c->stream));  // block 0 publishes the eligibility word; all return at once on an ineligible block
-    toc(c, PH_LEVEL3, t);
-    // K12f, K3a and K12g return at once on an ineligible block too, so they are queued before
-    // the host looks at the eligibility word (waiting first left a launch gap behind K3r)
-    t = tic(c);
-    HIP_TRY(c, launch_est_level2(p, c->stream));
-    toc(c, PH_LEVEL2, t);
-    HIP_TRY(c, launch_est_classify(p, c->stream));
-    ST_TRY(wait_word(3, p.seq_elig, "eligibility word"));
-    if (c->plan_trace)
-        fprintf(stderr, "gsort plan: n %llu sb %d koff %u eflag %llx children %llu maxc %llx\n",
-                (unsigned long long)n, sb, koff, (unsigned long long)mail[2],
-                (unsigned long long)mail[4], (unsigned long long)mail[23]);
-    if (mail[2] & 4u) {  // ineligible: the exact plan sorts -- unless the samples share leading
-        // key bits (a key range narrower than int32: 16-, 20-, 24-, 28-bit keys, dense or
-        // sorted ranges) whose removal leaves children K11e can take: then the caller retries
-        // with every digit that many bits lower (at most 16, the plan's two levels).  One or
-        // two shared bits (Zipf, any non-negative keys) rarely turn an ineligible block
-        // eligible and are not worth a second sample.
-        if (retry) {
-            retry->vary = (uint32_t)mail[5];
-            retry->lo = (uint32_t)mail[6];
-            retry->hi = (uint32_t)mail[7];
-            retry->maxc = (uint32_t)mail[23];
-            retry->valid = true;
-        }
-        return GSORT_OK;
-    }
-    // K11e of the class the average child falls in, queued right behind K12g (a grid of the
-    // sampled children: at least its entries, usually exactly), so no host round trip sits
-    // between K12g and the largest K11e launch; the other classes follow once the counts are in
-    const uint32_t sampled = (uint32_t)std::min<uint64_t>((uint64_t)mail[4], (uint64_t)kBuckets16);
-    // (class 4 children go to K18c unless the plan is shifted by 8+ bits: the speculative grid
-    // then is class 3's, whose blocks past its count return at once after block 0 has
-    // published the counters)
-    const int kmax = sb >= 8 ? kLocalClasses : kEstCx - 1;
-    const int kspec = sampled ? std::min(std::max(local_class(n / sampled), 1), kmax) : 0;
-    t = tic(c);
-    if (kspec) HIP_TRY(c, launch_local_sort_e(p, kspec, 0, sampled, true, c->stream));
-    else HIP_TRY(c, launch_est_publish(p, c->stream));
-    ST_TRY(wait_word(1, p.seq_done, "K12g counters"));
-    if (mail[0] != 0) {  // a region overflowed: *ok stays false
-        if (c->plan_trace) fprintf(stderr, "gsort plan: overflow %llx\n", (unsigned long long)mail[0]);
-        return GSORT_OK;
-    }
-    uint64_t h[3 * (kLocalClasses + 1)];
-    for (int i = 0; i < 3 * (kLocalClasses + 1); ++i) h[i] = mail[8 + i];
-    uint64_t keys = 0, ent = 0;  // (list 0: the children past kLocalMax, K18c)
-    for (int k = 0; k <= kLocalClasses; ++k) { keys += h[3 * k + 1]; ent += h[3 * k]; }
-    if (keys != n || ent > kBuckets16)  // every key in exactly one K11e entry
-        return set_err(c, GSORT_EINVAL, "sampled plan: K11e lists hold " + std::to_string(keys) +
-                                            " keys in " + std::to_string(ent) + " entries, want " +
-                                            std::to_string(n) + " keys");
-    for (int k = 1; k <= kmax; ++k) {
-        const uint32_t done = k == kspec ? sampled : 0u, cnt = (uint32_t)h[3 * k];
-        if (cnt > done) HIP_TRY(c, launch_local_sort_e(p, k, done, cnt - done, false, c->stream));
-    }
-    if (h[0]) HIP_TRY(c, launch_est_oversized(p, (uint32_t)h[0], c->ncu, c->stream));
-    toc(c, PH_BUCKET, t);
-    *ok = true;
-    if (stats) stats->buckets_local += ent;
-    if (*ok && stats) {
-        stats->keys_level[0] += n;
-        stats->keys_level[1] += n;
-        stats->keys_bucket_sort += n;
-        stats->passes_run = 2;
-    }
-    return GSORT_OK;
-}
-
-gsort_status msd_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *out,
-                      uint32_t *tmp, gsort_stats *stats, bool group16, uint16_t *out16,
-                      uint64_t *gb, bool allow_est, bool allow_giant);
-
-// One dominant 16-bit child (gsort_kernels.hip, "giant child"): K1m found child `child` in at
-// least half of the samples.  K1g histograms its keys' low 16 bits and compacts the other
-// (cold) keys per XCD shard into S_TMP; K12m / K12s turn the partials into output starts; the
-// cold keys are gathered, sorted by the regular local sort into out + n_child (below-child keys
-// then move to the front) and K18g writes the child's keys from the counts.  *ok = false: the
-// child held fewer than half of the keys after all (nothing is written; the caller goes on).
-gsort_status giant_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *out,
-                        uint32_t child, gsort_stats *stats, bool *ok) {
-    *ok = false;
-    uint32_t g = 0;
-    const uint64_t cap = (uint64_t)giant_wg_cap(n, &g) * g;
-    ST_TRY(ensure(c, c->slot[S_TMP], cap * 4));
-    ST_TRY(ensure(c, c->m_part, (size_t)kH16Blocks * kH16PartWords * 4));
-    constexpr size_t kFixBytes = (size_t)kH16Shards * kBuckets16 * 8;
-    ST_TRY(ensure(c, c->m_fix, kFixBytes));
-    const uint64_t nchunks_max = n / 2048 + 2;  // K18g chunks of >= 2048 keys
-    ST_TRY(ensure(c, c->m_gplan, ((size_t)2 * kBuckets16 + 1 + 64) * 8 + nchunks_max * 4));
-    if (c->fix_clean != c->m_fix.p) HIP_TRY(c, hipMemsetAsync(c->m_fix.p, 0, kFixBytes, c->stream));
-    c->fix_clean = nullptr;
-    // ctr: [0] cold keys below the child, [1 + b] workgroup b's cold keys (1 + g <= 257 u64,
-    // inside OFF_GIANT's 4 KiB)
-    static_assert(OFF_GIANT + (4 + 1 + kH16Blocks) * 8 <= OFF_PLAN, "giant counters");
-    uint64_t *d_ctr = reinterpret_cast<uint64_t *>(c->d_small + OFF_GIANT) + 4;
-    uint64_t *h_ctr = reinterpret_cast<uint64_t *>(c->h_small + OFF_GIANT) + 4;
-    uint64_t *counts = static_cast<uint64_t *>(c->m_gplan.p), *starts = counts + kBuckets16;
-    uint32_t *chunk_bin = reinterpret_cast<uint32_t *>(starts + kBuckets16 + 1 + 64);  // (K12s scratch before it)
-    uint32_t *cold = slot_ptr<uint32_t>(c, S_TMP);
-    HIP_TRY(c, hipMemsetAsync(d_ctr, 0, (1 + g) * 8, c->stream));
-    hipEvent_t t = tic(c);
-    HIP_TRY(c, launch_giant_hist(in, n, child, reinterpret_cast<uint32_t *>(c->m_part.p),
-                                 reinterpret_cast<uint64_t *>(c->m_fix.p), cold, d_ctr, c->stream));
-    HIP_TRY(c, launch_giant_plan(reinterpret_cast<uint32_t *>(c->m_part.p), g,
-                                 reinterpret_cast<uint64_t *>(c->m_fix.p), d_ctr, counts, starts,
-                                 c->stream));
-    c->fix_clean = c->m_fix.p;  // K12m left it zeroed
-    toc(c, PH_COUNT, t);
-    HIP_TRY(c, hipMemcpyAsync(h_ctr, d_ctr, (1 + g) * 8, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
-    uint64_t n_cold = 0;
-    const uint64_t n_lo = h_ctr[0];
-    for (uint32_t b = 0; b < g; ++b) n_cold += h_ctr[1 + b];
-    const uint64_t n_child = n - n_cold;
-    if (c->plan_trace)
-        fprintf(stderr, "gsort plan: giant child %x n %llu cold %llu below %llu\n", child,
-                (unsigned long long)n, (unsigned long long)n_cold, (unsigned long long)n_lo);
-    if (n_cold > n || n_lo > n_cold)
-        return set_err(c, GSORT_EINVAL, "giant child: inconsistent cold counts");
-    // the sample misjudged: not worth it.  2 n_child >= n also gives n_cold <= n_child, which
-    // the cold-key sort below relies on (odd n with n_child = (n - 1) / 2 would overlap)
-    if (2 * n_child < n) return GSORT_OK;
-    // the cold keys: gathered from the workgroups' segments into out[0, n_cold), sorted into
-    // out[n_child, n) (disjoint: n_cold <= n_child) with S_TMP as scratch, and their part below
-    // the child moved to the front (n_lo <= n_cold <= n_child: no overlap either); the child's
-    // keys then fill [n_lo, n_lo + n_child)
-    if (n_cold) {
-        HIP_TRY(c, launch_giant_gather(cold, n, d_ctr, out, c->stream));
-        gsort_stats cst;
-        memset(&cst, 0, sizeof(cst));
-        const int lp = c->last_plan;
-        ST_TRY(msd_sort(c, out, n_cold, out + n_child, cold, &cst, false, nullptr, nullptr, true,
-                        false));
-        c->last_plan = lp;
-        if (n_lo)
-            HIP_TRY(c, hipMemcpyAsync(out, out + n_child, n_lo * 4, hipMemcpyDeviceToDevice,
-                                      c->stream));
-        if (stats) stats->keys_bucket_sort += n_cold;
-    }
-    t = tic(c);
-    HIP_TRY(c, launch_giant_expand(starts, n_child, child, chunk_bin, out, c->stream));
-    toc(c, PH_BUCKET, t);
-    if (stats) {
-        stats->passes_run = 1;
-        stats->keys_level[0] += n;
-        stats->keys_bucket_sort += n_child;
-        stats->buckets_local += 1;
-    }
-    *ok = true;
-    return GSORT_OK;
-}
-
-// group16: stop after level 2 -- out holds the keys (int32) grouped by their top 16 bits
-// (ordered u32) but not sorted inside a group (the sender side of the distributed radix);
-// with out16 and n > kLocalMax, level 2 stores only the low 16 bits of every key, at out16.
-// With the two-level plan (c->plan16) and group16, gb (65537 u64) receives the 16-bit bucket
-// bounds of the grouped block.
-// allow_est: the sampled plan may run (it waits on the host for its mailbox words mid-sort, so
-// callers that must not block -- the distributed sender's grouping -- keep it off).
-// allow_giant: an ineligible block may take the one-dominant-child path (its cold keys are
-// sorted with allow_giant off).
-gsort_status msd_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *out,
-                      uint32_t *tmp, gsort_stats *stats, bool group16 = false,
-                      uint16_t *out16 = nullptr, uint64_t *gb = nullptr, bool allow_est = false,
-                      bool allow_giant = true) {
-    c->last_plan = 0;
-    if (n == 0) return GSORT_OK;
-    if (allow_est && c->plan_est && c->plan16 && !group16 && n >= kEstMinKeys &&
-        n <= kEstMaxKeys) {
-        bool ok = false;
-        EstRetry r;
-        ST_TRY(msd_sort_est(c, in, n, out, stats, &ok, 0, 0, &r));
-        c->last_plan = ok ? 1 : 2;
-        if (ok) return GSORT_OK;
-        // the block's exact min / max (one read pass + a host round trip), once
-        bool have_mm = false;
-        uint32_t mlo = 0, mhi = 0;
-        auto minmax = [&]() -> gsort_status {
-            if (have_mm) return GSORT_OK;
-            int *mm = reinterpret_cast<int *>(c->d_small + OFF_MINMAX);
-            int *hmm = reinterpret_cast<int *>(c->h_small + OFF_MINMAX);
-            HIP_TRY(c, hipStreamSynchronize(c->stream));  // hmm may feed an earlier copy
-            hmm[0] = 2147483647;
-            hmm[1] = -2147483647 - 1;
-            HIP_TRY(c, hipMemcpyAsync(mm, hmm, 8, hipMemcpyHostToDevice, c->stream));
-            HIP_TRY(c, launch_minmax(reinterpret_cast<const int32_t *>(in), n, mm, c->stream));
-            HIP_TRY(c, hipMemcpyAsync(hmm, mm, 8, hipMemcpyDeviceToHost, c->stream));
-            HIP_TRY(c, hipStreamSynchronize(c->stream));
-            mlo = (uint32_t)hmm[0] ^ 0x80000000u;
-            mhi = (uint32_t)hmm[1] ^ 0x80000000u;
-            have_mm = true;
-            return GSORT_OK;
-        };
-        // one value: the sorted block is the block (copied)
-        auto one_value = [&]() -> gsort_status {
-            HIP_TRY(c, hipMemcpyAsync(out, in, n * 4, hipMemcpyDeviceToDevice, c->stream));
-            ok = true;
-            if (stats) {  // one bucket, finished without a partition level
-                stats->passes_run = 0;
-                stats->buckets_local += 1;
-                stats->keys_bucket_sort += n;
-            }
-            return GSORT_OK;
-        };
-        // every sample one value: most likely the whole block is (all-equal 2^28 keys: the
-        // copy 0.60 ms, the counted child below 1.11 ms)
-        if (r.valid && span_lead(r.lo, r.hi) == 32) {
-            ST_TRY(minmax());
-            if (mlo == mhi) {
-                ST_TRY(one_value());
-                c->last_plan = 3;
-                return GSORT_OK;
-            }
-        }
-        // one 16-bit child holding at least half of the keys (Zipf, 8- / 16-bit keys, one
-        // frequent value): counted, not partitioned (K1m decides from 16384 strided samples)
-        // (skipped when the first sample's child counts are known -- no u8 counter wrapped --
-        // and its largest child holds well under half of the samples: K1m is a 40 us strided
-        // read; a dominant child always wraps, >= 512 samples in one workgroup's counter)
-        const bool known = r.maxc != 0xffffffffu;
-        if (allow_giant && c->plan_giant && r.valid && !(known && (uint64_t)r.maxc * 160 < n)) {
-            uint64_t *d_res = reinterpret_cast<uint64_t *>(c->d_small + OFF_GIANT);
-            uint64_t *h_res = reinterpret_cast<uint64_t *>(c->h_small + OFF_GIANT);
-            HIP_TRY(c, launch_est_mode(in, n, d_res, c->stream));
-            HIP_TRY(c, hipMemcpyAsync(h_res, d_res, 24, hipMemcpyDeviceToHost, c->stream));
-            HIP_TRY(c, hipStreamSynchronize(c->stream));
-            if (c->plan_trace)
-                fprintf(stderr, "gsort plan: mode child %llx %llu of %llu samples\n",
-                        (unsigned long long)h_res[0], (unsigned long long)h_res[1],
-                        (unsigned long long)h_res[2]);
-            if (h_res[2] && 2 * h_res[1] >= h_res[2]) {
-                ST_TRY(giant_sort(c, in, n, out, (uint32_t)h_res[0], stats, &ok));
-                if (ok) {
-                    c->last_plan = 4;
-                    return GSORT_OK;
-                }
-            }
-        }
-        // An ineligible block whose keys span a narrow range: retry with every digit below the
-        // bits the range's keys share (children of at most kLocalMax / 2 on average), either
-        // a prefix the samples share (free: K3r checks it on every key) or -- when the range
-        // crosses a power of two, e.g. around zero -- the exact min / max (one read pass) as an
-        // offset.  One or two shared bits (Zipf, any non-negative keys) rarely make a block
-        // eligible and are not worth a second sample.
-        // fits: the children after a shift by min(lead, 16) bits average at most kLocalMax / 2,
-        // and -- when the first sample's child counts are known (no u8 counter wrapped) -- the
-        // largest one now (~64 keys per sample) split 2^shift ways stays below 5/8 of it.  The
-        // prefix retry costs a failed sample when wrong; the offset retry also a read pass, so
-        // it needs known counts (no u8 counter wrapped) and a fit after the shift, or -- counts
-        // wrapped, i.e. a peaked block -- a span of at most 24 bits (>= 8 shared): Gaussian keys
-        // (the first sample wraps on their peak; after the offset their children hold <= ~27K
-        // keys at 2^28, sigma 1e6) pass it, Zipf keys, whose densest child holds ~29 % of the
-        // block, do not.
-        auto fits = [&](int lead) {
-            const int sb = std::min(lead, 16);
-            const int fixed = std::max(0, std::min(lead - sb, 16));  // bits fixed below the shift
-            return n / (1ull << (16 - fixed)) <= kLocalMax / 2 &&
-                   (!known || ((uint64_t)r.maxc * 64) >> sb <= kLocalMax * 5 / 8);
-        };
-        if (r.valid) {
-            const int lead = r.vary ? __builtin_clz(r.vary) : 32;
-            const int slead = span_lead(r.lo, r.hi);
-            const bool by_prefix = lead >= 3 && lead < 32 && fits(lead);
-            const bool by_offset =
-                !by_prefix && (slead == 32 || ((known || slead >= 8) && slead >= 4 && fits(slead - 1)));
-            if (by_prefix) {
-                ST_TRY(msd_sort_est(c, in, n, out, stats, &ok, std::min(lead, 16)));
-            } else if (by_offset) {
-                // (the samples' span, one bit of margin: the block's may be wider)
-                // First the samples' range widened by an eighth of its width each way as the
-                // offset (no read pass: K3r checks every key against the constant prefix, so a
-                // key outside the guess fails the attempt); then the exact min / max.
-                if (slead < 32) {
-                    const uint64_t m = ((uint64_t)r.hi - r.lo) / 8 + 1;
-                    const uint32_t glo = r.lo > m ? (uint32_t)(r.lo - m) : 0u;
-                    const uint32_t ghi = (uint32_t)std::min<uint64_t>((uint64_t)r.hi + m, 0xffffffffull);
-                    const int gl = span_lead(glo, ghi);
-                    if (gl >= 3 && fits(gl))
-                        ST_TRY(msd_sort_est(c, in, n, out, stats, &ok, std::min(gl, 16), glo));
-                    if (c->plan_trace)
-                        fprintf(stderr, "gsort plan: offset guess %x..%x lead %d ok %d\n", glo, ghi,
-                                gl, (int)ok);
-                }
-            }
-            if (by_offset && !ok) {
-                ST_TRY(minmax());
-                const uint32_t lo = mlo, hi = mhi;
-                const int lead = span_lead(lo, hi);
-                if (lead == 32) {
-                    ST_TRY(one_value());
-                } else if (lead >= 3 && fits(lead)) {
-                    ST_TRY(msd_sort_est(c, in, n, out, stats, &ok, std::min(lead, 16), lo));
-                }
-            }
-        }
-        if (ok) {
-            c->last_plan = 3;
-            return GSORT_OK;
-        }
-    }
-    uint64_t *ctr = reinterpret_cast<uint64_t *>(c->d_small + OFF_CTR);
-    if (n <= kLocalMax) {  // one bucket: all four digits in LDS
-        uint64_t *h_one = reinterpret_cast<uint64_t *>(c->h_small + OFF_ONE);
-        uint64_t *d_one = reinterpret_cast<uint64_t *>(c->d_small + OFF_ONE);
-        HIP_TRY(c, hipStreamSynchronize(c->stream));  // h_one may feed an earlier copy
-        h_one[0] = 0;
-        h_one[1] = n;
-        HIP_TRY(c, hipMemcpyAsync(d_one, h_one, 16, hipMemcpyHostToDevice, c->stream));
-        hipEvent_t t = tic(c);
-        HIP_TRY(c, launch_local_sort(in, out, d_one, 1, local_class(n), 4, true, c->atomic_rank,
-                                     c->stream));
-        toc(c, PH_BUCKET, t);
-        if (stats) { stats->buckets_local += 1; stats->keys_bucket_sort += n; }
-        return GSORT_OK;
-    }
-    if (!tmp) {  // the exact plans' ping-pong buffer, allocated only when one of them runs
-        ST_TRY(ensure(c, c->slot[S_TMP], n * 4));
-        tmp = slot_ptr<uint32_t>(c, S_TMP);
-    }
-    if (c->plan16 && (!group16 || out16) && n < (1ull << 32)) {
-        const int lp = c->last_plan;
-        const gsort_status st =
-            msd_sort_h16(c, in, n, out, tmp, stats, group16, out16, group16 ? gb : nullptr);
-        c->last_plan = lp;
-        return st;
-    }
-    ST_TRY(ensure_pass_scratch(c, n));
-    uint64_t *totals = reinterpret_cast<uint64_t *>(c->d_small + OFF_TOT);
-    uint64_t *bases = reinterpret_cast<uint64_t *>(c->d_small + OFF_BASES);
-    ST_TRY(ensure_list(c, c->m_next[0], kRadix));
-    for (auto &b : c->m_local) ST_TRY(ensure_list(c, b, kRadix));
-    auto lists = [&](int next) { return work_lists(c, next); };
-
-    // level 3: global tiles
-    hipEvent_t t = tic(c);
-    HIP_TRY(c, launch_tile_counts1(in, n, 24, true, d_tcounts(c), c->stream));
-    HIP_TRY(c, launch_scan_tiles(d_tcounts(c), n, d_gsum(c), totals, bases, c->stream));
-    toc(c, PH_COUNT, t);
-    t = tic(c);
-    HIP_TRY(c, launch_partition(in, tmp, n, 24, d_tcounts(c), d_gsum(c), bases, true, c->stream));
-    toc(c, PH_LEVEL3, t);
-    if (stats) stats->keys_level[0] += n;
-    HIP_TRY(c, hipMemsetAsync(ctr, 0, kCtrBytes, c->stream));
-    WorkLists wl3 = lists(0);
-    wl3.force_next = group16;  // every level-3 bucket goes through level 2
-    HIP_TRY(c, launch_classify_buckets(bases, totals, wl3, c->stream));
-    uint64_t h[3 * (kLocalClasses + 1)];  // {entries, keys, longest}: next level, K11 classes
-    ST_TRY(read_counters(c, h));
-    c->group16_nseg = h[0];
-    int levels = 1;
-    ST_TRY(msd_levels(c, 2, tmp, out, tmp, 0, h, stats, &levels, group16 ? 2 : 0,
-                      group16 ? out16 : nullptr));
-    if (stats) stats->passes_run = levels;
-    return GSORT_OK;
-}
-
-// tmp == nullptr: S_TMP, ensured only if the plan that runs needs a second buffer
-gsort_status local_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *out,
-                        uint32_t *tmp, int *passes_run, gsort_stats *stats = nullptr,
-                        bool allow_est = false) {
-    if (stats) stats->local_algo = c->local_algo;
-    if (c->local_algo == GSORT_LOCAL_LSD) {
-        if (!tmp) {
-            ST_TRY(ensure(c, c->slot[S_TMP], std::max<uint64_t>(n, 1) * 4));
-            tmp = slot_ptr<uint32_t>(c, S_TMP);
-        }
-        return lsd_sort(c, in, n, out, tmp, passes_run);
-    }
-    gsort_stats tmp_st;
-    memset(&tmp_st, 0, sizeof(tmp_st));
-    gsort_stats *st = stats ? stats : &tmp_st;
-    const int before = st->passes_run;
-    ST_TRY(msd_sort(c, in, n, out, tmp, st, false, nullptr, nullptr, allow_est));
-    if (passes_run) *passes_run = st->passes_run;
-    if (stats) stats->passes_run = std::max(before, st->passes_run);
-    return GSORT_OK;
-}
-
-// ---- receive side: P sorted runs (after an exchange) -> one sorted block ---------------------
-// Replaces the re-sort of the received keys (the reference's final qsort, mpi_sample_sort.c:174;
-// for the radix path the last pass's placement, mpi_radix_sort.c:185-192).  The runs are
-// bucketed by their top 16 bits with binary searches (no pass over the keys), and K11g sorts
-// every bucket's low 16 bits straight from the P pieces: one read + one write per key.  Buckets
-// larger than kLocalMax are gathered into place and finish through the MSD levels 1 and 0.
-// recv holds the P runs back to back (run p has rlen[p] keys), each grouped by the top 16 bits
-// (ordered u32): int32 keys, or with packed16 only their low 16 bits, in which case the caller
-// has already filled c->m_rpos (pos[p][h], launch_pos_from_meta).
-// bucket sizes (65536) + starts (65537) + row-scan partials (64 x 64), u64
-constexpr size_t kBsizeBytes = ((size_t)2 * kBuckets16 + 1 + 65 * 64) * 8;
-
-// (a - b) / sizeof(T) for pointers into different allocations, as a u64 (two's complement for
-// a negative offset): integer arithmetic, never a pointer difference across allocations
-template <typename T>
-uint64_t elem_offset(const T *a, const T *b) {
-    const int64_t d = (int64_t)(reinterpret_cast<uintptr_t>(a) - reinterpret_cast<uintptr_t>(b));
-    return (uint64_t)(d / (int64_t)sizeof(T));
-}
-
-// self (int32 runs only): run `self_rank` was not received -- it lies at self_src (the
-// sender's sorted block), and the kernels read it there through a run offset taken relative to
-// recv (mod 2^64); the MSD fallback, which needs the runs back to back, copies it in first.
-// Every receive bucket of the lists wl (counts h, read_counters layout) sorted from its P
-// pieces into out: K11g by size class, K18c (or, GSORT_RECV_CX=-1, the two-read K18) past
-// kLocalMax; classes >= c->recv_cx go to K18c as well.  With list0, list 0 is sorted too (it
-// must then hold no bucket past kHxMax).
-gsort_status sort_recv_lists(gsort_ctx *c, const void *recv, bool packed16, const uint64_t *pos,
-                             const uint64_t *roff, int P, const uint64_t *bstart,
-                             const WorkLists &wl, const uint64_t *h, uint32_t *out,
-                             gsort_stats *stats, bool list0 = true) {
-    // K18c with u8 bins (recv_cb 8): its wrapped buckets collect in m_fb (count at OFF_FBCTR)
-    // and one u16 launch after the lists redoes them, reading their count on the device
-    uint64_t cx_entries = 0;
-    for (int k = 0; k < kLocalClasses; ++k)
-        if (c->recv_cx > 0 && k + 1 >= c->recv_cx) cx_entries += h[3 * (k + 1)];
-    if (list0 && c->recv_cx > 0) cx_entries += h[0];
-    const bool cb8 = c->recv_cb == 8 && cx_entries;
-    uint64_t *fb = nullptr;
-    uint32_t *fb_ctr = reinterpret_cast<uint32_t *>(c->d_small + OFF_FBCTR);
-    if (cb8) {
-        ST_TRY(ensure_list(c, c->m_fb, cx_entries));
-        fb = reinterpret_cast<uint64_t *>(c->m_fb.p);
-        HIP_TRY(c, hipMemsetAsync(fb_ctr, 0, 4, c->stream));
-    }
-    for (int k = 0; k < kLocalClasses; ++k) {
-        const uint64_t *hk = h + 3 * (k + 1);
-        if (!hk[0]) continue;
-        if (c->recv_cx > 0 && k + 1 >= c->recv_cx)
-            HIP_TRY(c, launch_count_expand(recv, packed16, pos, roff, P, bstart, wl.list[k + 1],
-                                           (uint32_t)hk[0], c->ncu, out, c->stream, fb,
-                                           cb8 ? fb_ctr : nullptr));
-        else
-            HIP_TRY(c, launch_gather_sort(recv, packed16, pos, roff, P, bstart, wl.list[k + 1],
-                                          (uint32_t)hk[0], k + 1, c->atomic_rank, out,
-                                          c->stream));
-        if (stats) { stats->buckets_local += hk[0]; stats->keys_bucket_sort += hk[1]; }
-    }
-    if (h[0] && list0) {
-        if (c->recv_cx > 0)
-            HIP_TRY(c, launch_count_expand(recv, packed16, pos, roff, P, bstart, wl.list[0],
-                                           (uint32_t)h[0], c->ncu, out, c->stream, fb,
-                                           cb8 ? fb_ctr : nullptr));
-        else
-            HIP_TRY(c, launch_hist_expand(recv, packed16, pos, roff, P, bstart, wl.list[0],
-                                          (uint32_t)h[0], out, c->stream));
-        if (stats) { stats->buckets_local += h[0]; stats->keys_bucket_sort += h[1]; }
-    }
-    if (cb8)  // the wrapped buckets (usually none: its workgroups return at once)
-        HIP_TRY(c, launch_count_expand(recv, packed16, pos, roff, P, bstart, fb,
-                                       (uint32_t)cx_entries, c->ncu, out, c->stream, nullptr,
-                                       nullptr, fb_ctr));
-    return GSORT_OK;
-}
-
-gsort_status recv_sort(gsort_ctx *c, const void *recv, bool packed16,
-                       const std::vector<uint64_t> &rlen, uint64_t n, uint32_t *out,
-                       uint32_t *tmp, gsort_stats *stats, int self_rank = -1,
-                       const int32_t *self_src = nullptr) {
-    const int P = (int)rlen.size();
-    if (n == 0) return GSORT_OK;
-    if (!packed16 && (P > 64 || c->local_algo == GSORT_LOCAL_LSD)) {  // K11g: <= 64 pieces
-        if (self_src && rlen[self_rank]) {
-            uint64_t o = 0;
-            for (int p = 0; p < self_rank; ++p) o += rlen[p];
-            HIP_TRY(c, hipMemcpyAsync(static_cast<int32_t *>(const_cast<void *>(recv)) + o,
-                                      self_src, rlen[self_rank] * 4, hipMemcpyDeviceToDevice,
-                                      c->stream));
-        }
-        int pr = 0;
-        return local_sort(c, reinterpret_cast<const uint32_t *>(recv), n, out, tmp, &pr, stats);
-    }
-    if (P > 64) return set_err(c, GSORT_EINVAL, "packed exchange supports at most 64 ranks");
-    hipEvent_t t = tic(c);
-    ST_TRY(ensure(c, c->m_rpos, (size_t)P * (kBuckets16 + 1) * 8));
-    ST_TRY(ensure(c, c->m_bsize, kBsizeBytes));
-    ST_TRY(ensure_list(c, c->m_next[0], kBuckets16));
-    for (auto &b : c->m_local) ST_TRY(ensure_list(c, b, kBuckets16));
-    uint64_t *h_r = reinterpret_cast<uint64_t *>(c->h_small + OFF_PLAN);
-    uint64_t *d_r = reinterpret_cast<uint64_t *>(c->d_small + OFF_PLAN);
-    HIP_TRY(c, hipStreamSynchronize(c->stream));  // h_r may still feed an earlier copy
-    uint64_t off = 0;
-    for (int p = 0; p < P; ++p) { h_r[p] = off; h_r[P + p] = rlen[p]; off += rlen[p]; }
-    if (self_src)
-        h_r[self_rank] = elem_offset(self_src, static_cast<const int32_t *>(recv));
-    HIP_TRY(c, hipMemcpyAsync(d_r, h_r, (size_t)2 * P * 8, hipMemcpyHostToDevice, c->stream));
-    uint64_t *pos = reinterpret_cast<uint64_t *>(c->m_rpos.p);
-    uint64_t *bsize = reinterpret_cast<uint64_t *>(c->m_bsize.p), *bstart = bsize + kBuckets16;
-    uint64_t *ctr = reinterpret_cast<uint64_t *>(c->d_small + OFF_CTR);
-    HIP_TRY(c, hipMemsetAsync(ctr, 0, kCtrBytes, c->stream));
-    if (!packed16)
-        HIP_TRY(c, launch_run_bounds(reinterpret_cast<const int32_t *>(recv), d_r, d_r + P, P, pos,
-                                     c->stream));
-    HIP_TRY(c, launch_recv_classify(pos, P, bsize, bstart, work_lists(c, 0),
-                                    bstart + kBuckets16 + 1, c->stream));
-    toc(c, PH_COUNT, t);
-    uint64_t h[3 * (kLocalClasses + 1)];
-    ST_TRY(read_counters(c, h));
-    if (check_mode()) {
-        uint64_t keys = h[1];
-        for (int k = 0; k < kLocalClasses; ++k) keys += h[3 * (k + 1) + 1];
-        if (keys != n)
-            return set_err(c, GSORT_EINVAL, "GSORT_CHECK receive lists hold " +
-                                                std::to_string(keys) + " keys, want " +
-                                                std::to_string(n) + " (rank " +
-                                                std::to_string(c->rank) + ")");
-        ST_TRY(check_bounds(c, bstart, kBuckets16 + 1, n, "receive bucket starts"));
-    }
-    const bool list0 = h[0] && h[2] <= kHxMax;  // else: a bucket past kHxMax (below)
-    t = tic(c);
-    ST_TRY(sort_recv_lists(c, recv, packed16, pos, d_r, P, bstart, work_lists(c, 0), h, out, stats,
-                           list0));
-    toc(c, PH_BUCKET, t);
-    if (h[0] && !list0) {  // all of list 0 into place, then MSD levels 1 and 0
-        HIP_TRY(c, launch_list_to_segments(reinterpret_cast<uint64_t *>(c->m_next[0].p),
-                                           (uint32_t)h[0], bstart, c->stream));
-        HIP_TRY(c, launch_gather_copy(recv, packed16, pos, d_r, P, bsize, bstart, out, c->stream));
-        for (int k = 3; k < 3 * (kLocalClasses + 1); ++k) h[k] = 0;
-        int levels = 0;
-        ST_TRY(msd_levels(c, 1, out, out, tmp, 0, h, stats, &levels));
-    }
-    return GSORT_OK;
-}
-
-// Allgather one u64 per rank into host memory (counts used to size RCCL messages).
-gsort_status allgather_u64(gsort_ctx *c, uint64_t v, std::vector<uint64_t> &out) {
-    out.assign(c->nranks, 0);
-    if (c->nranks == 1) { out[0] = v; return GSORT_OK; }
-    uint64_t *h = reinterpret_cast<uint64_t *>(c->h_small + OFF_PLAN);
-    uint64_t *d = reinterpret_cast<uint64_t *>(c->d_small + OFF_PLAN);
-    h[0] = v;
-    HIP_TRY(c, hipMemcpyAsync(d, h, 8, hipMemcpyHostToDevice, c->stream));
-    ST_TRY(comm_try(c, c->comm->allgather(d, d + 1, 8, c->stream)));
-    HIP_TRY(c, hipMemcpyAsync(h + 1, d + 1, 8 * c->nranks, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
-    for (int r = 0; r < c->nranks; ++r) out[r] = h[1 + r];
-    return GSORT_OK;
-}
-
-void block_of(uint64_t N, int P, int r, uint64_t *B, uint64_t *len) {
-    *B = P ? (N + P - 1) / P : 0;
-    const uint64_t lo = (uint64_t)r * *B;
-    *len = lo >= N ? 0 : std::min(*B, N - lo);
-}
-
-// Sort the listed groups {start, len} of an int32 block in place on their low 16 bits (their
-// top 16 bits are equal): K11 for groups of <= kLocalMax keys, the LSD passes otherwise.
-gsort_status sort_groups(gsort_ctx *c, int32_t *a,
-                         const std::vector<std::pair<uint64_t, uint64_t>> &groups) {
-    std::vector<uint64_t> small[kLocalClasses];
-    for (const auto &gr : groups) {
-        const int k = local_class(gr.second);
-        if (k) {
-            small[k - 1].push_back(gr.first);
-            small[k - 1].push_back(gr.second);
-            continue;
-        }
-        ST_TRY(ensure(c, c->m_bseg, gr.second * 8));
-        uint32_t *t0 = reinterpret_cast<uint32_t *>(c->m_bseg.p), *t1 = t0 + gr.second;
-        int pr = 0;  // lsd_sort leaves its result in its `out` (t0)
-        ST_TRY(lsd_sort(c, reinterpret_cast<const uint32_t *>(a + gr.first), gr.second, t0, t1,
-                        &pr));
-        HIP_TRY(c, hipMemcpyAsync(a + gr.first, t0, gr.second * 4, hipMemcpyDeviceToDevice,
-                                  c->stream));
-    }
-    for (int k = 0; k < kLocalClasses; ++k) {
-        if (small[k].empty()) continue;
-        ST_TRY(ensure(c, c->m_blist, small[k].size() * 8));
-        HIP_TRY(c, hipMemcpyAsync(c->m_blist.p, small[k].data(), small[k].size() * 8,
-                                  hipMemcpyHostToDevice, c->stream));
-        uint32_t *ab = reinterpret_cast<uint32_t *>(a);
-        HIP_TRY(c, launch_local_sort(ab, ab, reinterpret_cast<uint64_t *>(c->m_blist.p),
-                                     (uint32_t)(small[k].size() / 2), k + 1, 2, true,
-                                     c->atomic_rank, c->stream));
-        HIP_TRY(c, hipStreamSynchronize(c->stream));  // small[k] is host memory
-    }
-    return GSORT_OK;
-}
-
-// The same on the packed send buffer: groups = {16-bit bucket h, first position}, ends[i] =
-// the group's end (gb[h + 1]).  Each group is rebuilt as int32 keys in scratch, sorted by
-// sort_groups (K11 or LSD passes by size), and packed back in place.
-gsort_status sort_groups16(gsort_ctx *c, uint16_t *pack,
-                           const std::vector<std::pair<uint64_t, uint64_t>> &groups,
-                           const std::vector<uint64_t> &ends) {
-    uint64_t total = 0;
-    for (size_t i = 0; i < groups.size(); ++i) total += ends[i] - groups[i].second;
-    ST_TRY(ensure(c, c->m_g16, std::max<uint64_t>(total, 1) * 4));
-    int32_t *scr = reinterpret_cast<int32_t *>(c->m_g16.p);
-    std::vector<std::pair<uint64_t, uint64_t>> local;
-    uint64_t off = 0;
-    for (size_t i = 0; i < groups.size(); ++i) {
-        const uint64_t a = groups[i].second, len = ends[i] - a;
-        HIP_TRY(c, launch_unpack16(pack + a, len, (uint32_t)groups[i].first, scr + off,
-                                   c->stream));
-        local.push_back({off, len});
-        off += len;
-    }
-    ST_TRY(sort_groups(c, scr, local));
-    for (size_t i = 0; i < groups.size(); ++i)
-        HIP_TRY(c, launch_pack16(scr + local[i].first, local[i].second, pack + groups[i].second,
-                                 c->stream));
-    return GSORT_OK;
-}
-
-// ---- distributed radix (P > 1): local sort, exact splitters, ONE exchange, local sort ------
-// The reference keeps rank q on global positions [qB, (q+1)B) by routing every key through
-// rank 0 on each of its base-P passes (mpi_radix_sort.c:139 Scatter, :150-173 all-to-all,
-// :180-192 Gatherv).  Here: (1) each rank sorts its block (MSD local sort); (2) radix select of
-// the exact boundary keys: 4 rounds of 8 bits, each counting the keys below 257 thresholds per
-// boundary by binary search on the sorted blocks (K13) and all-gathering the counts; (3) the
-// cut of every block (gsort_plan_split: copies of a boundary key go left in rank order); (4) one
-// grouped send/recv of contiguous runs; (5) the received sorted runs are bucketed by their top
-// 16 bits and every bucket is finished in LDS (recv_sort).
-gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in,
-                              int32_t **d_out, uint64_t *n_out, gsort_stats *stats) {
-    const int P = c->nranks, me = c->rank;
-    std::vector<uint64_t> n_all;
-    ST_TRY(allgather_u64(c, n_in, n_all));
-    uint64_t N = 0;
-    for (uint64_t v : n_all) N += v;
-    uint64_t B, mine;
-    block_of(N, P, me, &B, &mine);
-    // the packed exchange sends one u32 count per (destination, 16-bit bucket): every rank's
-    // block, and so every count, must stay below 2^32 keys (decided identically on all ranks)
-    for (int r = 0; r < P; ++r)
-        if (n_all[r] >= (1ull << 32))
-            return set_err(c, GSORT_EINVAL, "radix: a rank holds >= 2^32 keys (rank " +
-                                                std::to_string(r) + "); split the input further");
-    const uint64_t cap = std::max<uint64_t>(std::max(n_in, mine), 1);
-    ST_TRY(ensure(c, c->slot[S_TMP], cap * 4));
-    ST_TRY(ensure(c, c->slot[S_RECV], std::max<uint64_t>(mine, 1) * 4));
-    ST_TRY(ensure(c, c->slot[S_OUT], std::max<uint64_t>(mine, 1) * 4));
-    ST_TRY(ensure(c, c->m_gb, (size_t)(kBuckets16 + 1) * 8));
-    ST_TRY(ensure(c, c->m_pack, std::max<uint64_t>(n_in, 1) * 2));
-    uint64_t *gb = reinterpret_cast<uint64_t *>(c->m_gb.p);
-    uint16_t *pack = reinterpret_cast<uint16_t *>(c->m_pack.p);
-    // (1) group the block by its top 16 bits (MSD levels 3 and 2 only: the receivers sort the
-    // low 16 bits anyway).  Level 2 stores just the low 16 bits of every key -- the packed send
-    // buffer -- and the 16-bit bucket bounds gb come from the MSD plan (K17), not the keys.  A
-    // block of <= kLocalMax keys is sorted whole in LDS instead, then bounded and packed.
-    if (stats) stats->local_algo = c->local_algo;
-    const bool packed_msd = n_in > kLocalMax;
-    hipEvent_t t;
-    {
-        gsort_stats tmp_st;
-        memset(&tmp_st, 0, sizeof(tmp_st));
-        int32_t *sorted = nullptr;
-        if (!packed_msd) {
-            ST_TRY(ensure(c, c->slot[S_SORTED], std::max<uint64_t>(n_in, 1) * 4));
-            sorted = slot_ptr<int32_t>(c, S_SORTED);
-        }
-        ST_TRY(msd_sort(c, reinterpret_cast<const uint32_t *>(d_keys), n_in,
-                        reinterpret_cast<uint32_t *>(sorted), slot_ptr<uint32_t>(c, S_TMP),
-                        stats ? stats : &tmp_st, true, packed_msd ? pack : nullptr, gb));
-        t = tic(c);
-        if (packed_msd && c->plan16) {
-            // gb written by the two-level plan
-        } else if (packed_msd) {
-            HIP_TRY(c, launch_gb_from_plan(reinterpret_cast<uint64_t *>(c->d_small + OFF_BASES),
-                                           reinterpret_cast<uint64_t *>(c->d_small + OFF_TOT),
-                                           reinterpret_cast<uint64_t *>(c->m_next[0].p),
-                                           (uint32_t)c->group16_nseg,
-                                           reinterpret_cast<uint64_t *>(c->m_cstart.p), n_in,
-                                           gb, c->stream));
-        } else {
-            uint64_t *h_one = reinterpret_cast<uint64_t *>(c->h_small + OFF_ONE);
-            uint64_t *d_one = reinterpret_cast<uint64_t *>(c->d_small + OFF_ONE);
-            HIP_TRY(c, hipStreamSynchronize(c->stream));  // h_one may feed an earlier copy
-            h_one[0] = 0;
-            h_one[1] = n_in;
-            HIP_TRY(c, hipMemcpyAsync(d_one, h_one, 16, hipMemcpyHostToDevice, c->stream));
-            HIP_TRY(c, launch_run_bounds(sorted, d_one, d_one + 1, 1, gb, c->stream));
-            HIP_TRY(c, launch_pack16(sorted, n_in, pack, c->stream));
-        }
-        toc(c, PH_PLACE, t);
-    }
-    int pr = stats ? stats->passes_run : 0;
-    if (check_mode()) ST_TRY(check_bounds(c, gb, kBuckets16 + 1, n_in, "sender bucket bounds"));
-
-    // (2) radix select of v_q, the g_q-th smallest key, for the P-1 inner boundaries: 4 rounds of
-    // 8 bits, every round decided on the device (K13s sums the all-gathered counts, picks the
-    // digit and writes the next round's thresholds), and after round 1 -- the boundaries'
-    // 16-bit groups known -- K13g sorts each boundary group in place in the packed buffer, so
-    // rounds 2 and 3 binary-search it and the cut splits it by value.  The host waits ONCE, for
-    // the last round's counts (the cut and the exchange sizes RCCL needs on the host).  A
-    // boundary group past K13g's 32 768 keys (skewed input) is flagged in the count rows of
-    // rounds 2 and 3, so every rank sees it: all ranks then sort the groups on the host path and
-    // repeat rounds 2 and 3 with the host between them (select_rounds below).
-    const int nb = P - 1, M = 257, W = nb * M + nb;  // count row: nb x M counts + nb K13g flags
-    std::vector<uint64_t> g(nb), prefix(nb, 0), hx((size_t)2 * nb + (size_t)nb * M),
-        all((size_t)P * W);
-    std::vector<int> dsel(nb, 0);
-    for (int q = 0; q < nb; ++q) g[q] = std::min<uint64_t>((uint64_t)(q + 1) * B, N);
-    ST_TRY(ensure(c, c->m_split, (size_t)std::max(nb, 1) * (M * 16 + 32)));
-    ST_TRY(ensure(c, c->slot[S_STAGE], (size_t)P * std::max(W, 1) * 8));
-    // m_split: prefix (nb) | g (nb) | thresholds (nb x M) | counts (nb x M) + flags (nb), u64
-    uint64_t *d_pref = reinterpret_cast<uint64_t *>(c->m_split.p), *d_g = d_pref + nb;
-    uint64_t *d_xs = d_g + nb;
-    uint64_t *d_cnt = d_xs + (size_t)nb * M;
-    const uint64_t *d_all = reinterpret_cast<const uint64_t *>(c->slot[S_STAGE].p);
-    // rounds k0 .. 3 from the thresholds in d_xs (K13g after round 1 when k0 == 0), then the last
-    // round's rows and the boundary keys to the host
-    auto select_rounds = [&](int k0) -> gsort_status {
-        for (int k = k0; k < 4; ++k) {
-            HIP_TRY(c, launch_count_below16(pack, gb, d_xs, nb * M, d_cnt, c->stream));
-            ST_TRY(comm_try(c, c->comm->allgather(d_cnt, c->slot[S_STAGE].p, (size_t)W * 8,
-                                                  c->stream)));
-            HIP_TRY(c, launch_select_digit(d_all, W, d_g, N, P, nb, M, 24 - 8 * k, d_pref, d_xs,
-                                           c->stream));
-            if (k == 1)
-                HIP_TRY(c, launch_boundary_sort16(pack, gb, d_pref, d_g, N, nb, c->atomic_rank,
-                                                  d_cnt + (size_t)nb * M, c->stream));
-        }
-        HIP_TRY(c, hipMemcpyAsync(all.data(), d_all, all.size() * 8, hipMemcpyDeviceToHost,
-                                  c->stream));
-        HIP_TRY(c, hipMemcpyAsync(prefix.data(), d_pref, (size_t)nb * 8, hipMemcpyDeviceToHost,
-                                  c->stream));
-        HIP_TRY(c, hipStreamSynchronize(c->stream));
-        return GSORT_OK;
-    };
-    // the thresholds of round 0 (prefix 0) and of round 2 after the host path (prefix: the top
-    // 16 bits); prefix and g go along
-    auto put_thresholds = [&](int shift) -> gsort_status {
-        for (int q = 0; q < nb; ++q) { hx[q] = prefix[q]; hx[nb + q] = g[q]; }
-        for (int q = 0; q < nb; ++q)
-            for (int d = 0; d < M; ++d)
-                hx[2 * nb + (size_t)q * M + d] = prefix[q] + ((uint64_t)d << shift);
-        HIP_TRY(c, hipMemcpyAsync(d_pref, hx.data(), hx.size() * 8, hipMemcpyHostToDevice,
-                                  c->stream));
-        return GSORT_OK;
-    };
-    t = tic_rec(c);
-    if (nb > 0) {  // (one rank: no boundary, nothing to select)
-        ST_TRY(put_thresholds(24));
-        ST_TRY(select_rounds(0));
-        bool big = false;
-        for (int p = 0; p < P; ++p)
-            for (int q = 0; q < nb; ++q) big |= all[(size_t)p * W + (size_t)nb * M + q] != 0;
-        if (big) {  // a boundary group past K13g's reach on some rank: every rank takes this
-            std::vector<std::pair<uint64_t, uint64_t>> groups;  // {h, first position}
-            for (int q = 0; q < nb; ++q)
-                if (g[q] < N) groups.push_back({prefix[q] >> 16, 0});
-            std::sort(groups.begin(), groups.end());
-            groups.erase(std::unique(groups.begin(), groups.end()), groups.end());
-            std::vector<uint64_t> h_gb(2 * groups.size());
-            for (size_t i = 0; i < groups.size(); ++i)
-                HIP_TRY(c, hipMemcpyAsync(&h_gb[2 * i], gb + groups[i].first, 16,
-                                          hipMemcpyDeviceToHost, c->stream));
-            HIP_TRY(c, hipStreamSynchronize(c->stream));
-            std::vector<std::pair<uint64_t, uint64_t>> nonempty;
-            std::vector<uint64_t> ends;
-            for (size_t i = 0; i < groups.size(); ++i)
-                if (h_gb[2 * i + 1] > h_gb[2 * i]) {
-                    nonempty.push_back({groups[i].first, h_gb[2 * i]});
-                    ends.push_back(h_gb[2 * i + 1]);
-                }
-            if (!nonempty.empty()) ST_TRY(sort_groups16(c, pack, nonempty, ends));
-            for (int q = 0; q < nb; ++q) prefix[q] = prefix[q] >> 16 << 16;
-            ST_TRY(put_thresholds(8));
-            ST_TRY(select_rounds(2));
-        }
-        for (int q = 0; q < nb; ++q) dsel[q] = (int)(prefix[q] & 255u);
-    }
-    toc_rec(c, PH_SAMPLE, t);
-    // (3) cut points from the last round: lt = count(< v_q), le = count(< v_q + 1)
-    std::vector<uint64_t> lt((size_t)P * nb), le((size_t)P * nb), send(P), recv(P);
-    for (int p = 0; p < P; ++p)
-        for (int q = 0; q < nb; ++q) {
-            const uint64_t *row = &all[(size_t)p * W + (size_t)q * M];
-            lt[(size_t)p * nb + q] = g[q] >= N ? n_all[p] : row[dsel[q]];
-            le[(size_t)p * nb + q] = g[q] >= N ? n_all[p] : row[dsel[q] + 1];
-        }
-    gsort_status ps = gsort_plan_split(P, n_all.data(), lt.data(), le.data(), me, send.data(),
-                                       recv.data());
-    if (ps != GSORT_OK) return set_err(c, ps, "inconsistent splitter counts");
-    // (4) one exchange of the keys' low 16 bits: every destination block's keys lie in a known
-    // range of 16-bit buckets (from the boundary keys), so the top 16 bits travel as one count
-    // per (destination, bucket) instead of 2 bytes per key
-    std::vector<uint64_t> hlo(P), nh(P), cut(P + 1, 0);
-    for (int q = 0; q < P; ++q) {
-        const uint64_t lo = q == 0 ? 0 : (g[q - 1] >= N ? 0xFFFFFFFFull : prefix[q - 1]);
-        const uint64_t hi = q == P - 1 ? 0xFFFFFFFFull : (g[q] >= N ? 0xFFFFFFFFull : prefix[q]);
-        hlo[q] = lo >> 16;
-        nh[q] = (hi >> 16) - hlo[q] + 1;
-        cut[q + 1] = cut[q] + send[q];
-    }
-    // test hook GSORT_RCCL_SELF=1: the self pieces do go through the transport (RcclComm then
-    // sends them through ncclSend / ncclRecv: tests/test_gpu_rccl.py pins RCCL's message limit)
-    static const bool self_moved = getenv("GSORT_RCCL_SELF") && getenv("GSORT_RCCL_SELF")[0] == '1';
-    uint64_t meta_n = 0, meta_self = ~0ull;  // meta_self: this rank's own count section
-    std::vector<uint64_t> rng;
-    for (int q = 0; q < P; ++q)
-        if (send[q]) {
-            rng.insert(rng.end(), {cut[q], cut[q + 1], hlo[q], nh[q], meta_n});
-            if (q == me) meta_self = meta_n;
-            meta_n += nh[q];
-        }
-    uint64_t nsrc = 0;
-    for (int p = 0; p < P; ++p) nsrc += recv[p] ? 1 : 0;
-    ST_TRY(ensure(c, c->m_meta, (std::max<uint64_t>(meta_n, 1) + nsrc * nh[me] + 1) * 4 +
-                                    (rng.size() + P + 2) * 8));
-    uint32_t *meta_s = reinterpret_cast<uint32_t *>(c->m_meta.p);
-    // (one word of gap: an in-place self offset below, meta_self - (meta_r - meta_s), is then
-    // at most -2 and never the "no source" mark ~0)
-    uint32_t *meta_r = meta_s + std::max<uint64_t>(meta_n, 1) + 1;
-    uint64_t *d_tab = reinterpret_cast<uint64_t *>(
-        reinterpret_cast<char *>(c->m_meta.p) +
-        (((std::max<uint64_t>(meta_n, 1) + nsrc * nh[me] + 1) * 4 + 7) & ~size_t(7)));
-    std::vector<uint64_t> tab(rng);
-    std::vector<uint64_t> moff(P, ~0ull);
-    {
-        uint64_t k = 0;
-        for (int p = 0; p < P; ++p)
-            if (recv[p]) moff[p] = (k++) * nh[me];
-    }
-    // the rank's own counts are read where K15 writes them (an offset relative to meta_r, mod
-    // 2^64), like its own keys below: no self copy in the count exchange either
-    const bool meta_in_place = !self_moved && recv[me] && meta_self != ~0ull;
-    if (meta_in_place) moff[me] = meta_self - (uint64_t)(meta_r - meta_s);
-    tab.insert(tab.end(), moff.begin(), moff.end());
-    // staged through pinned memory (a pageable copy blocks the host in the runtime's staging):
-    // OFF_PLAN + 8 KiB is free here -- step (5) below uses OFF_PLAN's first 2P words, and
-    // nothing copies from this range after the stream syncs of the previous call
-    uint64_t *h_tab = reinterpret_cast<uint64_t *>(c->h_small + OFF_PLAN + 8192);
-    if (OFF_PLAN + 8192 + tab.size() * 8 > kSmallBytes)
-        return set_err(c, GSORT_EINVAL, "exchange table too large");
-    std::copy(tab.begin(), tab.end(), h_tab);
-    HIP_TRY(c, hipMemcpyAsync(d_tab, h_tab, tab.size() * 8, hipMemcpyHostToDevice, c->stream));
-    const uint64_t *d_rng = d_tab, *d_moff = d_tab + rng.size();
-    t = tic(c);
-    HIP_TRY(c, launch_meta_counts(gb, d_rng, (int)(rng.size() / 5), meta_s, c->stream));
-    toc(c, PH_PLACE, t);
-    std::vector<size_t> sc(P, 0), sd(P, 0), rc(P, 0), rd(P, 0);
-    {
-        uint64_t mo = 0, ro = 0;
-        for (int q = 0; q < P; ++q) {
-            if (send[q]) { sc[q] = nh[q] * 4; sd[q] = mo * 4; mo += nh[q]; }
-            if (recv[q]) { rc[q] = nh[me] * 4; rd[q] = ro * 4; ro += nh[me]; }
-        }
-        if (meta_in_place) sc[me] = rc[me] = 0;
-    }
-    std::vector<uint64_t> roffs(P + 1, 0);
-    for (int p = 0; p < P; ++p) roffs[p + 1] = roffs[p] + recv[p];
-    t = tic_rec(c);
-    ST_TRY(comm_try(c, c->comm->alltoallv(meta_s, sc.data(), sd.data(), meta_r, rc.data(),
-                                          rd.data(), c->stream)));
-    toc_rec(c, PH_EXCH, t);
-    for (int q = 0; q < P; ++q)
-        if (stats && q != me) {
-            stats->bytes_sent += send[q] * 2;
-            stats->max_pair_bytes = std::max<uint64_t>(stats->max_pair_bytes, send[q] * 2);
-        }
-    if (roffs[P] != mine) return set_err(c, GSORT_EINVAL, "exchange plan does not fill the block");
-    // the payload, queued right behind the counts: the receive plan below overlaps it.  The
-    // rank's own piece is not moved at all: the receive kernels read it where it lies in the
-    // send buffer (its run offset below is taken relative to rbuf, mod 2^64) -- at P = 1 that is
-    // the whole 512 MiB of a 2^28-key block, at P = 8 an eighth of it
-    uint16_t *rbuf = slot_ptr<uint16_t>(c, S_RECV);
-    t = tic_rec(c);
-    for (int q = 0; q < P; ++q) {
-        const bool self = q == me && !self_moved;
-        sc[q] = self ? 0 : send[q] * 2;
-        sd[q] = cut[q] * 2;
-        rc[q] = self ? 0 : recv[q] * 2;
-        rd[q] = roffs[q] * 2;
-    }
-    ST_TRY(comm_try(c, c->comm->alltoallv(pack, sc.data(), sd.data(), rbuf, rc.data(), rd.data(),
-                                          c->stream)));
-    toc_rec(c, PH_EXCH, t);
-    if (stats) stats->exchanges = 1;
-    // (5) the receive plan from the counts alone: run bounds, bucket starts, the K11g / K18
-    // work lists of this rank's bucket range
-    t = tic(c);
-    ST_TRY(ensure(c, c->m_rpos, (size_t)P * (kBuckets16 + 1) * 8));
-    ST_TRY(ensure(c, c->m_bsize, kBsizeBytes));
-    ST_TRY(ensure_list(c, c->m_next[0], kBuckets16));
-    for (auto &b : c->m_local) ST_TRY(ensure_list(c, b, kBuckets16));
-    uint64_t *pos = reinterpret_cast<uint64_t *>(c->m_rpos.p);
-    uint64_t *bsize = reinterpret_cast<uint64_t *>(c->m_bsize.p), *bstart = bsize + kBuckets16;
-    uint64_t *h_r = reinterpret_cast<uint64_t *>(c->h_small + OFF_PLAN);
-    uint64_t *d_r = reinterpret_cast<uint64_t *>(c->d_small + OFF_PLAN);
-    // (no stream sync for h_r: nothing has copied from OFF_PLAN since allgather_u64's sync --
-    // the select stages through host vectors -- and a sync here idled the GPU ~40 us)
-    for (int p = 0; p < P; ++p) { h_r[p] = roffs[p]; h_r[P + p] = recv[p]; }
-    if (!self_moved)  // the self piece, in place: its offset from rbuf in keys, from integer
-        h_r[me] = elem_offset(pack + cut[me], rbuf);  // addresses (mod 2^64, run_ptr)
-    HIP_TRY(c, hipMemcpyAsync(d_r, h_r, (size_t)2 * P * 8, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(c, hipMemsetAsync(c->d_small + OFF_CTR, 0, kCtrBytes, c->stream));
-    // the runs' bucket bounds and the bucket starts in one row scan of P + 1 rows (the last
-    // row is every bucket's total over the sources); classify reads the sizes off bstart
-    HIP_TRY(c, launch_recv_plan_from_meta(meta_r, d_moff, (uint32_t)hlo[me], (uint32_t)nh[me], P,
-                                          pos, bstart, bstart + kBuckets16 + 1, c->stream));
-    const WorkLists wl = work_lists(c, 0);
-    HIP_TRY(c, launch_classify_range(nullptr, bstart, wl, (uint32_t)hlo[me],
-                                     (uint32_t)(hlo[me] + nh[me]), c->stream));
-    toc(c, PH_COUNT, t);
-    uint64_t h[3 * (kLocalClasses + 1)];
-    ST_TRY(read_counters(c, h));
-    if (check_mode()) {
-        for (int p = 0; p < P; ++p)
-            ST_TRY(check_bounds(c, pos + (size_t)p * (kBuckets16 + 1), kBuckets16 + 1, recv[p],
-                                "received run bounds"));
-        uint64_t keys = 0;
-        for (int l = 0; l <= kLocalClasses; ++l) keys += h[3 * l + 1];
-        if (keys != mine)
-            return set_err(c, GSORT_EINVAL, "GSORT_CHECK receive lists hold " +
-                                                std::to_string(keys) + " keys, want " +
-                                                std::to_string(mine) + " (rank " +
-                                                std::to_string(me) + ")");
-    }
-    // (6) every bucket sorted from its P pieces: K11g by size class, K18 past kLocalMax; a
-    // bucket past K18's reach sends the block through recv_sort's MSD levels 1 and 0
-    t = tic(c);
-    uint32_t *out = slot_ptr<uint32_t>(c, S_OUT);
-    if (h[0] && h[2] > kHxMax) {  // recv_sort wants the P runs back to back in rbuf
-        if (recv[me] && !self_moved)
-            HIP_TRY(c, hipMemcpyAsync(rbuf + roffs[me], pack + cut[me], recv[me] * 2,
-                                      hipMemcpyDeviceToDevice, c->stream));
-        ST_TRY(recv_sort(c, rbuf, true, recv, mine, out, slot_ptr<uint32_t>(c, S_TMP), stats));
-    } else {
-        ST_TRY(sort_recv_lists(c, rbuf, true, pos, d_r, P, bstart, wl, h, out, stats));
-    }
-    toc(c, PH_MERGE, t);
-    if (stats) stats->passes_run = pr;
-    *d_out = slot_ptr<int32_t>(c, S_OUT);
-    *n_out = mine;
-    return GSORT_OK;
-}
-
-// ---- distributed LSD radix (P > 1, GSORT_LOCAL_LSD) ----------------------------------------
-// Per non-trivial digit: local K1/K2 (tile counts; the digit totals of this rank), all-gather
-// of the P x 256 per-rank digit counts, local K3 (stable by digit), route contiguous slices to
-// the ranks owning their global positions (one grouped send/recv round), then place the
-// received runs (K8).  Keeps the reference's invariant that rank q holds positions
-// [qB, (q+1)B) after each pass (mpi_radix_sort.c:139,:192) without moving keys through rank 0.
-// sort_keys != nullptr (the reference-compat sort): the passes sort the u32 keys sort_keys[i]
-// (never flipped) stably and d_keys[i] travels with them as the value; the output is the
-// values.  Keys and values go through the same exchange and placement, so the order is
-// (key, source rank, source order), the reference's per-pass order (mpi_radix_sort.c:164-192).
-gsort_status radix_dist(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in, int32_t **d_out,
-                        uint64_t *n_out, gsort_stats *stats, const uint32_t *sort_keys = nullptr) {
-    const int P = c->nranks, me = c->rank;
-    const bool kv = sort_keys != nullptr, fl = !kv;
-    std::vector<uint64_t> n_all;
-    ST_TRY(allgather_u64(c, n_in, n_all));
-    uint64_t N = 0;
-    for (uint64_t v : n_all) N += v;
-    uint64_t B, mine;
-    block_of(N, P, me, &B, &mine);
-    const uint64_t cap = std::max<uint64_t>(std::max(n_in, B), 1);
-    for (Slot s : {S_CUR, S_SORTED, S_RECV, S_OUT}) ST_TRY(ensure(c, c->slot[s], cap * 4));
-    if (kv)
-        for (DevBuf *b : {&c->slot[S_TMP], &c->m_vtmp[0], &c->m_vtmp[1], &c->m_vtmp[2]})
-            ST_TRY(ensure(c, *b, cap * 4));
-    ST_TRY(ensure_pass_scratch(c, cap));
-    if (N == 0) { *d_out = slot_ptr<int32_t>(c, S_OUT); *n_out = 0; return GSORT_OK; }
-
-    // K1 on the input: tile counts of digit 0 + all four digit histograms; all-gathered they
-    // give the global digit totals (invariant under the exchange), so every rank skips the
-    // same trivial digits.
-    uint64_t *d_hist = reinterpret_cast<uint64_t *>(c->d_small + OFF_HIST);
-    uint64_t *d_tot = reinterpret_cast<uint64_t *>(c->d_small + OFF_TOT);
-    const uint32_t *src = kv ? sort_keys : reinterpret_cast<const uint32_t *>(d_keys);
-    HIP_TRY(c, hipMemsetAsync(d_hist, 0, 4 * kRadix * 8, c->stream));
-    hipEvent_t t = tic(c);
-    HIP_TRY(c, launch_tile_counts(src, n_in, 0, fl, d_tcounts(c), d_hist, c->stream));
-    toc(c, PH_COUNT, t);
-    DevBuf &allh = c->slot[S_STAGE];
-    ST_TRY(ensure(c, allh, (size_t)P * 4 * kRadix * 8));
-    ST_TRY(comm_try(c, c->comm->allgather(d_hist, allh.p, 4 * kRadix * 8, c->stream)));
-    std::vector<uint64_t> H((size_t)P * 4 * kRadix);
-    HIP_TRY(c, hipMemcpyAsync(H.data(), allh.p, H.size() * 8, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
-    std::vector<int> active;
-    for (int p = 0; p < 4; ++p) {
-        uint64_t mx = 0;
-        for (int d = 0; d < kRadix; ++d) {
-            uint64_t tot = 0;
-            for (int r = 0; r < P; ++r) tot += H[((size_t)r * 4 + p) * kRadix + d];
-            mx = std::max(mx, tot);
-        }
-        if (mx < N) active.push_back(p);
-    }
-    if (active.empty()) active.push_back(0);  // still redistribute to balanced blocks
-
-    std::vector<uint64_t> hp((size_t)P * kRadix), send(P), recv(P), seg((size_t)4 * P * kRadix);
-    std::vector<size_t> sc(P), sd(P), rc(P), rd(P);
-    uint64_t n_src = n_in;
-    uint32_t *placed[2] = {slot_ptr<uint32_t>(c, S_CUR), slot_ptr<uint32_t>(c, kv ? S_TMP : S_OUT)};
-    // kv: the values' source, sorted / received copies and placed blocks (the last into S_OUT)
-    const uint32_t *vsrc = reinterpret_cast<const uint32_t *>(d_keys);
-    uint32_t *vsorted = reinterpret_cast<uint32_t *>(c->m_vtmp[0].p);
-    uint32_t *vrecv = reinterpret_cast<uint32_t *>(c->m_vtmp[1].p);
-    uint32_t *vplaced = reinterpret_cast<uint32_t *>(c->m_vtmp[2].p);
-    const int k = (int)active.size();
-    for (int i = 0; i < k; ++i) {
-        const int p = active[i];
-        const bool first = i == 0, last = i == k - 1;
-        // this rank's tile counts and totals of digit p, then everyone's totals
-        if (!(first && p == 0)) ST_TRY(count_tiles(c, src, n_src, p, first && fl));
-        uint32_t *sorted = slot_ptr<uint32_t>(c, S_SORTED);
-        ST_TRY(scan_and_scatter(c, src, sorted, n_src, p, first && fl, false, kv ? vsrc : nullptr,
-                                kv ? vsorted : nullptr));
-        if (n_src == 0) HIP_TRY(c, hipMemsetAsync(d_tot, 0, kRadix * 8, c->stream));
-        uint64_t *d_allt = reinterpret_cast<uint64_t *>(allh.p);
-        ST_TRY(comm_try(c, c->comm->allgather(d_tot, d_allt, kRadix * 8, c->stream)));
-        HIP_TRY(c, hipMemcpyAsync(hp.data(), d_allt, hp.size() * 8, hipMemcpyDeviceToHost,
-                                  c->stream));
-        HIP_TRY(c, hipStreamSynchronize(c->stream));
-
-        size_t nseg = 0;
-        ST_TRY(gsort_plan_radix_route(P, hp.data(), B, me, send.data(), recv.data(), seg.data(),
-                                      &nseg));
-        size_t so = 0, ro = 0;
-        for (int q = 0; q < P; ++q) {
-            sc[q] = send[q] * 4; sd[q] = so; so += sc[q];
-            rc[q] = recv[q] * 4; rd[q] = ro; ro += rc[q];
-            if (stats && q != me) {
-                stats->bytes_sent += sc[q] * (kv ? 2 : 1);
-                stats->max_pair_bytes = std::max<uint64_t>(stats->max_pair_bytes, sc[q]);
-            }
-        }
-        uint32_t *rbuf = slot_ptr<uint32_t>(c, S_RECV);
-        t = tic_rec(c);
-        ST_TRY(comm_try(c, c->comm->alltoallv(sorted, sc.data(), sd.data(), rbuf, rc.data(),
-                                              rd.data(), c->stream)));
-        if (kv)
-            ST_TRY(comm_try(c, c->comm->alltoallv(vsorted, sc.data(), sd.data(), vrecv,
-                                                  rc.data(), rd.data(), c->stream)));
-        toc_rec(c, PH_EXCH, t);
-        if (stats) stats->exchanges++;
-        // placement table: {offset in recv buffer, dest offset, length}
-        uint64_t *h_seg = reinterpret_cast<uint64_t *>(c->h_small + OFF_PLAN);
-        uint64_t *d_seg = reinterpret_cast<uint64_t *>(c->d_small + OFF_PLAN);
-        if (nseg * 24 > kSmallBytes - OFF_PLAN) return set_err(c, GSORT_EINVAL, "segment table");
-        HIP_TRY(c, hipStreamSynchronize(c->stream));  // h_seg may still feed an earlier copy
-        for (size_t s = 0; s < nseg; ++s) {
-            const uint64_t r = seg[4 * s];
-            h_seg[3 * s + 0] = rd[r] / 4 + seg[4 * s + 1];
-            h_seg[3 * s + 1] = seg[4 * s + 2];
-            h_seg[3 * s + 2] = seg[4 * s + 3];
-        }
-        HIP_TRY(c, hipMemcpyAsync(d_seg, h_seg, nseg * 24, hipMemcpyHostToDevice, c->stream));
-        uint32_t *dst = last && !kv ? slot_ptr<uint32_t>(c, S_OUT) : placed[i & 1];
-        t = tic(c);
-        if (!(kv && last))  // kv: the keys of the last pass are not needed
-            HIP_TRY(c, launch_place(rbuf, dst, d_seg, (int)nseg, mine, nullptr, 0, last && fl,
-                                    c->stream));
-        if (kv) {
-            uint32_t *vdst = last ? slot_ptr<uint32_t>(c, S_OUT) : vplaced;
-            HIP_TRY(c, launch_place(vrecv, vdst, d_seg, (int)nseg, mine, nullptr, 0, false,
-                                    c->stream));
-            vsrc = vdst;
-        }
-        toc(c, PH_PLACE, t);
-        src = dst;
-        n_src = mine;
-    }
-    if (stats) stats->passes_run = k;
-    *d_out = slot_ptr<int32_t>(c, S_OUT);
-    *n_out = mine;
-    return GSORT_OK;
-}
-
-// ---- reference-compat radix (gsort_set_ref_compat) -----------------------
-// The reference's radix sort is a stable sort of the values by the base-P digits of |v| that
-// number_digit_at extracts (mpi_radix_sort.c:54-58), loop = number_digits(max) of them (:100).
-// K20 + an all-gather give the global min / max, gsort_plan_ref_digits the reference's digit
-// plan, K19 the composite key of every value; then stable key-value LSD passes: locally, or
-// through radix_dist's exchange (kv), so rank q ends with positions [qB, (q+1)B).
-gsort_status radix_compat(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in, int32_t **d_out,
-                          uint64_t *n_out, gsort_stats *stats) {
-    const int Pref = c->ref_compat > 0 ? c->ref_compat : c->nranks;
-    std::vector<uint64_t> n_all;
-    ST_TRY(allgather_u64(c, n_in, n_all));
-    uint64_t N = 0;
-    for (uint64_t v : n_all) N += v;
-    const uint64_t Bref = (N + Pref - 1) / Pref;
-    if (N > 0 && (int64_t)N - (int64_t)(Bref * (uint64_t)(Pref - 1)) <= 0)
-        return set_err(c, GSORT_EINVAL, "ref compat: the reference's last block would be empty "
-                                        "(N < (P-1)*ceil(N/P) + 1, quirk Q8)");
-    const size_t cap = std::max<uint64_t>(n_in, 1) * 4;
-    ST_TRY(ensure(c, c->m_cmm, 16));
-    ST_TRY(ensure(c, c->m_ckey[0], cap));
-    // global min / max (K20)
-    int32_t *h_mm = reinterpret_cast<int32_t *>(c->h_small + OFF_PLAN);
-    HIP_TRY(c, hipStreamSynchronize(c->stream));  // h_small may feed an earlier copy
-    h_mm[0] = INT32_MAX;
-    h_mm[1] = INT32_MIN;
-    memset(h_mm + 2, 0, 8);  // K19's bad-key counter
-    HIP_TRY(c, hipMemcpyAsync(c->m_cmm.p, h_mm, 16, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(c, launch_minmax(d_keys, n_in, reinterpret_cast<int *>(c->m_cmm.p), c->stream));
-    HIP_TRY(c, hipMemcpyAsync(h_mm, c->m_cmm.p, 8, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
-    std::vector<uint64_t> mm;
-    ST_TRY(allgather_u64(c, (uint64_t)(uint32_t)h_mm[0] | ((uint64_t)(uint32_t)h_mm[1] << 32), mm));
-    int32_t gmin = INT32_MAX, gmax = -1;  // the reference's max_element starts at -1 (:77)
-    for (int r = 0; r < c->nranks; ++r) {
-        if (!n_all[r]) continue;
-        gmin = std::min(gmin, (int32_t)(uint32_t)mm[r]);
-        gmax = std::max(gmax, (int32_t)(uint32_t)(mm[r] >> 32));
-    }
-    if (N > 0 && gmin == INT32_MIN)
-        return set_err(c, GSORT_EINVAL, "ref compat: an INT_MIN key has no |v|; the reference "
-                                        "indexes a negative bucket there (quirk Q5)");
-    int loop = 0;
-    int32_t mod[64];
-    double scale[64];
-    if (gsort_plan_ref_digits(Pref, gmax, &loop, mod, scale, 64) != GSORT_OK)
-        return set_err(c, GSORT_EINVAL, "ref compat: digit plan");
-    uint32_t *key = reinterpret_cast<uint32_t *>(c->m_ckey[0].p);
-    if (loop < 1) {  // no pass (P = 1, Q1): the input order, only redistributed
-        HIP_TRY(c, hipMemsetAsync(key, 0, cap, c->stream));
-    } else {
-        HIP_TRY(c, launch_compat_keys(d_keys, n_in, Pref, loop, mod, scale, key,
-                                      reinterpret_cast<uint64_t *>(c->m_cmm.p) + 1, c->stream));
-        uint64_t *h_bad = reinterpret_cast<uint64_t *>(c->h_small + OFF_PLAN);
-        HIP_TRY(c, hipMemcpyAsync(h_bad, reinterpret_cast<uint64_t *>(c->m_cmm.p) + 1, 8,
-                                  hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(c, hipStreamSynchronize(c->stream));
-        std::vector<uint64_t> bad;
-        ST_TRY(allgather_u64(c, *h_bad, bad));
-        for (uint64_t b : bad)
-            if (b) return set_err(c, GSORT_EINVAL, "ref compat: a digit outside [0, P) (the "
-                                                   "reference indexes outside its buckets)");
-    }
-    if (c->comm) return radix_dist(c, d_keys, n_in, d_out, n_out, stats, key);
-    // one rank: the stable key-value LSD passes locally (K1 + four histograms, K2, K3 kv)
-    ST_TRY(ensure(c, c->slot[S_OUT], cap));
-    ST_TRY(ensure(c, c->m_ckey[1], cap));
-    ST_TRY(ensure(c, c->m_vtmp[0], cap));
-    ST_TRY(ensure(c, c->m_vtmp[1], cap));
-    ST_TRY(ensure_pass_scratch(c, n_in));
-    *d_out = slot_ptr<int32_t>(c, S_OUT);
-    *n_out = n_in;
-    if (n_in == 0) return GSORT_OK;
-    uint64_t *d_hist = reinterpret_cast<uint64_t *>(c->d_small + OFF_HIST);
-    uint64_t *h_hist = reinterpret_cast<uint64_t *>(c->h_small + OFF_HIST);
-    HIP_TRY(c, hipMemsetAsync(d_hist, 0, 4 * kRadix * 8, c->stream));
-    hipEvent_t t = tic(c);
-    HIP_TRY(c, launch_tile_counts(key, n_in, 0, false, d_tcounts(c), d_hist, c->stream));
-    toc(c, PH_COUNT, t);
-    HIP_TRY(c, hipMemcpyAsync(h_hist, d_hist, 4 * kRadix * 8, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
-    std::vector<int> active;
-    for (int p = 0; p < 4; ++p) {
-        const uint64_t *h = h_hist + p * kRadix;
-        if (*std::max_element(h, h + kRadix) < n_in) active.push_back(p);
-    }
-    if (active.empty()) {
-        HIP_TRY(c, launch_copy(reinterpret_cast<const uint32_t *>(d_keys),
-                               slot_ptr<uint32_t>(c, S_OUT), n_in, c->stream));
-        return GSORT_OK;
-    }
-    uint32_t *kb[2] = {key, reinterpret_cast<uint32_t *>(c->m_ckey[1].p)};
-    uint32_t *vb[2] = {reinterpret_cast<uint32_t *>(c->m_vtmp[0].p),
-                       reinterpret_cast<uint32_t *>(c->m_vtmp[1].p)};
-    const uint32_t *vsrc = reinterpret_cast<const uint32_t *>(d_keys);
-    const int k = (int)active.size();
-    for (int i = 0; i < k; ++i) {
-        const bool last = i == k - 1;
-        uint32_t *vdst = last ? slot_ptr<uint32_t>(c, S_OUT) : vb[i & 1];
-        if (!(i == 0 && active[0] == 0)) ST_TRY(count_tiles(c, kb[i & 1], n_in, active[i], false));
-        ST_TRY(scan_and_scatter(c, kb[i & 1], kb[(i & 1) ^ 1], n_in, active[i], false, false, vsrc,
-                                vdst));
-        vsrc = vdst;
-    }
-    if (stats) stats->passes_run = k;
-    return GSORT_OK;
-}
-
-// ---- sample sort ------------------------------------------------------------------------
-gsort_status sample_dist(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in, int32_t **d_out,
-                         uint64_t *n_out, gsort_stats *stats) {
-    const int P = c->nranks, me = c->rank;
-    std::vector<uint64_t> n_all;
-    ST_TRY(allgather_u64(c, n_in, n_all));
-    uint64_t N = 0;
-    for (uint64_t v : n_all) N += v;
-    // mpi_sample_sort.c:72 size_bucket = ceil(N/P); :89-90 k = 2P-1, interval = B / k
-    const uint64_t B = (N + P - 1) / P;
-    const int k = 2 * P - 1;
-    const uint64_t interval = B / k;
-    if (P * k > 1024) return set_err(c, GSORT_EINVAL, "too many ranks for sample sort");
-    for (int r = 0; r < P; ++r)  // :94-99, decided identically on every rank
-        if ((uint64_t)(k - 1) * interval >= n_all[r])
-            return set_err(c, GSORT_ENOSAMPLE,
-                           "no enough sample: rank " + std::to_string(r) + " holds " +
-                               std::to_string(n_all[r]) + " keys, needs index " +
-                               std::to_string((uint64_t)(k - 1) * interval));
-    const uint64_t cap = std::max<uint64_t>(n_in, 1);
-    ST_TRY(ensure(c, c->slot[S_SORTED], cap * 4));
-    int32_t *sorted = slot_ptr<int32_t>(c, S_SORTED);
-    int pr = 0;
-    ST_TRY(local_sort(c, reinterpret_cast<const uint32_t *>(d_keys), n_in,
-                      reinterpret_cast<uint32_t *>(sorted), nullptr, &pr, nullptr, true));
-
-    // K4 samples -> root (grouped send/recv), K5 on root, broadcast splitters
-    hipEvent_t t = tic_rec(c);
-    int32_t *d_samp = reinterpret_cast<int32_t *>(c->d_small + OFF_PLAN);
-    int32_t *d_all = d_samp + 64;
-    int32_t *d_spl = d_all + 1024 + 64;
-    uint64_t *d_bounds = reinterpret_cast<uint64_t *>(d_spl + 64);
-    HIP_TRY(c, launch_regular_sample(sorted, interval, k, d_samp, c->stream));
-    std::vector<size_t> sc(P, 0), sd(P, 0), rc(P, 0), rd(P, 0);
-    sc[0] = (size_t)k * 4;
-    if (me == 0)
-        for (int r = 0; r < P; ++r) { rc[r] = (size_t)k * 4; rd[r] = (size_t)r * k * 4; }
-    ST_TRY(comm_try(c, c->comm->alltoallv(d_samp, sc.data(), sd.data(), d_all, rc.data(),
-                                          rd.data(), c->stream)));
-    if (me == 0) HIP_TRY(c, launch_select_splitters(d_all, P * k, k, P - 1, d_spl, c->stream));
-    ST_TRY(comm_try(c, c->comm->bcast(d_spl, (size_t)(P - 1) * 4, 0, c->stream)));
-    HIP_TRY(c, launch_bucket_bounds(sorted, n_in, d_spl, P - 1, d_bounds, c->stream));
-    toc_rec(c, PH_SAMPLE, t);
-    int32_t *h_spl = reinterpret_cast<int32_t *>(c->h_small + OFF_PLAN);
-    uint64_t *h_bounds = reinterpret_cast<uint64_t *>(c->h_small + OFF_PLAN + 1024);
-    HIP_TRY(c, hipMemcpyAsync(h_spl, d_spl, (size_t)(P - 1) * 4, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipMemcpyAsync(h_bounds, d_bounds, (size_t)(P - 1) * 8, hipMemcpyDeviceToHost,
-                              c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
-    c->splitters.assign(h_spl, h_spl + P - 1);
-    c->bucket_counts.assign(P, 0);
-    uint64_t prev = 0;
-    for (int j = 0; j < P; ++j) {
-        const uint64_t end = j < P - 1 ? h_bounds[j] : n_in;
-        c->bucket_counts[j] = end - prev;
-        prev = end;
-    }
-    // bucket-count matrix: allgather P counts per rank (mpi_sample_sort.c:161,:168 sends the
-    // length in the MPI tag of a fixed-size message; here exact lengths size the messages)
-    uint64_t *d_cnt = reinterpret_cast<uint64_t *>(c->d_small + OFF_PLAN + 16384);
-    uint64_t *d_mat = d_cnt + 64;
-    uint64_t *h_cnt = reinterpret_cast<uint64_t *>(c->h_small + OFF_PLAN + 16384);
-    std::vector<uint64_t> M((size_t)P * P);
-    if (!c->sample_balanced) {
-        memcpy(h_cnt, c->bucket_counts.data(), (size_t)P * 8);
-        HIP_TRY(c, hipMemcpyAsync(d_cnt, h_cnt, (size_t)P * 8, hipMemcpyHostToDevice, c->stream));
-        ST_TRY(comm_try(c, c->comm->allgather(d_cnt, d_mat, (size_t)P * 8, c->stream)));
-        HIP_TRY(c, hipMemcpyAsync(M.data(), d_mat, M.size() * 8, hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(c, hipStreamSynchronize(c->stream));
-    } else {
-        // duplicate-aware buckets: keys < s_j (strict K6) and <= s_j of every rank, then the
-        // same cut rule as the distributed radix with the boundary clamped into s_j's copies
-        const int S = P - 1;
-        uint64_t *d_lt = d_bounds + 64;
-        HIP_TRY(c, launch_bucket_bounds(sorted, n_in, d_spl, S, d_lt, c->stream, true));
-        uint64_t *d_ll = d_cnt;  // this rank: [lt x S | le x S]
-        HIP_TRY(c, hipMemcpyAsync(d_ll, d_lt, (size_t)S * 8, hipMemcpyDeviceToDevice, c->stream));
-        HIP_TRY(c, hipMemcpyAsync(d_ll + S, d_bounds, (size_t)S * 8, hipMemcpyDeviceToDevice,
-                                  c->stream));
-        uint64_t *d_all2 = d_cnt + 64;
-        ST_TRY(comm_try(c, c->comm->allgather(d_ll, d_all2, (size_t)2 * S * 8, c->stream)));
-        std::vector<uint64_t> A((size_t)P * 2 * S), lt((size_t)P * S), le((size_t)P * S);
-        HIP_TRY(c, hipMemcpyAsync(A.data(), d_all2, A.size() * 8, hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(c, hipStreamSynchronize(c->stream));
-        for (int p = 0; p < P; ++p)
-            for (int j = 0; j < S; ++j) {
-                lt[(size_t)p * S + j] = A[(size_t)p * 2 * S + j];
-                le[(size_t)p * S + j] = A[(size_t)p * 2 * S + S + j];
-            }
-        // every rank plans every rank's row (host, identical inputs) -> the full matrix
-        std::vector<uint64_t> snd(P), rcv(P);
-        for (int p = 0; p < P; ++p) {
-            const gsort_status st =
-                gsort_plan_split_balanced(P, n_all.data(), lt.data(), le.data(), p, snd.data(),
-                                          rcv.data());
-            if (st != GSORT_OK) return set_err(c, st, "inconsistent sample bucket bounds");
-            for (int q = 0; q < P; ++q) M[(size_t)p * P + q] = snd[q];
-        }
-        for (int q = 0; q < P; ++q) c->bucket_counts[q] = M[(size_t)me * P + q];
-    }
-    uint64_t total = 0;
-    size_t so = 0, ro = 0;
-    for (int q = 0; q < P; ++q) {
-        sc[q] = c->bucket_counts[q] * 4; sd[q] = so; so += sc[q];
-        rc[q] = M[(size_t)q * P + me] * 4; rd[q] = ro; ro += rc[q];
-        total += M[(size_t)q * P + me];
-        if (stats && q != me) {
-            stats->bytes_sent += sc[q];
-            stats->max_pair_bytes = std::max<uint64_t>(stats->max_pair_bytes, sc[q]);
-        }
-    }
-    const uint64_t cap2 = std::max<uint64_t>(total, 1);
-    ST_TRY(ensure(c, c->slot[S_RECV], cap2 * 4));
-    ST_TRY(ensure(c, c->slot[S_OUT], cap2 * 4));
-    ST_TRY(ensure(c, c->slot[S_TMP], cap2 * 4));
-    int32_t *rbuf = slot_ptr<int32_t>(c, S_RECV);
-    // the rank's own bucket stays where it is (recv_sort reads it in place)
-    const size_t self_off = sd[me];
-    sc[me] = 0;
-    rc[me] = 0;
-    t = tic_rec(c);
-    ST_TRY(comm_try(c, c->comm->alltoallv(sorted, sc.data(), sd.data(), rbuf, rc.data(),
-                                          rd.data(), c->stream)));
-    toc_rec(c, PH_EXCH, t);
-    if (stats) stats->exchanges = 1;
-    // final local order of the received bucket (mpi_sample_sort.c:174): the P received runs
-    // are sorted slices of the senders' sorted blocks -> recv_sort
-    std::vector<uint64_t> rlen(P);
-    for (int q = 0; q < P; ++q) rlen[q] = M[(size_t)q * P + me];
-    t = tic(c);
-    ST_TRY(recv_sort(c, rbuf, false, rlen, total, slot_ptr<uint32_t>(c, S_OUT),
-                     slot_ptr<uint32_t>(c, S_TMP), stats, me, sorted + self_off / 4));
-    toc(c, PH_MERGE, t);
-    if (stats) stats->passes_run = pr;
-    *d_out = slot_ptr<int32_t>(c, S_OUT);
-    *n_out = total;
-    return GSORT_OK;
-}
-
 gsort_status check_ctx(gsort_ctx *c) { return c ? GSORT_OK : GSORT_EINVAL; }
 
-// The sort writes its scratch slots; an input living in one of them would be overwritten.
 gsort_status check_input(gsort_ctx *c, const int32_t *d_keys) {
     for (int s = 0; s < S_NSLOTS; ++s)
         if (s != S_IN && c->slot[s].p && (const void *)d_keys == c->slot[s].p)
@@ -2490,7 +609,8 @@ gsort_status create_common(gsort_ctx *c, int hip_device) {
     return check_lds_order(c);
 }
 
-}  // namespace
+}  // namespace rt
+}  // namespace gsort
 
 // =========================================================================================
 // C-ABI
