@@ -109,6 +109,8 @@ def lib():
     P, VP, SZ, I, U64 = (ctypes.POINTER, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
                          ctypes.c_uint64)
     for name in EXPORTS:
+        if os.environ.get("GSORT_LIB") and not hasattr(L, name):
+            continue  # (an older build loaded for a same-box A/B: what it lacks stays unused)
         getattr(L, name).restype = ctypes.c_int
     L.gsort_strerror.restype = ctypes.c_char_p
     L.gsort_last_error.restype = ctypes.c_char_p
@@ -116,7 +118,8 @@ def lib():
     L.gsort_get_uid.argtypes = [P(Uid)]
     L.gsort_get_uid_ipc.argtypes = [I, P(Uid)]
     L.gsort_visible_devices.argtypes = []
-    L.gsort_runtime_info.argtypes = [P(RuntimeInfo)]
+    if hasattr(L, "gsort_runtime_info"):
+        L.gsort_runtime_info.argtypes = [P(RuntimeInfo)]
     L.gsort_write_report.argtypes = [P(Report), I]
     L.gsort_create.argtypes = [P(VP), I, I, I, P(Uid)]
     L.gsort_group_create.argtypes = [P(VP), I]
