@@ -12,8 +12,13 @@ canonical splitmix64 generator on device (K10), so the data is synthetic and ide
 the oracle and the reference CPU run see.
 
 The timed region is K steps bracketed by a barrier + torch.cuda.synchronize() on both sides;
-the slowest rank's time is reported.  `roofline` prices the dominant kernel class (by total
-device time: K3u partition, K11 bucket sort or K3 LSD pass, 8 B/key algorithmic traffic each)
+the slowest rank's time is reported.  Before the W warm-up steps every rank runs the library's
+streaming copy for --settle-ms (default 100 ms; reported as `settle`): from idle the GPU needs
+tens of ms of load to reach its sustained clocks, and 5 warm-up sorts (~7 ms) did not get
+there -- the same build measured 1.364-1.369 ms per step without it, 1.331-1.335 ms with
+30-300 ms of copies first, 1.353 ms with 50 warm-up sorts.
+
+`roofline` prices the dominant kernel class (by total device time: K3u partition, K11 bucket sort or K3 LSD pass, 8 B/key algorithmic traffic each)
 with its average duration measured live by HIP events recorded on libgsort's own stream
 around every launch; `traffic` is the HBM bytes per launch from the rocprofv3 PMC summary in
 profiles/ (FETCH_SIZE x 2 + WRITE_SIZE, gfx950 correction) when one exists for this
@@ -51,6 +56,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--settle-ms", type=float, default=100.0,
+                    help="streaming copies for this long before the warm-up steps (0: none)")
     ap.add_argument("--algo", choices=["radix", "sample"], default="radix")
     ap.add_argument("--keys-log2", type=int, default=28)
     ap.add_argument("--dist", choices=["uniform", "zipf"], default="uniform")
@@ -543,6 +550,15 @@ def main():
     ctx.set_local_algo(gsort.LOCAL_MSD if a.local == "msd" else gsort.LOCAL_LSD)
     fn = ctx.radix if a.algo == "radix" else ctx.sample
 
+    settle = {"ms": 0.0, "copies": 0}
+    if a.settle_ms > 0:  # (module docstring: from idle to the sustained clocks)
+        t_s = time.perf_counter()
+        while (time.perf_counter() - t_s) * 1e3 < a.settle_ms:
+            ctx.copy_ceiling(n_local * 4, 10)
+            settle["copies"] += 10
+        settle["ms"] = round((time.perf_counter() - t_s) * 1e3, 1)
+    settle["how"] = ("gsort_copy_ceiling's streaming copy of the 4 * n_local-byte buffer, "
+                     "before the warm-up steps (untimed)")
     for _ in range(a.warmup):
         fn(d_in, n_local)
     barrier()
@@ -612,6 +628,7 @@ def main():
         "n_gpus": world,
         "steps": a.steps,
         "warmup": a.warmup,
+        "settle": settle,
         "ms_per_step": round(ms_step, 4),
         "higher_is_better": True,
         "scaling": "weak",

@@ -283,10 +283,15 @@ class GroupComm : public Comm {
     // barrier, the stream made to wait for every peer's ready event
     gsort_status open(hipStream_t s) {
         gsort_status st = GSORT_OK;
+        // (the ranks share one device: a device-scope release orders a rank's writes before a
+        // peer stream's copies; default flags if the runtime refuses that one)
         for (hipEvent_t *e : {&g_->ready[rank_], &g_->done[rank_]})
             if (!*e && st == GSORT_OK)
-                st = hip([&] { return hipEventCreateWithFlags(e, hipEventDisableTiming); },
-                         "hipEventCreateWithFlags");
+                st = hip([&] {
+                    const hipError_t r = hipEventCreateWithFlags(
+                        e, hipEventDisableTiming | hipEventDisableSystemFence);
+                    return r == hipSuccess ? r : hipEventCreateWithFlags(e, hipEventDisableTiming);
+                }, "hipEventCreateWithFlags");
         if (st == GSORT_OK)
             st = hip([&] { return hipEventRecord(g_->ready[rank_], s); }, "hipEventRecord");
         // (a failed rank still meets the barrier: the others must not wait for it in vain)

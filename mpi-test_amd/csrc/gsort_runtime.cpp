@@ -276,10 +276,16 @@ gsort_status ensure(gsort_ctx *c, DevBuf &b, size_t bytes) {
 
 
 // ---- timing ---------------------------------------------------------------------------
+// Timing events release at device scope (hipEventDisableSystemFence): they only feed
+// hipEventElapsedTime, and a default event's system-scope release at the end of every timed
+// dispatch cost a 2^28-key sort 12 us (1.339 -> 1.351 ms, tools/event_cost.py).  A runtime that
+// refuses the flag gets default events.
 hipEvent_t next_event(gsort_ctx *c) {
     if (c->ev_used == c->ev_pool.size()) {
         hipEvent_t e;
-        if (hipEventCreateWithFlags(&e, 0u) != hipSuccess) return nullptr;
+        if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess &&
+            hipEventCreateWithFlags(&e, 0u) != hipSuccess)
+            return nullptr;
         c->ev_pool.push_back(e);
     }
     return c->ev_pool[c->ev_used++];

@@ -6,6 +6,7 @@
 #   bench              bench.py (the driver's default line) -> TAG_bench.json
 #   prof               tools/profile_pmc.sh TAG (kernel trace + PMC passes of the bench configuration)
 #   pipes              tools/profile_pipes.sh TAG (LDS / TA / wait counters per kernel)
+#   dpipes=BITS        the same over tools/recv_probe.py 28 BITS (distributed path, one key width)
 #   probe              tools/dist_probe.py (2^28 keys, every distribution)
 #   recv               tools/recv_probe.py 28 (receive-sort bucket sizes)
 #   group=P[:LOG2[:LIB]]  tools/group_bench.py --ranks P (P in-process ranks on one GPU)
@@ -23,6 +24,7 @@ for step in "$@"; do
     bench) timeout -k 10 400 python3 bench.py > $O/${TAG}_bench.json 2> $O/${TAG}_bench.err; rc=$? ;;
     prof) bash tools/profile_pmc.sh $TAG --steps 5 --warmup 2 > $O/${TAG}_prof.log 2>&1; rc=$? ;;
     pipes) bash tools/profile_pipes.sh $TAG --steps 5 --warmup 2 > $O/${TAG}_pipes.log 2>&1; rc=$? ;;
+    dpipes) PIPES_CMD="python3 tools/recv_probe.py 28 $arg" bash tools/profile_pipes.sh ${TAG}_d$arg > $O/${TAG}_dpipes$arg.log 2>&1; rc=$? ;;
     probe) timeout -k 10 300 python3 tools/dist_probe.py > $O/${TAG}_dist_probe.txt 2>&1; rc=$? ;;
     recv) timeout -k 10 150 python3 tools/recv_probe.py 28 > $O/${TAG}_recv_probe.txt 2>&1; rc=$? ;;
     group) IFS=: read -r P LG LIB <<< "$arg"

@@ -1,5 +1,6 @@
 #!/bin/bash
 # profile_pipes.sh TAG [bench args...] -- per-kernel pipe counters of one bench configuration
+# (or of PIPES_CMD, e.g. PIPES_CMD="python3 tools/recv_probe.py 28 29" for the distributed path)
 # (LDS array / bank conflicts / LDS instruction mix, vector-memory instruction cycles, TA busy),
 # each group its own rocprofv3 --pmc pass (MI355X_MICROARCH.md: at most 8 SQ, 2 TA, 2 GRBM
 # counters per pass).  Run on the GPU box from the repo root; summary in
@@ -13,7 +14,7 @@ ARGS=("$@")
 run() {  # name, rocprof options...
     local name=$1; shift
     timeout -k 10 120 rocprofv3 "$@" -f csv -d "$OUT/$name" -o run -- \
-        python3 bench.py --no-cpu-baseline --no-dist-p1 "${ARGS[@]}" > "$OUT/$name.json" 2> "$OUT/$name.err"
+        ${PIPES_CMD:-python3 bench.py --no-cpu-baseline --no-dist-p1 "${ARGS[@]}"} > "$OUT/$name.json" 2> "$OUT/$name.err"
 }
 run stats --kernel-trace --stats
 run lds --pmc SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_LDS_ATOMIC SQ_INSTS_LDS_STORE SQ_INSTS_LDS_LOAD SQ_LDS_ADDR_CONFLICT SQ_BUSY_CU_CYCLES
