@@ -28,6 +28,33 @@ uint64_t elem_offset(const T *a, const T *b) {
     return (uint64_t)(d / (int64_t)sizeof(T));
 }
 
+// K18c's lists: the K11 classes >= recv_cx, and list 0 (with list0)
+bool cx_class(const gsort_ctx *c, int k) { return c->recv_cx > 0 && k >= c->recv_cx; }
+
+// K18c over cl: with u8 bins (recv_cb 8) the wrapped buckets collect in m_fb (count at
+// OFF_FBCTR, at most cl.bound() of them) and one u16 launch right behind redoes them, reading
+// their count on the device (usually none: its workgroups return at once).
+gsort_status count_expand_lists(gsort_ctx *c, const void *recv, bool packed16, const uint64_t *pos,
+                                const uint64_t *roff, int P, const uint64_t *bstart,
+                                const CxLists &cl, uint32_t *out) {
+    const uint32_t bound = cl.bound();
+    if (!bound) return GSORT_OK;
+    if (c->recv_cb != 8) {
+        HIP_TRY(c, launch_count_expand_lists(recv, packed16, pos, roff, P, bstart, cl, c->ncu,
+                                             out, c->stream));
+        return GSORT_OK;
+    }
+    uint32_t *fb_ctr = reinterpret_cast<uint32_t *>(c->d_small + OFF_FBCTR);
+    ST_TRY(ensure_list(c, c->m_fb, bound));
+    uint64_t *fb = reinterpret_cast<uint64_t *>(c->m_fb.p);
+    HIP_TRY(c, hipMemsetAsync(fb_ctr, 0, 4, c->stream));
+    HIP_TRY(c, launch_count_expand_lists(recv, packed16, pos, roff, P, bstart, cl, c->ncu, out,
+                                         c->stream, fb, fb_ctr));
+    HIP_TRY(c, launch_count_expand(recv, packed16, pos, roff, P, bstart, fb, bound, c->ncu, out,
+                                   c->stream, nullptr, nullptr, fb_ctr));
+    return GSORT_OK;
+}
+
 // self (int32 runs only): run `self_rank` was not received -- it lies at self_src (the
 // sender's sorted block), and the kernels read it there through a run offset taken relative to
 // recv (mod 2^64); the MSD fallback, which needs the runs back to back, copies it in first.
@@ -39,48 +66,26 @@ gsort_status sort_recv_lists(gsort_ctx *c, const void *recv, bool packed16, cons
                              const uint64_t *roff, int P, const uint64_t *bstart,
                              const WorkLists &wl, const uint64_t *h, uint32_t *out,
                              gsort_stats *stats, bool list0 = true) {
-    // K18c with u8 bins (recv_cb 8): its wrapped buckets collect in m_fb (count at OFF_FBCTR)
-    // and one u16 launch after the lists redoes them, reading their count on the device
-    uint64_t cx_entries = 0;
-    for (int k = 0; k < kLocalClasses; ++k)
-        if (c->recv_cx > 0 && k + 1 >= c->recv_cx) cx_entries += h[3 * (k + 1)];
-    if (list0 && c->recv_cx > 0) cx_entries += h[0];
-    const bool cb8 = c->recv_cb == 8 && cx_entries;
-    uint64_t *fb = nullptr;
-    uint32_t *fb_ctr = reinterpret_cast<uint32_t *>(c->d_small + OFF_FBCTR);
-    if (cb8) {
-        ST_TRY(ensure_list(c, c->m_fb, cx_entries));
-        fb = reinterpret_cast<uint64_t *>(c->m_fb.p);
-        HIP_TRY(c, hipMemsetAsync(fb_ctr, 0, 4, c->stream));
-    }
-    for (int k = 0; k < kLocalClasses; ++k) {
-        const uint64_t *hk = h + 3 * (k + 1);
+    CxLists cl;  // every K18c list in ONE persistent launch (a tail per launch otherwise)
+    for (int k = 1; k <= kLocalClasses; ++k) {
+        const uint64_t *hk = h + 3 * k;
         if (!hk[0]) continue;
-        if (c->recv_cx > 0 && k + 1 >= c->recv_cx)
-            HIP_TRY(c, launch_count_expand(recv, packed16, pos, roff, P, bstart, wl.list[k + 1],
-                                           (uint32_t)hk[0], c->ncu, out, c->stream, fb,
-                                           cb8 ? fb_ctr : nullptr));
-        else
-            HIP_TRY(c, launch_gather_sort(recv, packed16, pos, roff, P, bstart, wl.list[k + 1],
-                                          (uint32_t)hk[0], k + 1, c->atomic_rank, out,
-                                          c->stream));
         if (stats) { stats->buckets_local += hk[0]; stats->keys_bucket_sort += hk[1]; }
+        if (cx_class(c, k))
+            cl.add(wl.list[k], (uint32_t)hk[0]);
+        else
+            HIP_TRY(c, launch_gather_sort(recv, packed16, pos, roff, P, bstart, wl.list[k],
+                                          (uint32_t)hk[0], k, c->atomic_rank, out, c->stream));
     }
     if (h[0] && list0) {
+        if (stats) { stats->buckets_local += h[0]; stats->keys_bucket_sort += h[1]; }
         if (c->recv_cx > 0)
-            HIP_TRY(c, launch_count_expand(recv, packed16, pos, roff, P, bstart, wl.list[0],
-                                           (uint32_t)h[0], c->ncu, out, c->stream, fb,
-                                           cb8 ? fb_ctr : nullptr));
+            cl.add(wl.list[0], (uint32_t)h[0]);
         else
             HIP_TRY(c, launch_hist_expand(recv, packed16, pos, roff, P, bstart, wl.list[0],
                                           (uint32_t)h[0], out, c->stream));
-        if (stats) { stats->buckets_local += h[0]; stats->keys_bucket_sort += h[1]; }
     }
-    if (cb8)  // the wrapped buckets (usually none: its workgroups return at once)
-        HIP_TRY(c, launch_count_expand(recv, packed16, pos, roff, P, bstart, fb,
-                                       (uint32_t)cx_entries, c->ncu, out, c->stream, nullptr,
-                                       nullptr, fb_ctr));
-    return GSORT_OK;
+    return count_expand_lists(c, recv, packed16, pos, roff, P, bstart, cl, out);
 }
 
 gsort_status recv_sort(gsort_ctx *c, const void *recv, bool packed16,
@@ -539,8 +544,9 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
                                                 std::to_string(mine) + " (rank " +
                                                 std::to_string(me) + ")");
     }
-    // (6) every bucket sorted from its P pieces: K11g by size class, K18 past kLocalMax; a
-    // bucket past K18's reach sends the block through recv_sort's MSD levels 1 and 0
+    // (6) every bucket sorted from its P pieces: K11g by size class, K18c past them (classes
+    // >= recv_cx and list 0, one persistent launch); a bucket past K18c's reach sends the block
+    // through recv_sort's MSD levels 1 and 0
     t = tic(c);
     uint32_t *out = slot_ptr<uint32_t>(c, S_OUT);
     if (h[0] && h[2] > kHxMax) {  // recv_sort wants the P runs back to back in rbuf

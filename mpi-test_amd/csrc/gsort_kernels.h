@@ -200,6 +200,33 @@ hipError_t launch_count_expand(const void *recv, bool packed16, const uint64_t *
                                const uint64_t *list, uint32_t nlist, int ncu, uint32_t *out,
                                hipStream_t s, uint64_t *fb_list = nullptr,
                                uint32_t *fb_ctr = nullptr, const uint32_t *nlist_dev = nullptr);
+// K18c's work as several {h, len} lists walked as one index space (round 5: the class-4 list and
+// list 0 in one persistent launch instead of two launches with a tail each).  List q holds n[q]
+// entries or, with ndev[q] set, the count read on the device (n[q] is then only the grid's
+// bound): the u8 kernel's wrapped buckets, redone by a u16 launch queued right behind it.
+// skip: a list left out on the device when *skip_max > kHxMax (list 0, whose oversized buckets
+// take the MSD levels), -1: none.
+constexpr int kCxLists = 5;
+struct CxLists {
+    const uint64_t *list[kCxLists] = {};
+    const uint32_t *ndev[kCxLists] = {};
+    uint32_t n[kCxLists] = {};
+    int nl = 0;
+    int skip = -1;
+    const uint64_t *skip_max = nullptr;
+    void add(const uint64_t *l, uint32_t cnt, const uint32_t *dev = nullptr) {
+        list[nl] = l; n[nl] = cnt; ndev[nl] = dev; ++nl;
+    }
+    uint32_t bound() const {
+        uint32_t t = 0;
+        for (int q = 0; q < nl; ++q) t += n[q];
+        return t;
+    }
+};
+hipError_t launch_count_expand_lists(const void *recv, bool packed16, const uint64_t *pos,
+                                     const uint64_t *roff, int P, const uint64_t *bstart,
+                                     const CxLists &cl, int ncu, uint32_t *out, hipStream_t s,
+                                     uint64_t *fb_list = nullptr, uint32_t *fb_ctr = nullptr);
 // {h, len} list entries -> {bstart[h], len}.
 hipError_t launch_list_to_segments(uint64_t *list, uint32_t n, const uint64_t *bstart,
                                    hipStream_t s);

@@ -2304,20 +2304,20 @@ struct CxTable {  // one bucket's pieces (LDS, double-buffered)
     uint32_t h, keys;    // bucket, keys (0: no bucket)
 };
 
+// (ent: the bucket's list entry {h, len}, null past the lists' end)
 template <typename T>
 __device__ __forceinline__ void cx_fill_table(CxTable<T> &t, const T *recv,
                                               const unsigned long long *pos,
                                               const unsigned long long *roff, int P,
                                               const unsigned long long *bstart,
-                                              const unsigned long long *list, uint32_t i,
-                                              uint32_t nlist) {  // wave 0 only
+                                              const unsigned long long *ent) {  // wave 0 only
     constexpr uint32_t E = 16 / sizeof(T);
     const uint32_t lane = threadIdx.x & 63;
-    if (i >= nlist) {
+    if (!ent) {
         if (lane == 0) t.keys = 0;
         return;
     }
-    const uint32_t h = (uint32_t)list[2 * i];
+    const uint32_t h = (uint32_t)ent[0];
     uint64_t a = 0, b = 0, src = 0;
     if ((int)lane < P) {
         a = pos[(uint64_t)lane * (kBuckets16 + 1) + h];
@@ -2338,7 +2338,7 @@ __device__ __forceinline__ void cx_fill_table(CxTable<T> &t, const T *recv,
     if ((int)lane == P - 1) t.cumv[P] = x;
     if (lane == 0) {
         t.h = h;
-        t.keys = (uint32_t)list[2 * i + 1];
+        t.keys = (uint32_t)ent[1];
         t.dst = bstart[h];
     }
 }
@@ -2347,16 +2347,15 @@ __device__ __forceinline__ void cx_fill_table(CxTable<T> &t, const T *recv,
 // 16 bits << 40, dst | len << 40}, as K11e's): one piece each, read from Y.
 template <typename T>
 __device__ __forceinline__ void cx_fill_table_est(CxTable<T> &t, const T *y,
-                                                  const unsigned long long *list, uint32_t i,
-                                                  uint32_t nlist) {  // wave 0 only
+                                                  const unsigned long long *ent) {  // wave 0 only
     constexpr uint32_t E = 16 / sizeof(T);
     const uint32_t lane = threadIdx.x & 63;
-    if (i >= nlist) {
+    if (!ent) {
         if (lane == 0) t.keys = 0;
         return;
     }
     if (lane == 0) {
-        const uint64_t sw = list[2 * i], e = list[2 * i + 1];
+        const uint64_t sw = ent[0], e = ent[1];
         const uint64_t src = sw & ((1ull << 40) - 1);
         const uint32_t n = (uint32_t)(e >> 40);
         const uint32_t mis = (uint32_t)((reinterpret_cast<uintptr_t>(y + src) / sizeof(T)) & (E - 1));
@@ -2440,15 +2439,15 @@ __device__ __forceinline__ void cx_count_bucket(const T *recv, const CxTable<T> 
 // per bucket and CU with u16 bins, i.e. 0.29 of the 0.58 ms per 2^28 keys of the P = 4 shape's
 // 32 768-key buckets).  A byte that wraps (>= 256 copies of one key) shows as a total below the
 // bucket's size: the bucket goes to fb_list (fb_ctr entries, the {h, len} entry as given) with
-// its bins cleared, and the u16 kernel redoes it (nlist_dev: that count, read on the device).
+// its bins cleared, and the u16 kernel redoes it (a list whose count it reads on the device).
+// The buckets are the entries of cl's lists walked as one index space (CxLists).
 template <typename T, bool EST = false, int CB = 16>
 __global__ __launch_bounds__(CB == 8 ? 512 : 1024) void k_count_expand(
     const T *__restrict__ recv, const unsigned long long *__restrict__ pos,
     const unsigned long long *__restrict__ roff, int P,
-    const unsigned long long *__restrict__ bstart, const unsigned long long *__restrict__ list,
-    uint32_t nlist, uint32_t *__restrict__ out, uint32_t koff = 0,
-    unsigned long long *__restrict__ fb_list = nullptr, uint32_t *__restrict__ fb_ctr = nullptr,
-    const uint32_t *__restrict__ nlist_dev = nullptr) {
+    const unsigned long long *__restrict__ bstart, CxLists cl, uint32_t *__restrict__ out,
+    uint32_t koff = 0, unsigned long long *__restrict__ fb_list = nullptr,
+    uint32_t *__restrict__ fb_ctr = nullptr) {
     static_assert(CB == 8 || CB == 16, "u8 or u16 bins");
     constexpr uint32_t NT = CB == 8 ? 512 : 1024, NW = NT / 64;
     constexpr uint32_t WORDS = 65536 * CB / 32;  // 16 384 (u8) / 32 768 (u16) words of bins
@@ -2457,10 +2456,28 @@ __global__ __launch_bounds__(CB == 8 ? 512 : 1024) void k_count_expand(
                                                  // with u8 bins measured slower: r05_recv_u8_bins)
     constexpr uint32_t CH = WORDS / NW / CW;     // chunks per wave (32 / 16)
     constexpr uint32_t PF = 8;  // prefetched 16-B vectors per thread
-    if (nlist_dev) {  // (the u8 kernel's wrapped buckets: usually none)
-        nlist = *nlist_dev;
-        if (blockIdx.x >= nlist) return;
+    // the lists' lengths (read on the device for a launch queued before the host knew them;
+    // the u8 kernel's wrapped buckets: usually none)
+    uint32_t nn[kCxLists], nlist = 0;
+#pragma unroll
+    for (int q = 0; q < kCxLists; ++q) {
+        nn[q] = 0;
+        if (q < cl.nl) {
+            nn[q] = cl.ndev[q] ? *cl.ndev[q] : cl.n[q];
+            if (q == cl.skip && *reinterpret_cast<const unsigned long long *>(cl.skip_max) > kHxMax)
+                nn[q] = 0;
+        }
+        nlist += nn[q];
     }
+    if (blockIdx.x >= nlist) return;
+    auto entry = [&](uint32_t i) -> const unsigned long long * {  // entry i of the joined lists
+#pragma unroll
+        for (int q = 0; q < kCxLists; ++q) {
+            if (i < nn[q]) return reinterpret_cast<const unsigned long long *>(cl.list[q]) + 2 * i;
+            i -= nn[q];
+        }
+        return nullptr;
+    };
     __shared__ uint32_t s_h[WORDS];
     // per wave: 256 window slots + 64 dummy words (a lane's marks outside the window)
     __shared__ uint4 s_mark[NW * 80];
@@ -2473,8 +2490,8 @@ __global__ __launch_bounds__(CB == 8 ? 512 : 1024) void k_count_expand(
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     uint32_t cur = 0;
     auto fill = [&](CxTable<T> &t, uint32_t i) {
-        if (EST) cx_fill_table_est(t, recv, list, i, nlist);
-        else cx_fill_table(t, recv, pos, roff, P, bstart, list, i, nlist);
+        if (EST) cx_fill_table_est(t, recv, entry(i));
+        else cx_fill_table(t, recv, pos, roff, P, bstart, entry(i));
     };
     if (tid < 64) fill(s_t[0], blockIdx.x);
     __syncthreads();
@@ -2561,8 +2578,9 @@ __global__ __launch_bounds__(CB == 8 ? 512 : 1024) void k_count_expand(
             if constexpr (CB == 8) {
                 if (tid == 0) {
                     const uint32_t e = atomicAdd(fb_ctr, 1u);
-                    fb_list[2 * e] = list[2 * i];
-                    fb_list[2 * e + 1] = list[2 * i + 1];
+                    const unsigned long long *en = entry(i);
+                    fb_list[2 * e] = en[0];
+                    fb_list[2 * e + 1] = en[1];
                 }
                 skip = true;
                 if (tid < NW) s_wsum[tid] = 0;  // no keys to expand (s_base below)
@@ -4025,41 +4043,50 @@ hipError_t launch_hist_expand(const void *recv, bool packed16, const uint64_t *p
     return hipGetLastError();
 }
 
+hipError_t launch_count_expand_lists(const void *recv, bool packed16, const uint64_t *pos,
+                                     const uint64_t *roff, int P, const uint64_t *bstart,
+                                     const CxLists &cl, int ncu, uint32_t *out, hipStream_t s,
+                                     uint64_t *fb_list, uint32_t *fb_ctr) {
+    using ull = unsigned long long;
+    const uint32_t nb = cl.bound();
+    if (nb == 0) return hipSuccess;
+    if (P < 1 || P > 64 || ncu < 1 || cl.nl < 1 || cl.nl > kCxLists ||
+        (cl.skip >= 0 && (cl.skip >= cl.nl || !cl.skip_max)))
+        return hipErrorInvalidValue;
+    auto *ps = reinterpret_cast<const ull *>(pos);
+    auto *ro = reinterpret_cast<const ull *>(roff);
+    auto *bs = reinterpret_cast<const ull *>(bstart);
+    ull *fl = reinterpret_cast<ull *>(fb_list);
+    if (fb_list) {  // u8 bins, two workgroups per CU; wrapped buckets appended to fb_list
+        const uint32_t grid = std::min<uint32_t>(nb, 2u * (uint32_t)ncu);
+        if (packed16)
+            launch_k(k_count_expand<uint16_t, false, 8>, grid, 512, 0, s,
+                     reinterpret_cast<const uint16_t *>(recv), ps, ro, P, bs, cl, out, 0u, fl, fb_ctr);
+        else
+            launch_k(k_count_expand<int32_t, false, 8>, grid, 512, 0, s,
+                     reinterpret_cast<const int32_t *>(recv), ps, ro, P, bs, cl, out, 0u, fl, fb_ctr);
+        return hipGetLastError();
+    }
+    // u16 bins, one workgroup per CU
+    const uint32_t grid = std::min<uint32_t>(nb, (uint32_t)ncu);
+    if (packed16)
+        launch_k(k_count_expand<uint16_t>, grid, 1024, 0, s, reinterpret_cast<const uint16_t *>(recv), ps, ro, P,
+                 bs, cl, out, 0u, (ull *)nullptr, (uint32_t *)nullptr);
+    else
+        launch_k(k_count_expand<int32_t>, grid, 1024, 0, s, reinterpret_cast<const int32_t *>(recv), ps, ro, P,
+                 bs, cl, out, 0u, (ull *)nullptr, (uint32_t *)nullptr);
+    return hipGetLastError();
+}
+
 hipError_t launch_count_expand(const void *recv, bool packed16, const uint64_t *pos,
                                const uint64_t *roff, int P, const uint64_t *bstart,
                                const uint64_t *list, uint32_t nlist, int ncu, uint32_t *out,
                                hipStream_t s, uint64_t *fb_list, uint32_t *fb_ctr,
                                const uint32_t *nlist_dev) {
-    using ull = unsigned long long;
-    if (nlist == 0) return hipSuccess;
-    if (P < 1 || P > 64 || ncu < 1) return hipErrorInvalidValue;
-    auto *ps = reinterpret_cast<const ull *>(pos);
-    auto *ro = reinterpret_cast<const ull *>(roff);
-    auto *bs = reinterpret_cast<const ull *>(bstart);
-    auto *l = reinterpret_cast<const ull *>(list);
-    ull *fl = reinterpret_cast<ull *>(fb_list);
-    if (fb_list) {  // u8 bins, two workgroups per CU; wrapped buckets appended to fb_list
-        const uint32_t grid = std::min<uint32_t>(nlist, 2u * (uint32_t)ncu);
-        if (packed16)
-            launch_k(k_count_expand<uint16_t, false, 8>, grid, 512, 0, s,
-                     reinterpret_cast<const uint16_t *>(recv), ps, ro, P, bs, l, nlist, out, 0u,
-                     fl, fb_ctr, (const uint32_t *)nullptr);
-        else
-            launch_k(k_count_expand<int32_t, false, 8>, grid, 512, 0, s,
-                     reinterpret_cast<const int32_t *>(recv), ps, ro, P, bs, l, nlist, out, 0u,
-                     fl, fb_ctr, (const uint32_t *)nullptr);
-        return hipGetLastError();
-    }
-    // u16 bins, one workgroup per CU; nlist_dev: the list's length is read on the device (the
-    // u8 kernel's wrapped buckets; nlist is then the grid's bound)
-    const uint32_t grid = std::min<uint32_t>(nlist, (uint32_t)ncu);
-    if (packed16)
-        launch_k(k_count_expand<uint16_t>, grid, 1024, 0, s, reinterpret_cast<const uint16_t *>(recv), ps, ro, P,
-                 bs, l, nlist, out, 0u, (ull *)nullptr, (uint32_t *)nullptr, nlist_dev);
-    else
-        launch_k(k_count_expand<int32_t>, grid, 1024, 0, s, reinterpret_cast<const int32_t *>(recv), ps, ro, P,
-                 bs, l, nlist, out, 0u, (ull *)nullptr, (uint32_t *)nullptr, nlist_dev);
-    return hipGetLastError();
+    CxLists cl;
+    cl.add(list, nlist, nlist_dev);
+    return launch_count_expand_lists(recv, packed16, pos, roff, P, bstart, cl, ncu, out, s,
+                                     fb_list, fb_ctr);
 }
 
 hipError_t launch_list_to_segments(uint64_t *list, uint32_t n, const uint64_t *bstart,
@@ -4205,10 +4232,11 @@ hipError_t launch_est_oversized(const EstPlan &p, uint32_t nlist, int ncu, hipSt
     using ull = unsigned long long;
     if (nlist == 0) return hipSuccess;
     const unsigned grid = (unsigned)std::min<uint32_t>(nlist, (uint32_t)std::max(ncu, 1));
+    CxLists cl;
+    cl.add(p.wl.list[0], nlist);
     launch_k(k_count_expand<uint16_t, true>, grid, 1024, 0, s, (const uint16_t *)p.y,
-             (const ull *)nullptr, (const ull *)nullptr, 1, (const ull *)nullptr,
-             reinterpret_cast<const ull *>(p.wl.list[0]), nlist, p.out, p.koff, (ull *)nullptr,
-             (uint32_t *)nullptr, (const uint32_t *)nullptr);
+             (const ull *)nullptr, (const ull *)nullptr, 1, (const ull *)nullptr, cl, p.out,
+             p.koff, (ull *)nullptr, (uint32_t *)nullptr);
     return hipGetLastError();
 }
 
