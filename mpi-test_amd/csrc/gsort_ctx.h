@@ -145,7 +145,9 @@ constexpr size_t OFF_HIST = 0, OFF_TOT = 8192, OFF_BASES = 10240, OFF_CTR = 1228
 constexpr size_t OFF_FLAGS = 12408;  // K12b's trivial-level word, inside the published range
 constexpr size_t OFF_MINMAX = 12480;  // the offset retry's exact min / max (2 int32)
 constexpr size_t OFF_FBCTR = 12800;   // K18c (u8): the count of wrapped buckets (u32)
-constexpr size_t OFF_GIANT = 16384;   // K1m result (3 u64) + K1g counters (16 u64)
+// K1m result (3 u64, word 3 spare), then K1g's counters from word 4: ctr[0] (cold keys of all
+// workgroups) + one per K1g workgroup (1 + kH16Blocks u64; static_assert in giant_sort)
+constexpr size_t OFF_GIANT = 16384;
 
 constexpr size_t kCtrBytes = 3 * 8 * (kLocalClasses + 1);
 static_assert(OFF_CTR + kCtrBytes <= OFF_FLAGS && OFF_FLAGS + 4 <= OFF_ONE, "counter area");
