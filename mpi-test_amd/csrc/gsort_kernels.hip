@@ -2431,6 +2431,128 @@ __device__ __forceinline__ void cx_count_bucket(const T *recv, const CxTable<T> 
     }
 }
 
+// Lane's 4 bins of one 256-bin chunk whose first word is wd0 (u8: word wd0 + lane; u16: words
+// wd0 + 2 lane, +1), with the u16 kernel's wrap corrections (nw entries) applied.
+template <int CB>
+__device__ __forceinline__ void cx_counts(const uint32_t *s_h, uint32_t wd0, uint32_t lane,
+                                          uint32_t nw, const uint32_t *s_wb, const int32_t *s_wd,
+                                          uint32_t (&c)[4]) {
+    if (CB == 8) {
+        const uint32_t y = s_h[wd0 + lane];
+        c[0] = y & 255u;
+        c[1] = (y >> 8) & 255u;
+        c[2] = (y >> 16) & 255u;
+        c[3] = y >> 24;
+        return;
+    }
+    const uint32_t wd = wd0 + 2 * lane;
+    const uint2 y = *reinterpret_cast<const uint2 *>(s_h + wd);
+    c[0] = y.x & 0xFFFFu;
+    c[1] = y.x >> 16;
+    c[2] = y.y & 0xFFFFu;
+    c[3] = y.y >> 16;
+    for (uint32_t e = 0; e < nw; ++e) {
+        const uint32_t b = s_wb[e] - 2 * wd;  // bin relative to the lane's first
+        if (b < 4u) {
+            const uint32_t dd = (uint32_t)s_wd[e];
+            c[0] += b == 0 ? dd : 0u;
+            c[1] += b == 1 ? dd : 0u;
+            c[2] += b == 2 ? dd : 0u;
+            c[3] += b == 3 ? dd : 0u;
+        }
+    }
+}
+
+// Words of bins each expanding wave owns: 2048 (u8: 8 waves x 8192 bins; u16: 16 x 4096)
+constexpr uint32_t kCxWaveWords = 2048;
+
+// One wave's expansion (K18c): its bins -- words w0 .. w0 + kCxWaveWords of s_h -- hold
+// nkw keys, written as ONE run at d in windows of 256 slots aligned to 16 B; the chunks are
+// streamed through registers (a window marks the bins of every chunk starting in it; the last
+// chunk it touched carries over) and every bin word is zeroed after its read.  mk4: the wave's
+// 80 uint4 of marks (256 window slots + 64 dummy words: a lane's marks outside the window).
+// hk: the bucket's top 16 bits (flipped unless EST); EST stores add koff and flip.
+template <int CB, bool EST>
+__device__ __forceinline__ void cx_expand_wave(uint32_t *s_h, uint32_t w0, uint4 *mk4,
+                                               uint32_t *d, uint32_t nkw, uint32_t hk,
+                                               uint32_t koff, uint32_t nw,
+                                               const uint32_t *s_wb, const int32_t *s_wd) {
+    constexpr uint32_t BPW = 32 / CB;            // bins per word
+    constexpr uint32_t CW = 256 / BPW;           // words per chunk: 4 bins per lane (8 per lane
+                                                 // with u8 bins measured slower: r05_recv_u8_bins)
+    constexpr uint32_t CH = kCxWaveWords / CW;   // chunks per wave (u8: 32, u16: 16)
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t *mk = reinterpret_cast<uint32_t *>(mk4);
+    const uint32_t off = (uint32_t)(reinterpret_cast<uintptr_t>(d) >> 2) & 3u;
+    // windows [ws, ws + 256) of the wave's run; chunk j's bins mark the windows they start in
+    // (an empty bin is parked at 2^31, past every window), and a window is finished once the
+    // chunk being marked reaches past it
+    // (wave-uniform values kept scalar: the window loop below then stays a scalar loop -- with
+    // them in VGPRs the compiler ran it as a divergent one)
+    uint32_t ws = 0u - off, lo = 0, carry = 0;
+    auto finish = [&]() {  // window ws: keys from the marks, stored; next window cleared
+        __builtin_amdgcn_wave_barrier();
+        const uint4 m = mk4[lane];
+        const uint32_t a0 = m.x, a1 = max(a0, m.y), a2 = max(a1, m.z), a3 = max(a2, m.w);
+        const uint32_t S = wave_incl_max(a3);
+        // the lanes below: S of lane - 1 (DPP wave shift right by one; lane 0 reads 0)
+        const uint32_t prev = max(carry, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)S, 0x138, 0xf, 0xf, true));
+        carry = max(carry, (uint32_t)__builtin_amdgcn_readlane((int)S, 63));
+        const uint32_t q = ws + 4 * lane;  // this lane's first slot
+        uint4 v = make_uint4(max(prev, a0), max(prev, a1), max(prev, a2), max(prev, a3));
+        if (EST) {  // relative ordered keys -> int32
+            v.x = (v.x + koff) ^ kFlip;
+            v.y = (v.y + koff) ^ kFlip;
+            v.z = (v.z + koff) ^ kFlip;
+            v.w = (v.w + koff) ^ kFlip;
+        }
+        if (q + 4 <= nkw && q < nkw) {
+            *reinterpret_cast<uint4 *>(d + q) = v;  // 16-B aligned (nontemporal: slower, r04_ab_nt_stores)
+        } else {
+            if (q < nkw) d[q] = v.x;
+            if (q + 1 < nkw) d[q + 1] = v.y;
+            if (q + 2 < nkw) d[q + 2] = v.z;
+            if (q + 3 < nkw) d[q + 3] = v.w;
+        }
+        __builtin_amdgcn_wave_barrier();
+        mk4[lane] = make_uint4(0, 0, 0, 0);
+        ws += 256;
+    };
+    mk4[lane] = make_uint4(0, 0, 0, 0);
+#pragma unroll 1
+    for (uint32_t j = 0; j < CH; ++j) {
+        uint32_t c[4];
+        cx_counts<CB>(s_h, w0 + CW * j, lane, nw, s_wb, s_wd, c);
+        // the chunk's last read: its words are zeroed for the next bucket here
+        if (CB == 8) s_h[w0 + CW * j + lane] = 0;
+        else *reinterpret_cast<uint2 *>(s_h + w0 + CW * j + 2 * lane) = make_uint2(0, 0);
+        const uint32_t tc = c[0] + c[1] + c[2] + c[3];
+        const uint32_t y = wave_incl_add(tc);
+        uint32_t sm[4], st = lo + y - tc;
+        const uint32_t k0 = hk | (CB == 8 ? 4 * (w0 + CW * j + lane) : 2 * (w0 + CW * j + 2 * lane));
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            sm[q] = c[q] ? st : 0x80000000u;
+            st += c[q];
+        }
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane(
+            (int)(lo + (uint32_t)__builtin_amdgcn_readlane((int)y, 63)));
+#pragma unroll 1
+        while (true) {
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {  // no branch: a bin off the window marks the dummy
+                const uint32_t r = sm[q] - ws;
+                mk[r < 256u ? r : 256u + lane] = k0 + q;
+            }
+            if (hi - ws <= 256u) break;  // every bin of chunk j starts before ws + 256
+            finish();
+        }
+        lo = hi;
+    }
+    while (ws + off < nkw + off) finish();
+}
+
 // EST: the sampled plan's oversized children (cx_fill_table_est: recv = Y, P = 1): keys are
 // relative to the block's minimum koff, so the expansion marks relative keys (monotonic in the
 // slot, as the max-scan needs) and the stores add koff and flip.
@@ -2455,6 +2577,7 @@ __global__ __launch_bounds__(CB == 8 ? 512 : 1024) void k_count_expand(
     constexpr uint32_t CW = 256 / BPW;           // words per chunk: 4 bins per lane (8 per lane
                                                  // with u8 bins measured slower: r05_recv_u8_bins)
     constexpr uint32_t CH = WORDS / NW / CW;     // chunks per wave (32 / 16)
+    static_assert(WORDS / NW == kCxWaveWords, "cx_expand_wave's range per wave");
     constexpr uint32_t PF = 8;  // prefetched 16-B vectors per thread
     // the lists' lengths (read on the device for a launch queued before the host knew them;
     // the u8 kernel's wrapped buckets: usually none)
@@ -2479,6 +2602,7 @@ __global__ __launch_bounds__(CB == 8 ? 512 : 1024) void k_count_expand(
         return nullptr;
     };
     __shared__ uint32_t s_h[WORDS];
+    // per wave: 256 window slots + 64 dummy words (a lane's marks outside the window)
     // per wave: 256 window slots + 64 dummy words (a lane's marks outside the window)
     __shared__ uint4 s_mark[NW * 80];
     __shared__ uint32_t s_base[2 * NW];  // waves' output offsets, totals
@@ -2525,32 +2649,8 @@ __global__ __launch_bounds__(CB == 8 ? 512 : 1024) void k_count_expand(
         // wraps tracked (returning atomics)
         uint32_t nw = 0;
         const uint32_t w0 = w * (WORDS / NW);
-        // lane's 4 bins of chunk j: counts (wrap corrections applied)
-        auto counts = [&](uint32_t j, uint32_t (&c)[4]) {
-            if (CB == 8) {
-                const uint32_t y = s_h[w0 + CW * j + lane];
-                c[0] = y & 255u;
-                c[1] = (y >> 8) & 255u;
-                c[2] = (y >> 16) & 255u;
-                c[3] = y >> 24;
-                return;
-            }
-            const uint32_t wd = w0 + CW * j + 2 * lane;
-            const uint2 y = *reinterpret_cast<const uint2 *>(s_h + wd);
-            c[0] = y.x & 0xFFFFu;
-            c[1] = y.x >> 16;
-            c[2] = y.y & 0xFFFFu;
-            c[3] = y.y >> 16;
-            for (uint32_t e = 0; e < nw; ++e) {
-                const uint32_t b = s_wb[e] - 2 * wd;  // bin relative to the lane's first
-                if (b < 4u) {
-                    const uint32_t dd = (uint32_t)s_wd[e];
-                    c[0] += b == 0 ? dd : 0u;
-                    c[1] += b == 1 ? dd : 0u;
-                    c[2] += b == 2 ? dd : 0u;
-                    c[3] += b == 3 ? dd : 0u;
-                }
-            }
+        auto counts = [&](uint32_t j, uint32_t (&c)[4]) {  // lane's 4 bins of chunk j
+            cx_counts<CB>(s_h, w0 + CW * j, lane, nw, s_wb, s_wd, c);
         };
         auto wave_totals = [&]() -> uint32_t {  // the waves' totals into s_wsum; the bucket's
             uint32_t tw = 0;
@@ -2609,84 +2709,12 @@ __global__ __launch_bounds__(CB == 8 ? 512 : 1024) void k_count_expand(
             for (uint32_t u = 0; u < PF; ++u)
                 if (u * NT + tid < nv) x[u] = *cx_vec(recv, s_t[nxt], P, u * NT + tid);
         }
-        // expansion: the wave's keys are ONE run of out, walked in windows of 256 slots
-        // aligned to 16 B; the chunks are streamed through registers (a window marks the bins
-        // of every chunk starting in it; the last chunk it touched carries over)
-        // (wave-uniform values read from LDS made scalar: the window loop below then stays a
-        // scalar loop -- with them in VGPRs the compiler ran it as a divergent one)
+        // expansion: the wave's keys are ONE run of out (cx_expand_wave)
         const uint32_t nkw = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_base[NW + w]);
         if (nkw) {
-            uint4 *mk4 = s_mark + 80 * w;
-            uint32_t *mk = reinterpret_cast<uint32_t *>(mk4);
             const uint64_t dst0 = tdst + (uint32_t)__builtin_amdgcn_readfirstlane((int)s_base[w]);
-            uint32_t *d = out + dst0;
-            const uint32_t hk = EST ? h << 16 : (h << 16) ^ kFlip;
-            const uint32_t off = (uint32_t)(reinterpret_cast<uintptr_t>(d) >> 2) & 3u;
-            // windows [ws, ws + 256) of the wave's run; chunk j's bins mark the windows they
-            // start in (an empty bin is parked at 2^31, past every window), and a window is
-            // finished once the chunk being marked reaches past it
-            uint32_t ws = 0u - off, lo = 0, carry = 0;
-            auto finish = [&]() {  // window ws: keys from the marks, stored; next window cleared
-                __builtin_amdgcn_wave_barrier();
-                const uint4 m = mk4[lane];
-                const uint32_t a0 = m.x, a1 = max(a0, m.y), a2 = max(a1, m.z), a3 = max(a2, m.w);
-                const uint32_t S = wave_incl_max(a3);
-                // the lanes below: S of lane - 1 (DPP wave shift right by one; lane 0 reads 0)
-                const uint32_t prev = max(carry, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)S, 0x138, 0xf, 0xf, true));
-                carry = max(carry, (uint32_t)__builtin_amdgcn_readlane((int)S, 63));
-                const uint32_t q = ws + 4 * lane;  // this lane's first slot
-                uint4 v = make_uint4(max(prev, a0), max(prev, a1), max(prev, a2), max(prev, a3));
-                if (EST) {  // relative ordered keys -> int32
-                    v.x = (v.x + koff) ^ kFlip;
-                    v.y = (v.y + koff) ^ kFlip;
-                    v.z = (v.z + koff) ^ kFlip;
-                    v.w = (v.w + koff) ^ kFlip;
-                }
-                if (q + 4 <= nkw && q < nkw) {
-                    *reinterpret_cast<uint4 *>(d + q) = v;  // 16-B aligned (nontemporal: slower, r04_ab_nt_stores)
-                } else {
-                    if (q < nkw) d[q] = v.x;
-                    if (q + 1 < nkw) d[q + 1] = v.y;
-                    if (q + 2 < nkw) d[q + 2] = v.z;
-                    if (q + 3 < nkw) d[q + 3] = v.w;
-                }
-                __builtin_amdgcn_wave_barrier();
-                mk4[lane] = make_uint4(0, 0, 0, 0);
-                ws += 256;
-            };
-            mk4[lane] = make_uint4(0, 0, 0, 0);
-#pragma unroll 1
-            for (uint32_t j = 0; j < CH; ++j) {
-                uint32_t c[4];
-                counts(j, c);
-                // the chunk's last read: its words are zeroed for the next bucket here
-                if (CB == 8) s_h[w0 + CW * j + lane] = 0;
-                else *reinterpret_cast<uint2 *>(s_h + w0 + CW * j + 2 * lane) = make_uint2(0, 0);
-                const uint32_t tc = c[0] + c[1] + c[2] + c[3];
-                const uint32_t y = wave_incl_add(tc);
-                uint32_t sm[4], st = lo + y - tc;
-                const uint32_t k0 = hk | (CB == 8 ? 4 * (w0 + CW * j + lane) : 2 * (w0 + CW * j + 2 * lane));
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    sm[q] = c[q] ? st : 0x80000000u;
-                    st += c[q];
-                }
-                const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane(
-                    (int)(lo + (uint32_t)__builtin_amdgcn_readlane((int)y, 63)));
-#pragma unroll 1
-                while (true) {
-                    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {  // no branch: a bin off the window marks the dummy
-                        const uint32_t r = sm[q] - ws;
-                        mk[r < 256u ? r : 256u + lane] = k0 + q;
-                    }
-                    if (hi - ws <= 256u) break;  // every bin of chunk j starts before ws + 256
-                    finish();
-                }
-                lo = hi;
-            }
-            while (ws + off < nkw + off) finish();
+            cx_expand_wave<CB, EST>(s_h, w0, s_mark + 80 * w, out + dst0, nkw,
+                                    EST ? h << 16 : (h << 16) ^ kFlip, koff, nw, s_wb, s_wd);
         }
         __syncthreads();  // the bins, the marks and table cur are reused
         cur = nxt;
