@@ -3479,7 +3479,7 @@ __global__ __launch_bounds__(BLOCK) void k_local_sort_e(const uint16_t *__restri
 // fit it instead of half of them going to K18c's 65 536 counters; 2 workgroups still fit a CU
 // (76 KiB of LDS each)
 constexpr int kC3Block = 512, kC3Items = 33;
-constexpr int kC2Block = 512, kC2Items = 18;
+constexpr int kC2Block = 512, kC2Items = 18;  // (1024 x 9: 1.36 -> 1.73 ms per 2^28-key sort, r05_ab_k11e_1024x9_rejected)
 
 constexpr int cls_of(int block, int items) {
     return block * items == 16896 ? 3 : block * items == 9216 ? 2 : block * items == 4608 ? 1 : 4;
