@@ -362,7 +362,8 @@ def kernel_rooflines(stats, n_local, plan=0):
             [s["keys_level"][0] for s in stats], PASS_BYTES_PER_KEY)
         # the sampled plan's K3a stores only the low 16 bits of every key (its Y regions are
         # u16) and K11e reads those back: 4 + 2 and 2 + 4 B/key
-        add("k_partition_res L2 (K3a: level 2, runs reserved on the K12b child cursors)",
+        add("k_partition_res L2 (K3a: level 2, runs reserved on the child cursors; the span "
+            "also holds K12f's tile descriptors)",
             ("k_partition_res<1024, 8, false",), [s["ms_level"][1] for s in stats],
             [s["keys_level"][1] for s in stats], 6 if plan == 1 else PASS_BYTES_PER_KEY)
     else:
@@ -374,7 +375,7 @@ def kernel_rooflines(stats, n_local, plan=0):
         [k for s in stats for k in s["keys_level"][seg_from:]], PASS_BYTES_PER_KEY)
     if plan == 1:
         add("k_local_sort_e (K11e: in-LDS sort of every level-2 child into its exact place; "
-            "with K12g)", ("k_local_sort_e",),
+            "span from K12g's end: K11e + one launch gap)", ("k_local_sort_e",),
             [s["ms_bucket_sort"] for s in stats], [s["keys_bucket_sort"] for s in stats], 6)
     else:
         add("k_local_sort (K11: in-LDS sort of the small buckets)", ("k_local_sort",),
