@@ -323,8 +323,7 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
     // rounds 2 and 3, so every rank sees it: all ranks then sort the groups on the host path and
     // repeat rounds 2 and 3 with the host between them (select_rounds below).
     const int nb = P - 1, M = 257, W = nb * M + nb;  // count row: nb x M counts + nb K13g flags
-    std::vector<uint64_t> g(nb), prefix(nb, 0), hx((size_t)2 * nb + (size_t)nb * M),
-        all((size_t)P * W);
+    std::vector<uint64_t> g(nb), prefix(nb, 0), all((size_t)P * W);
     std::vector<int> dsel(nb, 0);
     for (int q = 0; q < nb; ++q) g[q] = std::min<uint64_t>((uint64_t)(q + 1) * B, N);
     ST_TRY(ensure(c, c->m_split, (size_t)std::max(nb, 1) * (M * 16 + 32)));
@@ -355,14 +354,20 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
         return GSORT_OK;
     };
     // the thresholds of round 0 (prefix 0) and of round 2 after the host path (prefix: the top
-    // 16 bits); prefix and g go along
+    // 16 bits); prefix and g go along.  Staged in pinned memory at OFF_PLAN + 8 KiB (free: the
+    // exchange table below reuses it after select_rounds' synchronisation): a pageable copy
+    // would hold the host in the runtime's staging until the stream had drained the sender's
+    // K1h .. K3a, and the select's kernels would then be queued behind an idle GPU
+    const size_t nx = (size_t)2 * nb + (size_t)nb * M;
+    if (OFF_PLAN + 8192 + nx * 8 > kSmallBytes)
+        return set_err(c, GSORT_EINVAL, "select thresholds too large");
+    uint64_t *hx = reinterpret_cast<uint64_t *>(c->h_small + OFF_PLAN + 8192);
     auto put_thresholds = [&](int shift) -> gsort_status {
         for (int q = 0; q < nb; ++q) { hx[q] = prefix[q]; hx[nb + q] = g[q]; }
         for (int q = 0; q < nb; ++q)
             for (int d = 0; d < M; ++d)
                 hx[2 * nb + (size_t)q * M + d] = prefix[q] + ((uint64_t)d << shift);
-        HIP_TRY(c, hipMemcpyAsync(d_pref, hx.data(), hx.size() * 8, hipMemcpyHostToDevice,
-                                  c->stream));
+        HIP_TRY(c, hipMemcpyAsync(d_pref, hx, nx * 8, hipMemcpyHostToDevice, c->stream));
         return GSORT_OK;
     };
     t = tic_rec(c);

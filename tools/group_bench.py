@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--keys-log2", type=int, default=25)
     ap.add_argument("--algo", default="radix")
     ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1, help="untimed calls per rank first")
     ap.add_argument("--local", default="msd")
     a = ap.parse_args()
     import torch  # noqa: F401
@@ -40,7 +41,9 @@ def main():
             c.generate(gsort.UNIFORM, 42, r * n, n, d)
             c.reserve(n)
             fn = c.radix if a.algo == "radix" else c.sample
-            fn(d, n)
+            for _ in range(a.warmup):
+                barrier.wait()
+                fn(d, n)
             sts, walls = [], []
             for _ in range(a.steps):  # each step between two barriers of all ranks
                 barrier.wait()
@@ -64,12 +67,14 @@ def main():
         t.join()
     grp.close()
     tot = {k: round(sum(o[k] for o in out), 4) for k in out[0]}
-    steps = sorted(max(w[i] for w in out_walls) * 1e3 for i in range(a.steps))
+    in_order = [round(max(w[i] for w in out_walls) * 1e3, 4) for i in range(a.steps)]
+    steps = sorted(in_order)
     med = steps[len(steps) // 2]
     print(json.dumps({"ranks": P, "keys_per_rank": n, "algo": a.algo,
                       "sum_over_ranks_ms": tot,
                       "wall_ms": round(max(o["wall_ms"] for o in out), 4),
                       "step_ms": [round(x, 4) for x in steps],
+                      "step_ms_in_order": in_order, "warmup": a.warmup,
                       "median_step_ms": round(med, 4),
                       "median_ms_per_2p28_keys": round(med / P * (1 << 28) / n, 4)}))
 
