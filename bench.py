@@ -524,7 +524,14 @@ def main():
     import torch.distributed as dist
     import gsort
 
-    torch.cuda.set_device(local)
+    # More ranks than GPUs (a one-GPU box rehearsing the N > 1 path): the ranks share the GPUs
+    # through the library's IPC transport (RCCL refuses two ranks on one device).  Such a run
+    # checks the multi-process flow end to end -- exchange, verify_rows, the strong-scaling
+    # block -- but its numbers price nothing (`transport` in the line says so).
+    ndev = torch.cuda.device_count()  # (counting devices does not initialise the GPU)
+    shared = world > max(ndev, 1)
+    dev = local % max(ndev, 1)
+    torch.cuda.set_device(dev)
     if world > 1:
         dist.init_process_group("gloo")  # bootstrap only: uid broadcast, barrier, max-time
     uid = None
@@ -533,7 +540,8 @@ def main():
     if world > 1 or os.environ.get("GSORT_FORCE_DIST") == "1":
         buf = torch.zeros(128, dtype=torch.uint8)
         if rank == 0:
-            buf = torch.tensor(list(gsort.get_uid()), dtype=torch.uint8)
+            u = gsort.get_uid(ipc_ranks=world) if shared else gsort.get_uid()
+            buf = torch.tensor(list(u), dtype=torch.uint8)
         if world > 1:
             dist.broadcast(buf, 0)
         uid = bytes(buf.tolist())
@@ -543,14 +551,20 @@ def main():
             dist.barrier()
 
     n_local = 1 << a.keys_log2
-    ctx = gsort.Context(rank=rank, nranks=world, device=local, uid=uid)
+    ctx = gsort.Context(rank=rank, nranks=world, device=dev, uid=uid)
     d_in = ctx.alloc(n_local * 4)
     ctx.generate(gsort.UNIFORM if dist_name == "uniform" else gsort.ZIPF, a.seed,
                  rank * n_local, n_local, d_in)
     ctx.reserve(n_local)
     ctx.set_local_algo(gsort.LOCAL_MSD if a.local == "msd" else gsort.LOCAL_LSD)
     fn = ctx.radix if a.algo == "radix" else ctx.sample
+    t_start = time.perf_counter()
 
+    def log(msg):  # progress on stderr (the JSON line goes to stdout)
+        print(f"[bench r{rank} +{time.perf_counter() - t_start:.1f}s] {msg}", file=sys.stderr,
+              flush=True)
+
+    log(f"context ready: {n_local} keys, transport {'ipc (shared GPUs)' if shared else 'rccl' if world > 1 else 'none'}")
     settle = {"ms": 0.0, "copies": 0}
     if a.settle_ms > 0:  # (module docstring: from idle to the sustained clocks)
         t_s = time.perf_counter()
@@ -560,8 +574,10 @@ def main():
         settle["ms"] = round((time.perf_counter() - t_s) * 1e3, 1)
     settle["how"] = ("gsort_copy_ceiling's streaming copy of the 4 * n_local-byte buffer, "
                      "before the warm-up steps (untimed)")
+    log("settled")
     for _ in range(a.warmup):
         fn(d_in, n_local)
+    log("warm-up steps done")
     barrier()
     torch.cuda.synchronize()
     # one gsort_stats per step, filled in place and converted after the timed region
@@ -582,6 +598,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    log("timed steps done")
     # correctness of the last step's output, checked on device (K9)
     out_ptr, n_out, _ = fn(d_in, n_local)
     fp = ctx.fingerprint(out_ptr, n_out)
@@ -630,6 +647,9 @@ def main():
         "steps": a.steps,
         "warmup": a.warmup,
         "settle": settle,
+        "transport": (None if world == 1 else
+                      "ipc: ranks share GPUs (a rehearsal of the N > 1 path; prices nothing)"
+                      if shared else "rccl over xGMI"),
         "ms_per_step": round(ms_step, 4),
         "higher_is_better": True,
         "scaling": "weak",
@@ -680,6 +700,7 @@ def main():
         # configs[2]'s strong-scaling point: 2^31 keys in total (the canonical stream, rank r's
         # block = its slice), a few timed steps bracketed like the headline's, max over ranks
         n_s = (1 << 31) // world
+        log(f"strong-scaling block: {n_s} keys per rank")
         d_s = ctx.alloc(n_s * 4)
         ctx.generate(gsort.UNIFORM, a.seed, rank * n_s, n_s, d_s)
         ctx.reserve(n_s)
@@ -706,6 +727,7 @@ def main():
                                                   [r_.as_dict() for r_ in raw_s])
         ctx.free(d_s)
         ok = ok and ok_s
+        log("strong-scaling block done")
     ctx.close()
     if world == 1 and a.algo == "radix" and not a.no_dist_p1 and \
             os.environ.get("GSORT_FORCE_DIST") != "1":

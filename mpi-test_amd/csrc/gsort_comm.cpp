@@ -388,13 +388,23 @@ Comm *make_group_comm(GroupState *g, int rank) { return new GroupComm(g, rank); 
 namespace gsort {
 namespace {
 
-constexpr char kIpcMagic[8] = {'G', 'S', 'I', 'P', 'C', 0, 0, 1};
+constexpr char kIpcMagic[8] = {'G', 'S', 'I', 'P', 'C', 0, 0, 2};
 constexpr int kIpcMaxRanks = 64;
+// A staging buffer past 2^30 bytes is exported as chunks of 2^30, each its own allocation and
+// handle: with one exported 2^31-byte buffer (2^30 keys per rank at P = 2, packed) both ranks
+// stopped inside their first pull from the peer's buffer (hipIpcOpenMemHandle or the copy
+// from the mapping; GSORT_IPC_LOG, profiles/r05_ipc_2gib_hang.txt) and never returned, while
+// every run with buffers of at most 2^30 bytes passed.  16 chunks cover the largest send range
+// (2^31 keys of 4 B).
+constexpr size_t kIpcChunk = size_t(1) << 30;
+constexpr int kIpcChunks = 16;
 constexpr size_t kIpcNameOff = 8, kIpcNameMax = 88, kIpcRanksOff = 96;
 
 struct IpcSlot {
-    hipIpcMemHandle_t handle;  // the rank's staging buffer
-    uint64_t gen;              // bumped whenever the staging buffer is replaced
+    hipIpcMemHandle_t handle[kIpcChunks];  // the rank's staging buffer, chunk by chunk
+    uint64_t gen;                          // bumped whenever the staging buffer grows
+    uint64_t chunk;                        // bytes per chunk
+    uint32_t nchunk;
     uint64_t count[kIpcMaxRanks], displ[kIpcMaxRanks];  // bytes to / offsets for each rank
 };
 struct IpcShared {
@@ -439,13 +449,27 @@ IpcShared *map_shared(const char *name, bool create, std::string *err) {
     return static_cast<IpcShared *>(p);
 }
 
+// GSORT_IPC_LOG=1 (diagnostics): every step of every IPC collective to stderr
+static bool ipc_log_on() {
+    static const bool on = getenv("GSORT_IPC_LOG") && getenv("GSORT_IPC_LOG")[0] == '1';
+    return on;
+}
+
 class IpcComm : public Comm {
+    void log(const char *what, size_t a = 0, size_t b = 0) const {
+        if (!ipc_log_on()) return;
+        const double t = std::chrono::duration<double>(std::chrono::steady_clock::now() -
+                                                       std::chrono::steady_clock::time_point{}).count();
+        fprintf(stderr, "[ipc r%d %.6f] %s %zu %zu\n", rank_, t, what, a, b);
+        fflush(stderr);
+    }
+
   public:
     IpcComm(IpcShared *sh, int rank, int n)
-        : sh_(sh), peer_(n, nullptr), peer_gen_(n, 0) { rank_ = rank; size_ = n; }
+        : sh_(sh), peer_(n), peer_chunk_(n, 0), peer_gen_(n, 0) { rank_ = rank; size_ = n; }
     ~IpcComm() override {
-        for (void *p : peer_)
-            if (p) (void)hipIpcCloseMemHandle(p);
+        for (auto &v : peer_)
+            for (void *p : v) (void)hipIpcCloseMemHandle(p);
         // peers may still hold this rank's staging buffers open; the memory goes with the
         // process (or with their close), so the buffers are freed last
         for (void *p : stages_) (void)hipFree(p);
@@ -485,64 +509,110 @@ class IpcComm : public Comm {
         err = std::string("ipc group: ") + what + ": " + hipGetErrorString(e);
         return GSORT_EHIP;
     }
+    gsort_status copy(void *dst, const void *src, size_t bytes, hipStream_t s, const char *what) {
+        return hip(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s), what);
+    }
+    // chunk size of a staging buffer for `span` bytes (GSORT_IPC_CHUNK: a smaller one, the test
+    // hook that runs the chunked path on small inputs)
+    static size_t chunk_limit() {
+        static const size_t v = [] {
+            const char *e = getenv("GSORT_IPC_CHUNK");
+            const size_t c = e ? (size_t)strtoull(e, nullptr, 0) : 0;
+            return c ? c : kIpcChunk;
+        }();
+        return v;
+    }
     // the send range [0, span) into this rank's staging buffer (grown and re-exported as
     // needed), the counts into the control block
     gsort_status publish(const void *send, size_t span, const size_t *count, const size_t *displ,
                          hipStream_t s) {
+        log("publish", span, chunk_ * chunks_.size());
         IpcSlot &me = sh_->slot[rank_];
         for (int q = 0; q < size_ && count; ++q) {
             me.count[q] = count[q];
             me.displ[q] = displ[q];
         }
-        if (span > cap_) {
-            size_t cap = size_t(1) << 20;
-            while (cap < span) cap <<= 1;
-            void *p = nullptr;
-            gsort_status st = hip(hipMalloc(&p, cap), "hipMalloc (staging)");
-            if (st == GSORT_OK) st = hip(hipIpcGetMemHandle(&me.handle, p), "hipIpcGetMemHandle");
-            if (st != GSORT_OK) {
-                if (p) (void)hipFree(p);
-                return st;
+        if (span > chunk_ * chunks_.size()) {
+            // up to the chunk limit one power-of-two chunk, past it whole chunks (the ones
+            // already at the limit are kept, a smaller one is replaced)
+            const size_t lim = chunk_limit();
+            size_t chunk = size_t(1) << 20;
+            while (chunk < span && chunk < lim) chunk <<= 1;
+            chunk = std::min(chunk, lim);
+            const size_t n = (span + chunk - 1) / chunk;
+            if (n > (size_t)kIpcChunks) return fail("send range over the staging limit");
+            if (chunk != chunk_) chunks_.clear();
+            while (chunks_.size() < n) {
+                void *p = nullptr;
+                gsort_status st = hip(hipMalloc(&p, chunk), "hipMalloc (staging)");
+                if (st == GSORT_OK)
+                    st = hip(hipIpcGetMemHandle(&me.handle[chunks_.size()], p), "hipIpcGetMemHandle");
+                if (st != GSORT_OK) {
+                    if (p) (void)hipFree(p);
+                    return st;
+                }
+                // never freed while the group lives: freeing an exported allocation and
+                // exporting its replacement is what broke the peers' imports (header comment)
+                stages_.push_back(p);
+                chunks_.push_back(p);
             }
-            // never freed while the group lives: freeing an exported allocation and exporting
-            // its replacement is what broke the peers' imports (see the header comment)
-            stages_.push_back(p);
-            stage_ = p;
-            cap_ = cap;
+            chunk_ = chunk;
+            me.chunk = chunk;
+            me.nchunk = (uint32_t)n;
             me.gen = ++gen_;
         }
         gsort_status st = GSORT_OK;
-        if (span) st = hip(hipMemcpyAsync(stage_, send, span, hipMemcpyDeviceToDevice, s),
-                           "hipMemcpyAsync (stage)");
+        for (size_t o = 0; o < span && st == GSORT_OK; o += chunk_)
+            st = copy(chunks_[o / chunk_], static_cast<const char *>(send) + o,
+                      std::min(chunk_, span - o), s, "hipMemcpyAsync (stage)");
+        log("publish: staged, synchronising");
         if (st == GSORT_OK) st = hip(hipStreamSynchronize(s), "hipStreamSynchronize");
+        log("publish: done");
         return st;
     }
     // bytes [a, a + len) of rank r's send range into dst
     gsort_status pull(int r, const void *own, uint64_t a, size_t len, void *dst, hipStream_t s) {
         if (!len) return GSORT_OK;
-        const char *src = nullptr;
-        if (r == rank_) {
-            src = static_cast<const char *>(own);
-        } else {
-            const IpcSlot &ps = sh_->slot[r];
-            if (peer_gen_[r] != ps.gen) {
-                if (peer_[r]) (void)hipIpcCloseMemHandle(peer_[r]);
-                peer_[r] = nullptr;
+        if (r == rank_) return copy(dst, static_cast<const char *>(own) + a, len, s, "hipMemcpyAsync");
+        const IpcSlot &ps = sh_->slot[r];
+        std::vector<void *> &pv = peer_[r];
+        if (peer_gen_[r] != ps.gen) {
+            log("pull: opening peer", (size_t)r, (size_t)ps.gen);
+            // chunks of an unchanged size are the same allocations: only the new ones open
+            if (peer_chunk_[r] != ps.chunk) {
+                for (void *p : pv) (void)hipIpcCloseMemHandle(p);
+                pv.clear();
+                peer_chunk_[r] = ps.chunk;
+            }
+            while (pv.size() < ps.nchunk) {
                 void *p = nullptr;
-                gsort_status st = hip(hipIpcOpenMemHandle(&p, ps.handle,
+                gsort_status st = hip(hipIpcOpenMemHandle(&p, ps.handle[pv.size()],
                                                           hipIpcMemLazyEnablePeerAccess),
                                       "hipIpcOpenMemHandle");
                 if (st != GSORT_OK) return st;
-                peer_[r] = p;
-                peer_gen_[r] = ps.gen;
+                pv.push_back(p);
             }
-            src = static_cast<const char *>(peer_[r]);
+            peer_gen_[r] = ps.gen;
+            log("pull: opened", (size_t)r, pv.size());
         }
-        return hip(hipMemcpyAsync(dst, src + a, len, hipMemcpyDeviceToDevice, s), "hipMemcpyAsync");
+        const size_t c = peer_chunk_[r];
+        gsort_status st = GSORT_OK;
+        for (size_t end = a + len; a < end && st == GSORT_OK;) {
+            const size_t i = a / c, off = a % c, l = std::min(end - a, c - off);
+            if (i >= pv.size()) return fail("pull past the peer's staging buffer");
+            st = copy(dst, static_cast<const char *>(pv[i]) + off, l, s, "hipMemcpyAsync");
+            dst = static_cast<char *>(dst) + l;
+            a += l;
+        }
+        log("pull: queued", (size_t)r, len);
+        return st;
     }
     gsort_status finish(hipStream_t s, gsort_status st) {
+        log("finish: synchronising");
         gsort_status st2 = hip(hipStreamSynchronize(s), "hipStreamSynchronize");
+        log("finish: barrier");
         if (!barrier()) return fail("barrier timeout");
+        log("finish: done");
         return st != GSORT_OK ? st : st2;
     }
 
@@ -588,12 +658,13 @@ class IpcComm : public Comm {
 
   private:
     IpcShared *sh_;
-    void *stage_ = nullptr;
-    size_t cap_ = 0;
+    std::vector<void *> chunks_;               // this rank's staging buffer, chunk by chunk
+    size_t chunk_ = 0;                         // ... of this many bytes each
     uint64_t gen_ = 0;
-    std::vector<void *> stages_;            // every staging buffer this rank made
-    std::vector<void *> peer_;              // the peers' staging buffers, opened
-    std::vector<uint64_t> peer_gen_;        // ... at these generations
+    std::vector<void *> stages_;               // every staging chunk this rank made
+    std::vector<std::vector<void *>> peer_;    // the peers' staging chunks, opened
+    std::vector<size_t> peer_chunk_;           // ... of this size
+    std::vector<uint64_t> peer_gen_;           // ... at these generations
 };
 
 }  // namespace
