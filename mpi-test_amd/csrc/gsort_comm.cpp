@@ -540,7 +540,10 @@ class IpcComm : public Comm {
             while (chunk < span && chunk < lim) chunk <<= 1;
             chunk = std::min(chunk, lim);
             const size_t n = (span + chunk - 1) / chunk;
-            if (n > (size_t)kIpcChunks) return fail("send range over the staging limit");
+            if (n > (size_t)kIpcChunks) {
+                sh_->broken.store(1);  // the peers must not read this rank's stale staging
+                return fail("send range over the staging limit");
+            }
             if (chunk != chunk_) chunks_.clear();
             while (chunks_.size() < n) {
                 void *p = nullptr;
@@ -549,6 +552,7 @@ class IpcComm : public Comm {
                     st = hip(hipIpcGetMemHandle(&me.handle[chunks_.size()], p), "hipIpcGetMemHandle");
                 if (st != GSORT_OK) {
                     if (p) (void)hipFree(p);
+                    sh_->broken.store(1);
                     return st;
                 }
                 // never freed while the group lives: freeing an exported allocation and
@@ -575,6 +579,7 @@ class IpcComm : public Comm {
         if (!len) return GSORT_OK;
         if (r == rank_) return copy(dst, static_cast<const char *>(own) + a, len, s, "hipMemcpyAsync");
         const IpcSlot &ps = sh_->slot[r];
+        if (!ps.chunk || !ps.nchunk) return fail("pull from a peer without a staging buffer");
         std::vector<void *> &pv = peer_[r];
         if (peer_gen_[r] != ps.gen) {
             log("pull: opening peer", (size_t)r, (size_t)ps.gen);
@@ -618,7 +623,7 @@ class IpcComm : public Comm {
 
     gsort_status allgather(const void *send, void *recv, size_t bytes, hipStream_t s) override {
         gsort_status st = publish(send, bytes, nullptr, nullptr, s);
-        if (!barrier()) return fail("barrier timeout");
+        if (!barrier()) return st != GSORT_OK ? st : fail("barrier timeout or a peer failed");
         for (int r = 0; r < size_ && st == GSORT_OK; ++r)
             st = pull(r, send, 0, bytes, (char *)recv + (size_t)r * bytes, s);
         return finish(s, st);
@@ -631,7 +636,7 @@ class IpcComm : public Comm {
         for (int q = 0; q < size_; ++q)
             if (q != rank_ && scount[q]) span = std::max(span, sdispl[q] + scount[q]);
         gsort_status st = publish(send, span, scount, sdispl, s);
-        if (!barrier()) return fail("barrier timeout");
+        if (!barrier()) return st != GSORT_OK ? st : fail("barrier timeout or a peer failed");
         for (int r = 0; r < size_ && st == GSORT_OK; ++r) {
             const IpcSlot &ps = sh_->slot[r];
             if (ps.count[rank_] != rcount[r]) { st = fail("send/recv count mismatch"); break; }
@@ -641,7 +646,7 @@ class IpcComm : public Comm {
     }
     gsort_status bcast(void *buf, size_t bytes, int root, hipStream_t s) override {
         gsort_status st = publish(buf, rank_ == root ? bytes : 0, nullptr, nullptr, s);
-        if (!barrier()) return fail("barrier timeout");
+        if (!barrier()) return st != GSORT_OK ? st : fail("barrier timeout or a peer failed");
         if (st == GSORT_OK && rank_ != root) st = pull(root, buf, 0, bytes, buf, s);
         return finish(s, st);
     }

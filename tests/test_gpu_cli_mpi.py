@@ -57,7 +57,7 @@ def test_mpirun_stdout_equals_reference(orc, ref_cases, tmp_path, name, prog, P)
     assert err0.startswith("Endtime()-Starttime() = ") and err0.endswith(" sec\n")
 
 
-@pytest.mark.parametrize("chunk", [None, 1 << 19])
+@pytest.mark.parametrize("chunk", [None, 1 << 21])
 @pytest.mark.parametrize("prog", ["radix_sort", "sample_sort"])
 def test_mpirun_ipc_staging_regrowth_2p22(orc, ref_large, tmp_path, prog, chunk):
     """the IPC group's staging buffers start at 1 MiB and are re-allocated,
@@ -65,9 +65,10 @@ def test_mpirun_ipc_staging_regrowth_2p22(orc, ref_large, tmp_path, prog, chunk)
     per-collective export / open once failed.  The reference's 2^22-key uniform stream at P = 4
     moves ~1 M keys per rank (2-4 MiB payloads), so every rank's staging buffer grows mid-run;
     every rank's stdout must still equal the reference's own (tests/golden/ref_large.json).
-    chunk: staging buffers exported as 512 KiB chunks (GSORT_IPC_CHUNK; the product's chunks are
+    chunk: staging buffers exported as 2 MiB chunks (GSORT_IPC_CHUNK; the product's chunks are
     2^30 bytes -- one exported 2 GiB buffer hung both ranks in their first pull, 2^30 keys per
-    rank at P = 2), so growth by appended chunks and pulls across chunk boundaries run here."""
+    rank at P = 2), so a 1 MiB chunk replaced by 2 MiB ones, growth by appended chunks (rank 0's
+    16 MiB scatter: 8 chunks) and pulls across chunk boundaries all run here."""
     c = next(x for x in ref_large if x["id"] == f"uniform4194304s42__{prog}__P4")
     s = c["input"]
     keys = orc.gen(orc.UNIFORM, s["seed"], s["n"])
