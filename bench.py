@@ -534,24 +534,51 @@ def main():
     torch.cuda.set_device(dev)
     if world > 1:
         dist.init_process_group("gloo")  # bootstrap only: uid broadcast, barrier, max-time
-    uid = None
-    # GSORT_FORCE_DIST=1 (test hook, tests/test_gpu_rccl.py): one rank still runs the
-    # distributed algorithm over a one-rank RCCL communicator
-    if world > 1 or os.environ.get("GSORT_FORCE_DIST") == "1":
-        buf = torch.zeros(128, dtype=torch.uint8)
-        if rank == 0:
-            u = gsort.get_uid(ipc_ranks=world) if shared else gsort.get_uid()
-            buf = torch.tensor(list(u), dtype=torch.uint8)
-        if world > 1:
-            dist.broadcast(buf, 0)
-        uid = bytes(buf.tolist())
+    # GSORT_TRANSPORT=rccl|ipc overrides the choice (as in the drop-in CLIs)
+    forced = os.environ.get("GSORT_TRANSPORT")
+    use_ipc = (shared and forced != "rccl") or forced == "ipc"
+
+    def make_ctx(ipc):
+        uid = None
+        # GSORT_FORCE_DIST=1 (test hook, tests/test_gpu_rccl.py): one rank still runs the
+        # distributed algorithm over a one-rank RCCL communicator
+        if world > 1 or os.environ.get("GSORT_FORCE_DIST") == "1":
+            buf = torch.zeros(128, dtype=torch.uint8)
+            if rank == 0:
+                u = gsort.get_uid(ipc_ranks=world) if ipc else gsort.get_uid()
+                buf = torch.tensor(list(u), dtype=torch.uint8)
+            if world > 1:
+                dist.broadcast(buf, 0)
+            uid = bytes(buf.tolist())
+        return gsort.Context(rank=rank, nranks=world, device=dev, uid=uid)
+
+    # An RCCL communicator that fails to form (on any rank: the ranks agree over gloo) is not
+    # the end of the run: the ranks re-form over the IPC group and the line says so in
+    # `transport` (a hang inside RCCL's setup is not caught here)
+    fallback = None
+    try:
+        ctx, err = make_ctx(use_ipc), None
+    except gsort.GsortError as e:
+        ctx, err = None, e
+    if world > 1:
+        bad = torch.tensor([0 if ctx is not None else 1], dtype=torch.int32)
+        dist.all_reduce(bad, op=dist.ReduceOp.MAX)
+        if bad.item() and not use_ipc:
+            if ctx is not None:
+                ctx.close()
+            fallback = f"rccl communicator setup failed ({err if err else 'on another rank'})"
+            print(f"[bench r{rank}] {fallback}; re-forming over the IPC group", file=sys.stderr,
+                  flush=True)
+            use_ipc = True
+            ctx, err = make_ctx(True), None
+    if ctx is None:
+        raise err
 
     def barrier():
         if world > 1:
             dist.barrier()
 
     n_local = 1 << a.keys_log2
-    ctx = gsort.Context(rank=rank, nranks=world, device=dev, uid=uid)
     d_in = ctx.alloc(n_local * 4)
     ctx.generate(gsort.UNIFORM if dist_name == "uniform" else gsort.ZIPF, a.seed,
                  rank * n_local, n_local, d_in)
@@ -564,7 +591,7 @@ def main():
         print(f"[bench r{rank} +{time.perf_counter() - t_start:.1f}s] {msg}", file=sys.stderr,
               flush=True)
 
-    log(f"context ready: {n_local} keys, transport {'ipc (shared GPUs)' if shared else 'rccl' if world > 1 else 'none'}")
+    log(f"context ready: {n_local} keys, transport {'ipc' if use_ipc else 'rccl' if world > 1 else 'none'}")
     settle = {"ms": 0.0, "copies": 0}
     if a.settle_ms > 0:  # (module docstring: from idle to the sustained clocks)
         t_s = time.perf_counter()
@@ -648,8 +675,12 @@ def main():
         "warmup": a.warmup,
         "settle": settle,
         "transport": (None if world == 1 else
+                      f"ipc, after {fallback}" + ("; ranks share GPUs (prices nothing)"
+                                                  if shared else "")
+                      if fallback else
                       "ipc: ranks share GPUs (a rehearsal of the N > 1 path; prices nothing)"
-                      if shared else "rccl over xGMI"),
+                      if use_ipc and shared else
+                      "ipc over xGMI (GSORT_TRANSPORT=ipc)" if use_ipc else "rccl over xGMI"),
         "ms_per_step": round(ms_step, 4),
         "higher_is_better": True,
         "scaling": "weak",

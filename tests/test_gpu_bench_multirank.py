@@ -23,7 +23,7 @@ def _port():
         return s.getsockname()[1]
 
 
-def _run(args, ranks, torchrun, timeout=110):
+def _run(args, ranks, torchrun, timeout=110, env=None):
     bench = os.path.join(ROOT, "bench.py")
     tail = ["--gpus", str(ranks), "--steps", "2", "--warmup", "1", "--settle-ms", "0"] + args
     if torchrun:
@@ -32,7 +32,8 @@ def _run(args, ranks, torchrun, timeout=110):
                "--master-port", str(_port()), bench] + tail
     else:
         cmd = [sys.executable, bench] + tail
-    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=timeout)
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=timeout,
+                       env=dict(os.environ, **(env or {})))
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
@@ -70,3 +71,15 @@ def test_bench_torchrun_radix_3_ranks_zipf():
     line, _ = _run(["--keys-log2", "20", "--dist", "zipf", "--no-strong"], 3, torchrun=True)
     _common(line, 3, 20)
     assert "strong_scaling_cfg2" not in line
+
+
+def test_bench_rccl_setup_failure_falls_back_to_ipc():
+    """GSORT_TRANSPORT=rccl with two ranks on one GPU: RCCL refuses the communicator, every
+    rank sees the failure (gloo all-reduce), the group re-forms over IPC, the run completes
+    verified and the line names the fallback -- what bench.py does if RCCL cannot form on a
+    multi-GPU node instead of ending without a line."""
+    line, err = _run(["--keys-log2", "20", "--no-strong"], 2, torchrun=True,
+                     env={"GSORT_TRANSPORT": "rccl"})
+    assert line["verified"] is True
+    assert "rccl communicator setup failed" in line["transport"], line["transport"]
+    assert "re-forming over the IPC group" in err
