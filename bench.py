@@ -69,6 +69,9 @@ def parse():
                     help="skip the one-rank distributed-path block")
     ap.add_argument("--no-strong", action="store_true",
                     help="N > 1: skip the configs[2] strong-scaling block (2^31 keys in total)")
+    ap.add_argument("--strong", action="store_true",
+                    help="N > 1 with ranks sharing GPUs (the IPC rehearsal): run the "
+                         "strong-scaling block anyway (off by default there: it prices nothing)")
     ap.add_argument("--no-stats", action="store_true",
                     help="experiment: time the steps without per-phase events")
     ap.add_argument("--local", choices=["msd", "lsd"], default="msd",
@@ -271,9 +274,9 @@ def dist_p1(gsort, n_local, dist_id, seed, steps=5, algo="radix"):
     """The distributed path at N = 1 (one-rank RCCL communicator, GSORT_FORCE_DIST) -- the
     per-GPU cost the multi-GPU points pay before any xGMI time:
       radix:  sender grouping, radix select, packed self-exchange through RCCL, receive sort;
-      sample: local sort, regular samples + device splitter selection + broadcast, bucket
-              bounds, exchange of exact sizes, receive sort of the received sorted runs
-              (mpi_sample_sort.c:85, 89-128, 148-174)."""
+      sample: the same sender grouping (no local sort, round 6), regular samples and bucket
+              bounds read off the grouped block, device splitter selection + broadcast, the
+              same packed exchange and receive sort (mpi_sample_sort.c:85, 89-128, 148-174)."""
     os.environ["GSORT_FORCE_DIST"] = "1"
     try:
         ctx = gsort.Context(rank=0, nranks=1, device=0, uid=gsort.get_uid())
@@ -302,8 +305,9 @@ def dist_p1(gsort, n_local, dist_id, seed, steps=5, algo="radix"):
                      "ms_place", "ms_merge", "ms_bucket_sort")}
     avg["ms_level"] = [round(sum(s["ms_level"][i] for s in st) / len(st), 4) for i in range(2)]
     merge = avg["ms_merge"]
-    # the radix receive side reads the 2-B packed key; the sample sort exchanges int32 keys
-    bpk = 6 if algo == "radix" else 8
+    # both receive sides read the 2-B packed key (the sample sort's int32 exchange is only its
+    # fallback for the LSD local algorithm and ranks past 2^32 keys) and write the 4-B key
+    bpk = 6
     return {"algo": algo, "ms_per_step": round(ms, 4),
             "GKeys_s": round(n_local / (ms * 1e-3) / 1e9, 2),
             "phases_ms_avg": avg, "verified": bool(ok),
@@ -313,8 +317,7 @@ def dist_p1(gsort, n_local, dist_id, seed, steps=5, algo="radix"):
                              "frac": (round(n_local * bpk / (merge * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
                                       if merge else None),
                              "note": ("K11g (<= 9216-key buckets) + K18c (larger): read the "
-                                      "received key (2-B packed for radix, int32 for sample), "
-                                      "write the 4-B key")},
+                                      "received 2-B packed key, write the 4-B key")},
             "note": "GSORT_FORCE_DIST=1, one-rank RCCL communicator (self-exchange = HBM copy); "
                     "untimed steps, then 3 timed for phases"}
 
@@ -537,6 +540,12 @@ def main():
     # GSORT_TRANSPORT=rccl|ipc overrides the choice (as in the drop-in CLIs)
     forced = os.environ.get("GSORT_TRANSPORT")
     use_ipc = (shared and forced != "rccl") or forced == "ipc"
+    if world > 1:
+        # preflight: every rank forms the same kind of group -- if any rank's view
+        # (device count, GSORT_TRANSPORT) picks the IPC group, all of them do
+        flag = torch.tensor([int(use_ipc), int(shared)], dtype=torch.int32)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+        use_ipc, shared = bool(flag[0].item()), bool(flag[1].item())
 
     def make_ctx(ipc):
         uid = None
@@ -563,6 +572,12 @@ def main():
     if world > 1:
         bad = torch.tensor([0 if ctx is not None else 1], dtype=torch.int32)
         dist.all_reduce(bad, op=dist.ReduceOp.MAX)
+        if bad.item() and use_ipc:  # no second transport to try: every rank ends, non-zero
+            if ctx is not None:
+                ctx.close()
+            dist.destroy_process_group()
+            sys.exit(f"bench r{rank}: ipc group setup failed "
+                     f"({err if err else 'on another rank'})")
         if bad.item() and not use_ipc:
             if ctx is not None:
                 ctx.close()
@@ -727,7 +742,9 @@ def main():
     if last["exchanges"]:
         line["exchange"] = exchange_line(stats)
     ctx.free(d_in)
-    if world > 1 and a.algo == "radix" and not a.no_strong:
+    # (ranks sharing one GPU -- the IPC rehearsal -- skip it unless --strong: 2^31 keys plus
+    # scratch on one GPU and 2 GiB of staging per rank, for a number that prices nothing)
+    if world > 1 and a.algo == "radix" and not a.no_strong and (a.strong or not shared):
         # configs[2]'s strong-scaling point: 2^31 keys in total (the canonical stream, rank r's
         # block = its slice), a few timed steps bracketed like the headline's, max over ranks
         n_s = (1 << 31) // world

@@ -105,8 +105,10 @@ gsort_status gsort_runtime_info(gsort_runtime_info_t *out);
 gsort_status gsort_create(gsort_ctx **ctx, int rank, int nranks, int hip_device,
                           const gsort_uid *uid);
 /* In-process rank group: nranks contexts driven by nranks threads of ONE process, exchanging
- * through device-to-device copies (all on one GPU or on xGMI peers).  Used to run the
- * distributed algorithm with P ranks on a single GPU. */
+ * through device-to-device copies, all on ONE GPU (gsort_create_in_group refuses a rank on a
+ * device other than the first rank's with GSORT_EINVAL: the group's collectives are ordered by
+ * device-scope events).  Used to run the distributed algorithm with P ranks on a single GPU;
+ * ranks on several GPUs use gsort_create (RCCL, one process per GPU). */
 gsort_status gsort_group_create(gsort_group **grp, int nranks);
 gsort_status gsort_group_destroy(gsort_group *grp);
 gsort_status gsort_create_in_group(gsort_ctx **ctx, gsort_group *grp, int rank, int hip_device);

@@ -225,6 +225,7 @@ struct GroupState {
     std::vector<const void *> ptr;
     std::vector<const size_t *> count, displ;
     std::vector<hipEvent_t> ready, done;  // per rank, created by the rank on first use
+    int device = -1;                      // every rank's HIP device (group_state_join)
     explicit GroupState(int n_)
         : n(n_), ptr(n_), count(n_), displ(n_), ready(n_, nullptr), done(n_, nullptr) {}
     ~GroupState() {
@@ -238,6 +239,11 @@ struct GroupState {
 GroupState *group_state_create(int nranks) { return new GroupState(nranks); }
 void group_state_destroy(GroupState *g) { delete g; }
 int group_state_size(const GroupState *g) { return g->n; }
+bool group_state_join(GroupState *g, int device) {
+    std::lock_guard<std::mutex> lk(g->m);
+    if (g->device < 0) g->device = device;
+    return g->device == device;
+}
 
 class GroupComm : public Comm {
   public:
@@ -268,6 +274,11 @@ class GroupComm : public Comm {
         err = std::string("in-process group: ") + what;
         return GSORT_ECOMM;
     }
+    void break_group() {
+        std::lock_guard<std::mutex> lk(g_->m);
+        g_->broken = true;
+        g_->cv.notify_all();
+    }
     // every HIP call goes through hip_op (GSORT_SERIAL: serialized with all other contexts)
     template <class F>
     gsort_status hip(F &&f, const char *what) {
@@ -283,8 +294,9 @@ class GroupComm : public Comm {
     // barrier, the stream made to wait for every peer's ready event
     gsort_status open(hipStream_t s) {
         gsort_status st = GSORT_OK;
-        // (the ranks share one device: a device-scope release orders a rank's writes before a
-        // peer stream's copies; default flags if the runtime refuses that one)
+        // (the ranks share one device -- group_state_join refuses any other -- so a device-scope
+        // release orders a rank's writes before a peer stream's copies; default flags if the
+        // runtime refuses that one)
         for (hipEvent_t *e : {&g_->ready[rank_], &g_->done[rank_]})
             if (!*e && st == GSORT_OK)
                 st = hip([&] {
@@ -294,7 +306,9 @@ class GroupComm : public Comm {
                 }, "hipEventCreateWithFlags");
         if (st == GSORT_OK)
             st = hip([&] { return hipEventRecord(g_->ready[rank_], s); }, "hipEventRecord");
-        // (a failed rank still meets the barrier: the others must not wait for it in vain)
+        // a local failure breaks the group before the barrier: the peers must neither wait for
+        // this rank in vain nor copy its buffers behind a stale ready event
+        if (st != GSORT_OK) { break_group(); return st; }
         if (!barrier()) return fail("barrier timeout");
         for (int r = 0; r < size_ && st == GSORT_OK; ++r)
             if (r != rank_)
@@ -307,6 +321,7 @@ class GroupComm : public Comm {
     gsort_status close(hipStream_t s, gsort_status st) {
         if (st == GSORT_OK)
             st = hip([&] { return hipEventRecord(g_->done[rank_], s); }, "hipEventRecord");
+        if (st != GSORT_OK) { break_group(); return st; }  // every rank fails this collective
         if (!barrier()) return fail("barrier timeout");
         for (int r = 0; r < size_ && st == GSORT_OK; ++r)
             if (r != rank_)
@@ -392,10 +407,12 @@ constexpr char kIpcMagic[8] = {'G', 'S', 'I', 'P', 'C', 0, 0, 2};
 constexpr int kIpcMaxRanks = 64;
 // A staging buffer past 2^30 bytes is exported as chunks of 2^30, each its own allocation and
 // handle: with one exported 2^31-byte buffer (2^30 keys per rank at P = 2, packed) both ranks
-// stopped inside their first pull from the peer's buffer (hipIpcOpenMemHandle or the copy
-// from the mapping; GSORT_IPC_LOG, profiles/r05_ipc_2gib_hang.txt) and never returned, while
-// every run with buffers of at most 2^30 bytes passed.  16 chunks cover the largest send range
-// (2^31 keys of 4 B).
+// logged "pull: opening peer" and never "pull: opened" (GSORT_IPC_LOG,
+// profiles/r05_ipc_2gib_hang.txt): they hung inside hipIpcOpenMemHandle of the peer's 2^31-byte
+// export, before any copy, while every run with buffers of at most 2^30 bytes passed.  16
+// chunks = 16 GiB of staging per rank: 2^32 keys of 4 B, 2^33 packed keys of 2 B.  The
+// distributed radix caps a rank below 2^32 keys; the int32 send paths (sample sort's fallback,
+// the LSD passes) check their largest send range against kIpcStageMax up front.
 constexpr size_t kIpcChunk = size_t(1) << 30;
 constexpr int kIpcChunks = 16;
 constexpr size_t kIpcNameOff = 8, kIpcNameMax = 88, kIpcRanksOff = 96;
@@ -612,6 +629,7 @@ class IpcComm : public Comm {
         log("pull: queued", (size_t)r, len);
         return st;
     }
+    uint64_t max_send_bytes() const override { return (uint64_t)kIpcChunks * chunk_limit(); }
     gsort_status finish(hipStream_t s, gsort_status st) {
         log("finish: synchronising");
         gsort_status st2 = hip(hipStreamSynchronize(s), "hipStreamSynchronize");

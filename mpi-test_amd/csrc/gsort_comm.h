@@ -36,6 +36,9 @@ class Comm {
                                    void *recv, const size_t *rcount, const size_t *rdispl,
                                    hipStream_t s) = 0;
     virtual gsort_status bcast(void *buf, size_t bytes, int root, hipStream_t s) = 0;
+    // the largest send range (bytes of one rank's send buffer its peers read in one alltoallv)
+    // the transport carries: the IPC group's staging limit, unbounded otherwise
+    virtual uint64_t max_send_bytes() const { return ~0ull; }
     std::string err;
 
   protected:
@@ -56,5 +59,8 @@ Comm *make_group_comm(GroupState *g, int rank);
 GroupState *group_state_create(int nranks);
 void group_state_destroy(GroupState *g);
 int group_state_size(const GroupState *g);
+// The group's device: the first rank to join sets it, a rank on another device is refused (the
+// group's ordering events are device-scope).  false: refused.
+bool group_state_join(GroupState *g, int device);
 
 }  // namespace gsort

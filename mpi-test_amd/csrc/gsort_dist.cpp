@@ -238,15 +238,282 @@ gsort_status sort_groups16(gsort_ctx *c, uint16_t *pack,
     return GSORT_OK;
 }
 
-// ---- distributed radix (P > 1): local sort, exact splitters, ONE exchange, local sort ------
+// The listed 16-bit groups of the packed block (ids < 65536, any order, duplicates allowed)
+// sorted in place through sort_groups16 -- the host path for groups past K13g's 32 768 keys
+// (their bounds read from gb: one host round trip).
+gsort_status sort_groups16_host(gsort_ctx *c, uint16_t *pack, const uint64_t *gb,
+                                std::vector<uint64_t> hs) {
+    std::sort(hs.begin(), hs.end());
+    hs.erase(std::unique(hs.begin(), hs.end()), hs.end());
+    if (hs.empty()) return GSORT_OK;
+    std::vector<uint64_t> h_gb(2 * hs.size());
+    for (size_t i = 0; i < hs.size(); ++i)
+        HIP_TRY(c, hipMemcpyAsync(&h_gb[2 * i], gb + hs[i], 16, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    std::vector<std::pair<uint64_t, uint64_t>> nonempty;  // {h, first position}
+    std::vector<uint64_t> ends;
+    for (size_t i = 0; i < hs.size(); ++i)
+        if (h_gb[2 * i + 1] > h_gb[2 * i]) {
+            nonempty.push_back({hs[i], h_gb[2 * i]});
+            ends.push_back(h_gb[2 * i + 1]);
+        }
+    if (!nonempty.empty()) ST_TRY(sort_groups16(c, pack, nonempty, ends));
+    return GSORT_OK;
+}
+
+
+// ---- the packed distributed sorts (P ranks, one exchange of 2 B per key) ----------------------
+// Both distributed sorts share one sender and one receiver; they differ only in how the block
+// boundaries are found:
+//   radix  (mpi_radix_sort.c:133-195): rank q ends with global positions [qB, (q+1)B) -- the
+//          boundary keys by an exact radix select;
+//   sample (mpi_sample_sort.c:85-174): rank q ends with the keys in (s_{q-1}, s_q] of the
+//          reference's splitters -- regular samples, splitters on the root, bucket bounds.
+// (1) group_block16: the block grouped by its top 16 bits (MSD levels 3 and 2 only: every
+//     receiver sorts the low 16 bits anyway), the low 16 bits of every key stored as the packed
+//     send buffer, the 65 537 group bounds from the plan;
+// (2) the boundaries (select_radix / select_sample): small device kernels + collectives on the
+//     grouped block; only the groups holding a boundary (and, for the sample sort, a regular
+//     sample) are sorted, in place, by K13g -- never the whole block;
+// (3) the cut of every rank's block into P contiguous runs (host, from the gathered counts);
+// (4) packed_exchange_sort: one u32 count per (destination, 16-bit bucket) and the packed keys
+//     in two grouped send/recv rounds, then every received bucket sorted from its P pieces.
+
+// The block of n_in keys grouped by its top 16 bits (ordered u32): *pack (n_in u16, m_pack) =
+// the low 16 bits, grouped; *gb (65 537 u64, m_gb) = the group bounds.  A block of <= kLocalMax
+// keys is sorted whole in LDS instead, then bounded and packed.
+gsort_status group_block16(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in,
+                           gsort_stats *stats, uint16_t **pack_out, uint64_t **gb_out) {
+    ST_TRY(ensure(c, c->slot[S_TMP], std::max<uint64_t>(n_in, 1) * 4));
+    ST_TRY(ensure(c, c->m_gb, (size_t)(kBuckets16 + 1) * 8));
+    ST_TRY(ensure(c, c->m_pack, std::max<uint64_t>(n_in, 1) * 2));
+    uint64_t *gb = reinterpret_cast<uint64_t *>(c->m_gb.p);
+    uint16_t *pack = reinterpret_cast<uint16_t *>(c->m_pack.p);
+    if (stats) stats->local_algo = c->local_algo;
+    const bool packed_msd = n_in > kLocalMax;
+    gsort_stats tmp_st;
+    memset(&tmp_st, 0, sizeof(tmp_st));
+    int32_t *sorted = nullptr;
+    if (!packed_msd) {
+        ST_TRY(ensure(c, c->slot[S_SORTED], std::max<uint64_t>(n_in, 1) * 4));
+        sorted = slot_ptr<int32_t>(c, S_SORTED);
+    }
+    ST_TRY(msd_sort(c, reinterpret_cast<const uint32_t *>(d_keys), n_in,
+                    reinterpret_cast<uint32_t *>(sorted), slot_ptr<uint32_t>(c, S_TMP),
+                    stats ? stats : &tmp_st, true, packed_msd ? pack : nullptr, gb));
+    hipEvent_t t = tic(c);
+    if (packed_msd && c->plan16) {
+        // gb written by the two-level plan
+    } else if (packed_msd) {
+        HIP_TRY(c, launch_gb_from_plan(reinterpret_cast<uint64_t *>(c->d_small + OFF_BASES),
+                                       reinterpret_cast<uint64_t *>(c->d_small + OFF_TOT),
+                                       reinterpret_cast<uint64_t *>(c->m_next[0].p),
+                                       (uint32_t)c->group16_nseg,
+                                       reinterpret_cast<uint64_t *>(c->m_cstart.p), n_in, gb,
+                                       c->stream));
+    } else {
+        uint64_t *h_one = reinterpret_cast<uint64_t *>(c->h_small + OFF_ONE);
+        uint64_t *d_one = reinterpret_cast<uint64_t *>(c->d_small + OFF_ONE);
+        HIP_TRY(c, hipStreamSynchronize(c->stream));  // h_one may feed an earlier copy
+        h_one[0] = 0;
+        h_one[1] = n_in;
+        HIP_TRY(c, hipMemcpyAsync(d_one, h_one, 16, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(c, launch_run_bounds(sorted, d_one, d_one + 1, 1, gb, c->stream));
+        HIP_TRY(c, launch_pack16(sorted, n_in, pack, c->stream));
+    }
+    toc(c, PH_PLACE, t);
+    if (check_mode()) ST_TRY(check_bounds(c, gb, kBuckets16 + 1, n_in, "sender bucket bounds"));
+    *pack_out = pack;
+    *gb_out = gb;
+    return GSORT_OK;
+}
+
+// Every rank's block size must stay within what the transport can carry in one alltoallv
+// (the IPC group's staging limit), bytes_per_key of it: checked on all ranks from the gathered
+// sizes, so all of them fail alike before any key moves.
+gsort_status check_send_limit(gsort_ctx *c, const std::vector<uint64_t> &n_all,
+                              uint64_t bytes_per_key, const char *what) {
+    const uint64_t lim = c->comm ? c->comm->max_send_bytes() : ~0ull;
+    for (size_t r = 0; r < n_all.size(); ++r)
+        if (n_all[r] > lim / bytes_per_key)
+            return set_err(c, GSORT_EINVAL, std::string(what) + ": rank " + std::to_string(r) +
+                                                " would send up to " +
+                                                std::to_string(n_all[r] * bytes_per_key) +
+                                                " bytes, over the transport's " +
+                                                std::to_string(lim) + "-byte limit");
+    return GSORT_OK;
+}
+
+// (4)-(6): the packed exchange and the receive sort.  cut (P + 1): this rank's runs, run q =
+// [cut[q], cut[q+1]) of the grouped block goes to rank q; recv[p] = the keys rank p sends here;
+// destination q's keys lie in the 16-bit buckets [hlo[q], hlo[q] + nh[q]) (every rank computes
+// the same hlo / nh).  The sorted result (sum of recv keys) is left in S_OUT.
+gsort_status packed_exchange_sort(gsort_ctx *c, uint16_t *pack, const uint64_t *gb,
+                                  const std::vector<uint64_t> &cut,
+                                  const std::vector<uint64_t> &recv,
+                                  const std::vector<uint64_t> &hlo,
+                                  const std::vector<uint64_t> &nh, gsort_stats *stats,
+                                  int32_t **d_out, uint64_t *n_out) {
+    const int P = c->nranks, me = c->rank;
+    std::vector<uint64_t> send(P);
+    for (int q = 0; q < P; ++q) send[q] = cut[q + 1] - cut[q];
+    uint64_t mine = 0;
+    for (int p = 0; p < P; ++p) mine += recv[p];
+    ST_TRY(ensure(c, c->slot[S_RECV], std::max<uint64_t>(mine, 1) * 2));
+    ST_TRY(ensure(c, c->slot[S_OUT], std::max<uint64_t>(mine, 1) * 4));
+    // test hook GSORT_RCCL_SELF=1: the self pieces do go through the transport (RcclComm then
+    // sends them through ncclSend / ncclRecv: tests/test_gpu_rccl.py pins RCCL's message limit)
+    static const bool self_moved = getenv("GSORT_RCCL_SELF") && getenv("GSORT_RCCL_SELF")[0] == '1';
+    uint64_t meta_n = 0, meta_self = ~0ull;  // meta_self: this rank's own count section
+    std::vector<uint64_t> rng;
+    for (int q = 0; q < P; ++q)
+        if (send[q]) {
+            rng.insert(rng.end(), {cut[q], cut[q + 1], hlo[q], nh[q], meta_n});
+            if (q == me) meta_self = meta_n;
+            meta_n += nh[q];
+        }
+    uint64_t nsrc = 0;
+    for (int p = 0; p < P; ++p) nsrc += recv[p] ? 1 : 0;
+    ST_TRY(ensure(c, c->m_meta, (std::max<uint64_t>(meta_n, 1) + nsrc * nh[me] + 1) * 4 +
+                                    (rng.size() + P + 2) * 8));
+    uint32_t *meta_s = reinterpret_cast<uint32_t *>(c->m_meta.p);
+    // (one word of gap: an in-place self offset below, meta_self - (meta_r - meta_s), is then
+    // at most -2 and never the "no source" mark ~0)
+    uint32_t *meta_r = meta_s + std::max<uint64_t>(meta_n, 1) + 1;
+    uint64_t *d_tab = reinterpret_cast<uint64_t *>(
+        reinterpret_cast<char *>(c->m_meta.p) +
+        (((std::max<uint64_t>(meta_n, 1) + nsrc * nh[me] + 1) * 4 + 7) & ~size_t(7)));
+    std::vector<uint64_t> tab(rng);
+    std::vector<uint64_t> moff(P, ~0ull);
+    {
+        uint64_t k = 0;
+        for (int p = 0; p < P; ++p)
+            if (recv[p]) moff[p] = (k++) * nh[me];
+    }
+    // the rank's own counts are read where K15 writes them (an offset relative to meta_r, mod
+    // 2^64), like its own keys below: no self copy in the count exchange either
+    const bool meta_in_place = !self_moved && recv[me] && meta_self != ~0ull;
+    if (meta_in_place) moff[me] = meta_self - (uint64_t)(meta_r - meta_s);
+    tab.insert(tab.end(), moff.begin(), moff.end());
+    // staged through pinned memory (a pageable copy blocks the host in the runtime's staging):
+    // OFF_PLAN + 8 KiB is free here -- the select's host reads synchronised the stream, and
+    // step (5) below uses only OFF_PLAN's first 2P words
+    uint64_t *h_tab = reinterpret_cast<uint64_t *>(c->h_small + OFF_PLAN + 8192);
+    if (OFF_PLAN + 8192 + tab.size() * 8 > kSmallBytes)
+        return set_err(c, GSORT_EINVAL, "exchange table too large");
+    std::copy(tab.begin(), tab.end(), h_tab);
+    HIP_TRY(c, hipMemcpyAsync(d_tab, h_tab, tab.size() * 8, hipMemcpyHostToDevice, c->stream));
+    const uint64_t *d_rng = d_tab, *d_moff = d_tab + rng.size();
+    hipEvent_t t = tic(c);
+    HIP_TRY(c, launch_meta_counts(gb, d_rng, (int)(rng.size() / 5), meta_s, c->stream));
+    toc(c, PH_PLACE, t);
+    std::vector<size_t> sc(P, 0), sd(P, 0), rc(P, 0), rd(P, 0);
+    {
+        uint64_t mo = 0, ro = 0;
+        for (int q = 0; q < P; ++q) {
+            if (send[q]) { sc[q] = nh[q] * 4; sd[q] = mo * 4; mo += nh[q]; }
+            if (recv[q]) { rc[q] = nh[me] * 4; rd[q] = ro * 4; ro += nh[me]; }
+        }
+        if (meta_in_place) sc[me] = rc[me] = 0;
+    }
+    std::vector<uint64_t> roffs(P + 1, 0);
+    for (int p = 0; p < P; ++p) roffs[p + 1] = roffs[p] + recv[p];
+    t = tic_rec(c);
+    ST_TRY(comm_try(c, c->comm->alltoallv(meta_s, sc.data(), sd.data(), meta_r, rc.data(),
+                                          rd.data(), c->stream)));
+    toc_rec(c, PH_EXCH, t);
+    for (int q = 0; q < P; ++q)
+        if (stats && q != me) {
+            stats->bytes_sent += send[q] * 2;
+            stats->max_pair_bytes = std::max<uint64_t>(stats->max_pair_bytes, send[q] * 2);
+        }
+    // the payload, queued right behind the counts: the receive plan below overlaps it.  The
+    // rank's own piece is not moved at all: the receive kernels read it where it lies in the
+    // send buffer (its run offset below is taken relative to rbuf, mod 2^64) -- at P = 1 that is
+    // the whole 512 MiB of a 2^28-key block, at P = 8 an eighth of it
+    uint16_t *rbuf = slot_ptr<uint16_t>(c, S_RECV);
+    t = tic_rec(c);
+    for (int q = 0; q < P; ++q) {
+        const bool self = q == me && !self_moved;
+        sc[q] = self ? 0 : send[q] * 2;
+        sd[q] = cut[q] * 2;
+        rc[q] = self ? 0 : recv[q] * 2;
+        rd[q] = roffs[q] * 2;
+    }
+    ST_TRY(comm_try(c, c->comm->alltoallv(pack, sc.data(), sd.data(), rbuf, rc.data(), rd.data(),
+                                          c->stream)));
+    toc_rec(c, PH_EXCH, t);
+    if (stats) stats->exchanges = 1;
+    // (5) the receive plan from the counts alone: run bounds, bucket starts, the K11g / K18 work
+    // lists of this rank's bucket range
+    t = tic(c);
+    ST_TRY(ensure(c, c->m_rpos, (size_t)P * (kBuckets16 + 1) * 8));
+    ST_TRY(ensure(c, c->m_bsize, kBsizeBytes));
+    ST_TRY(ensure_list(c, c->m_next[0], kBuckets16));
+    for (auto &b : c->m_local) ST_TRY(ensure_list(c, b, kBuckets16));
+    uint64_t *pos = reinterpret_cast<uint64_t *>(c->m_rpos.p);
+    uint64_t *bsize = reinterpret_cast<uint64_t *>(c->m_bsize.p), *bstart = bsize + kBuckets16;
+    uint64_t *h_r = reinterpret_cast<uint64_t *>(c->h_small + OFF_PLAN);
+    uint64_t *d_r = reinterpret_cast<uint64_t *>(c->d_small + OFF_PLAN);
+    // (no stream sync for h_r: nothing has copied from OFF_PLAN since the select's host read
+    // synchronised the stream -- the selects stage through OFF_PLAN + 8 KiB and m_split -- and
+    // a sync here idled the GPU ~40 us)
+    for (int p = 0; p < P; ++p) { h_r[p] = roffs[p]; h_r[P + p] = recv[p]; }
+    if (!self_moved)  // the self piece, in place: its offset from rbuf in keys, from integer
+        h_r[me] = elem_offset(pack + cut[me], rbuf);  // addresses (mod 2^64, run_ptr)
+    HIP_TRY(c, hipMemcpyAsync(d_r, h_r, (size_t)2 * P * 8, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemsetAsync(c->d_small + OFF_CTR, 0, kCtrBytes, c->stream));
+    // the runs' bucket bounds and the bucket starts in one row scan of P + 1 rows (the last
+    // row is every bucket's total over the sources); classify reads the sizes off bstart
+    HIP_TRY(c, launch_recv_plan_from_meta(meta_r, d_moff, (uint32_t)hlo[me], (uint32_t)nh[me], P,
+                                          pos, bstart, bstart + kBuckets16 + 1, c->stream));
+    const WorkLists wl = work_lists(c, 0);
+    HIP_TRY(c, launch_classify_range(nullptr, bstart, wl, (uint32_t)hlo[me],
+                                     (uint32_t)(hlo[me] + nh[me]), c->stream));
+    toc(c, PH_COUNT, t);
+    uint64_t h[3 * (kLocalClasses + 1)];
+    ST_TRY(read_counters(c, h));
+    if (check_mode()) {
+        for (int p = 0; p < P; ++p)
+            ST_TRY(check_bounds(c, pos + (size_t)p * (kBuckets16 + 1), kBuckets16 + 1, recv[p],
+                                "received run bounds"));
+        uint64_t keys = 0;
+        for (int l = 0; l <= kLocalClasses; ++l) keys += h[3 * l + 1];
+        if (keys != mine)
+            return set_err(c, GSORT_EINVAL, "GSORT_CHECK receive lists hold " +
+                                                std::to_string(keys) + " keys, want " +
+                                                std::to_string(mine) + " (rank " +
+                                                std::to_string(me) + ")");
+    }
+    // (6) every bucket sorted from its P pieces: K11g by size class, K18c past them (classes
+    // >= recv_cx and list 0, one persistent launch); a bucket past K18c's reach sends the block
+    // through recv_sort's MSD levels 1 and 0
+    t = tic(c);
+    uint32_t *out = slot_ptr<uint32_t>(c, S_OUT);
+    if (h[0] && h[2] > kHxMax) {  // recv_sort wants the P runs back to back in rbuf
+        if (recv[me] && !self_moved)
+            HIP_TRY(c, hipMemcpyAsync(rbuf + roffs[me], pack + cut[me], recv[me] * 2,
+                                      hipMemcpyDeviceToDevice, c->stream));
+        ST_TRY(ensure(c, c->slot[S_TMP], std::max<uint64_t>(mine, 1) * 4));
+        ST_TRY(recv_sort(c, rbuf, true, recv, mine, out, slot_ptr<uint32_t>(c, S_TMP), stats));
+    } else {
+        ST_TRY(sort_recv_lists(c, rbuf, true, pos, d_r, P, bstart, wl, h, out, stats));
+    }
+    toc(c, PH_MERGE, t);
+    *d_out = slot_ptr<int32_t>(c, S_OUT);
+    *n_out = mine;
+    return GSORT_OK;
+}
+
+// ---- distributed radix (P > 1): group, exact splitters, ONE exchange, receive sort --------
 // The reference keeps rank q on global positions [qB, (q+1)B) by routing every key through
 // rank 0 on each of its base-P passes (mpi_radix_sort.c:139 Scatter, :150-173 all-to-all,
-// :180-192 Gatherv).  Here: (1) each rank sorts its block (MSD local sort); (2) radix select of
-// the exact boundary keys: 4 rounds of 8 bits, each counting the keys below 257 thresholds per
-// boundary by binary search on the sorted blocks (K13) and all-gathering the counts; (3) the
+// :180-192 Gatherv).  Here: (1) each rank groups its block by the top 16 bits; (2) radix select
+// of the exact boundary keys: 4 rounds of 8 bits, each counting the keys below 257 thresholds
+// per boundary by binary search on the grouped block (K13) and all-gathering the counts; (3) the
 // cut of every block (gsort_plan_split: copies of a boundary key go left in rank order); (4) one
-// grouped send/recv of contiguous runs; (5) the received sorted runs are bucketed by their top
-// 16 bits and every bucket is finished in LDS (recv_sort).
+// grouped send/recv of contiguous runs; (5) the received runs are bucketed by their top 16 bits
+// and every bucket is finished in LDS (packed_exchange_sort).
 gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in,
                               int32_t **d_out, uint64_t *n_out, gsort_stats *stats) {
     const int P = c->nranks, me = c->rank;
@@ -262,56 +529,14 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
         if (n_all[r] >= (1ull << 32))
             return set_err(c, GSORT_EINVAL, "radix: a rank holds >= 2^32 keys (rank " +
                                                 std::to_string(r) + "); split the input further");
-    const uint64_t cap = std::max<uint64_t>(std::max(n_in, mine), 1);
-    ST_TRY(ensure(c, c->slot[S_TMP], cap * 4));
-    ST_TRY(ensure(c, c->slot[S_RECV], std::max<uint64_t>(mine, 1) * 4));
+    ST_TRY(check_send_limit(c, n_all, 2, "radix"));
+    // (the receive side's buffers first: allocated before the grouping, as they always were)
+    ST_TRY(ensure(c, c->slot[S_RECV], std::max<uint64_t>(mine, 1) * 2));
     ST_TRY(ensure(c, c->slot[S_OUT], std::max<uint64_t>(mine, 1) * 4));
-    ST_TRY(ensure(c, c->m_gb, (size_t)(kBuckets16 + 1) * 8));
-    ST_TRY(ensure(c, c->m_pack, std::max<uint64_t>(n_in, 1) * 2));
-    uint64_t *gb = reinterpret_cast<uint64_t *>(c->m_gb.p);
-    uint16_t *pack = reinterpret_cast<uint16_t *>(c->m_pack.p);
-    // (1) group the block by its top 16 bits (MSD levels 3 and 2 only: the receivers sort the
-    // low 16 bits anyway).  Level 2 stores just the low 16 bits of every key -- the packed send
-    // buffer -- and the 16-bit bucket bounds gb come from the MSD plan (K17), not the keys.  A
-    // block of <= kLocalMax keys is sorted whole in LDS instead, then bounded and packed.
-    if (stats) stats->local_algo = c->local_algo;
-    const bool packed_msd = n_in > kLocalMax;
-    hipEvent_t t;
-    {
-        gsort_stats tmp_st;
-        memset(&tmp_st, 0, sizeof(tmp_st));
-        int32_t *sorted = nullptr;
-        if (!packed_msd) {
-            ST_TRY(ensure(c, c->slot[S_SORTED], std::max<uint64_t>(n_in, 1) * 4));
-            sorted = slot_ptr<int32_t>(c, S_SORTED);
-        }
-        ST_TRY(msd_sort(c, reinterpret_cast<const uint32_t *>(d_keys), n_in,
-                        reinterpret_cast<uint32_t *>(sorted), slot_ptr<uint32_t>(c, S_TMP),
-                        stats ? stats : &tmp_st, true, packed_msd ? pack : nullptr, gb));
-        t = tic(c);
-        if (packed_msd && c->plan16) {
-            // gb written by the two-level plan
-        } else if (packed_msd) {
-            HIP_TRY(c, launch_gb_from_plan(reinterpret_cast<uint64_t *>(c->d_small + OFF_BASES),
-                                           reinterpret_cast<uint64_t *>(c->d_small + OFF_TOT),
-                                           reinterpret_cast<uint64_t *>(c->m_next[0].p),
-                                           (uint32_t)c->group16_nseg,
-                                           reinterpret_cast<uint64_t *>(c->m_cstart.p), n_in,
-                                           gb, c->stream));
-        } else {
-            uint64_t *h_one = reinterpret_cast<uint64_t *>(c->h_small + OFF_ONE);
-            uint64_t *d_one = reinterpret_cast<uint64_t *>(c->d_small + OFF_ONE);
-            HIP_TRY(c, hipStreamSynchronize(c->stream));  // h_one may feed an earlier copy
-            h_one[0] = 0;
-            h_one[1] = n_in;
-            HIP_TRY(c, hipMemcpyAsync(d_one, h_one, 16, hipMemcpyHostToDevice, c->stream));
-            HIP_TRY(c, launch_run_bounds(sorted, d_one, d_one + 1, 1, gb, c->stream));
-            HIP_TRY(c, launch_pack16(sorted, n_in, pack, c->stream));
-        }
-        toc(c, PH_PLACE, t);
-    }
-    int pr = stats ? stats->passes_run : 0;
-    if (check_mode()) ST_TRY(check_bounds(c, gb, kBuckets16 + 1, n_in, "sender bucket bounds"));
+    uint16_t *pack = nullptr;
+    uint64_t *gb = nullptr;
+    ST_TRY(group_block16(c, d_keys, n_in, stats, &pack, &gb));
+    const int pr = stats ? stats->passes_run : 0;
 
     // (2) radix select of v_q, the g_q-th smallest key, for the P-1 inner boundaries: 4 rounds of
     // 8 bits, every round decided on the device (K13s sums the all-gathered counts, picks the
@@ -355,9 +580,9 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
     };
     // the thresholds of round 0 (prefix 0) and of round 2 after the host path (prefix: the top
     // 16 bits); prefix and g go along.  Staged in pinned memory at OFF_PLAN + 8 KiB (free: the
-    // exchange table below reuses it after select_rounds' synchronisation): a pageable copy
-    // would hold the host in the runtime's staging until the stream had drained the sender's
-    // K1h .. K3a, and the select's kernels would then be queued behind an idle GPU
+    // exchange table reuses it after select_rounds' synchronisation): a pageable copy would
+    // hold the host in the runtime's staging until the stream had drained the sender's K1h ..
+    // K3a, and the select's kernels would then be queued behind an idle GPU
     const size_t nx = (size_t)2 * nb + (size_t)nb * M;
     if (OFF_PLAN + 8192 + nx * 8 > kSmallBytes)
         return set_err(c, GSORT_EINVAL, "select thresholds too large");
@@ -370,7 +595,7 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
         HIP_TRY(c, hipMemcpyAsync(d_pref, hx, nx * 8, hipMemcpyHostToDevice, c->stream));
         return GSORT_OK;
     };
-    t = tic_rec(c);
+    hipEvent_t t = tic_rec(c);
     if (nb > 0) {  // (one rank: no boundary, nothing to select)
         ST_TRY(put_thresholds(24));
         ST_TRY(select_rounds(0));
@@ -378,24 +603,10 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
         for (int p = 0; p < P; ++p)
             for (int q = 0; q < nb; ++q) big |= all[(size_t)p * W + (size_t)nb * M + q] != 0;
         if (big) {  // a boundary group past K13g's reach on some rank: every rank takes this
-            std::vector<std::pair<uint64_t, uint64_t>> groups;  // {h, first position}
+            std::vector<uint64_t> hs;
             for (int q = 0; q < nb; ++q)
-                if (g[q] < N) groups.push_back({prefix[q] >> 16, 0});
-            std::sort(groups.begin(), groups.end());
-            groups.erase(std::unique(groups.begin(), groups.end()), groups.end());
-            std::vector<uint64_t> h_gb(2 * groups.size());
-            for (size_t i = 0; i < groups.size(); ++i)
-                HIP_TRY(c, hipMemcpyAsync(&h_gb[2 * i], gb + groups[i].first, 16,
-                                          hipMemcpyDeviceToHost, c->stream));
-            HIP_TRY(c, hipStreamSynchronize(c->stream));
-            std::vector<std::pair<uint64_t, uint64_t>> nonempty;
-            std::vector<uint64_t> ends;
-            for (size_t i = 0; i < groups.size(); ++i)
-                if (h_gb[2 * i + 1] > h_gb[2 * i]) {
-                    nonempty.push_back({groups[i].first, h_gb[2 * i]});
-                    ends.push_back(h_gb[2 * i + 1]);
-                }
-            if (!nonempty.empty()) ST_TRY(sort_groups16(c, pack, nonempty, ends));
+                if (g[q] < N) hs.push_back(prefix[q] >> 16);
+            ST_TRY(sort_groups16_host(c, pack, gb, hs));
             for (int q = 0; q < nb; ++q) prefix[q] = prefix[q] >> 16 << 16;
             ST_TRY(put_thresholds(8));
             ST_TRY(select_rounds(2));
@@ -414,9 +625,8 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
     gsort_status ps = gsort_plan_split(P, n_all.data(), lt.data(), le.data(), me, send.data(),
                                        recv.data());
     if (ps != GSORT_OK) return set_err(c, ps, "inconsistent splitter counts");
-    // (4) one exchange of the keys' low 16 bits: every destination block's keys lie in a known
-    // range of 16-bit buckets (from the boundary keys), so the top 16 bits travel as one count
-    // per (destination, bucket) instead of 2 bytes per key
+    // every destination block's keys lie in a known range of 16-bit buckets (from the boundary
+    // keys), so the top 16 bits travel as one count per (destination, bucket)
     std::vector<uint64_t> hlo(P), nh(P), cut(P + 1, 0);
     for (int q = 0; q < P; ++q) {
         const uint64_t lo = q == 0 ? 0 : (g[q - 1] >= N ? 0xFFFFFFFFull : prefix[q - 1]);
@@ -425,147 +635,11 @@ gsort_status radix_dist_exact(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in
         nh[q] = (hi >> 16) - hlo[q] + 1;
         cut[q + 1] = cut[q] + send[q];
     }
-    // test hook GSORT_RCCL_SELF=1: the self pieces do go through the transport (RcclComm then
-    // sends them through ncclSend / ncclRecv: tests/test_gpu_rccl.py pins RCCL's message limit)
-    static const bool self_moved = getenv("GSORT_RCCL_SELF") && getenv("GSORT_RCCL_SELF")[0] == '1';
-    uint64_t meta_n = 0, meta_self = ~0ull;  // meta_self: this rank's own count section
-    std::vector<uint64_t> rng;
-    for (int q = 0; q < P; ++q)
-        if (send[q]) {
-            rng.insert(rng.end(), {cut[q], cut[q + 1], hlo[q], nh[q], meta_n});
-            if (q == me) meta_self = meta_n;
-            meta_n += nh[q];
-        }
-    uint64_t nsrc = 0;
-    for (int p = 0; p < P; ++p) nsrc += recv[p] ? 1 : 0;
-    ST_TRY(ensure(c, c->m_meta, (std::max<uint64_t>(meta_n, 1) + nsrc * nh[me] + 1) * 4 +
-                                    (rng.size() + P + 2) * 8));
-    uint32_t *meta_s = reinterpret_cast<uint32_t *>(c->m_meta.p);
-    // (one word of gap: an in-place self offset below, meta_self - (meta_r - meta_s), is then
-    // at most -2 and never the "no source" mark ~0)
-    uint32_t *meta_r = meta_s + std::max<uint64_t>(meta_n, 1) + 1;
-    uint64_t *d_tab = reinterpret_cast<uint64_t *>(
-        reinterpret_cast<char *>(c->m_meta.p) +
-        (((std::max<uint64_t>(meta_n, 1) + nsrc * nh[me] + 1) * 4 + 7) & ~size_t(7)));
-    std::vector<uint64_t> tab(rng);
-    std::vector<uint64_t> moff(P, ~0ull);
-    {
-        uint64_t k = 0;
-        for (int p = 0; p < P; ++p)
-            if (recv[p]) moff[p] = (k++) * nh[me];
-    }
-    // the rank's own counts are read where K15 writes them (an offset relative to meta_r, mod
-    // 2^64), like its own keys below: no self copy in the count exchange either
-    const bool meta_in_place = !self_moved && recv[me] && meta_self != ~0ull;
-    if (meta_in_place) moff[me] = meta_self - (uint64_t)(meta_r - meta_s);
-    tab.insert(tab.end(), moff.begin(), moff.end());
-    // staged through pinned memory (a pageable copy blocks the host in the runtime's staging):
-    // OFF_PLAN + 8 KiB is free here -- step (5) below uses OFF_PLAN's first 2P words, and
-    // nothing copies from this range after the stream syncs of the previous call
-    uint64_t *h_tab = reinterpret_cast<uint64_t *>(c->h_small + OFF_PLAN + 8192);
-    if (OFF_PLAN + 8192 + tab.size() * 8 > kSmallBytes)
-        return set_err(c, GSORT_EINVAL, "exchange table too large");
-    std::copy(tab.begin(), tab.end(), h_tab);
-    HIP_TRY(c, hipMemcpyAsync(d_tab, h_tab, tab.size() * 8, hipMemcpyHostToDevice, c->stream));
-    const uint64_t *d_rng = d_tab, *d_moff = d_tab + rng.size();
-    t = tic(c);
-    HIP_TRY(c, launch_meta_counts(gb, d_rng, (int)(rng.size() / 5), meta_s, c->stream));
-    toc(c, PH_PLACE, t);
-    std::vector<size_t> sc(P, 0), sd(P, 0), rc(P, 0), rd(P, 0);
-    {
-        uint64_t mo = 0, ro = 0;
-        for (int q = 0; q < P; ++q) {
-            if (send[q]) { sc[q] = nh[q] * 4; sd[q] = mo * 4; mo += nh[q]; }
-            if (recv[q]) { rc[q] = nh[me] * 4; rd[q] = ro * 4; ro += nh[me]; }
-        }
-        if (meta_in_place) sc[me] = rc[me] = 0;
-    }
-    std::vector<uint64_t> roffs(P + 1, 0);
-    for (int p = 0; p < P; ++p) roffs[p + 1] = roffs[p] + recv[p];
-    t = tic_rec(c);
-    ST_TRY(comm_try(c, c->comm->alltoallv(meta_s, sc.data(), sd.data(), meta_r, rc.data(),
-                                          rd.data(), c->stream)));
-    toc_rec(c, PH_EXCH, t);
-    for (int q = 0; q < P; ++q)
-        if (stats && q != me) {
-            stats->bytes_sent += send[q] * 2;
-            stats->max_pair_bytes = std::max<uint64_t>(stats->max_pair_bytes, send[q] * 2);
-        }
-    if (roffs[P] != mine) return set_err(c, GSORT_EINVAL, "exchange plan does not fill the block");
-    // the payload, queued right behind the counts: the receive plan below overlaps it.  The
-    // rank's own piece is not moved at all: the receive kernels read it where it lies in the
-    // send buffer (its run offset below is taken relative to rbuf, mod 2^64) -- at P = 1 that is
-    // the whole 512 MiB of a 2^28-key block, at P = 8 an eighth of it
-    uint16_t *rbuf = slot_ptr<uint16_t>(c, S_RECV);
-    t = tic_rec(c);
-    for (int q = 0; q < P; ++q) {
-        const bool self = q == me && !self_moved;
-        sc[q] = self ? 0 : send[q] * 2;
-        sd[q] = cut[q] * 2;
-        rc[q] = self ? 0 : recv[q] * 2;
-        rd[q] = roffs[q] * 2;
-    }
-    ST_TRY(comm_try(c, c->comm->alltoallv(pack, sc.data(), sd.data(), rbuf, rc.data(), rd.data(),
-                                          c->stream)));
-    toc_rec(c, PH_EXCH, t);
-    if (stats) stats->exchanges = 1;
-    // (5) the receive plan from the counts alone: run bounds, bucket starts, the K11g / K18
-    // work lists of this rank's bucket range
-    t = tic(c);
-    ST_TRY(ensure(c, c->m_rpos, (size_t)P * (kBuckets16 + 1) * 8));
-    ST_TRY(ensure(c, c->m_bsize, kBsizeBytes));
-    ST_TRY(ensure_list(c, c->m_next[0], kBuckets16));
-    for (auto &b : c->m_local) ST_TRY(ensure_list(c, b, kBuckets16));
-    uint64_t *pos = reinterpret_cast<uint64_t *>(c->m_rpos.p);
-    uint64_t *bsize = reinterpret_cast<uint64_t *>(c->m_bsize.p), *bstart = bsize + kBuckets16;
-    uint64_t *h_r = reinterpret_cast<uint64_t *>(c->h_small + OFF_PLAN);
-    uint64_t *d_r = reinterpret_cast<uint64_t *>(c->d_small + OFF_PLAN);
-    // (no stream sync for h_r: nothing has copied from OFF_PLAN since allgather_u64's sync --
-    // the select stages through host vectors -- and a sync here idled the GPU ~40 us)
-    for (int p = 0; p < P; ++p) { h_r[p] = roffs[p]; h_r[P + p] = recv[p]; }
-    if (!self_moved)  // the self piece, in place: its offset from rbuf in keys, from integer
-        h_r[me] = elem_offset(pack + cut[me], rbuf);  // addresses (mod 2^64, run_ptr)
-    HIP_TRY(c, hipMemcpyAsync(d_r, h_r, (size_t)2 * P * 8, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(c, hipMemsetAsync(c->d_small + OFF_CTR, 0, kCtrBytes, c->stream));
-    // the runs' bucket bounds and the bucket starts in one row scan of P + 1 rows (the last
-    // row is every bucket's total over the sources); classify reads the sizes off bstart
-    HIP_TRY(c, launch_recv_plan_from_meta(meta_r, d_moff, (uint32_t)hlo[me], (uint32_t)nh[me], P,
-                                          pos, bstart, bstart + kBuckets16 + 1, c->stream));
-    const WorkLists wl = work_lists(c, 0);
-    HIP_TRY(c, launch_classify_range(nullptr, bstart, wl, (uint32_t)hlo[me],
-                                     (uint32_t)(hlo[me] + nh[me]), c->stream));
-    toc(c, PH_COUNT, t);
-    uint64_t h[3 * (kLocalClasses + 1)];
-    ST_TRY(read_counters(c, h));
-    if (check_mode()) {
-        for (int p = 0; p < P; ++p)
-            ST_TRY(check_bounds(c, pos + (size_t)p * (kBuckets16 + 1), kBuckets16 + 1, recv[p],
-                                "received run bounds"));
-        uint64_t keys = 0;
-        for (int l = 0; l <= kLocalClasses; ++l) keys += h[3 * l + 1];
-        if (keys != mine)
-            return set_err(c, GSORT_EINVAL, "GSORT_CHECK receive lists hold " +
-                                                std::to_string(keys) + " keys, want " +
-                                                std::to_string(mine) + " (rank " +
-                                                std::to_string(me) + ")");
-    }
-    // (6) every bucket sorted from its P pieces: K11g by size class, K18c past them (classes
-    // >= recv_cx and list 0, one persistent launch); a bucket past K18c's reach sends the block
-    // through recv_sort's MSD levels 1 and 0
-    t = tic(c);
-    uint32_t *out = slot_ptr<uint32_t>(c, S_OUT);
-    if (h[0] && h[2] > kHxMax) {  // recv_sort wants the P runs back to back in rbuf
-        if (recv[me] && !self_moved)
-            HIP_TRY(c, hipMemcpyAsync(rbuf + roffs[me], pack + cut[me], recv[me] * 2,
-                                      hipMemcpyDeviceToDevice, c->stream));
-        ST_TRY(recv_sort(c, rbuf, true, recv, mine, out, slot_ptr<uint32_t>(c, S_TMP), stats));
-    } else {
-        ST_TRY(sort_recv_lists(c, rbuf, true, pos, d_r, P, bstart, wl, h, out, stats));
-    }
-    toc(c, PH_MERGE, t);
+    uint64_t got = 0;
+    for (int p = 0; p < P; ++p) got += recv[p];
+    if (got != mine) return set_err(c, GSORT_EINVAL, "exchange plan does not fill the block");
+    ST_TRY(packed_exchange_sort(c, pack, gb, cut, recv, hlo, nh, stats, d_out, n_out));
     if (stats) stats->passes_run = pr;
-    *d_out = slot_ptr<int32_t>(c, S_OUT);
-    *n_out = mine;
     return GSORT_OK;
 }
 
@@ -589,6 +663,10 @@ gsort_status radix_dist(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in, int3
     for (uint64_t v : n_all) N += v;
     uint64_t B, mine;
     block_of(N, P, me, &B, &mine);
+    // a pass sends at most a rank's block (n_in, then B) of int32 keys
+    ST_TRY(check_send_limit(c, std::vector<uint64_t>(1, std::max<uint64_t>(
+                                   *std::max_element(n_all.begin(), n_all.end()), B)),
+                            4, "radix (LSD passes)"));
     const uint64_t cap = std::max<uint64_t>(std::max(n_in, B), 1);
     for (Slot s : {S_CUR, S_SORTED, S_RECV, S_OUT}) ST_TRY(ensure(c, c->slot[s], cap * 4));
     if (kv)
@@ -812,24 +890,23 @@ gsort_status radix_compat(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in, in
 }
 
 // ---- sample sort ------------------------------------------------------------------------
-gsort_status sample_dist(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in, int32_t **d_out,
-                         uint64_t *n_out, gsort_stats *stats) {
+// The reference (mpi_sample_sort.c:85-174): local qsort, 2P-1 regular samples of the sorted
+// block to the root, P-1 splitters from the sorted samples, each key to the first bucket whose
+// splitter is >= it, all-to-all, final qsort.
+
+// The int32 form (the LSD local algorithm, a rank past 2^32 keys, or -- rarely -- below): a
+// full local sort, K4 samples, K5 + broadcast, K6 bounds on the sorted block, an int32
+// exchange and the receive sort of the P sorted runs.
+gsort_status sample_dist_sorted(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in,
+                                const std::vector<uint64_t> &n_all, int32_t **d_out,
+                                uint64_t *n_out, gsort_stats *stats) {
     const int P = c->nranks, me = c->rank;
-    std::vector<uint64_t> n_all;
-    ST_TRY(allgather_u64(c, n_in, n_all));
     uint64_t N = 0;
     for (uint64_t v : n_all) N += v;
-    // mpi_sample_sort.c:72 size_bucket = ceil(N/P); :89-90 k = 2P-1, interval = B / k
     const uint64_t B = (N + P - 1) / P;
     const int k = 2 * P - 1;
     const uint64_t interval = B / k;
-    if (P * k > 1024) return set_err(c, GSORT_EINVAL, "too many ranks for sample sort");
-    for (int r = 0; r < P; ++r)  // :94-99, decided identically on every rank
-        if ((uint64_t)(k - 1) * interval >= n_all[r])
-            return set_err(c, GSORT_ENOSAMPLE,
-                           "no enough sample: rank " + std::to_string(r) + " holds " +
-                               std::to_string(n_all[r]) + " keys, needs index " +
-                               std::to_string((uint64_t)(k - 1) * interval));
+    ST_TRY(check_send_limit(c, n_all, 4, "sample"));
     const uint64_t cap = std::max<uint64_t>(n_in, 1);
     ST_TRY(ensure(c, c->slot[S_SORTED], cap * 4));
     int32_t *sorted = slot_ptr<int32_t>(c, S_SORTED);
@@ -947,6 +1024,169 @@ gsort_status sample_dist(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in, int
     if (stats) stats->passes_run = pr;
     *d_out = slot_ptr<int32_t>(c, S_OUT);
     *n_out = total;
+    return GSORT_OK;
+}
+
+// The packed form (default, round 6): no local sort.  The block is grouped
+// by its top 16 bits exactly as the distributed radix's sender groups it (group_block16), and
+// the reference's quantities are read off the grouped block:
+//   * regular sample i = sorted[i * interval] (mpi_sample_sort.c:94-104) is the
+//     (i * interval - gb[h])-th smallest key of the group h holding that position: K4g finds
+//     the k = 2P-1 groups, K13g sorts them in place (the only keys sorted before the exchange),
+//     K4r reads the samples;
+//   * the splitters: the root's K5 over the gathered samples + ncclBroadcast, as before
+//     (:107-133);
+//   * bucket bounds #keys <= s_j (:148-155): K6g + K13g sort the splitters' groups, K13
+//     binary-searches them (count_below16), and #keys < s_j for the duplicate-aware rule;
+//   * the bucket matrix (the lengths the reference sends in its MPI tags, :161-168) by one
+//     all-gather of those counts, read on the host with the K13g flags: the ONE host wait;
+//   * the exchange of 2 B per key and the receive sort of the radix path (packed_exchange_sort).
+// A group past K13g's 32 768 keys (skewed keys: Zipf) is flagged; every rank sees the flags in
+// the gathered rows and all of them redo the select with those groups sorted on the host path
+// (sort_groups16_host: K11 or the LSD passes), waiting on the host between the steps.
+gsort_status sample_dist(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in, int32_t **d_out,
+                         uint64_t *n_out, gsort_stats *stats) {
+    const int P = c->nranks, me = c->rank;
+    std::vector<uint64_t> n_all;
+    ST_TRY(allgather_u64(c, n_in, n_all));
+    uint64_t N = 0;
+    for (uint64_t v : n_all) N += v;
+    // mpi_sample_sort.c:72 size_bucket = ceil(N/P); :89-90 k = 2P-1, interval = B / k
+    const uint64_t B = (N + P - 1) / P;
+    const int k = 2 * P - 1, S = P - 1;
+    const uint64_t interval = B / k;
+    if (P * k > 1024) return set_err(c, GSORT_EINVAL, "too many ranks for sample sort");
+    for (int r = 0; r < P; ++r)  // :94-99, decided identically on every rank
+        if ((uint64_t)(k - 1) * interval >= n_all[r])
+            return set_err(c, GSORT_ENOSAMPLE,
+                           "no enough sample: rank " + std::to_string(r) + " holds " +
+                               std::to_string(n_all[r]) + " keys, needs index " +
+                               std::to_string((uint64_t)(k - 1) * interval));
+    bool packed = c->local_algo != GSORT_LOCAL_LSD;
+    for (int r = 0; r < P; ++r) packed &= n_all[r] < (1ull << 32);  // u32 bucket counts
+    if (!packed) return sample_dist_sorted(c, d_keys, n_in, n_all, d_out, n_out, stats);
+    ST_TRY(check_send_limit(c, n_all, 2, "sample"));
+    uint16_t *pack = nullptr;
+    uint64_t *gb = nullptr;
+    ST_TRY(group_block16(c, d_keys, n_in, stats, &pack, &gb));
+    const int pr = stats ? stats->passes_run : 0;
+
+    // count row per rank: le (S) | lt (S) | K13g flags of the sample groups (k) and of the
+    // splitter groups (S)
+    const int W = 3 * S + k;
+    const size_t nw = (size_t)2 * (k + S) + 2 * S + W;  // u64 words of m_split, then int32s
+    ST_TRY(ensure(c, c->m_split, nw * 8 + ((size_t)k + (size_t)P * k + S + 64) * 4));
+    ST_TRY(ensure(c, c->slot[S_STAGE], (size_t)P * W * 8));
+    uint64_t *d_pref = reinterpret_cast<uint64_t *>(c->m_split.p);  // k sample + S splitter groups
+    uint64_t *d_g = d_pref + k + S;                                  // (zeros: K13g's "g < N")
+    uint64_t *d_xs = d_g + k + S;                                    // 2S thresholds
+    uint64_t *d_row = d_xs + 2 * S;
+    int32_t *d_samp = reinterpret_cast<int32_t *>(d_row + W);
+    int32_t *d_sall = d_samp + k;
+    int32_t *d_spl = d_sall + (size_t)P * k;
+    const uint64_t *d_all = reinterpret_cast<const uint64_t *>(c->slot[S_STAGE].p);
+    std::vector<uint64_t> all((size_t)P * W);
+    std::vector<int32_t> spl(S);
+    std::vector<size_t> sc(P, 0), sd(P, 0), rc(P, 0), rd(P, 0);
+    sc[0] = (size_t)k * 4;
+    if (me == 0)
+        for (int r = 0; r < P; ++r) { rc[r] = (size_t)k * 4; rd[r] = (size_t)r * k * 4; }
+    // host == false: the common path, no host wait until the gathered rows.  host == true: the
+    // groups holding samples and splitters sorted on the host path (after a K13g flag)
+    auto select = [&](bool host) -> gsort_status {
+        HIP_TRY(c, launch_sample_groups(gb, interval, k, d_pref, d_g, c->stream));
+        if (!host) {
+            HIP_TRY(c, launch_boundary_sort16(pack, gb, d_pref, d_g, 1, k, c->atomic_rank,
+                                              d_row + 2 * S, c->stream));
+        } else {
+            std::vector<uint64_t> pf(k), hs;
+            HIP_TRY(c, hipMemcpyAsync(pf.data(), d_pref, (size_t)k * 8, hipMemcpyDeviceToHost,
+                                      c->stream));
+            HIP_TRY(c, hipStreamSynchronize(c->stream));
+            for (uint64_t v : pf) hs.push_back(v >> 16);
+            ST_TRY(sort_groups16_host(c, pack, gb, hs));
+        }
+        HIP_TRY(c, launch_read_samples16(pack, d_pref, interval, k, d_samp, c->stream));
+        ST_TRY(comm_try(c, c->comm->alltoallv(d_samp, sc.data(), sd.data(), d_sall, rc.data(),
+                                              rd.data(), c->stream)));
+        if (me == 0) HIP_TRY(c, launch_select_splitters(d_sall, P * k, k, S, d_spl, c->stream));
+        ST_TRY(comm_try(c, c->comm->bcast(d_spl, (size_t)S * 4, 0, c->stream)));
+        HIP_TRY(c, launch_splitter_groups(d_spl, S, d_pref + k, d_g + k, d_xs, c->stream));
+        if (!host) {
+            HIP_TRY(c, launch_boundary_sort16(pack, gb, d_pref + k, d_g + k, 1, S,
+                                              c->atomic_rank, d_row + 2 * S + k, c->stream));
+        } else {
+            HIP_TRY(c, hipMemcpyAsync(spl.data(), d_spl, (size_t)S * 4, hipMemcpyDeviceToHost,
+                                      c->stream));
+            HIP_TRY(c, hipStreamSynchronize(c->stream));
+            std::vector<uint64_t> hs;
+            for (int32_t v : spl) hs.push_back(((uint32_t)v ^ 0x80000000u) >> 16);
+            ST_TRY(sort_groups16_host(c, pack, gb, hs));
+            HIP_TRY(c, hipMemsetAsync(d_row + 2 * S, 0, (size_t)(k + S) * 8, c->stream));
+        }
+        HIP_TRY(c, launch_count_below16(pack, gb, d_xs, 2 * S, d_row, c->stream));
+        ST_TRY(comm_try(c, c->comm->allgather(d_row, c->slot[S_STAGE].p, (size_t)W * 8,
+                                              c->stream)));
+        HIP_TRY(c, hipMemcpyAsync(all.data(), d_all, all.size() * 8, hipMemcpyDeviceToHost,
+                                  c->stream));
+        if (S)
+            HIP_TRY(c, hipMemcpyAsync(spl.data(), d_spl, (size_t)S * 4, hipMemcpyDeviceToHost,
+                                      c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        return GSORT_OK;
+    };
+    hipEvent_t t = tic_rec(c);
+    ST_TRY(select(false));
+    bool big = false;
+    for (int p = 0; p < P; ++p)
+        for (int i = 2 * S; i < W; ++i) big |= all[(size_t)p * W + i] != 0;
+    if (c->plan_trace && big) fprintf(stderr, "gsort sample: a group past K13g, host path\n");
+    if (big) ST_TRY(select(true));
+    toc_rec(c, PH_SAMPLE, t);
+    // (3) the bucket matrix M[p][q] (rank p's keys for bucket q) and this rank's cut
+    c->splitters.assign(spl.begin(), spl.end());
+    std::vector<uint64_t> M((size_t)P * P), lt((size_t)P * S), le((size_t)P * S);
+    for (int p = 0; p < P; ++p)
+        for (int j = 0; j < S; ++j) {
+            le[(size_t)p * S + j] = all[(size_t)p * W + j];
+            lt[(size_t)p * S + j] = all[(size_t)p * W + S + j];
+        }
+    for (int p = 0; p < P; ++p) {
+        if (!c->sample_balanced) {
+            uint64_t prev = 0;
+            for (int q = 0; q < P; ++q) {
+                const uint64_t end = q < S ? le[(size_t)p * S + q] : n_all[p];
+                if (end < prev || end > n_all[p])
+                    return set_err(c, GSORT_EINVAL, "inconsistent sample bucket bounds");
+                M[(size_t)p * P + q] = end - prev;
+                prev = end;
+            }
+        } else {
+            // duplicate-aware buckets: the distributed radix's cut rule with the boundary
+            // clamped into s_j's copies; every rank plans every rank's row (identical inputs)
+            std::vector<uint64_t> snd(P), rcv(P);
+            const gsort_status st = gsort_plan_split_balanced(P, n_all.data(), lt.data(),
+                                                              le.data(), p, snd.data(), rcv.data());
+            if (st != GSORT_OK) return set_err(c, st, "inconsistent sample bucket bounds");
+            for (int q = 0; q < P; ++q) M[(size_t)p * P + q] = snd[q];
+        }
+    }
+    c->bucket_counts.assign(P, 0);
+    std::vector<uint64_t> cut(P + 1, 0), recv(P), hlo(P), nh(P);
+    for (int q = 0; q < P; ++q) {
+        c->bucket_counts[q] = M[(size_t)me * P + q];
+        cut[q + 1] = cut[q] + M[(size_t)me * P + q];
+        recv[q] = M[(size_t)q * P + me];
+        // bucket q holds keys in [s_{q-1}, s_q] (the reference's (s_{q-1}, s_q]; the balanced
+        // rule may also give it copies of s_{q-1}): 16-bit buckets from s_{q-1}'s to s_q's
+        const uint64_t lo = q == 0 ? 0 : ((uint32_t)spl[q - 1] ^ 0x80000000u);
+        const uint64_t hi = q == S ? 0xFFFFFFFFull : ((uint32_t)spl[q] ^ 0x80000000u);
+        hlo[q] = lo >> 16;
+        nh[q] = (hi >> 16) - hlo[q] + 1;
+    }
+    if (cut[P] != n_in) return set_err(c, GSORT_EINVAL, "sample cut does not cover the block");
+    ST_TRY(packed_exchange_sort(c, pack, gb, cut, recv, hlo, nh, stats, d_out, n_out));
+    if (stats) stats->passes_run = pr;
     return GSORT_OK;
 }
 

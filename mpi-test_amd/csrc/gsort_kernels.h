@@ -253,6 +253,16 @@ hipError_t launch_select_digit(const uint64_t *all, int W, const uint64_t *g, ui
 hipError_t launch_boundary_sort16(uint16_t *pack, const uint64_t *gb, const uint64_t *prefix,
                                   const uint64_t *g, uint64_t N, int nb, bool atomic_rank,
                                   uint64_t *big, hipStream_t s);
+// Sample sort on the grouped block: K4g pref[i] = (16-bit group of position
+// i * interval) << 16, g[i] = 0, i < k <= 128 (K13g's inputs: it then sorts those groups);
+// K4r out[i] = the int32 key at position i * interval (its group sorted); K6g splitter j's
+// group (pref, g) and count_below16 thresholds xs[j] = ord(s_j) + 1, xs[S + j] = ord(s_j).
+hipError_t launch_sample_groups(const uint64_t *gb, uint64_t interval, int k, uint64_t *pref,
+                                uint64_t *g, hipStream_t s);
+hipError_t launch_read_samples16(const uint16_t *pack, const uint64_t *pref, uint64_t interval,
+                                 int k, int32_t *out, hipStream_t s);
+hipError_t launch_splitter_groups(const int32_t *spl, int S, uint64_t *pref, uint64_t *g,
+                                  uint64_t *xs, hipStream_t s);
 // K13 on the packed buffer (bucket bounds gb): out[i] = #keys < xs[i] (ordered u32).
 hipError_t launch_count_below16(const uint16_t *a, const uint64_t *gb, const uint64_t *xs,
                                 int m, uint64_t *out, hipStream_t s);

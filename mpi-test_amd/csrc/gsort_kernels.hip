@@ -3901,6 +3901,84 @@ hipError_t launch_boundary_sort16(uint16_t *pack, const uint64_t *gb, const uint
     return hipGetLastError();
 }
 
+// ---- sample sort on the grouped (packed) block: the reference's regular samples and bucket
+// bounds without sorting the block (mpi_sample_sort.c:85-105, :148-155) ---------
+// K4g: sample i sits at position x = i * interval of the sorted block (mpi_sample_sort.c:95);
+// in the grouped block that is the (x - gb[h])-th smallest key of group h, gb[h] <= x <
+// gb[h + 1].  pref[i] = h << 16 and g[i] = 0 make K13g sort exactly those groups in place
+// (ascending i gives ascending h, so K13g's shared-group skip applies).
+__global__ __launch_bounds__(128) void k_sample_groups(const unsigned long long *__restrict__ gb,
+                                                       unsigned long long interval, int k,
+                                                       unsigned long long *__restrict__ pref,
+                                                       unsigned long long *__restrict__ g) {
+    const int i = threadIdx.x;
+    if (i >= k) return;
+    const unsigned long long x = (unsigned long long)i * interval;
+    uint32_t lo = 0, hi = kBuckets16;  // the last h with gb[h] <= x lies in [lo, hi); gb[0] = 0
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (gb[mid] <= x) lo = mid; else hi = mid;
+    }
+    pref[i] = (unsigned long long)lo << 16;
+    g[i] = 0;
+}
+
+// K4r: the samples from their sorted groups, int32 (mpi_sample_sort.c:101-103).
+__global__ __launch_bounds__(128) void k_read_samples16(const uint16_t *__restrict__ pack,
+                                                        const unsigned long long *__restrict__ pref,
+                                                        unsigned long long interval, int k,
+                                                        int32_t *__restrict__ out) {
+    const int i = threadIdx.x;
+    if (i >= k) return;
+    const uint32_t key = (uint32_t)pref[i] | (uint32_t)pack[(unsigned long long)i * interval];
+    out[i] = (int32_t)(key ^ 0x80000000u);
+}
+
+// K6g: splitter j's group for K13g (pref[j] = its top 16 bits << 16, g[j] = 0) and the
+// thresholds of count_below16: xs[j] = ord(s_j) + 1 (keys <= s_j: the reference's bucket rule,
+// mpi_sample_sort.c:150), xs[S + j] = ord(s_j) (keys < s_j: the duplicate-aware cut).
+__global__ __launch_bounds__(64) void k_splitter_groups(const int32_t *__restrict__ spl, int S,
+                                                        unsigned long long *__restrict__ pref,
+                                                        unsigned long long *__restrict__ g,
+                                                        unsigned long long *__restrict__ xs) {
+    for (int j = threadIdx.x; j < S; j += 64) {
+        const unsigned long long o = (uint32_t)spl[j] ^ 0x80000000u;
+        pref[j] = o >> 16 << 16;
+        g[j] = 0;
+        xs[j] = o + 1;  // (2^32 for the largest key: count_below16 answers n)
+        xs[S + j] = o;
+    }
+}
+
+hipError_t launch_sample_groups(const uint64_t *gb, uint64_t interval, int k, uint64_t *pref,
+                                uint64_t *g, hipStream_t s) {
+    using ull = unsigned long long;
+    if (k <= 0) return hipSuccess;
+    if (k > 128) return hipErrorInvalidValue;
+    launch_k(k_sample_groups, 1, 128, 0, s, reinterpret_cast<const ull *>(gb), (ull)interval, k,
+             reinterpret_cast<ull *>(pref), reinterpret_cast<ull *>(g));
+    return hipGetLastError();
+}
+
+hipError_t launch_read_samples16(const uint16_t *pack, const uint64_t *pref, uint64_t interval,
+                                 int k, int32_t *out, hipStream_t s) {
+    using ull = unsigned long long;
+    if (k <= 0) return hipSuccess;
+    if (k > 128) return hipErrorInvalidValue;
+    launch_k(k_read_samples16, 1, 128, 0, s, pack, reinterpret_cast<const ull *>(pref),
+             (ull)interval, k, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_splitter_groups(const int32_t *spl, int S, uint64_t *pref, uint64_t *g,
+                                  uint64_t *xs, hipStream_t s) {
+    using ull = unsigned long long;
+    if (S <= 0) return hipSuccess;
+    launch_k(k_splitter_groups, 1, 64, 0, s, spl, S, reinterpret_cast<ull *>(pref),
+             reinterpret_cast<ull *>(g), reinterpret_cast<ull *>(xs));
+    return hipGetLastError();
+}
+
 hipError_t launch_select_digit(const uint64_t *all, int W, const uint64_t *g, uint64_t N, int P,
                                int nb, int M, int shift, uint64_t *prefix, uint64_t *xs,
                                hipStream_t s) {

@@ -714,6 +714,9 @@ gsort_status gsort_group_destroy(gsort_group *grp) {
 gsort_status gsort_create_in_group(gsort_ctx **ctx, gsort_group *grp, int rank, int hip_device) {
     if (!ctx || !grp || rank < 0 || rank >= group_state_size(grp->st)) return GSORT_EINVAL;
     *ctx = nullptr;
+    // one device per group: its collectives are ordered by device-scope events (ranks on
+    // several GPUs are RCCL's job, one process per GPU)
+    if (!group_state_join(grp->st, hip_device)) return GSORT_EINVAL;
     gsort_ctx *c = new gsort_ctx();
     c->rank = rank;
     c->nranks = group_state_size(grp->st);

@@ -51,7 +51,7 @@ def _common(line, ranks, keys_log2):
 def test_bench_torchrun_radix_2_ranks_with_strong_block():
     """The driver's launcher: 2 ranks, 2^22 keys each, then configs[2]'s strong-scaling block
     (2^31 keys in total: 2^30 per rank -- the staging size that once hung the IPC group)."""
-    line, err = _run(["--keys-log2", "22"], 2, torchrun=True)
+    line, err = _run(["--keys-log2", "22", "--strong"], 2, torchrun=True)
     _common(line, 2, 22)
     assert line["exchange"]["max_pair_bytes"] > 0
     st = line["strong_scaling_cfg2"]
@@ -67,8 +67,9 @@ def test_bench_self_spawn_sample_2_ranks():
 
 
 def test_bench_torchrun_radix_3_ranks_zipf():
-    """An odd world size and skewed keys (Zipf: most keys in a few 16-bit buckets)."""
-    line, _ = _run(["--keys-log2", "20", "--dist", "zipf", "--no-strong"], 3, torchrun=True)
+    """An odd world size and skewed keys (Zipf: most keys in a few 16-bit buckets); ranks
+    sharing the GPU skip the strong-scaling block by default."""
+    line, _ = _run(["--keys-log2", "20", "--dist", "zipf"], 3, torchrun=True)
     _common(line, 3, 20)
     assert "strong_scaling_cfg2" not in line
 

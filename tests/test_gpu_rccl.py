@@ -8,11 +8,10 @@ and over RCCL itself (ncclCommInitRank from a gsort_get_uid, ncclAllGather, grou
 ncclSend/ncclRecv, ncclBroadcast).  Output must equal the oracle's sort, bit for bit.
 
 The cases run in ONE child process (this file with --child), as a real rank does: one process
-per GPU and one communicator in it.  In the pytest process itself, an 8-rank in-process group
-started after an RCCL communicator had lived and been destroyed there failed on the MI355X
-box (first a failed 512 KiB hipMalloc, then an illegal-address fault surfacing at the next
-launch; the same tests pass when the group runs first), so the RCCL communicator never shares
-a process with the in-process groups.
+per GPU and one communicator in it, never beside the in-process groups of the other test
+files.  (Round 1 blamed a fault of an 8-rank group on a preceding RCCL communicator; its cause
+was K1h reading past the end of a short block, fixed in v8 -- DESIGN.md 8 -- not RCCL.  The
+separation stays because it is how a real rank runs.)
 """
 import json
 import os
