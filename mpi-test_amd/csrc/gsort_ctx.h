@@ -62,6 +62,10 @@ using namespace gsort::rt;
 struct gsort_ctx {
     int rank = 0, nranks = 1, device = 0;
     hipStream_t stream = nullptr;
+    // the distributed sorts' receive plan runs on stream2 behind the count exchange (ev_meta)
+    // while the payload moves on stream; stream then waits for it (ev_plan)
+    hipStream_t stream2 = nullptr;
+    hipEvent_t ev_meta = nullptr, ev_plan = nullptr;
     Comm *comm = nullptr;
     std::string err;
     DevBuf slot[S_NSLOTS];
@@ -97,6 +101,10 @@ struct gsort_ctx {
     // bins) or 16
     int recv_cb = 8;
     DevBuf m_fb;  // K18c (u8): the wrapped buckets' {h, len} entries
+    // the previous packed receive sort's list counts (list 0, classes 1..4): the shape of the
+    // next call's receive launches, queued before its counts are read (spec_recv_launch)
+    uint32_t recv_hint[kLocalClasses + 1] = {};
+    bool recv_hint_ok = false;
     int ncu = 256;
     int last_plan = 0;      // gsort_last_plan: 0 exact, 1 sampled, 2 sampled then exact
     bool plan_trace = false; // GSORT_PLAN_TRACE: one stderr line per plan decision
@@ -175,6 +183,9 @@ bool check_mode();
 gsort_status check_bounds(gsort_ctx *c, const uint64_t *d, size_t m, uint64_t last,
     const char *what);
 gsort_status read_counters(gsort_ctx *c, uint64_t *h);
+// K12p's mailbox: wait for sequence number seq (the counters behind it are then visible); a
+// stream `s` (default: the context's) that goes idle without it, or fails, is an error
+gsort_status wait_mail(gsort_ctx *c, uint64_t seq, hipStream_t s = nullptr);
 WorkLists work_lists(gsort_ctx *c, int next);
 gsort_status check_ctx(gsort_ctx *c);
 template <class T>

@@ -277,15 +277,18 @@ hipError_t launch_run_bounds(const int32_t *recv, const uint64_t *roff, const ui
 // scratch: 64 x P u64.
 // pos (as launch_pos_from_meta) and bstart[0 .. 65536] (exclusive scan of every bucket's total
 // over the sources) in one two-kernel row scan of P + 1 rows; classify then takes bsize =
-// nullptr (sizes from bstart).  scratch: (P + 1) x 64 u64.
+// nullptr (sizes from bstart).  scratch: (P + 1) x 64 u64.  zero[0 .. nzero) (<= 1024 u64) is
+// cleared by the first kernel (the work-list counters the classification adds into).
 hipError_t launch_recv_plan_from_meta(const uint32_t *meta, const uint64_t *moff, uint32_t h_lo,
                                      uint32_t nh, int P, uint64_t *pos, uint64_t *bstart,
-                                     uint64_t *scratch, hipStream_t s);
+                                     uint64_t *scratch, hipStream_t s, uint64_t *zero = nullptr,
+                                     uint32_t nzero = 0);
 hipError_t launch_pos_from_meta(const uint32_t *meta, const uint64_t *moff, uint32_t h_lo,
                                 uint32_t nh, int P, uint64_t *pos, uint64_t *scratch,
                                 hipStream_t s);
 // bsize / bstart (65536 u64) = bucket sizes and their exclusive scan; buckets classified into
-// wl (next level: {bstart, len} segments; K11g classes: {h, len}).
+// wl as {h | bstart[h] << 16, len} entries (the K11g classes and list 0; list_to_segments turns
+// list 0 into {bstart, len} segments).
 hipError_t launch_recv_classify(const uint64_t *pos, int P, uint64_t *bsize, uint64_t *bstart,
                                 const WorkLists &wl, uint64_t *scratch, hipStream_t s);
 // The two halves of launch_recv_classify (the distributed radix classifies only its own bucket
@@ -295,11 +298,14 @@ hipError_t launch_recv_bounds(const uint64_t *pos, int P, uint64_t *bsize, uint6
 hipError_t launch_classify_range(const uint64_t *bsize, const uint64_t *bstart,
                                  const WorkLists &wl, uint32_t h0, uint32_t h1, hipStream_t s);
 // K11g: gather the P pieces of every listed bucket (int32 keys, or packed16: the low 16 bits),
-// sort its low 16 bits in LDS, store int32 at out[bstart[h] ..).
+// sort its low 16 bits in LDS, store int32 at out[bstart[h] ..).  Entries first .. first +
+// nlist - 1; with ndev, only those below the count *ndev read on the device (nlist is then the
+// grid: a guess made before the host knew the list's length).
 hipError_t launch_gather_sort(const void *recv, bool packed16, const uint64_t *pos,
                               const uint64_t *roff, int P, const uint64_t *bstart,
                               const uint64_t *list, uint32_t nlist, int cls, bool atomic_rank,
-                              uint32_t *out, hipStream_t s);
+                              uint32_t *out, hipStream_t s, const uint32_t *ndev = nullptr,
+                              uint32_t first = 0);
 // Copy the pieces of every bucket > kLocalMax keys to out[bstart[h] ..) as ordered u32.
 hipError_t launch_gather_copy(const void *recv, bool packed16, const uint64_t *pos,
                               const uint64_t *roff, int P, const uint64_t *bsize,

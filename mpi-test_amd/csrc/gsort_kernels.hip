@@ -1983,41 +1983,57 @@ __global__ __launch_bounds__(BLOCK) void k_gather_sort(const T *__restrict__ rec
                                                        int P,
                                                        const unsigned long long *__restrict__ bstart,
                                                        const unsigned long long *__restrict__ list,
-                                                       uint32_t *__restrict__ out) {
+                                                       uint32_t *__restrict__ out,
+                                                       const uint32_t *__restrict__ ndev,
+                                                       uint32_t first) {
     constexpr int WAVES = BLOCK / 64;
     constexpr int TILE = BLOCK * ITEMS;
     constexpr int MAXP = 64;
+    // entry first + blockIdx.x; ndev: the list's length read on the device (a launch queued
+    // before the host knew it -- the grid is a guess, the blocks past the length return)
+    const uint32_t ei = first + blockIdx.x;
+    if (ndev && ei >= *ndev) return;
     __shared__ uint32_t s_a[lds_slots(TILE)];
     __shared__ uint32_t s_wc[WAVES * kRadix];
     __shared__ uint64_t s_src[MAXP];  // piece p: first key in recv
     __shared__ uint64_t s_delta[MAXP];
     __shared__ uint32_t s_cum[MAXP + 1];
     const int tid = threadIdx.x;
-    const uint64_t h = list[2 * blockIdx.x];
-    const uint32_t len = (uint32_t)list[2 * blockIdx.x + 1];
+    const uint64_t e0 = list[2 * ei];  // h | bstart[h] << 16 (k_classify_gather)
+    const uint64_t h = e0 & 0xFFFFu, dst = e0 >> 16;
+    const uint32_t len = (uint32_t)list[2 * ei + 1];
     if (tid < kRadix) s_wc[tid] = 0;
-    if (tid < 64) {  // lane p: piece p; wave scan of the piece lengths
+    uint32_t k[ITEMS];
+    if (P == 1) {
+        // one run, whose bucket offsets are the bucket starts: the keys straight from the entry
+        // (no pos load, no piece table, no barrier in front of the loads -- round 6)
+        const T *src = run_ptr(recv, roff[0] + dst);
+        const uint32_t last = len ? len - 1 : 0u;
+        T v[ITEMS];
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i) v[i] = src[min((uint32_t)(i * BLOCK + tid), last)];
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i) k[i] = recv_key(v[i], (uint32_t)h);
+        __syncthreads();
+        sort_bucket<BLOCK, ITEMS, ATOMIC>(k, len, 2, out + dst, s_a, s_wc);
+        return;
+    }
+    if (tid < 64) {  // lane p: piece p; wave scan of the piece lengths (DPP)
         uint64_t a = 0, b = 0;
         if (tid < P) {
             a = pos[(uint64_t)tid * (kBuckets16 + 1) + h];
             b = pos[(uint64_t)tid * (kBuckets16 + 1) + h + 1];
         }
         const uint32_t l = (uint32_t)(b - a);
-        uint32_t v = l;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t t = __shfl_up(v, o);
-            if (tid >= o) v += t;
-        }
+        const uint32_t v = wave_incl_add(l);
         if (tid < P) {
             s_src[tid] = roff[tid] + a;
             s_cum[tid] = v - l;
+            s_delta[tid] = roff[tid] + a - (v - l);  // key j of piece p: recv[delta + j]
         }
         if (tid == P - 1) s_cum[P] = v;
     }
-    if (tid < P) s_delta[tid] = s_src[tid] - s_cum[tid];  // key j of piece p: recv[delta + j]
     __syncthreads();
-    uint32_t k[ITEMS];
     if (P <= kGatherDirectP) {
         // every key straight into registers, all loads in flight: key j lies in piece
         // p(j) = #{q >= 1 : j >= cum[q]} (the boundaries are wave-uniform scalars)
@@ -2027,21 +2043,13 @@ __global__ __launch_bounds__(BLOCK) void k_gather_sort(const T *__restrict__ rec
             cum[q] = q < P ? (uint32_t)__builtin_amdgcn_readfirstlane((int)s_cum[q]) : 0xFFFFFFFFu;
         const uint32_t last = len ? len - 1 : 0u;
         T v[ITEMS];
-        if (P == 1) {  // one piece: a scalar base (no per-key piece lookup)
-            const uint64_t d0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(s_delta[0] >> 32)) << 32) |
-                                (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)s_delta[0]);
-            const T *src = run_ptr(recv, d0);
 #pragma unroll
-            for (int i = 0; i < ITEMS; ++i) v[i] = src[min((uint32_t)(i * BLOCK + tid), last)];
-        } else {
+        for (int i = 0; i < ITEMS; ++i) {
+            const uint32_t j = min((uint32_t)(i * BLOCK + tid), last);
+            uint32_t q = 0;
 #pragma unroll
-            for (int i = 0; i < ITEMS; ++i) {
-                const uint32_t j = min((uint32_t)(i * BLOCK + tid), last);
-                uint32_t q = 0;
-#pragma unroll
-                for (int b = 1; b < kGatherDirectP; ++b) q += j >= cum[b] ? 1u : 0u;
-                v[i] = *run_ptr(recv, s_delta[q] + j);
-            }
+            for (int b = 1; b < kGatherDirectP; ++b) q += j >= cum[b] ? 1u : 0u;
+            v[i] = *run_ptr(recv, s_delta[q] + j);
         }
 #pragma unroll
         for (int i = 0; i < ITEMS; ++i) k[i] = recv_key(v[i], (uint32_t)h);
@@ -2075,7 +2083,8 @@ __global__ __launch_bounds__(BLOCK) void k_gather_sort(const T *__restrict__ rec
         }
     }
     __syncthreads();
-    sort_bucket<BLOCK, ITEMS, ATOMIC>(k, len, 2, out + bstart[h], s_a, s_wc);
+    sort_bucket<BLOCK, ITEMS, ATOMIC>(k, len, 2, out + dst, s_a, s_wc);
+    (void)bstart;
 }
 
 // Receive side, K11g bookkeeping.  pos[p][h] = keys of sorted run p whose top 16 bits (ordered
@@ -2115,9 +2124,13 @@ __global__ __launch_bounds__(kRadix) void k_classify_gather(
     const unsigned long long *__restrict__ bsize, const unsigned long long *__restrict__ bstart,
     WorkLists wl, uint32_t h0, uint32_t h1) {
     const uint32_t h = blockIdx.x * kRadix + threadIdx.x;
-    const uint64_t len = h >= h0 && h < h1 ? (bsize ? bsize[h] : bstart[h + 1] - bstart[h]) : 0ull;
-    // {bucket id, len}: K11g classes, and list 0 (K18 or, past kHxMax, the MSD levels)
-    classify_block(h, len, wl);
+    const uint64_t b0 = bstart[h];
+    const uint64_t len = h >= h0 && h < h1 ? (bsize ? bsize[h] : bstart[h + 1] - b0) : 0ull;
+    // {bucket id | its output start << 16, len}: K11g classes, and list 0 (K18 or, past
+    // kHxMax, the MSD levels).  The start rides in the entry so that K11g reaches its output
+    // (and, at P = 1, its keys: the one run's offset of bucket h IS bstart[h]) without a
+    // dependent load behind the entry's (round 6)
+    classify_block((uint64_t)h | (b0 << 16), len, wl);
 }
 
 // K18 (receive side, buckets of kLocalMax < len <= kHxMax keys): a counting sort of the
@@ -2140,7 +2153,7 @@ __global__ __launch_bounds__(1024) void k_hist_expand(const T *__restrict__ recv
     __shared__ uint32_t s_len[64];
     __shared__ uint32_t s_w[NT / 64];
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const uint32_t h = (uint32_t)list[2 * blockIdx.x];
+    const uint32_t h = (uint32_t)list[2 * blockIdx.x] & 0xFFFFu;  // (bstart[h] above bit 16)
     if ((int)tid < P) {
         const uint64_t a = pos[(uint64_t)tid * (kBuckets16 + 1) + h];
         const uint64_t b = pos[(uint64_t)tid * (kBuckets16 + 1) + h + 1];
@@ -2317,7 +2330,7 @@ __device__ __forceinline__ void cx_fill_table(CxTable<T> &t, const T *recv,
         if (lane == 0) t.keys = 0;
         return;
     }
-    const uint32_t h = (uint32_t)ent[0];
+    const uint32_t h = (uint32_t)ent[0] & 0xFFFFu;  // (bstart[h] rides above bit 16)
     uint64_t a = 0, b = 0, src = 0;
     if ((int)lane < P) {
         a = pos[(uint64_t)lane * (kBuckets16 + 1) + h];
@@ -2721,12 +2734,14 @@ __global__ __launch_bounds__(CB == 8 ? 512 : 1024) void k_count_expand(
     }
 }
 
-// list 0 of the receive side, {h, len} -> {bstart[h], len} (segments of out for the MSD levels).
+// list 0 of the receive side, {h | bstart[h] << 16, len} -> {bstart[h], len} (segments of out
+// for the MSD levels).
 __global__ __launch_bounds__(256) void k_list_to_segments(unsigned long long *__restrict__ list,
                                                           uint32_t n,
                                                           const unsigned long long *__restrict__ bstart) {
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-    if (i < n) list[2 * i] = bstart[list[2 * i]];
+    if (i < n) list[2 * i] = list[2 * i] >> 16;  // (the entry carries bstart[h] above bit 16)
+    (void)bstart;
 }
 
 // Oversized receive buckets: gather their pieces into out[bstart[h] ..) as ordered u32 (they
@@ -2858,12 +2873,17 @@ struct RowValues {  // v[h] (one row)
 };
 constexpr uint32_t kScanBlocks = kBuckets16 / 1024;  // 64
 
+// zero[0 .. nzero) := 0 by block (0, 0) (the receive side's work-list counters, which the
+// classification after the scan adds into: no memset of their own on the stream)
 template <typename Gen>
 __global__ __launch_bounds__(1024) void k_rowscan_reduce(Gen gen,
-                                                         unsigned long long *__restrict__ part) {
+                                                         unsigned long long *__restrict__ part,
+                                                         unsigned long long *zero = nullptr,
+                                                         uint32_t nzero = 0) {
     __shared__ unsigned long long s_w[16];
     const uint32_t row = blockIdx.y, b = blockIdx.x, tid = threadIdx.x, lane = tid & 63,
                    w = tid >> 6;
+    if (zero && (row | b) == 0 && tid < nzero) zero[tid] = 0;
     unsigned long long x = gen(row, b * 1024 + tid);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
@@ -4036,7 +4056,8 @@ hipError_t launch_pos_from_meta(const uint32_t *meta, const uint64_t *moff, uint
     if (P < 1 || P > 64) return hipErrorInvalidValue;
     const MetaCounts gen{meta, reinterpret_cast<const ull *>(moff), h_lo, nh};
     ull *part = reinterpret_cast<ull *>(scratch);
-    launch_k(k_rowscan_reduce<decltype(gen)>, dim3(kScanBlocks, P), 1024, 0, s, gen, part);
+    launch_k(k_rowscan_reduce<decltype(gen)>, dim3(kScanBlocks, P), 1024, 0, s, gen, part,
+             (ull *)nullptr, 0u);
     launch_k(k_rowscan_apply<decltype(gen)>, dim3(kScanBlocks, P), 1024, 0, s, gen, part, reinterpret_cast<ull *>(pos),
                                                           kBuckets16 + 1, (ull *)nullptr);
     return hipGetLastError();
@@ -4044,13 +4065,15 @@ hipError_t launch_pos_from_meta(const uint32_t *meta, const uint64_t *moff, uint
 
 hipError_t launch_recv_plan_from_meta(const uint32_t *meta, const uint64_t *moff, uint32_t h_lo,
                                      uint32_t nh, int P, uint64_t *pos, uint64_t *bstart,
-                                     uint64_t *scratch, hipStream_t s) {
+                                     uint64_t *scratch, hipStream_t s, uint64_t *zero,
+                                     uint32_t nzero) {
     using ull = unsigned long long;
-    if (P < 1 || P > 64) return hipErrorInvalidValue;
+    if (P < 1 || P > 64 || nzero > 1024) return hipErrorInvalidValue;
     const MetaCountsSum gen{MetaCounts{meta, reinterpret_cast<const ull *>(moff), h_lo, nh},
                             (uint32_t)P};
     ull *part = reinterpret_cast<ull *>(scratch);
-    launch_k(k_rowscan_reduce<decltype(gen)>, dim3(kScanBlocks, P + 1), 1024, 0, s, gen, part);
+    launch_k(k_rowscan_reduce<decltype(gen)>, dim3(kScanBlocks, P + 1), 1024, 0, s, gen, part,
+             reinterpret_cast<ull *>(zero), nzero);
     launch_k(k_rowscan_apply<decltype(gen)>, dim3(kScanBlocks, P + 1), 1024, 0, s, gen, part,
              reinterpret_cast<ull *>(pos), kBuckets16 + 1, reinterpret_cast<ull *>(bstart));
     return hipGetLastError();
@@ -4063,7 +4086,8 @@ hipError_t launch_recv_bounds(const uint64_t *pos, int P, uint64_t *bsize, uint6
                                                      reinterpret_cast<ull *>(bsize));
     const RowValues gen{reinterpret_cast<const ull *>(bsize)};
     ull *part = reinterpret_cast<ull *>(scratch);
-    launch_k(k_rowscan_reduce<decltype(gen)>, dim3(kScanBlocks, 1), 1024, 0, s, gen, part);
+    launch_k(k_rowscan_reduce<decltype(gen)>, dim3(kScanBlocks, 1), 1024, 0, s, gen, part,
+             (ull *)nullptr, 0u);
     launch_k(k_rowscan_apply<decltype(gen)>, dim3(kScanBlocks, 1), 1024, 0, s, gen, part, reinterpret_cast<ull *>(bstart),
                                                           kBuckets16 + 1, (ull *)nullptr);
     return hipGetLastError();
@@ -4087,7 +4111,8 @@ hipError_t launch_recv_classify(const uint64_t *pos, int P, uint64_t *bsize, uin
 hipError_t launch_gather_sort(const void *recv, bool packed16, const uint64_t *pos,
                               const uint64_t *roff, int P, const uint64_t *bstart,
                               const uint64_t *list, uint32_t nlist, int cls, bool atomic_rank,
-                              uint32_t *out, hipStream_t s) {
+                              uint32_t *out, hipStream_t s, const uint32_t *ndev,
+                              uint32_t first) {
     using ull = unsigned long long;
     if (nlist == 0) return hipSuccess;
     if (cls < 1 || cls > kLocalClasses || P < 1 || P > 64) return hipErrorInvalidValue;
@@ -4099,8 +4124,8 @@ hipError_t launch_gather_sort(const void *recv, bool packed16, const uint64_t *p
     auto *r16 = reinterpret_cast<const uint16_t *>(recv);
 #define GSORT_K11G(B, I, AT)                                                                   \
     do {                                                                                       \
-        if (packed16) launch_k(k_gather_sort<B, I, AT, uint16_t>, nlist, B, 0, s, r16, ps, ro, P, bs, l, out); \
-        else launch_k(k_gather_sort<B, I, AT, int32_t>, nlist, B, 0, s, r32, ps, ro, P, bs, l, out);          \
+        if (packed16) launch_k(k_gather_sort<B, I, AT, uint16_t>, nlist, B, 0, s, r16, ps, ro, P, bs, l, out, ndev, first); \
+        else launch_k(k_gather_sort<B, I, AT, int32_t>, nlist, B, 0, s, r32, ps, ro, P, bs, l, out, ndev, first);          \
     } while (0)
     switch (cls) {
         case 1: if (atomic_rank) GSORT_K11G(256, 18, true); else GSORT_K11G(256, 18, false); break;

@@ -143,12 +143,13 @@ struct QueryTimer {  // (every 1024 spins the waiting thread yields; the query o
 // Wait for K12p's sequence number seq in the mailbox (the counters behind it are then
 // visible).  A stream error, or the stream going idle without the flag, returns GSORT_EHIP
 // instead of spinning forever.
-gsort_status wait_mail(gsort_ctx *c, uint64_t seq) {
+gsort_status wait_mail(gsort_ctx *c, uint64_t seq, hipStream_t s) {
     volatile uint64_t *flag = c->h_mail;
     QueryTimer qt;
+    if (!s) s = c->stream;
     for (uint64_t spin = 0; *flag != seq; ++spin) {
         if ((spin & 1023) == 1023) {
-            const hipError_t q = qt.due() ? hipStreamQuery(c->stream) : hipErrorNotReady;
+            const hipError_t q = qt.due() ? hipStreamQuery(s) : hipErrorNotReady;
             if (q != hipErrorNotReady && *flag != seq) {
                 if (q != hipSuccess)
                     return set_err(c, GSORT_EHIP, std::string("K12p counters: ") +

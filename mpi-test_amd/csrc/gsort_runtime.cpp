@@ -591,6 +591,10 @@ gsort_status create_common(gsort_ctx *c, int hip_device) {
     c->device = hip_device;
     HIP_TRY(c, hipSetDevice(hip_device));
     HIP_TRY(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    // the receive plan's side stream and its two ordering events (packed_exchange_sort)
+    HIP_TRY(c, hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
+    HIP_TRY(c, hipEventCreateWithFlags(&c->ev_meta, hipEventDisableTiming));
+    HIP_TRY(c, hipEventCreateWithFlags(&c->ev_plan, hipEventDisableTiming));
     ST_TRY(ensure(c, c->small, kSmallBytes));
     c->d_small = static_cast<char *>(c->small.p);
     HIP_TRY(c, hipHostMalloc(&c->h_small, kSmallBytes, hipHostMallocDefault));
@@ -747,6 +751,9 @@ gsort_status gsort_destroy(gsort_ctx *c) {
     if (c->h_mail) (void)hipHostFree(c->h_mail);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->stream2) (void)hipStreamDestroy(c->stream2);
+    if (c->ev_meta) (void)hipEventDestroy(c->ev_meta);
+    if (c->ev_plan) (void)hipEventDestroy(c->ev_plan);
     delete c;
     return GSORT_OK;
 }

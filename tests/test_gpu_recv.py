@@ -98,3 +98,65 @@ def test_receive_one_rank_forced(gsort, monkeypatch, cx):
     keys = rng.integers(-2**31, 2**31, (1 << 22) + 77).astype(np.int32)
     res = run_group(gsort, [keys], "radix")
     _check(res, keys, 1, "radix")
+
+
+def _run_group_seq(gsort, seq_blocks, algo):
+    """Like run_group, but every rank's ONE context sorts the inputs of seq_blocks in turn (the
+    receive launches of call i are shaped by call i-1's list counts: spec_recv_launch)."""
+    import threading
+    P = len(seq_blocks[0])
+    grp = gsort.Group(P)
+    res, errs = [[None] * P for _ in seq_blocks], []
+
+    def worker(r):
+        try:
+            with gsort.Context(rank=r, group=grp) as c:
+                fn = c.radix if algo == "radix" else c.sample
+                for i, blocks in enumerate(seq_blocks):
+                    p = c.alloc(max(blocks[r].size, 1) * 4)
+                    c.to_device(blocks[r], p)
+                    out, n, _ = fn(p, blocks[r].size)
+                    res[i][r] = (c.to_host(out, n), None, None)
+                    c.free(p)
+        except Exception as e:
+            errs.append((r, e))
+
+    th = [threading.Thread(target=worker, args=(r,), daemon=True) for r in range(P)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=600)
+    assert not [r for r, t in enumerate(th) if t.is_alive()], "group ranks hung"
+    grp.close()
+    if errs:
+        raise errs[0][1]
+    return res
+
+
+@pytest.mark.parametrize("cx", [3, 4])
+@pytest.mark.parametrize("algo", ["radix", "sample"])
+@pytest.mark.parametrize("P", [2, 4])
+def test_receive_launch_shapes_from_previous_call(gsort, monkeypatch, algo, cx, P):
+    """The receive sort's launches are queued before the host reads the list counts, shaped by
+    the previous call's counts: a context sorting inputs whose bucket classes
+    differ call to call -- the guess too small, too large, for lists that are now empty or past
+    kHxMax -- still sorts every bucket exactly once."""
+    monkeypatch.setenv("GSORT_RECV_CX", str(cx))
+    rng = np.random.default_rng(77 + P)
+    order = ["classes", "bits22", "one_value", "classes", "few_values", "wraps", "bits22",
+             "big_bucket", "classes"]
+    gens = dict(CASES)
+    # one 16-bit bucket past kHxMax (2^20 keys) on the receiving rank: list 0 goes to the MSD
+    # levels (spec_recv_launch's K18c skips it on the device)
+    gens["big_bucket"] = lambda r: np.concatenate([0x00050000 + r.integers(0, 1 << 16, 3 << 20),
+                                                    r.integers(-2**31, 2**31, 1 << 20)])
+    seq, keys_all = [], []
+    for name in order:
+        keys = np.asarray(gens[name](rng)).astype(np.int32)
+        rng.shuffle(keys)
+        B = -(-keys.size // P)
+        seq.append(np.split(keys, np.arange(1, P) * B))
+        keys_all.append(keys)
+    res = _run_group_seq(gsort, seq, algo)
+    for i, keys in enumerate(keys_all):
+        _check(res[i], keys, P, algo)
