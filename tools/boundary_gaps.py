@@ -13,6 +13,8 @@ segs = [("tiny -> tiny", 2 * R)]
 for mib in (1, 16, 64, 256, 1024):
     segs += [(f"w{mib} MiB -> tiny / tiny -> w", 2 * R), (f"w{mib} MiB nt -> tiny / tiny -> w", 2 * R)]
 segs.append(("graph: w1024 -> tiny / tiny -> w", 40))
+for v in ("plain", "ext stop (device-scope)", "ext stop (system-scope)", "ext start+stop"):
+    segs.append((f"w256 -> w256, {v}", R))
 i = 0
 for name, n in segs:
     seg = rows[i:i + n]

@@ -8,7 +8,11 @@
 //   wN        a 1-block kernel after a kernel that wrote N MiB (streaming stores)
 //   wN-nt     the same with nontemporal stores
 //   graph     the w1024 pair captured in a hipGraph and replayed
+//   then 256 MiB writers back to back (20 each): plain launches; hipExtLaunchKernel with a stop
+//   event per kernel (device-scope events, as libgsort's timed launches); with default
+//   (system-scope) stop events; with start + stop events
 //   hipcc --offload-arch=gfx950 -O3 tools/experiments/kernel_boundary.hip -o /tmp/kernel_boundary
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -65,6 +69,23 @@ int main() {
     CK(hipStreamEndCapture(s, &g));
     CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
     for (int r = 0; r < 5; ++r) CK(hipGraphLaunch(ge, s));
+    CK(hipStreamSynchronize(s));
+    const size_t n256 = (size_t)256 * (1 << 20) / 16;
+    hipEvent_t evd[64], evs[64];
+    for (int i = 0; i < 64; ++i) {
+        CK(hipEventCreateWithFlags(&evd[i], hipEventDisableSystemFence));
+        CK(hipEventCreateWithFlags(&evs[i], 0));
+    }
+    for (int r = 0; r < R; ++r) k_write<false><<<2048, 256, 0, s>>>(buf, n256);
+    CK(hipStreamSynchronize(s));
+    for (int r = 0; r < R; ++r)
+        hipExtLaunchKernelGGL(k_write<false>, dim3(2048), dim3(256), 0, s, nullptr, evd[r], 0, buf, n256);
+    CK(hipStreamSynchronize(s));
+    for (int r = 0; r < R; ++r)
+        hipExtLaunchKernelGGL(k_write<false>, dim3(2048), dim3(256), 0, s, nullptr, evs[r], 0, buf, n256);
+    CK(hipStreamSynchronize(s));
+    for (int r = 0; r < R; ++r)
+        hipExtLaunchKernelGGL(k_write<false>, dim3(2048), dim3(256), 0, s, evd[2 * r], evd[2 * r + 1], 0, buf, n256);
     CK(hipStreamSynchronize(s));
     printf("done\n");
     return 0;

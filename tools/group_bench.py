@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1, help="untimed calls per rank first")
     ap.add_argument("--local", default="msd")
+    ap.add_argument("--detail", action="store_true",
+                    help="stderr: every step's wall time and phases per rank (outlier hunting)")
     a = ap.parse_args()
     import torch  # noqa: F401
     import gsort
@@ -54,6 +56,12 @@ def main():
                 walls.append(time.perf_counter() - t0)
             wall = sum(walls) / a.steps
             out_walls[r] = walls
+            if a.detail:
+                for i, (w_, st_) in enumerate(zip(walls, sts)):
+                    print(f"step {i} rank {r}: wall {w_ * 1e3:.3f} total {st_['ms_total']:.3f} "
+                          f"local {st_['ms_local_sort']:.3f} sample {st_['ms_sample']:.3f} "
+                          f"exch {st_['ms_exchange']:.3f} merge {st_['ms_merge']:.3f}",
+                          file=sys.stderr, flush=True)
             keys = ("ms_total", "ms_local_sort", "ms_sample", "ms_exchange", "ms_merge",
                     "ms_hist", "ms_bucket_sort")
             out[r] = {k: sum(s[k] for s in sts) / len(sts) for k in keys}
