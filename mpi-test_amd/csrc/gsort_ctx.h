@@ -202,6 +202,8 @@ gsort_status msd_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *ou
     bool allow_est = false, bool allow_giant = true);
 gsort_status local_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *out, uint32_t *tmp,
     int *passes_run, gsort_stats *stats = nullptr, bool allow_est = false);
+gsort_status giant_sort(gsort_ctx *c, const uint32_t *in, uint64_t n, uint32_t *out,
+    uint32_t child, gsort_stats *stats, bool *ok);
 
 // ---- the distributed sorts (gsort_dist.cpp) ----
 gsort_status allgather_u64(gsort_ctx *c, uint64_t v, std::vector<uint64_t> &out);

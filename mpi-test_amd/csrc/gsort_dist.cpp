@@ -200,7 +200,7 @@ gsort_status recv_sort(gsort_ctx *c, const void *recv, bool packed16,
     if (h[0] && !list0) {  // all of list 0 into place, then MSD levels 1 and 0
         HIP_TRY(c, launch_list_to_segments(reinterpret_cast<uint64_t *>(c->m_next[0].p),
                                            (uint32_t)h[0], bstart, c->stream));
-        HIP_TRY(c, launch_gather_copy(recv, packed16, pos, d_r, P, bsize, bstart, out, c->stream));
+        HIP_TRY(c, launch_gather_copy(recv, packed16, pos, d_r, P, bstart, n, out, c->stream));
         for (int k = 3; k < 3 * (kLocalClasses + 1); ++k) h[k] = 0;
         int levels = 0;
         ST_TRY(msd_levels(c, 1, out, out, tmp, 0, h, stats, &levels));
@@ -230,11 +230,17 @@ void block_of(uint64_t N, int P, int r, uint64_t *B, uint64_t *len) {
 }
 
 // Sort the listed groups {start, len} of an int32 block in place on their low 16 bits (their
-// top 16 bits are equal): K11 for groups of <= kLocalMax keys, the LSD passes otherwise.
+// top 16 bits are equal, ids[i] = group i's as ordered u32 >> 16 when given): K11 for groups of
+// <= kLocalMax keys; past that the counted-child sort (giant_sort: one 65 536-bin histogram of
+// the low halves and an expansion, 8 B/key -- round 6: a Zipf block's giant group took two LSD
+// passes, ~30 B/key, 93 ms of every rank's 135 ms step at P = 8, profiles/r06_zipf_p8.txt), or
+// the LSD passes without ids or with GSORT_GIANT=0.
 gsort_status sort_groups(gsort_ctx *c, int32_t *a,
-                         const std::vector<std::pair<uint64_t, uint64_t>> &groups) {
+                         const std::vector<std::pair<uint64_t, uint64_t>> &groups,
+                         const std::vector<uint32_t> *ids = nullptr) {
     std::vector<uint64_t> small[kLocalClasses];
-    for (const auto &gr : groups) {
+    for (size_t gi = 0; gi < groups.size(); ++gi) {
+        const auto &gr = groups[gi];
         const int k = local_class(gr.second);
         if (k) {
             small[k - 1].push_back(gr.first);
@@ -243,9 +249,17 @@ gsort_status sort_groups(gsort_ctx *c, int32_t *a,
         }
         ST_TRY(ensure(c, c->m_bseg, gr.second * 8));
         uint32_t *t0 = reinterpret_cast<uint32_t *>(c->m_bseg.p), *t1 = t0 + gr.second;
+        bool counted = false;
+        if (ids && c->plan_giant) {  // every key in the one child: counted, never "misjudged"
+            const int lp = c->last_plan;
+            ST_TRY(giant_sort(c, reinterpret_cast<const uint32_t *>(a + gr.first), gr.second, t0,
+                              (*ids)[gi], nullptr, &counted));
+            c->last_plan = lp;
+        }
         int pr = 0;  // lsd_sort leaves its result in its `out` (t0)
-        ST_TRY(lsd_sort(c, reinterpret_cast<const uint32_t *>(a + gr.first), gr.second, t0, t1,
-                        &pr));
+        if (!counted)
+            ST_TRY(lsd_sort(c, reinterpret_cast<const uint32_t *>(a + gr.first), gr.second, t0, t1,
+                            &pr));
         HIP_TRY(c, hipMemcpyAsync(a + gr.first, t0, gr.second * 4, hipMemcpyDeviceToDevice,
                                   c->stream));
     }
@@ -274,15 +288,17 @@ gsort_status sort_groups16(gsort_ctx *c, uint16_t *pack,
     ST_TRY(ensure(c, c->m_g16, std::max<uint64_t>(total, 1) * 4));
     int32_t *scr = reinterpret_cast<int32_t *>(c->m_g16.p);
     std::vector<std::pair<uint64_t, uint64_t>> local;
+    std::vector<uint32_t> ids;
     uint64_t off = 0;
     for (size_t i = 0; i < groups.size(); ++i) {
         const uint64_t a = groups[i].second, len = ends[i] - a;
         HIP_TRY(c, launch_unpack16(pack + a, len, (uint32_t)groups[i].first, scr + off,
                                    c->stream));
         local.push_back({off, len});
+        ids.push_back((uint32_t)groups[i].first);
         off += len;
     }
-    ST_TRY(sort_groups(c, scr, local));
+    ST_TRY(sort_groups(c, scr, local, &ids));
     for (size_t i = 0; i < groups.size(); ++i)
         HIP_TRY(c, launch_pack16(scr + local[i].first, local[i].second, pack + groups[i].second,
                                  c->stream));
@@ -1139,7 +1155,10 @@ gsort_status sample_dist(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in, int
                            "no enough sample: rank " + std::to_string(r) + " holds " +
                                std::to_string(n_all[r]) + " keys, needs index " +
                                std::to_string((uint64_t)(k - 1) * interval));
-    bool packed = c->local_algo != GSORT_LOCAL_LSD;
+    // GSORT_SAMPLE_INT32=1: the int32 form whatever the block (A/B and test hook)
+    static const bool force_int32 = getenv("GSORT_SAMPLE_INT32") &&
+                                    getenv("GSORT_SAMPLE_INT32")[0] == '1';
+    bool packed = c->local_algo != GSORT_LOCAL_LSD && !force_int32;
     for (int r = 0; r < P; ++r) packed &= n_all[r] < (1ull << 32);  // u32 bucket counts
     if (!packed) return sample_dist_sorted(c, d_keys, n_in, n_all, d_out, n_out, stats);
     ST_TRY(check_send_limit(c, n_all, 2, "sample"));
@@ -1169,7 +1188,15 @@ gsort_status sample_dist(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in, int
     if (me == 0)
         for (int r = 0; r < P; ++r) { rc[r] = (size_t)k * 4; rd[r] = (size_t)r * k * 4; }
     // host == false: the common path, no host wait until the gathered rows.  host == true: the
-    // groups holding samples and splitters sorted on the host path (after a K13g flag)
+    // groups holding samples and splitters sorted on the host path (after a K13g flag), each
+    // group once (a Zipf block's giant group holds samples and splitters alike)
+    std::set<uint64_t> host_sorted;
+    auto host_sort = [&](std::vector<uint64_t> hs) -> gsort_status {
+        std::vector<uint64_t> todo;
+        for (uint64_t g : hs)
+            if (host_sorted.insert(g).second) todo.push_back(g);
+        return sort_groups16_host(c, pack, gb, todo);
+    };
     auto select = [&](bool host) -> gsort_status {
         HIP_TRY(c, launch_sample_groups(gb, interval, k, d_pref, d_g, c->stream));
         if (!host) {
@@ -1181,7 +1208,7 @@ gsort_status sample_dist(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in, int
                                       c->stream));
             HIP_TRY(c, hipStreamSynchronize(c->stream));
             for (uint64_t v : pf) hs.push_back(v >> 16);
-            ST_TRY(sort_groups16_host(c, pack, gb, hs));
+            ST_TRY(host_sort(hs));
         }
         HIP_TRY(c, launch_read_samples16(pack, d_pref, interval, k, d_samp, c->stream));
         ST_TRY(comm_try(c, c->comm->alltoallv(d_samp, sc.data(), sd.data(), d_sall, rc.data(),
@@ -1198,7 +1225,7 @@ gsort_status sample_dist(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in, int
             HIP_TRY(c, hipStreamSynchronize(c->stream));
             std::vector<uint64_t> hs;
             for (int32_t v : spl) hs.push_back(((uint32_t)v ^ 0x80000000u) >> 16);
-            ST_TRY(sort_groups16_host(c, pack, gb, hs));
+            ST_TRY(host_sort(hs));
             HIP_TRY(c, hipMemsetAsync(d_row + 2 * S, 0, (size_t)(k + S) * 8, c->stream));
         }
         HIP_TRY(c, launch_count_below16(pack, gb, d_xs, 2 * S, d_row, c->stream));

@@ -306,10 +306,11 @@ hipError_t launch_gather_sort(const void *recv, bool packed16, const uint64_t *p
                               const uint64_t *list, uint32_t nlist, int cls, bool atomic_rank,
                               uint32_t *out, hipStream_t s, const uint32_t *ndev = nullptr,
                               uint32_t first = 0);
-// Copy the pieces of every bucket > kLocalMax keys to out[bstart[h] ..) as ordered u32.
+// Copy the pieces of every bucket > kLocalMax keys to out[bstart[h] ..) as ordered u32 (one
+// block per 64 Ki output positions; n_out = bstart[65536]).
 hipError_t launch_gather_copy(const void *recv, bool packed16, const uint64_t *pos,
-                              const uint64_t *roff, int P, const uint64_t *bsize,
-                              const uint64_t *bstart, uint32_t *out, hipStream_t s);
+                              const uint64_t *roff, int P, const uint64_t *bstart, uint64_t n_out,
+                              uint32_t *out, hipStream_t s);
 // Sender of the packed exchange: out[i] = low 16 bits of a[i]; meta counts per destination
 // range (rng: nrng x {a, b, h_lo, nh, out_off}; gb = 65537 bucket bounds of the block).
 hipError_t launch_pack16(const int32_t *a, uint64_t n, uint16_t *out, hipStream_t s);

@@ -2751,18 +2751,38 @@ __global__ __launch_bounds__(256) void k_gather_copy(const T *__restrict__ recv,
                                                      const unsigned long long *__restrict__ pos,
                                                      const unsigned long long *__restrict__ roff,
                                                      int P,
-                                                     const unsigned long long *__restrict__ bsize,
                                                      const unsigned long long *__restrict__ bstart,
-                                                     uint32_t *__restrict__ out) {
-    const uint32_t h = blockIdx.x;
-    if (bsize[h] <= kLocalMax) return;
-    uint32_t *dst = out + bstart[h];
-    for (int p = 0; p < P; ++p) {
-        const uint64_t a = pos[(uint64_t)p * (kBuckets16 + 1) + h];
-        const uint64_t b = pos[(uint64_t)p * (kBuckets16 + 1) + h + 1];
-        const T *src = run_ptr(recv, roff[p] + a);
-        for (uint64_t j = threadIdx.x; j < b - a; j += 256) dst[j] = recv_key(src[j], h);
-        dst += b - a;
+                                                     uint32_t *__restrict__ out,
+                                                     unsigned long long n_out) {
+    // block b copies output positions [b * CH, (b + 1) * CH): every bucket past kLocalMax
+    // overlapping them, piece by piece.  (Round 6: one block per BUCKET took 67 ms per call on a
+    // Zipf block's giant buckets -- 82 % of a P = 8 Zipf sample sort, profiles/r06_zipf_p8.txt.)
+    constexpr unsigned long long CH = 65536;
+    const unsigned long long c0 = (unsigned long long)blockIdx.x * CH;
+    if (c0 >= n_out) return;
+    const unsigned long long c1 = c0 + CH < n_out ? c0 + CH : n_out;
+    uint32_t lo = 0, hi = kBuckets16;  // the last bucket starting at or before c0
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (bstart[mid] <= c0) lo = mid; else hi = mid;
+    }
+    for (uint32_t h = lo; h < kBuckets16; ++h) {
+        const unsigned long long b0 = bstart[h], b1 = bstart[h + 1];
+        if (b0 >= c1) break;
+        if (b1 - b0 <= kLocalMax) continue;
+        unsigned long long cum = b0;  // piece p's first output position
+        for (int p = 0; p < P; ++p) {
+            const unsigned long long a = pos[(uint64_t)p * (kBuckets16 + 1) + h];
+            const unsigned long long len = pos[(uint64_t)p * (kBuckets16 + 1) + h + 1] - a;
+            const unsigned long long s0 = cum > c0 ? cum : c0;
+            const unsigned long long e0 = cum + len < c1 ? cum + len : c1;
+            if (s0 < e0) {
+                const T *src = run_ptr(recv, roff[p] + a);
+                for (unsigned long long i = s0 + threadIdx.x; i < e0; i += 256)
+                    out[i] = recv_key(src[i - cum], h);
+            }
+            cum += len;
+        }
     }
 }
 
@@ -4138,19 +4158,20 @@ hipError_t launch_gather_sort(const void *recv, bool packed16, const uint64_t *p
 }
 
 hipError_t launch_gather_copy(const void *recv, bool packed16, const uint64_t *pos,
-                              const uint64_t *roff, int P, const uint64_t *bsize,
-                              const uint64_t *bstart, uint32_t *out, hipStream_t s) {
+                              const uint64_t *roff, int P, const uint64_t *bstart, uint64_t n_out,
+                              uint32_t *out, hipStream_t s) {
     using ull = unsigned long long;
+    if (n_out == 0) return hipSuccess;
     auto *ps = reinterpret_cast<const ull *>(pos);
     auto *ro = reinterpret_cast<const ull *>(roff);
-    auto *bz = reinterpret_cast<const ull *>(bsize);
     auto *bs = reinterpret_cast<const ull *>(bstart);
+    const unsigned grid = (unsigned)((n_out + 65535) / 65536);
     if (packed16)
-        launch_k(k_gather_copy<uint16_t>, kBuckets16, 256, 0, s, reinterpret_cast<const uint16_t *>(recv), ps, ro,
-                                                 P, bz, bs, out);
+        launch_k(k_gather_copy<uint16_t>, grid, 256, 0, s, reinterpret_cast<const uint16_t *>(recv), ps, ro,
+                                                 P, bs, out, (ull)n_out);
     else
-        launch_k(k_gather_copy<int32_t>, kBuckets16, 256, 0, s, reinterpret_cast<const int32_t *>(recv), ps, ro,
-                                                 P, bz, bs, out);
+        launch_k(k_gather_copy<int32_t>, grid, 256, 0, s, reinterpret_cast<const int32_t *>(recv), ps, ro,
+                                                 P, bs, out, (ull)n_out);
     return hipGetLastError();
 }
 

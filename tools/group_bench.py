@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1, help="untimed calls per rank first")
     ap.add_argument("--local", default="msd")
+    ap.add_argument("--dist", choices=["uniform", "zipf"], default="uniform")
     ap.add_argument("--detail", action="store_true",
                     help="stderr: every step's wall time and phases per rank (outlier hunting)")
     a = ap.parse_args()
@@ -40,7 +41,7 @@ def main():
         with gsort.Context(rank=r, group=grp) as c:
             c.set_local_algo(gsort.LOCAL_MSD if a.local == "msd" else gsort.LOCAL_LSD)
             d = c.alloc(n * 4)
-            c.generate(gsort.UNIFORM, 42, r * n, n, d)
+            c.generate(gsort.UNIFORM if a.dist == "uniform" else gsort.ZIPF, 42, r * n, n, d)
             c.reserve(n)
             fn = c.radix if a.algo == "radix" else c.sample
             for _ in range(a.warmup):
@@ -78,7 +79,7 @@ def main():
     in_order = [round(max(w[i] for w in out_walls) * 1e3, 4) for i in range(a.steps)]
     steps = sorted(in_order)
     med = steps[len(steps) // 2]
-    print(json.dumps({"ranks": P, "keys_per_rank": n, "algo": a.algo,
+    print(json.dumps({"ranks": P, "keys_per_rank": n, "algo": a.algo, "dist": a.dist,
                       "sum_over_ranks_ms": tot,
                       "wall_ms": round(max(o["wall_ms"] for o in out), 4),
                       "step_ms": [round(x, 4) for x in steps],
