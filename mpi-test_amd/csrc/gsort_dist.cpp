@@ -1156,8 +1156,8 @@ gsort_status sample_dist(gsort_ctx *c, const int32_t *d_keys, uint64_t n_in, int
                                std::to_string(n_all[r]) + " keys, needs index " +
                                std::to_string((uint64_t)(k - 1) * interval));
     // GSORT_SAMPLE_INT32=1: the int32 form whatever the block (A/B and test hook)
-    static const bool force_int32 = getenv("GSORT_SAMPLE_INT32") &&
-                                    getenv("GSORT_SAMPLE_INT32")[0] == '1';
+    const char *fi = getenv("GSORT_SAMPLE_INT32");  // (read per call: tests flip it)
+    const bool force_int32 = fi && fi[0] == '1';
     bool packed = c->local_algo != GSORT_LOCAL_LSD && !force_int32;
     for (int r = 0; r < P; ++r) packed &= n_all[r] < (1ull << 32);  // u32 bucket counts
     if (!packed) return sample_dist_sorted(c, d_keys, n_in, n_all, d_out, n_out, stats);

@@ -368,10 +368,16 @@ def test_radix_multirank_splitter_edges(gsort, orc, case):
         assert np.array_equal(res[q][0], ref[q * B:(q + 1) * B]), (case, q)
 
 
+@pytest.mark.parametrize("form", ["packed", "int32"])
 @pytest.mark.parametrize("P", [2, 4, 8])
-def test_sample_multirank_matches_reference_semantics(gsort, orc, ref_cases, ref_outputs, P):
+def test_sample_multirank_matches_reference_semantics(gsort, orc, ref_cases, ref_outputs, P, form,
+                                                      monkeypatch):
     """Splitters, the P x P bucket matrix and the output equal the reference's own debug
-    output (golden fixtures) and the oracle's restatement."""
+    output (golden fixtures) and the oracle's restatement -- for the packed sample sort (the
+    default: samples and bounds read off the 16-bit grouped block, 2 B/key exchange) and its
+    int32 form (local sort first; GSORT_SAMPLE_INT32=1, what the LSD local algorithm and ranks
+    past 2^32 keys take)."""
+    monkeypatch.setenv("GSORT_SAMPLE_INT32", "1" if form == "int32" else "0")
     checked = 0
     for c in ref_cases:
         if c["prog"] != "sample_sort" or c["P"] != P or c["rc"] != 0:
@@ -399,9 +405,12 @@ def test_sample_not_enough_samples(gsort, orc):
     assert ei.value.status == gsort.ENOSAMPLE
 
 
-def test_sample_multirank_zipf_skew(gsort, orc):
+@pytest.mark.parametrize("form", ["packed", "int32"])
+def test_sample_multirank_zipf_skew(gsort, orc, form, monkeypatch):
     """Zipf at P=8 overflows the reference's fixed buckets (Q12); the build sizes receive
-    buffers from the exchanged counts, so it sorts correctly with one rank holding ~30%."""
+    buffers from the exchanged counts, so it sorts correctly with one rank holding ~30%.  (The
+    packed form's giant 16-bit group takes the host path of the select, counted.)"""
+    monkeypatch.setenv("GSORT_SAMPLE_INT32", "1" if form == "int32" else "0")
     P, n = 8, 1 << 18
     keys = orc.gen(orc.ZIPF, 11, n)
     assert orc.ref_sample(keys, P)[0] == orc.E_OVERFLOW
