@@ -1814,29 +1814,6 @@ __device__ __forceinline__ uint32_t wave_rank(uint32_t *wc, uint32_t d, bool val
 constexpr bool lds_pad(int tile) { return tile < 32768; }
 constexpr int lds_slots(int tile) { return lds_pad(tile) ? tile + tile / 32 : tile; }
 
-// GSORT_K11_BPERM (A/B build macro, round 6): the digit-start lookups of
-// both passes -- one random LDS read per key each, ~3.5-way bank conflicts on 32-lane groups --
-// through the LDS crossbar instead: every wave holds the 256 starts in two registers (u16
-// pairs) and fetches a key's start with two ds_bpermute (no bank access).
-#ifndef GSORT_K11_BPERM
-#define GSORT_K11_BPERM 0
-#endif
-struct Wave256 {  // lane L: lo = v[L] | v[L + 64] << 16, hi = v[L + 128] | v[L + 192] << 16
-    uint32_t lo, hi;
-    __device__ __forceinline__ void load(const uint32_t *t, uint32_t lane) {
-        lo = (t[lane] & 0xFFFFu) | (t[lane + 64] << 16);
-        hi = (t[lane + 128] & 0xFFFFu) | (t[lane + 192] << 16);
-    }
-    // v[d]; every lane of the wave must execute it (a bpermute reads inactive lanes as 0)
-    __device__ __forceinline__ uint32_t get(uint32_t d) const {
-        const int addr = (int)((d & 63u) << 2);
-        const uint32_t a = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)lo);
-        const uint32_t b = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)hi);
-        const uint32_t v = (d & 128u) ? b : a;
-        return (d & 64u) ? v >> 16 : v & 0xFFFFu;
-    }
-};
-
 // STORE16: dst holds u16 -- the sorted keys' low 16 bits are stored there (no flip): the
 // distributed sender's boundary groups, sorted in place in the packed send buffer.
 template <int BLOCK, int ITEMS, bool ATOMIC, bool STORE16 = false>
@@ -1884,19 +1861,9 @@ __device__ __forceinline__ void sort_bucket(uint32_t (&k)[ITEMS], uint32_t len, 
             cnt[tid] = excl;
         }
         __syncthreads();
-#if GSORT_K11_BPERM
-        Wave256 tb;
-        tb.load(cnt, (uint32_t)lane);
-#pragma unroll
-        for (int i = 0; i < ITEMS; ++i) {
-            const uint32_t base = tb.get(k[i] & 255u);  // (all lanes)
-            if ((uint32_t)tid < lim(i)) s_a[at(base + r[i])] = k[i];
-        }
-#else
 #pragma unroll
         for (int i = 0; i < ITEMS; ++i)
             if ((uint32_t)tid < lim(i)) s_a[at(cnt[k[i] & 255u] + r[i])] = k[i];
-#endif
         __syncthreads();
     }
 
@@ -1940,21 +1907,10 @@ __device__ __forceinline__ void sort_bucket(uint32_t (&k)[ITEMS], uint32_t len, 
             }
         }
         __syncthreads();
-#if GSORT_K11_BPERM
-        Wave256 tw;
-        tw.load(wc, (uint32_t)lane);
-#pragma unroll
-        for (int i = 0; i < ITEMS; ++i)
-            if ((uint32_t)i < R) {  // (wave-uniform)
-                const uint32_t base = tw.get((k[i] >> shift) & 255u);  // (all lanes)
-                if ((uint32_t)(i * 64 + lane) < wlen) s_a[at(base + rk[i])] = k[i];
-            }
-#else
 #pragma unroll
         for (int i = 0; i < ITEMS; ++i)
             if ((uint32_t)i < R && (uint32_t)(i * 64 + lane) < wlen)
                 s_a[at(wc[(k[i] >> shift) & 255u] + rk[i])] = k[i];
-#endif
         __syncthreads();
     }
     const __amdgpu_buffer_rsrc_t rs = bucket_rsrc(dst, len * (STORE16 ? 2u : 4u));  // stores past len dropped
