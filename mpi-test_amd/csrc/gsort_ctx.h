@@ -105,6 +105,10 @@ struct gsort_ctx {
     // next call's receive launches, queued before its counts are read (spec_recv_launch)
     uint32_t recv_hint[kLocalClasses + 1] = {};
     bool recv_hint_ok = false;
+    // K15s (the receive plan's single-pass lookback scan): the allocation whose status words and
+    // ticket were zeroed, and the per-call epoch its status words carry
+    void *scan_clean = nullptr;
+    uint32_t scan_epoch = 0;
     int ncu = 256;
     int last_plan = 0;      // gsort_last_plan: 0 exact, 1 sampled, 2 sampled then exact
     bool plan_trace = false; // GSORT_PLAN_TRACE: one stderr line per plan decision

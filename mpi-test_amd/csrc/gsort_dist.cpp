@@ -17,8 +17,9 @@ namespace rt {
 // recv holds the P runs back to back (run p has rlen[p] keys), each grouped by the top 16 bits
 // (ordered u32): int32 keys, or with packed16 only their low 16 bits, in which case the caller
 // has already filled c->m_rpos (pos[p][h], launch_pos_from_meta).
-// bucket sizes (65536) + starts (65537) + row-scan partials (64 x 64), u64
-constexpr size_t kBsizeBytes = ((size_t)2 * kBuckets16 + 1 + 65 * 64) * 8;
+// bucket sizes (65536) + starts (65537) + row-scan partials / K15s status words (65 x 64), u64,
+// + K15s's ticket (one u64 slot)
+constexpr size_t kBsizeBytes = ((size_t)2 * kBuckets16 + 1 + kRecvScanStatusWords + 1) * 8;
 
 // (a - b) / sizeof(T) for pointers into different allocations, as a u64 (two's complement for
 // a negative offset): integer arithmetic, never a pointer difference across allocations
@@ -193,11 +194,34 @@ gsort_status recv_sort(gsort_ctx *c, const void *recv, bool packed16,
         ST_TRY(check_bounds(c, bstart, kBuckets16 + 1, n, "receive bucket starts"));
     }
     const bool list0 = h[0] && h[2] <= kHxMax;  // else: a bucket past kHxMax (below)
+    // buckets past kHxMax (skewed keys: a Zipf block's frequent values) are counted in place
+    // (round 6): K18c takes list 0 and leaves them empty, then each is gathered as int32 into its
+    // place and sorted there by giant_sort -- all its keys share the bucket's top 16 bits, so
+    // that is one 65 536-bin count and an expansion (8 B/key), no cold keys.  Without K18c
+    // (GSORT_RECV_CX <= 0) or GSORT_GIANT=0, list 0 goes through the MSD levels 1 and 0.
+    const bool counted = h[0] && !list0 && c->recv_cx > 0 && c->plan_giant;
     t = tic(c);
     ST_TRY(sort_recv_lists(c, recv, packed16, pos, d_r, P, bstart, work_lists(c, 0), h, out, stats,
-                           list0));
+                           list0 || counted));
     toc(c, PH_BUCKET, t);
-    if (h[0] && !list0) {  // all of list 0 into place, then MSD levels 1 and 0
+    if (counted) {
+        t = tic(c);
+        HIP_TRY(c, launch_gather_copy(recv, packed16, pos, d_r, P, bstart, n, out, c->stream, kHxMax,
+                                      true));
+        std::vector<uint64_t> l0(2 * h[0]);
+        HIP_TRY(c, hipMemcpyAsync(l0.data(), c->m_next[0].p, l0.size() * 8, hipMemcpyDeviceToHost,
+                                  c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        for (uint64_t e = 0; e < h[0]; ++e) {
+            const uint64_t len = (uint32_t)l0[2 * e + 1];
+            if (len <= kHxMax) continue;
+            uint32_t *b = out + (l0[2 * e] >> 16);  // (entry: h | bstart[h] << 16)
+            bool ok = false;
+            ST_TRY(giant_sort(c, b, len, b, (uint32_t)(l0[2 * e] & 0xFFFFu), nullptr, &ok));
+            if (!ok) return set_err(c, GSORT_EINVAL, "receive bucket past kHxMax: counted sort refused");
+        }
+        toc(c, PH_BUCKET, t);
+    } else if (h[0] && !list0) {  // all of list 0 into place, then MSD levels 1 and 0
         HIP_TRY(c, launch_list_to_segments(reinterpret_cast<uint64_t *>(c->m_next[0].p),
                                            (uint32_t)h[0], bstart, c->stream));
         HIP_TRY(c, launch_gather_copy(recv, packed16, pos, d_r, P, bstart, n, out, c->stream));
@@ -504,7 +528,12 @@ gsort_status packed_exchange_sort(gsort_ctx *c, uint16_t *pack, const uint64_t *
     ST_TRY(comm_try(c, c->comm->alltoallv(meta_s, sc.data(), sd.data(), meta_r, rc.data(),
                                           rd.data(), c->stream)));
     toc_rec(c, PH_EXCH, t);
-    HIP_TRY(c, hipEventRecord(c->ev_meta, c->stream));
+    // (no payload from or to a peer -- one rank -- leaves nothing to overlap: the plan then
+    // stays on the main stream, where the cross-stream hand-off cost ~13 us of idle, and even
+    // the event record alone ~5 us)
+    bool peers = false;
+    for (int q = 0; q < P; ++q) peers |= q != me && (send[q] || recv[q]);
+    if (peers) HIP_TRY(c, hipEventRecord(c->ev_meta, c->stream));
     for (int q = 0; q < P; ++q)
         if (stats && q != me) {
             stats->bytes_sent += send[q] * 2;
@@ -536,18 +565,21 @@ gsort_status packed_exchange_sort(gsort_ctx *c, uint16_t *pack, const uint64_t *
     uint64_t *pos = reinterpret_cast<uint64_t *>(c->m_rpos.p);
     uint64_t *bsize = reinterpret_cast<uint64_t *>(c->m_bsize.p), *bstart = bsize + kBuckets16;
     uint64_t *ctr = reinterpret_cast<uint64_t *>(c->d_small + OFF_CTR);
-    // (no payload from or to a peer -- one rank -- leaves nothing to overlap: the plan then
-    // stays on the main stream, where the cross-stream hand-off cost ~13 us of idle)
-    bool peers = false;
-    for (int q = 0; q < P; ++q) peers |= q != me && (send[q] || recv[q]);
+    uint64_t *scan_scratch = bstart + kBuckets16 + 1;  // K15s status words, then its ticket
     hipStream_t ps = peers ? c->stream2 : c->stream;
     t = tic(c);
     if (peers) HIP_TRY(c, hipStreamWaitEvent(c->stream2, c->ev_meta, 0));
+    if (c->scan_clean != c->m_bsize.p) {  // a new allocation: status words and ticket zeroed
+        // once, on the stream the scan runs on (queued on the other one, behind the count
+        // exchange's event, it raced the scan: a ticket cleared mid-launch hung the IPC group)
+        HIP_TRY(c, hipMemsetAsync(scan_scratch, 0, (kRecvScanStatusWords + 1) * 8, ps));
+        c->scan_clean = c->m_bsize.p;
+    }
     // the runs' bucket bounds and the bucket starts in one row scan of P + 1 rows (the last
     // row is every bucket's total over the sources); classify reads the sizes off bstart
     HIP_TRY(c, launch_recv_plan_from_meta(meta_r, d_moff, (uint32_t)hlo[me], (uint32_t)nh[me], P,
-                                          pos, bstart, bstart + kBuckets16 + 1, ps, ctr,
-                                          (uint32_t)(kCtrBytes / 8)));
+                                          pos, bstart, scan_scratch, ps, ctr,
+                                          (uint32_t)(kCtrBytes / 8), ++c->scan_epoch));
     const WorkLists wl = work_lists(c, 0);
     HIP_TRY(c, launch_classify_range(nullptr, bstart, wl, (uint32_t)hlo[me],
                                      (uint32_t)(hlo[me] + nh[me]), ps));

@@ -276,13 +276,16 @@ hipError_t launch_run_bounds(const int32_t *recv, const uint64_t *roff, const ui
 // (moff[p] = ~0: nothing received from p) -- the packed exchange.
 // scratch: 64 x P u64.
 // pos (as launch_pos_from_meta) and bstart[0 .. 65536] (exclusive scan of every bucket's total
-// over the sources) in one two-kernel row scan of P + 1 rows; classify then takes bsize =
-// nullptr (sizes from bstart).  scratch: (P + 1) x 64 u64.  zero[0 .. nzero) (<= 1024 u64) is
-// cleared by the first kernel (the work-list counters the classification adds into).
+// over the sources) in ONE single-pass decoupled-lookback row scan of P + 1 rows (K15s); classify
+// then takes bsize = nullptr (sizes from bstart).  scratch: kRecvScanStatusWords status words
+// and a u32 ticket after them, both zero before a context's first scan; epoch: a number the
+// caller changes every call.  zero[0 .. nzero) (<= 1024 u64) is cleared by the kernel (the
+// work-list counters the classification adds into).
+constexpr size_t kRecvScanStatusWords = 65 * 64;
 hipError_t launch_recv_plan_from_meta(const uint32_t *meta, const uint64_t *moff, uint32_t h_lo,
                                      uint32_t nh, int P, uint64_t *pos, uint64_t *bstart,
-                                     uint64_t *scratch, hipStream_t s, uint64_t *zero = nullptr,
-                                     uint32_t nzero = 0);
+                                     uint64_t *scratch, hipStream_t s, uint64_t *zero,
+                                     uint32_t nzero, uint32_t epoch);
 hipError_t launch_pos_from_meta(const uint32_t *meta, const uint64_t *moff, uint32_t h_lo,
                                 uint32_t nh, int P, uint64_t *pos, uint64_t *scratch,
                                 hipStream_t s);
@@ -306,11 +309,12 @@ hipError_t launch_gather_sort(const void *recv, bool packed16, const uint64_t *p
                               const uint64_t *list, uint32_t nlist, int cls, bool atomic_rank,
                               uint32_t *out, hipStream_t s, const uint32_t *ndev = nullptr,
                               uint32_t first = 0);
-// Copy the pieces of every bucket > kLocalMax keys to out[bstart[h] ..) as ordered u32 (one
-// block per 64 Ki output positions; n_out = bstart[65536]).
+// Copy the pieces of every bucket of more than min_len keys to out[bstart[h] ..) as ordered u32
+// or, as_int32, int32 (one block per 64 Ki output positions; n_out = bstart[65536]).
 hipError_t launch_gather_copy(const void *recv, bool packed16, const uint64_t *pos,
                               const uint64_t *roff, int P, const uint64_t *bstart, uint64_t n_out,
-                              uint32_t *out, hipStream_t s);
+                              uint32_t *out, hipStream_t s, uint64_t min_len = kLocalMax,
+                              bool as_int32 = false);
 // Sender of the packed exchange: out[i] = low 16 bits of a[i]; meta counts per destination
 // range (rng: nrng x {a, b, h_lo, nh, out_off}; gb = 65537 bucket bounds of the block).
 hipError_t launch_pack16(const int32_t *a, uint64_t n, uint16_t *out, hipStream_t s);

@@ -2331,8 +2331,11 @@ __device__ __forceinline__ void cx_fill_table(CxTable<T> &t, const T *recv,
         return;
     }
     const uint32_t h = (uint32_t)ent[0] & 0xFFFFu;  // (bstart[h] rides above bit 16)
+    // a bucket past kHxMax is not K18c's: left as an empty one (recv_sort counts it in place,
+    // giant_sort) -- its bins' u16 counts could not hold it
+    const bool giant = (uint32_t)ent[1] > (uint32_t)kHxMax;
     uint64_t a = 0, b = 0, src = 0;
-    if ((int)lane < P) {
+    if ((int)lane < P && !giant) {
         a = pos[(uint64_t)lane * (kBuckets16 + 1) + h];
         b = pos[(uint64_t)lane * (kBuckets16 + 1) + h + 1];
         src = roff[lane] + a;
@@ -2351,7 +2354,7 @@ __device__ __forceinline__ void cx_fill_table(CxTable<T> &t, const T *recv,
     if ((int)lane == P - 1) t.cumv[P] = x;
     if (lane == 0) {
         t.h = h;
-        t.keys = (uint32_t)ent[1];
+        t.keys = giant ? 0u : (uint32_t)ent[1];
         t.dst = bstart[h];
     }
 }
@@ -2753,7 +2756,9 @@ __global__ __launch_bounds__(256) void k_gather_copy(const T *__restrict__ recv,
                                                      int P,
                                                      const unsigned long long *__restrict__ bstart,
                                                      uint32_t *__restrict__ out,
-                                                     unsigned long long n_out) {
+                                                     unsigned long long n_out,
+                                                     unsigned long long min_len, uint32_t xo) {
+    // (buckets of more than min_len keys; every key stored XOR xo: 0 ordered u32, kFlip int32)
     // block b copies output positions [b * CH, (b + 1) * CH): every bucket past kLocalMax
     // overlapping them, piece by piece.  (Round 6: one block per BUCKET took 67 ms per call on a
     // Zipf block's giant buckets -- 82 % of a P = 8 Zipf sample sort, profiles/r06_zipf_p8.txt.)
@@ -2769,7 +2774,7 @@ __global__ __launch_bounds__(256) void k_gather_copy(const T *__restrict__ recv,
     for (uint32_t h = lo; h < kBuckets16; ++h) {
         const unsigned long long b0 = bstart[h], b1 = bstart[h + 1];
         if (b0 >= c1) break;
-        if (b1 - b0 <= kLocalMax) continue;
+        if (b1 - b0 <= min_len) continue;
         unsigned long long cum = b0;  // piece p's first output position
         for (int p = 0; p < P; ++p) {
             const unsigned long long a = pos[(uint64_t)p * (kBuckets16 + 1) + h];
@@ -2777,9 +2782,17 @@ __global__ __launch_bounds__(256) void k_gather_copy(const T *__restrict__ recv,
             const unsigned long long s0 = cum > c0 ? cum : c0;
             const unsigned long long e0 = cum + len < c1 ? cum + len : c1;
             if (s0 < e0) {
-                const T *src = run_ptr(recv, roff[p] + a);
-                for (unsigned long long i = s0 + threadIdx.x; i < e0; i += 256)
-                    out[i] = recv_key(src[i - cum], h);
+                // indexed by output position: the offset formed as an integer (mod 2^64)
+                const T *src = run_ptr(recv, roff[p] + a - cum);
+                unsigned long long i = s0 + threadIdx.x;
+                for (; i + 3 * 256 < e0; i += 4 * 256) {  // four loads in flight per lane
+                    T v[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) v[u] = src[i + u * 256];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) out[i + u * 256] = recv_key(v[u], h) ^ xo;
+                }
+                for (; i < e0; i += 256) out[i] = recv_key(src[i], h) ^ xo;
             }
             cum += len;
         }
@@ -2914,6 +2927,100 @@ __global__ __launch_bounds__(1024) void k_rowscan_reduce(Gen gen,
         for (int i = 0; i < 16; ++i) t += s_w[i];
         part[row * kScanBlocks + b] = t;
     }
+}
+
+// K15s: the receive plan's row scans in ONE pass -- north_star's single-pass decoupled-lookback
+// exclusive scan, where it fits (round 6: the 2^16-bucket rows of the receive plan; the local
+// sort's passes lost to it in v0).  Every block of 1024 values publishes its
+// aggregate, then its inclusive prefix, in a status word; its wave 0 reads the status words of
+// all its predecessors in the row at once (one per lane: 64 blocks per row) and sums aggregates
+// back to the nearest inclusive prefix.  A block takes its place in the grid from an atomic
+// ticket as it starts, so every predecessor it waits on has started (no reliance on the order
+// of dispatch); the block holding the last ticket resets the ticket for the next call.
+// Status word: state (bits 62-63: 1 aggregate, 2 inclusive prefix) | epoch (bits 40-61: the
+// call, so a word left by an earlier call never counts) | value (bits 0-39).
+constexpr unsigned long long kLbValue = (1ull << 40) - 1, kLbEpoch = 0x3FFFFFull << 40;
+template <typename Gen>
+__global__ __launch_bounds__(1024) void k_rowscan_lookback(Gen gen,
+                                                           unsigned long long *__restrict__ status,
+                                                           unsigned int *__restrict__ ticket,
+                                                           uint32_t epoch,
+                                                           unsigned long long *__restrict__ out,
+                                                           uint64_t row_stride,
+                                                           unsigned long long *out_last,
+                                                           unsigned long long *zero,
+                                                           uint32_t nzero) {
+    __shared__ unsigned long long s_w[16];
+    __shared__ unsigned long long s_pre;
+    __shared__ uint32_t s_vb;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint32_t nblk = gridDim.x * gridDim.y;
+    if (tid == 0) s_vb = atomicAdd(ticket, 1u);
+    __syncthreads();
+    // (the ticket is zero on entry -- the runtime zeroes it with its buffer, the last block of
+    // every launch resets it; "% nblk" keeps even a stray value a permutation of the blocks)
+    const uint32_t vb = s_vb % nblk;
+    const uint32_t row = vb / kScanBlocks, b = vb % kScanBlocks;
+    if (zero && vb == 0 && tid < nzero) zero[tid] = 0;
+    const unsigned long long c = gen(row, b * 1024 + tid);
+    unsigned long long x = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned long long t = __shfl_up(x, o);
+        if ((int)lane >= o) x += t;
+    }
+    if (lane == 63) s_w[w] = x;
+    __syncthreads();
+    if (w == 0) {
+        unsigned long long tot = lane < 16 ? s_w[lane] : 0ull;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
+        const unsigned long long ep = ((unsigned long long)epoch << 40) & kLbEpoch;
+        unsigned long long *st = status + (uint64_t)row * kScanBlocks;
+        unsigned long long excl = 0;
+        if (b == 0) {
+            if (lane == 0)
+                __hip_atomic_store(&st[0], (2ull << 62) | ep | tot, __ATOMIC_RELEASE,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            if (lane == 0)
+                __hip_atomic_store(&st[b], (1ull << 62) | ep | tot, __ATOMIC_RELEASE,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            const int p = (int)b - 1 - (int)lane;  // lane j looks at predecessor b - 1 - j
+            while (true) {
+                unsigned long long v = 0;
+                if (p >= 0) v = __hip_atomic_load(&st[p], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                const bool cur = p >= 0 && (v & kLbEpoch) == ep && (v >> 62) != 0;
+                const uint64_t im = __ballot(cur && (v >> 62) == 2);
+                const uint64_t cm = __ballot(cur);
+                if (im) {  // the nearest inclusive prefix, and every aggregate before it in
+                    const uint32_t f = (uint32_t)__builtin_ctzll(im);
+                    const uint64_t need = f == 63 ? ~0ull : (2ull << f) - 1;
+                    if ((cm & need) == need) {
+                        unsigned long long sv = lane <= f ? (v & kLbValue) : 0ull;
+#pragma unroll
+                        for (int o = 32; o > 0; o >>= 1) sv += __shfl_xor(sv, o);
+                        excl = sv;
+                        break;
+                    }
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (lane == 0)
+                __hip_atomic_store(&st[b], (2ull << 62) | ep | (excl + tot), __ATOMIC_RELEASE,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (lane == 0) s_pre = excl;
+    }
+    __syncthreads();
+    unsigned long long run = s_pre + x - c;
+    for (uint32_t ww = 0; ww < w; ++ww) run += s_w[ww];
+    unsigned long long *o = out_last && row == gridDim.y - 1 ? out_last : out + row * row_stride;
+    o[b * 1024 + tid] = run;
+    if (b == kScanBlocks - 1 && tid == 1023) o[kBuckets16] = run + c;
+    // every other block has taken its ticket: the last one resets it for the next launch
+    if (tid == 0 && s_vb == nblk - 1)
+        __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <typename Gen>
@@ -4086,16 +4193,16 @@ hipError_t launch_pos_from_meta(const uint32_t *meta, const uint64_t *moff, uint
 hipError_t launch_recv_plan_from_meta(const uint32_t *meta, const uint64_t *moff, uint32_t h_lo,
                                      uint32_t nh, int P, uint64_t *pos, uint64_t *bstart,
                                      uint64_t *scratch, hipStream_t s, uint64_t *zero,
-                                     uint32_t nzero) {
+                                     uint32_t nzero, uint32_t epoch) {
     using ull = unsigned long long;
     if (P < 1 || P > 64 || nzero > 1024) return hipErrorInvalidValue;
     const MetaCountsSum gen{MetaCounts{meta, reinterpret_cast<const ull *>(moff), h_lo, nh},
                             (uint32_t)P};
-    ull *part = reinterpret_cast<ull *>(scratch);
-    launch_k(k_rowscan_reduce<decltype(gen)>, dim3(kScanBlocks, P + 1), 1024, 0, s, gen, part,
-             reinterpret_cast<ull *>(zero), nzero);
-    launch_k(k_rowscan_apply<decltype(gen)>, dim3(kScanBlocks, P + 1), 1024, 0, s, gen, part,
-             reinterpret_cast<ull *>(pos), kBuckets16 + 1, reinterpret_cast<ull *>(bstart));
+    ull *status = reinterpret_cast<ull *>(scratch);
+    unsigned int *ticket = reinterpret_cast<unsigned int *>(scratch + kRecvScanStatusWords);
+    launch_k(k_rowscan_lookback<decltype(gen)>, dim3(kScanBlocks, P + 1), 1024, 0, s, gen, status,
+             ticket, epoch, reinterpret_cast<ull *>(pos), (uint64_t)kBuckets16 + 1,
+             reinterpret_cast<ull *>(bstart), reinterpret_cast<ull *>(zero), nzero);
     return hipGetLastError();
 }
 
@@ -4159,7 +4266,7 @@ hipError_t launch_gather_sort(const void *recv, bool packed16, const uint64_t *p
 
 hipError_t launch_gather_copy(const void *recv, bool packed16, const uint64_t *pos,
                               const uint64_t *roff, int P, const uint64_t *bstart, uint64_t n_out,
-                              uint32_t *out, hipStream_t s) {
+                              uint32_t *out, hipStream_t s, uint64_t min_len, bool as_int32) {
     using ull = unsigned long long;
     if (n_out == 0) return hipSuccess;
     auto *ps = reinterpret_cast<const ull *>(pos);
@@ -4168,10 +4275,12 @@ hipError_t launch_gather_copy(const void *recv, bool packed16, const uint64_t *p
     const unsigned grid = (unsigned)((n_out + 65535) / 65536);
     if (packed16)
         launch_k(k_gather_copy<uint16_t>, grid, 256, 0, s, reinterpret_cast<const uint16_t *>(recv), ps, ro,
-                                                 P, bs, out, (ull)n_out);
+                                                 P, bs, out, (ull)n_out, (ull)min_len,
+                                                 as_int32 ? kFlip : 0u);
     else
         launch_k(k_gather_copy<int32_t>, grid, 256, 0, s, reinterpret_cast<const int32_t *>(recv), ps, ro,
-                                                 P, bs, out, (ull)n_out);
+                                                 P, bs, out, (ull)n_out, (ull)min_len,
+                                                 as_int32 ? kFlip : 0u);
     return hipGetLastError();
 }
 

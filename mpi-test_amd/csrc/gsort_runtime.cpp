@@ -247,6 +247,10 @@ gsort_status ensure(gsort_ctx *c, DevBuf &b, size_t bytes) {
                                             " over GSORT_ALLOC_LIMIT (rank " +
                                             std::to_string(c->rank) + ")");
     c->scratch_bytes -= std::min(c->scratch_bytes, b.cap);
+    // buffers known to hold zeros (K12a's fix[], K15s's status words and ticket) are no longer
+    // known to once replaced: a new allocation may come back at the same address
+    if (b.p && c->fix_clean == b.p) c->fix_clean = nullptr;
+    if (b.p && c->scan_clean == b.p) c->scan_clean = nullptr;
     hipError_t e = dev_free(b);
     if (e != hipSuccess)
         return set_err(c, GSORT_EHIP, "hipFree of " + buf_name(c, b) + " (rank " +
