@@ -292,6 +292,13 @@ __global__ __launch_bounds__(kRadix) void k_scan_digits(const unsigned long long
 // dispatch), so workgroup b runs on XCD b % 8.  Giving each XCD a contiguous range of tiles
 // keeps the partial 128-B lines shared by neighbouring tiles' digit runs in one L2, where they
 // merge before write-back.  Bijective for any tile count; speed only, never correctness.
+// A store through a pointer kept in LDS (a digit's output run) as a global, not flat, access:
+// flat stores also count against the LDS wait counter, so every later LDS wait waited on them
+template <typename T>
+__device__ __forceinline__ void st_global(T *p, T v) {
+    *reinterpret_cast<__attribute__((address_space(1))) T *>(reinterpret_cast<uintptr_t>(p)) = v;
+}
+
 __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t ntiles) {
     const uint32_t q = ntiles >> 3, r = ntiles & 7, x = b & 7, i = b >> 3;
     return x < r ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
@@ -447,7 +454,7 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(const uint32_t *__restrict__ 
         if (full || j < lim) {
             const uint32_t key = s_keys[j];
             uint32_t *dst = s_dst[(key >> shift) & 255u] + j;
-            *dst = FOUT ? (key ^ kFlip) : key;
+            st_global(dst, FOUT ? (key ^ kFlip) : key);
             if constexpr (KV) vout[dst - out] = s_vals[j];
         }
     }
@@ -830,7 +837,7 @@ __device__ __forceinline__ void partition_tile(const uint32_t *__restrict__ in, 
         const uint32_t j = (uint32_t)(i * BLOCK + tid);
         if (full || j < len) {
             const uint32_t key = s_keys[j];
-            s_dst[(key >> shift) & 255u][j] = (OT)(FOUT ? (key ^ kFlip) : key);
+            st_global(s_dst[(key >> shift) & 255u] + j, (OT)(FOUT ? (key ^ kFlip) : key));
         }
     }
 }
@@ -1932,6 +1939,138 @@ __device__ __forceinline__ void sort_bucket(uint32_t (&k)[ITEMS], uint32_t len, 
     }
 }
 
+// sort_bucket for keys that share their top 16 bits (top): the low halves travel two to a
+// register (kp[q] = key 2q | key 2q+1 << 16, ranks likewise) and one to an LDS slot, the two
+// digits below top are sorted as in sort_bucket, and top | key is stored flipped at dst.  Half
+// the VGPRs and LDS bytes of sort_bucket: a 16 896-key tile (K11g class 3) then fits three
+// workgroups per CU instead of two (112 -> <= 80 VGPRs, 76 -> 44 KiB).
+template <int BLOCK, int ITEMS>
+struct Pack16 {  // item i of a packed register array
+    static constexpr int NP = (ITEMS + 1) / 2;
+    __device__ static uint32_t get(const uint32_t (&a)[NP], int i) {
+        return (i & 1) ? a[i >> 1] >> 16 : a[i >> 1] & 0xFFFFu;
+    }
+    // the packed words as opaque values: without this the compiler keeps every key (rank)
+    // unpacked until its last use and packs late -- 33 live registers instead of 17
+    __device__ static void pin(uint32_t (&a)[NP]) {
+#pragma unroll
+        for (int q = 0; q < NP; ++q) asm volatile("" : "+v"(a[q]));
+    }
+    __device__ static void set(uint32_t (&a)[NP], int i, uint32_t v) {
+        a[i >> 1] = (i & 1) ? __builtin_amdgcn_perm(v, a[i >> 1], 0x05040100u)   // v.lo : a.lo
+                            : __builtin_amdgcn_perm(a[i >> 1], v, 0x07060100u);  // a.hi : v.lo
+    }
+};
+
+template <int BLOCK, int ITEMS, bool ATOMIC>
+__device__ __forceinline__ void sort_bucket16(uint32_t (&kp)[(ITEMS + 1) / 2], uint32_t len,
+                                              uint32_t top, uint32_t *__restrict__ dst,
+                                              uint16_t *s_a, uint32_t *s_wc, int ndigits = 2,
+                                              uint32_t koff = 0) {
+    using PK = Pack16<BLOCK, ITEMS>;
+    constexpr int NP = PK::NP;
+    constexpr int WAVES = BLOCK / 64;
+    constexpr int TILE = BLOCK * ITEMS;
+    static_assert(TILE <= 65536 && TILE % 2 == 0, "ranks fit 16 bits; the wave sums' words align");
+    static_assert(BLOCK >= kRadix, "one thread per digit in the scans");
+    uint32_t *s_wsum = reinterpret_cast<uint32_t *>(s_a + TILE - 2 * (kRadix / 64));
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    uint32_t *cnt = s_wc;
+    auto at = [](uint32_t j) constexpr -> uint32_t { return j + (j >> 5); };  // sort_bucket's pad
+    auto lim = [&](int i) -> uint32_t {
+        return len > (uint32_t)(i * BLOCK) ? len - (uint32_t)(i * BLOCK) : 0u;
+    };
+    auto block_scan = [&](uint32_t c) -> uint32_t {
+        const uint32_t v = wave_incl_add(c);
+        if (lane == 63) s_wsum[w] = v;
+        return v - c;
+    };
+    PK::pin(kp);
+    uint32_t rp[NP];
+#pragma unroll
+    for (int q = 0; q < NP; ++q) rp[q] = 0;
+    // digit 0: unstable counting sort into s_a
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i)
+        if ((uint32_t)tid < lim(i)) PK::set(rp, i, atomicAdd(&cnt[PK::get(kp, i) & 255u], 1u));
+    PK::pin(rp);
+    __syncthreads();
+    {
+        uint32_t excl = 0;
+        if (tid < kRadix) excl = block_scan(cnt[tid]);
+        __syncthreads();
+        if (tid < kRadix) {
+            for (int ww = 0; ww < w; ++ww) excl += s_wsum[ww];
+            cnt[tid] = excl;
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i)
+        if ((uint32_t)tid < lim(i)) {
+            const uint32_t x = PK::get(kp, i);
+            s_a[at(cnt[x & 255u] + PK::get(rp, i))] = (uint16_t)x;
+        }
+    __syncthreads();
+    // digit 1 (ndigits == 2): stable, wave-chunked (wave w owns [w*64*R, (w+1)*64*R))
+    if (ndigits > 1) {
+    const uint32_t R = (len + 64 * WAVES - 1) / (64 * WAVES);
+    uint32_t *wc = s_wc + w * kRadix;
+#pragma unroll
+    for (int j = 0; j < kRadix / 64; ++j) wc[j * 64 + lane] = 0;
+    const uint32_t base = (uint32_t)w * 64 * R;
+    const uint32_t wlen = len > base ? len - base : 0u;
+    const uint16_t *pa = s_a + at(base + lane);
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i)
+        if ((uint32_t)i < R && (uint32_t)(i * 64 + lane) < wlen) PK::set(kp, i, pa[i * at(64)]);
+    PK::pin(kp);
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i)
+        if ((uint32_t)i < R)
+            PK::set(rp, i, wave_rank<ATOMIC>(wc, PK::get(kp, i) >> 8,
+                                             (uint32_t)(i * 64 + lane) < wlen));
+    PK::pin(rp);
+    __syncthreads();
+    {
+        uint32_t tcount = 0, excl = 0;
+        if (tid < kRadix) {
+#pragma unroll
+            for (int ww = 0; ww < WAVES; ++ww) tcount += s_wc[ww * kRadix + tid];
+            excl = block_scan(tcount);
+        }
+        __syncthreads();
+        if (tid < kRadix) {
+            uint32_t off = excl;
+            for (int ww = 0; ww < w; ++ww) off += s_wsum[ww];
+#pragma unroll
+            for (int ww = 0; ww < WAVES; ++ww) {
+                const uint32_t cw = s_wc[ww * kRadix + tid];
+                s_wc[ww * kRadix + tid] = off;
+                off += cw;
+            }
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i)
+        if ((uint32_t)i < R && (uint32_t)(i * 64 + lane) < wlen) {
+            const uint32_t x = PK::get(kp, i);
+            s_a[at(wc[x >> 8] + PK::get(rp, i))] = (uint16_t)x;
+        }
+    __syncthreads();
+    }
+    const __amdgpu_buffer_rsrc_t rs = bucket_rsrc(dst, len * 4u);  // stores past len dropped
+    constexpr bool kNtFinal = TILE > 4608;  // (as sort_bucket)
+    static_assert(BLOCK % 32 == 0, "slot i * BLOCK + tid at at(tid) + i * at(BLOCK)");
+    const uint16_t *fa = s_a + at((uint32_t)tid);
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i)
+        __builtin_amdgcn_raw_buffer_store_b32(((top | fa[i * at(BLOCK)]) + koff) ^ kFlip, rs,
+                                              (i * BLOCK + tid) * 4, 0, kNtFinal ? 2 : 0);
+}
+
 // K11: sort each listed bucket {start, len} (<= BLOCK * ITEMS keys) of `in` on digits
 // 0 .. ndigits-1 in LDS and write it back flipped to int32 order at the same position of out.
 template <int BLOCK, int ITEMS, bool FIN, bool ATOMIC>
@@ -1962,6 +2101,20 @@ template <typename T>
 __device__ __forceinline__ const T *run_ptr(const T *recv, uint64_t off) {
     return reinterpret_cast<const T *>(reinterpret_cast<uintptr_t>(recv) + off * sizeof(T));
 }
+// A load through a run pointer as a global (not flat) access: the integer-formed address hides
+// the address space from the compiler, whose flat loads then keep a 64-bit address pair live
+// per load in flight (K11g class 3's one-run path: 84 VGPRs; global: SGPR base + 32-bit offset)
+template <typename T>
+__device__ __forceinline__ T ld_run(const T *p) {
+    return *reinterpret_cast<const __attribute__((address_space(1))) T *>(
+        reinterpret_cast<uintptr_t>(p));
+}
+__device__ __forceinline__ uint4 ld_run(const uint4 *p) {  // (HIP's uint4 is a class type)
+    typedef unsigned int v4 __attribute__((ext_vector_type(4)));
+    const v4 x = *reinterpret_cast<const __attribute__((address_space(1))) v4 *>(
+        reinterpret_cast<uintptr_t>(p));
+    return make_uint4(x.x, x.y, x.z, x.w);
+}
 
 // K11g (receive side of the distributed sorts): bucket h of the 2^16 top-16-bit buckets of
 // the P received sorted runs.  Its keys are the P pieces recv[roff[p] + pos[p][h] ..
@@ -1975,6 +2128,87 @@ __device__ __forceinline__ uint32_t recv_key(uint16_t x, uint32_t h) { return (h
 // pieces up to which K11g loads every key straight into registers (a piece lookup of P - 1
 // scalar compares per key); more pieces go through an LDS gather first
 constexpr int kGatherDirectP = 8;
+
+// K11g's loads of bucket h (entry: first output position dst, len keys) from its P pieces into
+// v[i] = key i * BLOCK + tid (past len: the last key again).  P == 1: the one run's bucket
+// offsets are the bucket starts, so the keys come straight from the entry (no pos load, no
+// piece table, no barrier in front of the loads -- round 6).  P <= kGatherDirectP: every key
+// straight into registers through the wave-uniform piece boundaries, all loads in flight.
+// Otherwise returns false with the piece table (s_src, s_cum) filled: the caller gathers the
+// pieces through LDS.
+template <int BLOCK, int ITEMS, typename T>
+__device__ __forceinline__ bool gather_direct(const T *recv, const unsigned long long *pos,
+                                              const unsigned long long *roff, int P, uint64_t h,
+                                              uint64_t dst, uint32_t len, uint64_t *s_src,
+                                              uint64_t *s_delta, uint32_t *s_cum, T (&v)[ITEMS]) {
+    const int tid = threadIdx.x;
+    const uint32_t last = len ? len - 1 : 0u;
+    if (P == 1) {
+        const T *src = run_ptr(recv, roff[0] + dst);
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i) v[i] = ld_run(src + min((uint32_t)(i * BLOCK + tid), last));
+        return true;
+    }
+    if (tid < 64) {  // lane p: piece p; wave scan of the piece lengths (DPP)
+        uint64_t a = 0, b = 0;
+        if (tid < P) {
+            a = pos[(uint64_t)tid * (kBuckets16 + 1) + h];
+            b = pos[(uint64_t)tid * (kBuckets16 + 1) + h + 1];
+        }
+        const uint32_t l = (uint32_t)(b - a);
+        const uint32_t vs = wave_incl_add(l);
+        if (tid < P) {
+            s_src[tid] = roff[tid] + a;
+            s_cum[tid] = vs - l;
+            s_delta[tid] = roff[tid] + a - (vs - l);  // key j of piece p: recv[delta + j]
+        }
+        if (tid == P - 1) s_cum[P] = vs;
+    }
+    __syncthreads();
+    if (P > kGatherDirectP) return false;
+    // key j lies in piece p(j) = #{q >= 1 : j >= cum[q]} (the boundaries are wave-uniform scalars)
+    uint32_t cum[kGatherDirectP];
+#pragma unroll
+    for (int q = 1; q < kGatherDirectP; ++q)
+        cum[q] = q < P ? (uint32_t)__builtin_amdgcn_readfirstlane((int)s_cum[q]) : 0xFFFFFFFFu;
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+        const uint32_t j = min((uint32_t)(i * BLOCK + tid), last);
+        uint32_t q = 0;
+#pragma unroll
+        for (int b = 1; b < kGatherDirectP; ++b) q += j >= cum[b] ? 1u : 0u;
+        v[i] = ld_run(run_ptr(recv, s_delta[q] + j));
+    }
+    return true;
+}
+
+// The pieces of bucket h into LDS slots 0 .. len (coalesced per piece, 8 loads in flight per
+// thread), each key as conv(value).
+template <int BLOCK, typename T, typename S, typename F>
+__device__ __forceinline__ void gather_lds(const T *recv, int P, const uint64_t *s_src,
+                                           const uint32_t *s_cum, S *s_a, F conv) {
+    const int tid = threadIdx.x;
+#pragma unroll 1
+    for (int p = 0; p < P; ++p) {
+        const T *src = run_ptr(recv, s_src[p]);
+        const uint32_t c0 = s_cum[p], c1 = s_cum[p + 1];
+#pragma unroll 1
+        for (uint32_t b = c0; b < c1; b += 8 * BLOCK) {
+            T v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const uint32_t j = b + u * BLOCK + tid;
+                v[u] = j < c1 ? ld_run(src + (j - c0)) : T(0);
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const uint32_t j = b + u * BLOCK + tid;
+                if (j < c1) s_a[j] = conv(v[u]);
+            }
+        }
+    }
+    __syncthreads();
+}
 
 template <int BLOCK, int ITEMS, bool ATOMIC, typename T>
 __global__ __launch_bounds__(BLOCK) void k_gather_sort(const T *__restrict__ recv,
@@ -2004,78 +2238,13 @@ __global__ __launch_bounds__(BLOCK) void k_gather_sort(const T *__restrict__ rec
     const uint32_t len = (uint32_t)list[2 * ei + 1];
     if (tid < kRadix) s_wc[tid] = 0;
     uint32_t k[ITEMS];
-    if (P == 1) {
-        // one run, whose bucket offsets are the bucket starts: the keys straight from the entry
-        // (no pos load, no piece table, no barrier in front of the loads -- round 6)
-        const T *src = run_ptr(recv, roff[0] + dst);
-        const uint32_t last = len ? len - 1 : 0u;
-        T v[ITEMS];
-#pragma unroll
-        for (int i = 0; i < ITEMS; ++i) v[i] = src[min((uint32_t)(i * BLOCK + tid), last)];
-#pragma unroll
-        for (int i = 0; i < ITEMS; ++i) k[i] = recv_key(v[i], (uint32_t)h);
-        __syncthreads();
-        sort_bucket<BLOCK, ITEMS, ATOMIC>(k, len, 2, out + dst, s_a, s_wc);
-        return;
-    }
-    if (tid < 64) {  // lane p: piece p; wave scan of the piece lengths (DPP)
-        uint64_t a = 0, b = 0;
-        if (tid < P) {
-            a = pos[(uint64_t)tid * (kBuckets16 + 1) + h];
-            b = pos[(uint64_t)tid * (kBuckets16 + 1) + h + 1];
-        }
-        const uint32_t l = (uint32_t)(b - a);
-        const uint32_t v = wave_incl_add(l);
-        if (tid < P) {
-            s_src[tid] = roff[tid] + a;
-            s_cum[tid] = v - l;
-            s_delta[tid] = roff[tid] + a - (v - l);  // key j of piece p: recv[delta + j]
-        }
-        if (tid == P - 1) s_cum[P] = v;
-    }
-    __syncthreads();
-    if (P <= kGatherDirectP) {
-        // every key straight into registers, all loads in flight: key j lies in piece
-        // p(j) = #{q >= 1 : j >= cum[q]} (the boundaries are wave-uniform scalars)
-        uint32_t cum[kGatherDirectP];
-#pragma unroll
-        for (int q = 1; q < kGatherDirectP; ++q)
-            cum[q] = q < P ? (uint32_t)__builtin_amdgcn_readfirstlane((int)s_cum[q]) : 0xFFFFFFFFu;
-        const uint32_t last = len ? len - 1 : 0u;
-        T v[ITEMS];
-#pragma unroll
-        for (int i = 0; i < ITEMS; ++i) {
-            const uint32_t j = min((uint32_t)(i * BLOCK + tid), last);
-            uint32_t q = 0;
-#pragma unroll
-            for (int b = 1; b < kGatherDirectP; ++b) q += j >= cum[b] ? 1u : 0u;
-            v[i] = *run_ptr(recv, s_delta[q] + j);
-        }
+    T v[ITEMS];
+    if (gather_direct<BLOCK, ITEMS>(recv, pos, roff, P, h, dst, len, s_src, s_delta, s_cum, v)) {
 #pragma unroll
         for (int i = 0; i < ITEMS; ++i) k[i] = recv_key(v[i], (uint32_t)h);
     } else {
-        // gather the pieces into s_a (coalesced per piece, 8 loads in flight per thread), then
-        // take the keys block-strided
-#pragma unroll 1
-        for (int p = 0; p < P; ++p) {
-            const T *src = run_ptr(recv, s_src[p]);
-            const uint32_t c0 = s_cum[p], c1 = s_cum[p + 1];
-#pragma unroll 1
-            for (uint32_t b = c0; b < c1; b += 8 * BLOCK) {
-                T v[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const uint32_t j = b + u * BLOCK + tid;
-                    v[u] = j < c1 ? src[j - c0] : T(0);
-                }
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const uint32_t j = b + u * BLOCK + tid;
-                    if (j < c1) s_a[j] = recv_key(v[u], (uint32_t)h);
-                }
-            }
-        }
-        __syncthreads();
+        gather_lds<BLOCK>(recv, P, s_src, s_cum, s_a,
+                          [&](T x) { return recv_key(x, (uint32_t)h); });
 #pragma unroll
         for (int i = 0; i < ITEMS; ++i) {
             const uint32_t j = (uint32_t)(i * BLOCK + tid);
@@ -2085,6 +2254,54 @@ __global__ __launch_bounds__(BLOCK) void k_gather_sort(const T *__restrict__ rec
     __syncthreads();
     sort_bucket<BLOCK, ITEMS, ATOMIC>(k, len, 2, out + dst, s_a, s_wc);
     (void)bstart;
+}
+
+// K11g over packed receive buckets (u16 low halves, the bucket's top 16 bits implied) with the
+// two-to-a-register body sort_bucket16 -- the 16 896-key class (P = 2's 16 384-key buckets).
+template <int BLOCK, int ITEMS, bool ATOMIC>
+__global__ __launch_bounds__(BLOCK) void k_gather_sort16(const uint16_t *__restrict__ recv,
+                                                         const unsigned long long *__restrict__ pos,
+                                                         const unsigned long long *__restrict__ roff,
+                                                         int P,
+                                                         const unsigned long long *__restrict__ list,
+                                                         uint32_t *__restrict__ out,
+                                                         const uint32_t *__restrict__ ndev,
+                                                         uint32_t first) {
+    constexpr int WAVES = BLOCK / 64;
+    constexpr int TILE = BLOCK * ITEMS;
+    constexpr int MAXP = 64;
+    constexpr int NP = (ITEMS + 1) / 2;
+    const uint32_t ei = first + blockIdx.x;
+    if (ndev && ei >= *ndev) return;
+    __shared__ uint16_t s_a[(lds_slots(TILE) + 1) & ~1];
+    __shared__ uint32_t s_wc[WAVES * kRadix];
+    __shared__ uint64_t s_src[MAXP];
+    __shared__ uint64_t s_delta[MAXP];
+    __shared__ uint32_t s_cum[MAXP + 1];
+    const int tid = threadIdx.x;
+    const uint64_t e0 = list[2 * ei];
+    const uint64_t h = e0 & 0xFFFFu, dst = e0 >> 16;
+    const uint32_t len = (uint32_t)list[2 * ei + 1];
+    if (tid < kRadix) s_wc[tid] = 0;
+    uint32_t kp[NP];
+    {
+        uint16_t v[ITEMS];
+        if (gather_direct<BLOCK, ITEMS>(recv, pos, roff, P, h, dst, len, s_src, s_delta, s_cum, v)) {
+#pragma unroll
+            for (int q = 0; q < NP; ++q)
+                kp[q] = (uint32_t)v[2 * q] | (2 * q + 1 < ITEMS ? (uint32_t)v[2 * q + 1] << 16 : 0u);
+        } else {
+            gather_lds<BLOCK>(recv, P, s_src, s_cum, s_a, [](uint16_t x) { return x; });
+#pragma unroll
+            for (int q = 0; q < NP; ++q) {
+                const uint32_t j0 = (uint32_t)(2 * q * BLOCK + tid), j1 = j0 + BLOCK;
+                kp[q] = (j0 < len ? (uint32_t)s_a[j0] : 0u) |
+                        (2 * q + 1 < ITEMS && j1 < len ? (uint32_t)s_a[j1] << 16 : 0u);
+            }
+        }
+    }
+    __syncthreads();
+    sort_bucket16<BLOCK, ITEMS, ATOMIC>(kp, len, (uint32_t)h << 16, out + dst, s_a, s_wc);
 }
 
 // Receive side, K11g bookkeeping.  pos[p][h] = keys of sorted run p whose top 16 bits (ordered
@@ -2101,7 +2318,7 @@ __global__ __launch_bounds__(256) void k_run_bounds(const int32_t *__restrict__ 
     uint64_t lo = 0, hi = rlen[p];
     while (lo < hi) {
         const uint64_t mid = (lo + hi) >> 1;
-        if ((uint64_t)((uint32_t)a[mid] ^ kFlip) < x) lo = mid + 1; else hi = mid;
+        if ((uint64_t)((uint32_t)ld_run(a + mid) ^ kFlip) < x) lo = mid + 1; else hi = mid;
     }
     pos[i] = lo;
 }
@@ -2176,7 +2393,7 @@ __global__ __launch_bounds__(1024) void k_hist_expand(const T *__restrict__ recv
 #pragma unroll
                 for (int u = 0; u < 8; ++u) {
                     const uint32_t j = j0 + u * NT + tid;
-                    v[u] = j < np ? (recv_key(src[j], h) & 0xFFFFu) : 0x10000u;
+                    v[u] = j < np ? (recv_key(ld_run(src + j), h) & 0xFFFFu) : 0x10000u;
                 }
 #pragma unroll
                 for (int u = 0; u < 8; ++u)
@@ -2330,10 +2547,11 @@ __device__ __forceinline__ void cx_fill_table(CxTable<T> &t, const T *recv,
         if (lane == 0) t.keys = 0;
         return;
     }
-    const uint32_t h = (uint32_t)ent[0] & 0xFFFFu;  // (bstart[h] rides above bit 16)
+    const uint64_t e0 = ld_run(ent), e1 = ld_run(ent + 1);  // (global loads: ent is a joined-list pointer)
+    const uint32_t h = (uint32_t)e0 & 0xFFFFu;  // (bstart[h] rides above bit 16)
     // a bucket past kHxMax is not K18c's: left as an empty one (recv_sort counts it in place,
     // giant_sort) -- its bins' u16 counts could not hold it
-    const bool giant = (uint32_t)ent[1] > (uint32_t)kHxMax;
+    const bool giant = (uint32_t)e1 > (uint32_t)kHxMax;
     uint64_t a = 0, b = 0, src = 0;
     if ((int)lane < P && !giant) {
         a = pos[(uint64_t)lane * (kBuckets16 + 1) + h];
@@ -2354,7 +2572,7 @@ __device__ __forceinline__ void cx_fill_table(CxTable<T> &t, const T *recv,
     if ((int)lane == P - 1) t.cumv[P] = x;
     if (lane == 0) {
         t.h = h;
-        t.keys = giant ? 0u : (uint32_t)ent[1];
+        t.keys = giant ? 0u : (uint32_t)e1;
         t.dst = bstart[h];
     }
 }
@@ -2371,7 +2589,7 @@ __device__ __forceinline__ void cx_fill_table_est(CxTable<T> &t, const T *y,
         return;
     }
     if (lane == 0) {
-        const uint64_t sw = ent[0], e = ent[1];
+        const uint64_t sw = ld_run(ent), e = ld_run(ent + 1);
         const uint64_t src = sw & ((1ull << 40) - 1);
         const uint32_t n = (uint32_t)(e >> 40);
         const uint32_t mis = (uint32_t)((reinterpret_cast<uintptr_t>(y + src) / sizeof(T)) & (E - 1));
@@ -2430,7 +2648,7 @@ __device__ __forceinline__ void cx_count_bucket(const T *recv, const CxTable<T> 
     for (uint32_t g0 = PF * NT; g0 < nv; g0 += U * NT) {
         uint4 y[U];
 #pragma unroll
-        for (uint32_t u = 0; u < U; ++u) y[u] = *cx_vec(recv, t, P, min(g0 + u * NT + tid, nv - 1));
+        for (uint32_t u = 0; u < U; ++u) y[u] = ld_run(cx_vec(recv, t, P, min(g0 + u * NT + tid, nv - 1)));
 #pragma unroll
         for (uint32_t u = 0; u < U; ++u)
             if (g0 + u * NT + tid < nv) cx_count_vec<WRAP, T, CB>(s_h, y[u], s_nw, s_wb, s_wd);
@@ -2443,7 +2661,7 @@ __device__ __forceinline__ void cx_count_bucket(const T *recv, const CxTable<T> 
         uint32_t j = ~0u;
         if (k < E) { if (k < hd) j = k; }
         else if (body + (k - E) < n) j = body + (k - E);
-        if (j != ~0u) cx_count<WRAP, CB>(s_h, (uint32_t)*run_ptr(recv, t.src[p] + j) & 0xFFFFu, s_nw, s_wb, s_wd);
+        if (j != ~0u) cx_count<WRAP, CB>(s_h, (uint32_t)ld_run(run_ptr(recv, t.src[p] + j)) & 0xFFFFu, s_nw, s_wb, s_wd);
     }
 }
 
@@ -2602,8 +2820,8 @@ __global__ __launch_bounds__(CB == 8 ? 512 : 1024) void k_count_expand(
     for (int q = 0; q < kCxLists; ++q) {
         nn[q] = 0;
         if (q < cl.nl) {
-            nn[q] = cl.ndev[q] ? *cl.ndev[q] : cl.n[q];
-            if (q == cl.skip && *reinterpret_cast<const unsigned long long *>(cl.skip_max) > kHxMax)
+            nn[q] = cl.ndev[q] ? ld_run(cl.ndev[q]) : cl.n[q];
+            if (q == cl.skip && ld_run(reinterpret_cast<const unsigned long long *>(cl.skip_max)) > kHxMax)
                 nn[q] = 0;
         }
         nlist += nn[q];
@@ -2646,7 +2864,7 @@ __global__ __launch_bounds__(CB == 8 ? 512 : 1024) void k_count_expand(
         const uint32_t nv = s_t[0].cumv[P];
 #pragma unroll
         for (uint32_t u = 0; u < PF; ++u)
-            if (u * NT + tid < nv) x[u] = *cx_vec(recv, s_t[0], P, u * NT + tid);
+            if (u * NT + tid < nv) x[u] = ld_run(cx_vec(recv, s_t[0], P, u * NT + tid));
     }
 #pragma unroll 1
     for (uint32_t i = blockIdx.x; i < nlist; i += gridDim.x) {
@@ -2695,8 +2913,8 @@ __global__ __launch_bounds__(CB == 8 ? 512 : 1024) void k_count_expand(
                 if (tid == 0) {
                     const uint32_t e = atomicAdd(fb_ctr, 1u);
                     const unsigned long long *en = entry(i);
-                    fb_list[2 * e] = en[0];
-                    fb_list[2 * e + 1] = en[1];
+                    fb_list[2 * e] = ld_run(en);
+                    fb_list[2 * e + 1] = ld_run(en + 1);
                 }
                 skip = true;
                 if (tid < NW) s_wsum[tid] = 0;  // no keys to expand (s_base below)
@@ -2723,7 +2941,7 @@ __global__ __launch_bounds__(CB == 8 ? 512 : 1024) void k_count_expand(
             const uint32_t nv = s_t[nxt].keys ? s_t[nxt].cumv[P] : 0u;
 #pragma unroll
             for (uint32_t u = 0; u < PF; ++u)
-                if (u * NT + tid < nv) x[u] = *cx_vec(recv, s_t[nxt], P, u * NT + tid);
+                if (u * NT + tid < nv) x[u] = ld_run(cx_vec(recv, s_t[nxt], P, u * NT + tid));
         }
         // expansion: the wave's keys are ONE run of out (cx_expand_wave)
         const uint32_t nkw = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_base[NW + w]);
@@ -2788,11 +3006,11 @@ __global__ __launch_bounds__(256) void k_gather_copy(const T *__restrict__ recv,
                 for (; i + 3 * 256 < e0; i += 4 * 256) {  // four loads in flight per lane
                     T v[4];
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) v[u] = src[i + u * 256];
+                    for (int u = 0; u < 4; ++u) v[u] = ld_run(src + (i + u * 256));
 #pragma unroll
                     for (int u = 0; u < 4; ++u) out[i + u * 256] = recv_key(v[u], h) ^ xo;
                 }
-                for (; i < e0; i += 256) out[i] = recv_key(src[i], h) ^ xo;
+                for (; i < e0; i += 256) out[i] = recv_key(ld_run(src + i), h) ^ xo;
             }
             cum += len;
         }
@@ -3619,6 +3837,47 @@ __global__ __launch_bounds__(BLOCK) void k_local_sort_e(const uint16_t *__restri
     sort_bucket<BLOCK, ITEMS, ATOMIC>(k, len, ndigits, dst, s_a, s_wc, koff);
 }
 
+// K11e's 16 896-key class on the packed body (sort_bucket16: two u16 keys per register, u16
+// LDS slots -- three workgroups per CU instead of two, as K11g class 3); ndigits 1 or 2.
+template <int BLOCK, int ITEMS, bool ATOMIC, int ND>
+__global__ __launch_bounds__(BLOCK) void k_local_sort_e16(const uint16_t *__restrict__ in,
+                                                          uint32_t *__restrict__ out,
+                                                          const unsigned long long *__restrict__ list,
+                                                          const unsigned long long *__restrict__ ctr,
+                                                          uint32_t first, int ndigits,
+                                                          unsigned long long *mail,
+                                                          const unsigned long long *ctr_all,
+                                                          const uint32_t *eflag,
+                                                          unsigned long long seq, uint32_t koff) {
+    constexpr int WAVES = BLOCK / 64;
+    constexpr int TILE = BLOCK * ITEMS;
+    constexpr int NP = (ITEMS + 1) / 2;
+    __shared__ uint16_t s_a[(lds_slots(TILE) + 1) & ~1];
+    __shared__ uint32_t s_wc[WAVES * kRadix];
+    if (mail && blockIdx.x == 0) publish_lists(mail, ctr_all, eflag, seq);  // K12g is done
+    const uint32_t i = first + blockIdx.x;
+    if (i >= (uint32_t)*ctr) return;
+    const uint64_t sw = list[2 * i];
+    const uint64_t e = list[2 * i + 1];
+    const uint32_t len = (uint32_t)(e >> 40), top = (uint32_t)(sw >> 40) << 16;
+    if (threadIdx.x < kRadix) s_wc[threadIdx.x] = 0;
+    uint32_t kp[NP];
+    {
+        const uint16_t *src = in + (sw & ((1ull << 40) - 1));
+        const uint32_t last = len ? len - 1 : 0u;
+        uint16_t v[ITEMS];
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) v[j] = src[min((uint32_t)(j * BLOCK) + threadIdx.x, last)];
+#pragma unroll
+        for (int q = 0; q < NP; ++q)
+            kp[q] = (uint32_t)v[2 * q] | (2 * q + 1 < ITEMS ? (uint32_t)v[2 * q + 1] << 16 : 0u);
+    }
+    __syncthreads();
+    (void)ndigits;
+    sort_bucket16<BLOCK, ITEMS, ATOMIC>(kp, len, top, out + (e & ((1ull << 40) - 1)), s_a, s_wc,
+                                        ND, koff);
+}
+
 // class geometries (block x items): class 3 as 1024 x 16 measured slower than 512 x 32 (local
 // 30-bit keys K11e 0.80 -> 0.90 ms, receive 16 384-key buckets 0.73 -> 0.87 ms per 2^28 keys,
 // round 4); class 2 as 256 x 36 needs 133 VGPRs (12 waves per CU).  Class 3 holds 512 x 33 =
@@ -4257,7 +4516,12 @@ hipError_t launch_gather_sort(const void *recv, bool packed16, const uint64_t *p
     switch (cls) {
         case 1: if (atomic_rank) GSORT_K11G(256, 18, true); else GSORT_K11G(256, 18, false); break;
         case 2: if (atomic_rank) GSORT_K11G(kC2Block, kC2Items, true); else GSORT_K11G(kC2Block, kC2Items, false); break;
-        case 3: if (atomic_rank) GSORT_K11G(kC3Block, kC3Items, true); else GSORT_K11G(kC3Block, kC3Items, false); break;
+        case 3:  // packed buckets: the two-to-a-register body (three workgroups per CU)
+            if (packed16) {
+                if (atomic_rank) launch_k(k_gather_sort16<kC3Block, kC3Items, true>, nlist, kC3Block, 0, s, r16, ps, ro, P, l, out, ndev, first);
+                else launch_k(k_gather_sort16<kC3Block, kC3Items, false>, nlist, kC3Block, 0, s, r16, ps, ro, P, l, out, ndev, first);
+            } else if (atomic_rank) GSORT_K11G(kC3Block, kC3Items, true); else GSORT_K11G(kC3Block, kC3Items, false);
+            break;
         default: if (atomic_rank) GSORT_K11G(1024, 32, true); else GSORT_K11G(1024, 32, false); break;
     }
 #undef GSORT_K11G
@@ -4537,7 +4801,18 @@ hipError_t launch_local_sort_e(const EstPlan &p, int cls, uint32_t first, uint32
     switch (cls) {
         case 1: GSORT_K11E(256, 18); break;
         case 2: GSORT_K11E(kC2Block, kC2Items); break;
-        case 3: GSORT_K11E(kC3Block, kC3Items); break;
+        case 3:  // the packed body (a one-value child: the copy kernel)
+            if (nd == 0) GSORT_K11E(kC3Block, kC3Items);
+            else if (nd == 1)
+                launch_k(k_local_sort_e16<kC3Block, kC3Items, true, 1>, nlist, kC3Block, 0, s, y,
+                         p.out, l, ctr, first, nd, mail, call, ef, seq, ko);
+            else if (p.atomic_rank)
+                launch_k(k_local_sort_e16<kC3Block, kC3Items, true, 2>, nlist, kC3Block, 0, s, y,
+                         p.out, l, ctr, first, nd, mail, call, ef, seq, ko);
+            else
+                launch_k(k_local_sort_e16<kC3Block, kC3Items, false, 2>, nlist, kC3Block, 0, s, y,
+                         p.out, l, ctr, first, nd, mail, call, ef, seq, ko);
+            break;
         default: GSORT_K11E(1024, 32); break;  // (shifted plans only: kEstCx)
     }
 #undef GSORT_K11E

@@ -160,3 +160,22 @@ def test_receive_launch_shapes_from_previous_call(gsort, monkeypatch, algo, cx, 
     res = _run_group_seq(gsort, seq, algo)
     for i, keys in enumerate(keys_all):
         _check(res[i], keys, P, algo)
+
+
+@pytest.mark.parametrize("algo", ["radix", "sample"])
+@pytest.mark.parametrize("P", [1, 2, 3, 12])
+def test_receive_class3_packed_body(gsort, monkeypatch, algo, P):
+    """16 384-key buckets (the P = 2 weak-scaling shape; 2^22 keys of 24 bits) on K11g class 3's
+    packed body (sort_bucket16: two u16 keys per register, u16 LDS slots): one run straight from
+    the entry (P = 1, forced distributed), pieces loaded directly (P = 2, 3) and gathered through
+    LDS (P = 12 > kGatherDirectP); plus a few buckets of one value and a ragged tail."""
+    if P == 1:
+        monkeypatch.setenv("GSORT_FORCE_DIST", "1")
+    rng = np.random.default_rng(300 + P)
+    keys = np.concatenate([rng.integers(0, 1 << 24, (1 << 22) - 30011),
+                           np.full(20000, 0x00A50000 + 7), np.full(10011, 0x00A60000)])
+    keys = keys.astype(np.int32)
+    rng.shuffle(keys)
+    B = -(-keys.size // P)
+    res = run_group(gsort, np.split(keys, np.arange(1, P) * B), algo)
+    _check(res, keys, P, algo)
