@@ -3795,7 +3795,7 @@ __global__ __launch_bounds__(64) void k_publish_lists(unsigned long long *mail,
 // block 0 first hands K12g's counters and status to the host (publish_lists), off the kernels'
 // critical path.
 // The child's keys come from Y as their low 16 bits; the entry's src word carries the top 16.
-template <int BLOCK, int ITEMS, bool ATOMIC, bool COPY = false>
+template <int BLOCK, int ITEMS, bool ATOMIC, bool COPY = false, int ND = 0>
 __global__ __launch_bounds__(BLOCK) void k_local_sort_e(const uint16_t *__restrict__ in,
                                                         uint32_t *__restrict__ out,
                                                         const unsigned long long *__restrict__ list,
@@ -3834,7 +3834,8 @@ __global__ __launch_bounds__(BLOCK) void k_local_sort_e(const uint16_t *__restri
         return;
     }
     __syncthreads();
-    sort_bucket<BLOCK, ITEMS, ATOMIC>(k, len, ndigits, dst, s_a, s_wc, koff);
+    // (ND: the digit count as a constant -- one straight-line pass pair, as K11g has)
+    sort_bucket<BLOCK, ITEMS, ATOMIC>(k, len, ND ? ND : ndigits, dst, s_a, s_wc, koff);
 }
 
 // K11e's 16 896-key class on the packed body (sort_bucket16: two u16 keys per register, u16
@@ -4791,6 +4792,9 @@ hipError_t launch_local_sort_e(const EstPlan &p, int cls, uint32_t first, uint32
         if (nd == 0)                                                                           \
             launch_k(k_local_sort_e<B, I, true, true>, nlist, B, 0, s, y, p.out, l, ctr, first, \
                      nd, mail, call, ef, seq, ko);                                             \
+        else if (p.atomic_rank && nd == 2)                                                     \
+            launch_k(k_local_sort_e<B, I, true, false, 2>, nlist, B, 0, s, y, p.out, l, ctr,   \
+                     first, nd, mail, call, ef, seq, ko);                                      \
         else if (p.atomic_rank)                                                                \
             launch_k(k_local_sort_e<B, I, true>, nlist, B, 0, s, y, p.out, l, ctr, first, nd,  \
                      mail, call, ef, seq, ko);                                                 \
