@@ -292,6 +292,26 @@ __global__ __launch_bounds__(kRadix) void k_scan_digits(const unsigned long long
 // dispatch), so workgroup b runs on XCD b % 8.  Giving each XCD a contiguous range of tiles
 // keeps the partial 128-B lines shared by neighbouring tiles' digit runs in one L2, where they
 // merge before write-back.  Bijective for any tile count; speed only, never correctness.
+// Items of a packed register array: item i in the low (even i) or high (odd i) half of word i/2
+// (values below 2^16: ranks, positions and keys of a tile whose keys share their top half).
+template <int BLOCK, int ITEMS>
+struct Pack16 {  // item i of a packed register array
+    static constexpr int NP = (ITEMS + 1) / 2;
+    __device__ static uint32_t get(const uint32_t (&a)[NP], int i) {
+        return (i & 1) ? a[i >> 1] >> 16 : a[i >> 1] & 0xFFFFu;
+    }
+    // the packed words as opaque values: without this the compiler keeps every key (rank)
+    // unpacked until its last use and packs late -- 33 live registers instead of 17
+    __device__ static void pin(uint32_t (&a)[NP]) {
+#pragma unroll
+        for (int q = 0; q < NP; ++q) asm volatile("" : "+v"(a[q]));
+    }
+    __device__ static void set(uint32_t (&a)[NP], int i, uint32_t v) {
+        a[i >> 1] = (i & 1) ? __builtin_amdgcn_perm(v, a[i >> 1], 0x05040100u)   // v.lo : a.lo
+                            : __builtin_amdgcn_perm(a[i >> 1], v, 0x07060100u);  // a.hi : v.lo
+    }
+};
+
 // A store through a pointer kept in LDS (a digit's output run) as a global, not flat, access:
 // flat stores also count against the LDS wait counter, so every later LDS wait waited on them
 template <typename T>
@@ -1868,9 +1888,23 @@ __device__ __forceinline__ void sort_bucket(uint32_t (&k)[ITEMS], uint32_t len, 
             cnt[tid] = excl;
         }
         __syncthreads();
+        // every digit start read before any key is written, and with no predicate (a slot past
+        // len reads some start, harmlessly; its write below stays masked): interleaved, or each
+        // read inside its own masked block, every write waited for its own read -- an LDS
+        // round trip per key-slot (the compiler cannot move a read of cnt above a write to s_a;
+        // K11e class 2 -1.5 %, profiles/r06_ab_batched_lds_reads.txt).  Not in the 32 768-key
+        // class, whose 128 VGPRs then spill.
+        if constexpr (lds_pad(TILE)) {
 #pragma unroll
-        for (int i = 0; i < ITEMS; ++i)
-            if ((uint32_t)tid < lim(i)) s_a[at(cnt[k[i] & 255u] + r[i])] = k[i];
+            for (int i = 0; i < ITEMS; ++i) r[i] += cnt[k[i] & 255u];
+#pragma unroll
+            for (int i = 0; i < ITEMS; ++i)
+                if ((uint32_t)tid < lim(i)) s_a[at(r[i])] = k[i];
+        } else {
+#pragma unroll
+            for (int i = 0; i < ITEMS; ++i)
+                if ((uint32_t)tid < lim(i)) s_a[at(cnt[k[i] & 255u] + r[i])] = k[i];
+        }
         __syncthreads();
     }
 
@@ -1914,10 +1948,19 @@ __device__ __forceinline__ void sort_bucket(uint32_t (&k)[ITEMS], uint32_t len, 
             }
         }
         __syncthreads();
+        if constexpr (lds_pad(TILE)) {
 #pragma unroll
-        for (int i = 0; i < ITEMS; ++i)
-            if ((uint32_t)i < R && (uint32_t)(i * 64 + lane) < wlen)
-                s_a[at(wc[(k[i] >> shift) & 255u] + rk[i])] = k[i];
+            for (int i = 0; i < ITEMS; ++i)  // (starts first, unpredicated, then the keys: as digit 0)
+                rk[i] += wc[(k[i] >> shift) & 255u];
+#pragma unroll
+            for (int i = 0; i < ITEMS; ++i)
+                if ((uint32_t)i < R && (uint32_t)(i * 64 + lane) < wlen) s_a[at(rk[i])] = k[i];
+        } else {
+#pragma unroll
+            for (int i = 0; i < ITEMS; ++i)
+                if ((uint32_t)i < R && (uint32_t)(i * 64 + lane) < wlen)
+                    s_a[at(wc[(k[i] >> shift) & 255u] + rk[i])] = k[i];
+        }
         __syncthreads();
     }
     const __amdgpu_buffer_rsrc_t rs = bucket_rsrc(dst, len * (STORE16 ? 2u : 4u));  // stores past len dropped
@@ -1944,23 +1987,6 @@ __device__ __forceinline__ void sort_bucket(uint32_t (&k)[ITEMS], uint32_t len, 
 // digits below top are sorted as in sort_bucket, and top | key is stored flipped at dst.  Half
 // the VGPRs and LDS bytes of sort_bucket: a 16 896-key tile (K11g class 3) then fits three
 // workgroups per CU instead of two (112 -> <= 80 VGPRs, 76 -> 44 KiB).
-template <int BLOCK, int ITEMS>
-struct Pack16 {  // item i of a packed register array
-    static constexpr int NP = (ITEMS + 1) / 2;
-    __device__ static uint32_t get(const uint32_t (&a)[NP], int i) {
-        return (i & 1) ? a[i >> 1] >> 16 : a[i >> 1] & 0xFFFFu;
-    }
-    // the packed words as opaque values: without this the compiler keeps every key (rank)
-    // unpacked until its last use and packs late -- 33 live registers instead of 17
-    __device__ static void pin(uint32_t (&a)[NP]) {
-#pragma unroll
-        for (int q = 0; q < NP; ++q) asm volatile("" : "+v"(a[q]));
-    }
-    __device__ static void set(uint32_t (&a)[NP], int i, uint32_t v) {
-        a[i >> 1] = (i & 1) ? __builtin_amdgcn_perm(v, a[i >> 1], 0x05040100u)   // v.lo : a.lo
-                            : __builtin_amdgcn_perm(a[i >> 1], v, 0x07060100u);  // a.hi : v.lo
-    }
-};
 
 template <int BLOCK, int ITEMS, bool ATOMIC>
 __device__ __forceinline__ void sort_bucket16(uint32_t (&kp)[(ITEMS + 1) / 2], uint32_t len,
@@ -2006,8 +2032,8 @@ __device__ __forceinline__ void sort_bucket16(uint32_t (&kp)[(ITEMS + 1) / 2], u
         __syncthreads();
     }
 #pragma unroll
-    for (int i = 0; i < ITEMS; ++i)
-        if ((uint32_t)tid < lim(i)) {
+    for (int i = 0; i < ITEMS; ++i)  // (interleaved: sort_bucket's batched start reads measured
+        if ((uint32_t)tid < lim(i)) {  // +5 % on this body, profiles/r06_ab_batched_lds_reads.txt)
             const uint32_t x = PK::get(kp, i);
             s_a[at(cnt[x & 255u] + PK::get(rp, i))] = (uint16_t)x;
         }
