@@ -18,7 +18,7 @@ tens of ms of load to reach its sustained clocks, and 5 warm-up sorts (~7 ms) di
 there -- the same build measured 1.364-1.369 ms per step without it, 1.331-1.335 ms with
 30-300 ms of copies first, 1.353 ms with 50 warm-up sorts.
 
-`roofline` prices the dominant kernel class (by total device time: K3u partition, K11 bucket sort or K3 LSD pass, 8 B/key algorithmic traffic each)
+`roofline` prices the dominant kernel class (by total device time: on the sampled plan K3r, K3a or K11e -- 8, 6 and 6 B/key of algorithmic traffic; K3u, K11 or an LSD pass on the other plans)
 with its average duration measured live by HIP events recorded on libgsort's own stream
 around every launch; `traffic` is the HBM bytes per launch from the rocprofv3 PMC summary in
 profiles/ (FETCH_SIZE x 2 + WRITE_SIZE, gfx950 correction) when one exists for this
