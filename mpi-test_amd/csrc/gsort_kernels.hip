@@ -2299,7 +2299,7 @@ __global__ __launch_bounds__(BLOCK) void k_gather_sort16(const uint16_t *__restr
     constexpr int NP = (ITEMS + 1) / 2;
     const uint32_t ei = first + blockIdx.x;
     if (ndev && ei >= *ndev) return;
-    __shared__ uint16_t s_a[(lds_slots(TILE) + 1) & ~1];
+    __shared__ __attribute__((aligned(16))) uint16_t s_a[(lds_slots(TILE) + 1) & ~1];  // (s_wsum: u32 words in it)
     __shared__ uint32_t s_wc[WAVES * kRadix];
     __shared__ uint64_t s_src[MAXP];
     __shared__ uint64_t s_delta[MAXP];
@@ -3879,7 +3879,7 @@ __global__ __launch_bounds__(BLOCK) void k_local_sort_e16(const uint16_t *__rest
     constexpr int WAVES = BLOCK / 64;
     constexpr int TILE = BLOCK * ITEMS;
     constexpr int NP = (ITEMS + 1) / 2;
-    __shared__ uint16_t s_a[(lds_slots(TILE) + 1) & ~1];
+    __shared__ __attribute__((aligned(16))) uint16_t s_a[(lds_slots(TILE) + 1) & ~1];  // (s_wsum: u32 words in it)
     __shared__ uint32_t s_wc[WAVES * kRadix];
     if (mail && blockIdx.x == 0) publish_lists(mail, ctr_all, eflag, seq);  // K12g is done
     const uint32_t i = first + blockIdx.x;
