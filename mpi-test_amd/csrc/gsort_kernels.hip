@@ -3526,10 +3526,45 @@ __global__ __launch_bounds__(kRadix) void k_est_plan(
     if (e == 0) { s_m = 0; s_bad = 0; s_ne = 0; s_maxc = 0; }
     __syncthreads();
     static_assert(kEstWG <= kRadix && kEstWG % (kRadix / 8) == 0, "K12e geometry");
-    if (e < kEstWG) {
-        const uint32_t v = msamp[e];
-        atomicAdd(&s_m, v & 0x7fffffffu);
-        if (v >> 31) s_bad = 1;
+    // every load issued before any is used: the partial words, the shard counts, then the
+    // per-workgroup sample totals (their adds used to wait for their own load first, and block 0's
+    // summaries with their global atomics ran ahead of its partial loads -- both in front of the
+    // kernel's one HBM round trip)
+    // bucket s's 64 packed words of every partial: lane l reads word l of the partials
+    // b = g, g + G, ..; four children per word
+    uint32_t c4[4] = {0, 0, 0, 0};
+    const uint32_t *pw = part8 + s * (kRadix / 4) + l;
+    constexpr uint32_t NB = kEstWG / G;  // all of a thread's partial words in flight at once
+    uint32_t pv[NB];
+#pragma unroll
+    for (uint32_t b = 0; b < NB; ++b) pv[b] = pw[(uint64_t)(g + b * G) * kEstPartWords];
+    // shard counts of bucket s: thread (b0 = e >> 3, x = e & 7) over partials b0, b0 + 32, ..
+    const uint32_t x3 = e & 7u, b0 = e >> 3;
+    constexpr uint32_t NB3 = kEstWG / (kRadix / 8);
+    uint32_t pv3[NB3];
+#pragma unroll
+    for (uint32_t b = 0; b < NB3; ++b)
+        pv3[b] = part3[((uint64_t)s * kEstWG + b0 + b * (kRadix / 8)) * kShards + x3];
+    const uint32_t mv = e < kEstWG ? msamp[e] : 0u;
+#pragma unroll
+    for (uint32_t b = 0; b < NB; ++b)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) c4[q] += (pv[b] >> (8 * q)) & 255u;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) s_c[g][4 * l + q] = c4[q];
+    {
+        uint32_t c3 = 0;
+#pragma unroll
+        for (uint32_t b = 0; b < NB3; ++b) c3 += pv3[b];
+        s_3[b0][x3] = c3;
+    }
+    {  // the samples' total (one atomic a wave) and any wrapped counter
+        const uint32_t tot = wave_incl_add(mv & 0x7fffffffu);
+        const bool wrapped = __ballot((mv >> 31) != 0u) != 0;
+        if (l == 63) {
+            atomicAdd(&s_m, tot);
+            if (wrapped) s_bad = 1;
+        }
     }
     if (s == 0) {  // block 0: the samples' varying bits, min, max and any wrap, one atomic a wave
         uint32_t vy = 0, lo = ~0u, hi = 0, wr = 0;
@@ -3552,31 +3587,6 @@ __global__ __launch_bounds__(kRadix) void k_est_plan(
             atomicMax(eflag + 7, hi);
             if (wr) atomicMax(eflag + 8, ~0u);  // wrapped: the child counts say nothing
         }
-    }
-    // bucket s's 64 packed words of every partial: lane l reads word l of the partials
-    // b = g, g + G, ..; four children per word
-    uint32_t c4[4] = {0, 0, 0, 0};
-    const uint32_t *pw = part8 + s * (kRadix / 4) + l;
-    constexpr uint32_t NB = kEstWG / G;  // all of a thread's partial words in flight at once
-    uint32_t pv[NB];
-#pragma unroll
-    for (uint32_t b = 0; b < NB; ++b) pv[b] = pw[(uint64_t)(g + b * G) * kEstPartWords];
-#pragma unroll
-    for (uint32_t b = 0; b < NB; ++b)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) c4[q] += (pv[b] >> (8 * q)) & 255u;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) s_c[g][4 * l + q] = c4[q];
-    {  // shard counts of bucket s: thread (b0 = e >> 3, x = e & 7) over partials b0, b0 + 32, ..
-        const uint32_t x = e & 7u, b0 = e >> 3;
-        constexpr uint32_t NB3 = kEstWG / (kRadix / 8);
-        uint32_t pv3[NB3], c3 = 0;
-#pragma unroll
-        for (uint32_t b = 0; b < NB3; ++b)
-            pv3[b] = part3[((uint64_t)s * kEstWG + b0 + b * (kRadix / 8)) * kShards + x];
-#pragma unroll
-        for (uint32_t b = 0; b < NB3; ++b) c3 += pv3[b];
-        s_3[b0][x] = c3;
     }
     __syncthreads();
     uint32_t cnt = 0;
