@@ -1346,6 +1346,25 @@ __device__ __forceinline__ unsigned long long block_excl_scan(unsigned long long
     return excl;
 }
 
+// block_excl_scan of values whose wave sums stay below 2^32 (counts of one block's <= 2^31 keys):
+// the wave scan in DPP (no LDS round trip per step, as __shfl_up's bpermute costs), the
+// cross-wave sums in 64 bits as above
+__device__ __forceinline__ unsigned long long block_excl_scan32(uint32_t v, unsigned long long *s_w,
+                                                                unsigned long long *total) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint32_t x = wave_incl_add(v);
+    __syncthreads();
+    if (lane == 63) s_w[w] = x;
+    __syncthreads();
+    unsigned long long excl = x - v, all = 0;
+    for (uint32_t ww = 0; ww < kRadix / 64; ++ww) {
+        if (ww < w) excl += s_w[ww];
+        all += s_w[ww];
+    }
+    *total = all;
+    return excl;
+}
+
 // K12a: block s = level-3 digit, thread e = level-2 digit.  The count of child (s, e) in shard
 // x = the e-half of word s*128 + e/2 summed over the partials b = x (mod 8), + fix[x][s*256+e].
 // Writes ccount[s*256+e] (all shards), t3[x*256+s] (bucket s in shard x) and tot[s].
@@ -3612,7 +3631,7 @@ __global__ __launch_bounds__(kRadix) void k_est_plan(
     const uint32_t i = s * kRadix + e;
     capc[i] = cc;
     unsigned long long tot;
-    const uint32_t off = (uint32_t)block_excl_scan(cc, s_w, &tot);
+    const uint32_t off = (uint32_t)block_excl_scan32(cc, s_w, &tot);  // (cc <= kHxMax: sums < 2^28)
     cur2[i] = off;
     init2[i] = off;
     lim2[i] = off + cc;
@@ -3689,12 +3708,7 @@ __global__ __launch_bounds__(256) void k_est_tiles(const uint32_t *__restrict__ 
             pieces[tid * kShards + x] = {bases3[tid] + init3[x * kRadix + tid], vs[x], vs[x + 1]};
     }
     const uint32_t nt = (vs[kShards] + kSweepTile - 1) / kSweepTile;
-    uint32_t v = nt;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t t = __shfl_up(v, o);
-        if ((int)lane >= o) v += t;
-    }
+    const uint32_t v = wave_incl_add(nt);  // (DPP: no LDS round trip per step)
     if (lane == 63) s_w[w] = v;
     __syncthreads();
     uint32_t run = v - nt;
@@ -3753,19 +3767,26 @@ __global__ __launch_bounds__(kRadix) void k_est_classify(
     __shared__ unsigned long long s_keys[NL], s_max[NL], s_base[NL];
     const uint32_t s = blockIdx.x, e = threadIdx.x;
     unsigned long long *ctr = reinterpret_cast<unsigned long long *>(wl.ctr);
+    // (the cursors loaded before the status word is looked at: every load in flight at once;
+    // an ineligible plan's stale cursors are read, never used)
+    const uint32_t i = s * kRadix + e;
+    const uint32_t c0 = init2[i], c2 = cur2[i], l2 = lim2[i];
+    uint32_t c3[kShards], i3[kShards];
+#pragma unroll
+    for (uint32_t x = 0; x < kShards; ++x) { c3[x] = cur3[x * kRadix + e]; i3[x] = init3[x * kRadix + e]; }
     if (!(*eflag & 4u)) {
         if (e < NL) { s_n[e] = 0; s_keys[e] = 0; s_max[e] = 0; }
-        unsigned long long te = 0;
-        for (uint32_t x = 0; x < kShards; ++x) te += cur3[x * kRadix + e] - init3[x * kRadix + e];
+        uint32_t te = 0;  // (bucket e's keys: at most the block's, < 2^32)
+#pragma unroll
+        for (uint32_t x = 0; x < kShards; ++x) te += c3[x] - i3[x];
         unsigned long long all;
-        const unsigned long long fb = block_excl_scan(te, s_w, &all);
+        const unsigned long long fb = block_excl_scan32(te, s_w, &all);
         if (e == s) s_fb = fb;
-        const uint32_t i = s * kRadix + e;
-        const uint32_t c0 = init2[i], len = cur2[i] - c0;
-        const bool over = cur2[i] > lim2[i];
+        const uint32_t len = c2 - c0;
+        const bool over = c2 > l2;
         if (over) atomicOr(eflag + 1, 1u);
         unsigned long long tot;
-        const unsigned long long ex = block_excl_scan(len, s_w, &tot);  // (syncs: s_fb visible)
+        const unsigned long long ex = block_excl_scan32(len, s_w, &tot);  // (syncs: s_fb visible)
         const unsigned long long dst = s_fb + ex;
         int which = -1;  // K11e class, or 0: past kLocalMax, K18c
         if (len > 0 && !over) {
